@@ -1,0 +1,41 @@
+"""Helpers shared by the parity tests: load a golden fixture and drive an env through the same inputs."""
+import os
+
+import numpy as np
+
+import synth
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16"]
+
+
+def load(name):
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    return {k: d[k] for k in d.files}
+
+
+def terrain_of(fx):
+    if str(fx["mesh_type"]) in ("trimesh", "heightfield"):
+        return {"terrain_origins": fx["init_terrain_origins"], "height_samples": fx["init_height_samples"]}
+    return None
+
+
+def synth_physics(fx):
+    seed = int(fx["synth_seed"])
+    n = int(fx["num_envs"])
+
+    def physics(g, torques, env):
+        root, dof, rigid, contact = synth.state(seed, n, g, np.asarray(env.env_origins))
+        return root, dof, rigid, contact
+    return physics
+
+
+def assert_close(name, got, ref, rtol=1e-4, atol=1e-4, ctx=""):
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, f"{name}{ctx}: shape {got.shape} vs {ref.shape}"
+    bad = ~np.isclose(got, ref, rtol=rtol, atol=atol)
+    if bad.any():
+        idx = np.argwhere(bad)[:5]
+        msg = ", ".join(f"{tuple(i)}: {got[tuple(i)]:.7g} vs {ref[tuple(i)]:.7g}" for i in idx)
+        raise AssertionError(f"{name}{ctx}: {bad.sum()} mismatches: {msg}")
