@@ -156,6 +156,10 @@ class T1Oracle:
         # sim state (Gym tensors)
         self.root = np.zeros((N, 13), f32)
         self.root[:, 6] = 1.0
+        # start pose (legged_robot.py:1380-1383): origin + U(-1,1) xy jitter; Gym reports it after prepare_sim
+        self.root[:, 0:3] = self.env_origins
+        self.root[:, 0] += R.rand_float(-1.0, 1.0, seed, self.ids, 0, R.SLOT_START_XY + 0)
+        self.root[:, 1] += R.rand_float(-1.0, 1.0, seed, self.ids, 0, R.SLOT_START_XY + 1)
         self.dof = np.zeros((N, 12, 2), f32)
         self.rigid = np.zeros((N, 13, 13), f32)
         self.rigid[:, :, 6] = 1.0

@@ -121,6 +121,8 @@ class FakeGym:
         return self.num_envs - 1
 
     def create_actor(self, env, asset, pose, name, group, filt, seg):
+        self.start_poses = getattr(self, "start_poses", {})
+        self.start_poses[env] = (pose.p.x, pose.p.y, pose.p.z)
         return 0
 
     def set_actor_dof_properties(self, env, actor, props):
@@ -144,6 +146,9 @@ class FakeGym:
         self.tensors = dict(root=torch.zeros(n, 13), dof=torch.zeros(n * nd, 2),
                             contact=torch.zeros(n * nb, 3), rigid=torch.zeros(n * nb, 13))
         self.tensors["root"][:, 6] = 1.0
+        # like Isaac Gym after prepare_sim: root states hold the actors' start poses
+        for e, p in getattr(self, "start_poses", {}).items():
+            self.tensors["root"][e, 0:3] = torch.tensor(p)
 
     def create_camera_sensor(self, env, props):
         return 0

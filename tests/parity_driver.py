@@ -1,0 +1,138 @@
+"""Drive the HIP env with injected physics through a golden scenario and compare with the reference.
+
+The reference outputs (tests/golden/*.npz) were produced by the reference's own env code running on the
+same synthetic physics states (tests/golden/synth.py) with the same counter-RNG draws.  Tolerance: 1e-4
+relative with a 1e-4 absolute floor (north_star), exact for bool / integer buffers.
+"""
+import copy
+
+import numpy as np
+import torch
+
+import synth
+from golden_util import assert_close, load
+
+REWARD_NAMES = sorted(["joint_pos", "feet_clearance", "feet_contact_number", "feet_air_time", "foot_slip",
+                       "feet_distance", "knee_distance", "feet_rotation", "feet_contact_forces",
+                       "tracking_lin_vel", "tracking_ang_vel", "vel_mismatch_exp", "low_speed",
+                       "track_vel_hard", "default_joint_pos", "orientation", "base_height", "base_acc",
+                       "action_smoothness", "torques", "dof_vel", "dof_acc", "collision", "stand_still"])
+
+
+def make_env_for(fx, device="cuda:0"):
+    from ti5_isaacgym_amd import make_t1_env
+
+    name_hook = None
+    if str(fx["mesh_type"]) == "trimesh":
+        def name_hook(cfg):
+            cfg.terrain.num_rows, cfg.terrain.num_cols, cfg.terrain.border_size = 6, 4, 5
+    return make_t1_env(num_envs=int(fx["num_envs"]), mesh_type=str(fx["mesh_type"]), seed=int(fx["seed"]),
+                       device=device, cfg_hook=name_hook)
+
+
+class Injector:
+    """Builds the t1env_injected struct for one env step from synth states."""
+
+    def __init__(self, env, seed):
+        self.env, self.seed, self.g = env, seed, 0
+
+    def next(self):
+        from ti5_isaacgym_amd import _lib
+        env = self.env
+        n = env.num_envs
+        origins = env.env_origins.cpu().numpy()
+        roots, dofs = [], []
+        for s in range(10):
+            r, d, rig, con = synth.state(self.seed, n, self.g + s, origins)
+            roots.append(r)
+            dofs.append(d)
+        self.g += 10
+        dev = env.device
+        self._keep = [torch.from_numpy(np.stack(roots)).to(dev), torch.from_numpy(np.stack(dofs)).to(dev),
+                      torch.from_numpy(rig).to(dev), torch.from_numpy(con).to(dev),
+                      torch.zeros(10, n, 12, device=dev)]
+        inj = _lib.Injected()
+        P = _lib.C.cast
+        inj.root, inj.dof, inj.rigid, inj.contact, inj.torque_log = [P(t.data_ptr(), _lib.fp) for t in self._keep]
+        return inj
+
+    @property
+    def torque_log(self):
+        return self._keep[4]
+
+
+def snapshot(env):
+    n = env.num_envs
+    ex = env.extras.get("episode", {})
+    return dict(
+        obs=env.obs_buf[:, -47:].cpu().numpy(), priv=env.privileged_obs_buf.cpu().numpy(),
+        rew=env.rew_buf.cpu().numpy(), reset=env.reset_buf.cpu().numpy(), time_out=env.time_out_buf.cpu().numpy(),
+        commands=env.commands.cpu().numpy(), gait_time=env.gait_time.cpu().numpy(),
+        ref_dof_pos=env.ref_dof_pos.cpu().numpy(), feet_air_time=env.feet_air_time.cpu().numpy(),
+        feet_height=env.feet_height.cpu().numpy(), episode_length_buf=env.episode_length_buf.cpu().numpy(),
+        ext_forces=env.ext_forces.cpu().numpy(), env_origins=env.env_origins.cpu().numpy(),
+        root_states=env.root_states.cpu().numpy(), dof_state=env.dof_state.view(n, 12, 2).cpu().numpy(),
+        episode_sums=np.stack([env.episode_sums[k].cpu().numpy() for k in REWARD_NAMES]),
+        extras_episode=np.array([float(ex["rew_" + k]) for k in REWARD_NAMES], np.float32) if ex else None,
+        max_command_x=ex.get("max_command_x") if ex else None, applied_force=env.applied_force.cpu().numpy(),
+        full_obs=env.obs_buf.cpu().numpy(), gait_start=env.gait_start.cpu().numpy(),
+        dof_lag=env.dof_lag_timestep.cpu().numpy(), imu_lag=env.imu_lag_timestep.cpu().numpy(),
+        lag=env.lag_timestep.cpu().numpy(), kp=env.randomized_p_gains.cpu().numpy(),
+        armature=env.joint_armatures.cpu().numpy())
+
+
+def run_parity(name, max_steps=None, device="cuda:0", check=True):
+    fx = load(name)
+    env = make_env_for(fx, device)
+    assert_close("env_frictions", env.env_frictions.cpu().numpy(), fx["init_env_frictions"])
+    assert_close("body_mass", env.body_mass.cpu().numpy(), fx["init_body_mass"])
+    if "init_terrain_levels" in fx:
+        np.testing.assert_array_equal(env.terrain_levels.cpu().numpy(), fx["init_terrain_levels"])
+        np.testing.assert_array_equal(env.terrain_types.cpu().numpy(), fx["init_terrain_types"])
+        assert_close("env_origins_init", env.env_origins.cpu().numpy(), fx["init_env_origins"])
+    inj = Injector(env, int(fx["synth_seed"]))
+    # reset(): reset_idx(all) + step(zeros) with injected physics
+    env.reset_idx_all()
+    env.step(torch.zeros(env.num_envs, 12, device=env.device), _injected=inj.next())
+    outs = [dict(snapshot(env), torques=inj.torque_log.cpu().numpy())]
+    if "override_episode_length_buf" in fx:
+        env.episode_length_buf = torch.from_numpy(fx["override_episode_length_buf"])
+    if "override_common_step_counter" in fx:
+        env.common_step_counter = int(fx["override_common_step_counter"])
+    if "override_episode_sums_tracking_lin_vel" in fx:
+        env.episode_sums["tracking_lin_vel"].copy_(torch.from_numpy(fx["override_episode_sums_tracking_lin_vel"]))
+    steps = fx["actions"].shape[0] if max_steps is None else min(max_steps, fx["actions"].shape[0])
+    for t in range(steps):
+        env.step(torch.from_numpy(fx["actions"][t]).to(env.device), _injected=inj.next())
+        outs.append(dict(snapshot(env), torques=inj.torque_log.cpu().numpy()))
+    if check:
+        compare(name, fx, outs)
+    return env, outs
+
+
+def compare(name, fx, outs):
+    for t, s in enumerate(outs):
+        ctx = f" [{name} step {t}]"
+        np.testing.assert_array_equal(s["reset"], fx["step_reset"][t], err_msg="reset" + ctx)
+        np.testing.assert_array_equal(s["time_out"], fx["step_time_out"][t], err_msg="time_out" + ctx)
+        np.testing.assert_array_equal(s["gait_time"], fx["step_gait_time"][t], err_msg="gait_time" + ctx)
+        np.testing.assert_array_equal(s["episode_length_buf"], fx["step_episode_length_buf"][t], err_msg="ep_len" + ctx)
+        np.testing.assert_array_equal(s["dof_lag"], fx["step_dof_lag_timestep"][t], err_msg="dof_lag" + ctx)
+        np.testing.assert_array_equal(s["imu_lag"], fx["step_imu_lag_timestep"][t], err_msg="imu_lag" + ctx)
+        np.testing.assert_array_equal(s["lag"], fx["step_lag_timestep"][t], err_msg="lag" + ctx)
+        assert_close("gait_start", s["gait_start"], fx["step_gait_start"][t], ctx=ctx)
+        for k in ("torques", "commands", "ref_dof_pos", "feet_air_time", "feet_height", "ext_forces",
+                  "env_origins", "root_states", "episode_sums", "dof_state"):
+            assert_close(k, s[k], fx["step_" + k][t], ctx=ctx)
+        assert_close("kp", s["kp"], fx["step_randomized_p_gains"][t], ctx=ctx)
+        assert_close("armature", s["armature"], fx["step_joint_armatures"][t], ctx=ctx)
+        assert_close("obs", s["obs"], fx["step_obs"][t], ctx=ctx)
+        assert_close("priv", s["priv"], fx["step_priv"][t], ctx=ctx)
+        assert_close("rew", s["rew"], fx["step_rew"][t], ctx=ctx)
+        if t > 0:
+            assert_close("extras_episode", s["extras_episode"], fx["step_extras_episode"][t], ctx=ctx)
+            assert abs(s["max_command_x"] - float(fx["step_extras_max_command_x"][t])) < 1e-6, ctx
+            if fx["step_force_applied"][t]:
+                assert_close("applied_force", s["applied_force"], fx["step_applied_force"][t][:, 0, :], ctx=ctx)
+    if len(outs) == len(fx["step_rew"]):
+        assert_close("obs_full_last", outs[-1]["full_obs"], fx["obs_full_last"])

@@ -1,0 +1,75 @@
+"""C-ABI checks that need no GPU: the library loads, exports every function include/t1env.h declares, and
+the ctypes mirrors have the same struct layout as the C header (compiled with gcc here)."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "t1env.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(t1env_\w+)\s*\(", src, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ti5_isaacgym_amd import _lib
+    from ti5_isaacgym_amd import build as b
+    b.build()
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), n
+    from ti5_isaacgym_amd import _lib
+    assert sorted(_lib.EXPORTS) == names
+
+
+def test_version_and_errors(lib):
+    assert b"gfx950" in lib.t1env_version()
+    from ti5_isaacgym_amd import _lib
+    rc = lib.t1env_create(None, None, None, None)
+    assert rc == -1 and b"null" in lib.t1env_last_error()
+
+
+def test_struct_layout_matches_header():
+    from ti5_isaacgym_amd import _lib
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "t1env.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\n", sizeof(t1env_model), sizeof(t1env_config), sizeof(t1env_buffers),
+         sizeof(t1env_step_args), sizeof(t1env_injected));
+  printf("%zu %zu %zu\n", offsetof(t1env_config, reset_xy_range), offsetof(t1env_buffers, ep_accum),
+         offsetof(t1env_model, base_init_state));
+  return 0;
+}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "sz.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "sz")
+        subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    sizes = list(map(int, out))
+    assert sizes[:5] == [ctypes.sizeof(_lib.Model), ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Buffers),
+                         ctypes.sizeof(_lib.StepArgs), ctypes.sizeof(_lib.Injected)]
+    assert sizes[5] == _lib.Config.reset_xy_range.offset
+    assert sizes[6] == _lib.Buffers.ep_accum.offset
+    assert sizes[7] == _lib.Model.base_init_state.offset
+
+
+def test_env_refuses_cpu_device():
+    import ti5_isaacgym_amd as t
+    with pytest.raises(RuntimeError):
+        t.make_t1_env(num_envs=4, mesh_type="plane", device="cpu")

@@ -1,0 +1,30 @@
+"""Build libt1env_hip.so for gfx950 in-tree (the .so travels to the GPU box with the repo snapshot).
+
+    python -m ti5_isaacgym_amd.build [--debug]
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "t1env.hip")
+OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("t1env.hip", "t1_dynamics.h", "t1_common.h", "t1env_post.h")] + \
+    [os.path.join(os.path.dirname(HERE), "include", "t1env.h")]
+ARCH = os.environ.get("T1ENV_ARCH", "gfx950")
+
+
+def build(force=False, extra=()):
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS):
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+           "-o", OUT + ".tmp", SRC, *extra]
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force=True, extra=[a for a in sys.argv[1:] if a.startswith("-")]))

@@ -1,0 +1,1072 @@
+// t1env.hip -- MI355X (gfx950) kernels + C ABI for the T1 humanoid LeggedRobot.step() hot path.
+//
+// Per env step (t1env_step), four launches on the caller's stream, no host sync:
+//   k_physics  : actions -> 10 x (PD torque with actuator lag + DR, dynamics substep, sensor-lag capture);
+//                writes root/dof/rigid/contact/torques.  One env per lane, state in registers.
+//   k_post_a   : base kinematics, command/ext-force callback, termination, 24 rewards (alphabetical),
+//                episode sums, per-step extras reduction (legged_robot.py:458-489, 509-517, 654-680)
+//   k_post_b   : masked reset_idx, compute_observations -> newest obs/priv frame, last_* bookkeeping
+//                (legged_robot.py:490-502, t1_dh_stand_env.py:368-559)
+//   k_stack    : 66-frame / 3-frame history shift into the ping-pong output buffers, thread per 4 floats,
+//                fully coalesced (the HBM-dominant part: ~24 KB per env per step)
+// See include/t1env.h for the ABI and DESIGN.md for layouts and rooflines.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdlib.h>
+
+#include "../../include/t1env.h"
+#include "t1_dynamics.h"
+
+using namespace t1;
+
+namespace {
+
+thread_local char g_err[512] = "";
+int fail(int code, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      snprintf(g_err, sizeof(g_err), "%s: %s", #expr, hipGetErrorString(e_));           \
+      return (int)e_;                                                                    \
+    }                                                                                    \
+  } while (0)
+
+constexpr int BLOCK = 64;  // one wave per workgroup: 8192 envs -> 128 workgroups spread over the CUs
+
+}  // namespace
+
+struct t1env {
+  t1env_config cfg;
+  t1env_buffers buf;
+  DynModel* d_model;
+  t1env_config* d_cfg;
+  Terrain terrain;
+  uint8_t* d_hist_clear;  // (N,) history rows to zero in the next stack pass (reset_idx)
+};
+
+// =====================================================================================================
+// physics: decimation loop (legged_robot.py:399-434)
+// =====================================================================================================
+struct DevWriter {
+  float* rootp;
+  float* rigidp;
+  float* contactp;
+  __device__ void root(const float* v) {
+#pragma unroll
+    for (int i = 0; i < 13; ++i) rootp[i] = v[i];
+  }
+  __device__ void rigid(int b, const float* v) {
+#pragma unroll
+    for (int i = 0; i < 13; ++i) rigidp[b * 13 + i] = v[i];
+  }
+  __device__ void contact(int b, V3<float> f) {
+    contactp[b * 3 + 0] = f.x;
+    contactp[b * 3 + 1] = f.y;
+    contactp[b * 3 + 2] = f.z;
+  }
+};
+
+__device__ __forceinline__ void load_params(const DynModel& M, const t1env_buffers& B, int n, EnvParams<float>& P,
+                                            float ground_friction) {
+  P.mass[0] = B.body_mass[n];
+  P.inertia_scale[0] = P.mass[0] / M.mass[0];
+#pragma unroll
+  for (int b = 1; b < NB; ++b) {
+    const float s = B.link_mass_scale[n * 12 + (b - 1)];
+    P.mass[b] = M.mass[b] * s;
+    P.inertia_scale[b] = s;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) P.com_disp[i] = B.com_disp[n * 3 + i];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) P.armature[j] = B.armature[n * 12 + j];
+  // PhysX combines shape and ground friction by averaging (third-party semantics, unpinned)
+  P.friction = 0.5f * (B.friction[n] + ground_friction);
+}
+
+// root state (COM velocity) -> internal state (base-origin velocity)
+__device__ __forceinline__ void load_state(const DynModel& M, const EnvParams<float>& P, const float* root,
+                                           const float* dof, EnvState<float>& s) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) s.pos[i] = root[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s.quat[i] = root[3 + i];
+  M3<float> R0 = quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]);
+  V3<float> c0 = mul(R0, v3<float>(M.com[0][0] + P.com_disp[0], M.com[0][1] + P.com_disp[1], M.com[0][2] + P.com_disp[2]));
+  V3<float> w = v3<float>(root[10], root[11], root[12]);
+  V3<float> vo = v3<float>(root[7], root[8], root[9]) - cross(w, c0);
+  s.w[0] = w.x; s.w[1] = w.y; s.w[2] = w.z;
+  s.vo[0] = vo.x; s.vo[1] = vo.y; s.vo[2] = vo.z;
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { s.q[j] = dof[2 * j]; s.qd[j] = dof[2 * j + 1]; }
+}
+
+#pragma clang fp contract(off)
+#include "t1env_post.h"
+
+// PD torque of one substep (legged_robot.py:1019-1074): lagged action, randomized gains, viscous +
+// Coulomb friction, torque multiplier redrawn every substep, clip to 0.85 * effort.
+__device__ __forceinline__ void pd_torques(const DynModel& M, const t1env_config& C, const t1env_buffers& B, int n,
+                                           uint32_t genv, uint32_t ctr, int sub, int lag, const float q[12],
+                                           const float qd[12], float tau[12]) {
+  const int d = lag > sub ? (lag - sub + 9) / 10 : 0;
+  const float* la = B.act_hist + ((size_t)n * 4 + ((ctr - (uint32_t)d) & 3u)) * 12;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const float kp = B.kp[n * 12 + j], kd = B.kd[n * 12 + j];
+    float t = kp * (((la[j] + M.default_dof_pos[j]) - q[j]) + B.motor_offsets[n * 12 + j]);
+    t = t - kd * qd[j];
+    t = t - B.viscous[n * 12 + j] * qd[j];
+    t = t - B.coulomb[n * 12 + j] * signf(qd[j]);
+    const float tm = rand_float(C.torque_mult_range[0], C.torque_mult_range[1], C.seed, genv, ctr,
+                                SLOT_TORQUE_MULT + sub * 12 + j);
+    t = t * tm;
+    const float lim = M.torque_limit[j];
+    tau[j] = fminf(fmaxf(t, -lim), lim);
+  }
+}
+
+__device__ __forceinline__ void capture_imu(const float quat[4], const float w_world[3], float* dst) {
+  float av[3], e[3];
+  quat_rotate_inverse(quat, w_world, av);
+  euler_xyz(quat, e);
+  dst[0] = av[0]; dst[1] = av[1]; dst[2] = av[2];
+  dst[3] = e[0]; dst[4] = e[1]; dst[5] = e[2];
+}
+
+template <bool INJECTED>
+__global__ __launch_bounds__(BLOCK) void k_physics(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
+                                                   t1env_buffers B, Terrain T, const float* __restrict__ actions,
+                                                   t1env_step_args A, t1env_injected inj) {
+  const int n = blockIdx.x * BLOCK + threadIdx.x;
+  const t1env_config& C = *Cp;
+  if (n >= C.num_envs) return;
+  const DynModel& M = *Mp;
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  const uint32_t ctr = A.counter;
+  // actions = clip(actions); push the scaled action into this step's history slot
+  float* slot = B.act_hist + ((size_t)n * 4 + (ctr & 3u)) * 12;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    float a = fminf(fmaxf(actions[n * 12 + j], -C.clip_actions), C.clip_actions);
+    B.actions[n * 12 + j] = a;
+    slot[j] = a * C.action_scale;
+  }
+  const int lag = B.lag_timestep[n];
+  const int dlag = B.dof_lag_timestep[n], ilag = B.imu_lag_timestep[n];
+  const int s_dof = 9 - dlag % 10, s_imu = 9 - ilag % 10;
+  float* dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
+  float* imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 6;
+  const float dt = C.sim_dt;
+  float tau[12];
+  if constexpr (!INJECTED) {
+    EnvParams<float> P;
+    load_params(M, B, n, P, M.ground_friction);
+    EnvState<float> s;
+    load_state(M, P, B.root_states + (size_t)n * 13, B.dof_state + (size_t)n * 24, s);
+    V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
+    for (int sub = 0; sub < C.decimation; ++sub) {
+      pd_torques(M, C, B, n, genv, ctr, sub, lag, s.q, s.qd, tau);
+      substep(M, T, P, s, tau, sub == 0 ? ef : v3<float>(0, 0, 0), dt);
+      if (sub == s_dof) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) { dof_dst[j] = s.q[j]; dof_dst[12 + j] = s.qd[j]; }
+      }
+      if (sub == s_imu) capture_imu(s.quat, s.w, imu_dst);
+    }
+    DevWriter W{B.root_states + (size_t)n * 13, B.rigid_state + (size_t)n * 169, B.contact_forces + (size_t)n * 39};
+    report(M, T, P, s, dt, W);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      B.dof_state[n * 24 + 2 * j] = s.q[j];
+      B.dof_state[n * 24 + 2 * j + 1] = s.qd[j];
+    }
+  } else {
+    const int N = C.num_envs;
+    for (int sub = 0; sub < C.decimation; ++sub) {
+      float q[12], qd[12];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) { q[j] = B.dof_state[n * 24 + 2 * j]; qd[j] = B.dof_state[n * 24 + 2 * j + 1]; }
+      pd_torques(M, C, B, n, genv, ctr, sub, lag, q, qd, tau);
+      if (inj.torque_log) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) inj.torque_log[((size_t)sub * N + n) * 12 + j] = tau[j];
+      }
+      const float* r = inj.root + ((size_t)sub * N + n) * 13;
+      const float* d = inj.dof + ((size_t)sub * N + n) * 24;
+#pragma unroll
+      for (int i = 0; i < 13; ++i) B.root_states[n * 13 + i] = r[i];
+#pragma unroll
+      for (int i = 0; i < 24; ++i) B.dof_state[n * 24 + i] = d[i];
+      if (sub == s_dof) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) { dof_dst[j] = d[2 * j]; dof_dst[12 + j] = d[2 * j + 1]; }
+      }
+      if (sub == s_imu) {
+        float quat[4] = {r[3], r[4], r[5], r[6]}, w[3] = {r[10], r[11], r[12]};
+        capture_imu(quat, w, imu_dst);
+      }
+    }
+    for (int i = 0; i < 169; ++i) B.rigid_state[(size_t)n * 169 + i] = inj.rigid[(size_t)n * 169 + i];
+    for (int i = 0; i < 39; ++i) B.contact_forces[(size_t)n * 39 + i] = inj.contact[(size_t)n * 39 + i];
+  }
+#pragma unroll
+  for (int j = 0; j < 12; ++j) B.torques[n * 12 + j] = tau[j];
+}
+
+// =====================================================================================================
+// post-physics helpers
+// =====================================================================================================
+struct Phase {
+  float sin_pos;
+  float stance[2];
+};
+
+// _get_phase + _get_gait_phase (t1_dh_stand_env.py:80-107); mutates phase_length_buf for standing envs.
+__device__ __forceinline__ float get_phase(const t1env_config& C, const t1env_buffers& B, int n, bool stand) {
+  if (stand) B.phase_length_buf[n] = 0;
+  const float dtf = (float)(C.sim_dt * C.decimation);
+  float ph = ((float)B.phase_length_buf[n] * dtf) / C.cycle_time;
+  ph = ph - floorf(ph);
+  ph = (ph + B.gait_start[n]) * (stand ? 0.0f : 1.0f);
+  return ph;
+}
+__device__ __forceinline__ Phase gait_phase(float phase) {
+  Phase p;
+  p.sin_pos = sinf(TWO_PI_F * phase);
+  p.stance[0] = p.sin_pos >= 0.0f ? 1.0f : 0.0f;
+  p.stance[1] = p.sin_pos < 0.0f ? 1.0f : 0.0f;
+  if (fabsf(p.sin_pos) < 0.1f) { p.stance[0] = 1.0f; p.stance[1] = 1.0f; }
+  return p;
+}
+__device__ __forceinline__ bool is_stand(const t1env_config& C, const float* cmd) {
+  return norm3(cmd[0], cmd[1], cmd[2]) <= C.stand_com_threshold;
+}
+
+// _resample_commands() (t1_dh_stand_env.py:126-177): every gait slot whose start equals the episode step
+__device__ __forceinline__ void resample_commands(const t1env_config& C, const t1env_buffers& B, const t1env_step_args& A,
+                                                  int n, uint32_t genv, uint32_t ctr) {
+  const int64_t el = B.episode_length_buf[n];
+  float* cmd = B.commands + n * 4;
+  for (int i = 0; i < 3; ++i) {
+    if (el != (int64_t)B.gait_time[n * 3 + i]) continue;
+    const int kind = C.gait_kind[i];
+    const float x = rand_float(A.cmd_ranges[0][0], A.cmd_ranges[0][1], C.seed, genv, ctr, SLOT_CMD_X);
+    const float y = rand_float(A.cmd_ranges[1][0], A.cmd_ranges[1][1], C.seed, genv, ctr, SLOT_CMD_Y);
+    const float z = rand_float(A.cmd_ranges[2][0], A.cmd_ranges[2][1], C.seed, genv, ctr, SLOT_CMD_YAW);
+    if (kind == 0) { cmd[0] = x; cmd[1] = y; cmd[2] = z; }              // walk_omnidirectional
+    else if (kind == 1) { cmd[0] = 0.0f; cmd[1] = 0.0f; cmd[2] = 0.0f; }  // stand
+    else if (kind == 2) { cmd[0] = x; cmd[1] = 0.0f; cmd[2] = 0.0f; }     // walk_sagittal
+    else if (kind == 3) { cmd[0] = 0.0f; cmd[1] = y; cmd[2] = 0.0f; }     // walk_lateral
+    else { cmd[0] = 0.0f; cmd[1] = 0.0f; cmd[2] = z; }                    // rotate
+  }
+}
+
+__device__ __forceinline__ void base_quantities(const t1env_buffers& B, int n) {
+  const float* r = B.root_states + n * 13;
+  float q[4] = {r[3], r[4], r[5], r[6]};
+  float v[3] = {r[7], r[8], r[9]}, w[3] = {r[10], r[11], r[12]}, g[3] = {0.0f, 0.0f, -1.0f}, o[3];
+  quat_rotate_inverse(q, v, o);
+  B.base_lin_vel[n * 3 + 0] = o[0]; B.base_lin_vel[n * 3 + 1] = o[1]; B.base_lin_vel[n * 3 + 2] = o[2];
+  quat_rotate_inverse(q, w, o);
+  B.base_ang_vel[n * 3 + 0] = o[0]; B.base_ang_vel[n * 3 + 1] = o[1]; B.base_ang_vel[n * 3 + 2] = o[2];
+  quat_rotate_inverse(q, g, o);
+  B.projected_gravity[n * 3 + 0] = o[0]; B.projected_gravity[n * 3 + 1] = o[1]; B.projected_gravity[n * 3 + 2] = o[2];
+  float e[3];
+  euler_xyz(q, e);
+  B.base_euler_xyz[n * 3 + 0] = e[0]; B.base_euler_xyz[n * 3 + 1] = e[1]; B.base_euler_xyz[n * 3 + 2] = e[2];
+}
+
+__device__ __forceinline__ void feet_euler(const t1env_buffers& B, int n) {
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const float* rb = B.rigid_state + (size_t)n * 169 + (f == 0 ? 6 : 12) * 13;
+    float q[4] = {rb[3], rb[4], rb[5], rb[6]}, e[3];
+    euler_xyz(q, e);
+    B.feet_euler_xyz[n * 6 + f * 3 + 0] = e[0];
+    B.feet_euler_xyz[n * 6 + f * 3 + 1] = e[1];
+    B.feet_euler_xyz[n * 6 + f * 3 + 2] = e[2];
+  }
+}
+
+// wave-level sum then one atomic per wave (extras reduction over reset envs)
+__device__ __forceinline__ void wave_atomic_add(float* dst, float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if ((threadIdx.x & 63) == 0 && v != 0.0f) atomicAdd(dst, v);
+}
+
+// =====================================================================================================
+// post-physics phase A: callback, termination, rewards (legged_robot.py:469-489)
+// =====================================================================================================
+__global__ __launch_bounds__(BLOCK) void k_post_a(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
+                                                  t1env_buffers B, t1env_step_args A) {
+  const int n0 = blockIdx.x * BLOCK + threadIdx.x;
+  const t1env_config& C = *Cp;
+  const DynModel& M = *Mp;
+  const bool live = n0 < C.num_envs;
+  const int n = live ? n0 : C.num_envs - 1;
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  const uint32_t ctr = A.counter + 1u;  // common_step_counter += 1 happened before the callback
+  float contrib[T1_NREW];
+  bool do_reset = false;
+  if (live) {
+    B.episode_length_buf[n] += 1;
+    base_quantities(B, n);
+    feet_euler(B, n);
+    // ---- _post_physics_step_callback (t1_dh_stand_env.py:179-215)
+    B.phase_length_buf[n] += 1;
+    resample_commands(C, B, A, n, genv, ctr);
+    float* cmd = B.commands + n * 4;
+    if (A.push_call) {  // _push_robots (t1:217-231): drawn every call (is_first_push reset is commented out)
+      float* r = B.root_states + n * 13;
+      r[7] = rand_float(-C.push_vel_xy, C.push_vel_xy, C.seed, genv, ctr, SLOT_PUSH_VEL + 0);
+      r[8] = rand_float(-C.push_vel_xy, C.push_vel_xy, C.seed, genv, ctr, SLOT_PUSH_VEL + 1);
+      r[10] = rand_float(-C.push_ang, C.push_ang, C.seed, genv, ctr, SLOT_PUSH_ANG + 0);
+      r[11] = rand_float(-C.push_ang, C.push_ang, C.seed, genv, ctr, SLOT_PUSH_ANG + 1);
+      r[12] = rand_float(-C.push_ang, C.push_ang, C.seed, genv, ctr, SLOT_PUSH_ANG + 2);
+    }
+    float* ef = B.ext_forces + n * 3;
+    float* et = B.ext_torques + n * 3;
+    float* af = B.applied_force + n * 3;
+    af[0] = 0.0f; af[1] = 0.0f; af[2] = 0.0f;
+    if (A.ext_force_call) {  // _add_ext_force (t1:233-247)
+      if (A.ext_force_first) {
+        ef[0] = rand_float(-C.ext_force_max[0] / 2, C.ext_force_max[0], C.seed, genv, ctr, SLOT_EXT_FORCE + 0);
+        ef[1] = rand_float(-C.ext_force_max[1], C.ext_force_max[1], C.seed, genv, ctr, SLOT_EXT_FORCE + 1);
+        ef[2] = rand_float(-C.ext_force_max[2], C.ext_force_max[2], C.seed, genv, ctr, SLOT_EXT_FORCE + 2);
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          et[k] = rand_float(-C.ext_torque_max, C.ext_torque_max, C.seed, genv, ctr, SLOT_EXT_TORQUE + k);
+      } else {
+        const float st = is_stand(C, cmd) ? 1.0f : 0.0f;
+        af[0] = ef[0] * st; af[1] = ef[1] * st; af[2] = ef[2] * st;
+      }
+    } else {
+      ef[0] = ef[1] = ef[2] = 0.0f;
+      et[0] = et[1] = et[2] = 0.0f;
+    }
+    // ---- check_termination (legged_robot.py:509-517)
+    const float* cf = B.contact_forces + (size_t)n * 39;
+    const bool term = norm3(cf[0], cf[1], cf[2]) > 1.0f;
+    const bool tout = (float)B.episode_length_buf[n] > C.max_episode_length;
+    do_reset = term || tout;
+    B.reset_buf[n] = do_reset ? 1 : 0;
+    B.time_out_buf[n] = tout ? 1 : 0;
+    // ---- rewards (t1:576-935), alphabetical order
+    const float* dof = B.dof_state + (size_t)n * 24;
+    const float* root = B.root_states + n * 13;
+    const float* rig = B.rigid_state + (size_t)n * 169;
+    const float* a = B.actions + n * 12;
+    const float* la = B.last_actions + n * 12;
+    const float* lla = B.last_last_actions + n * 12;
+    const float* blv = B.base_lin_vel + n * 3;
+    const float* bav = B.base_ang_vel + n * 3;
+    const float* pg = B.projected_gravity + n * 3;
+    const float* be = B.base_euler_xyz + n * 3;
+    const float* fe = B.feet_euler_xyz + n * 6;
+    const bool stand = is_stand(C, cmd);
+    const Phase ph = gait_phase(get_phase(C, B, n, stand));
+    const float dtf = (float)(C.sim_dt * C.decimation);
+    const float* f0 = rig + 6 * 13;
+    const float* f1 = rig + 12 * 13;
+    const bool contact0 = cf[6 * 3 + 2] > 5.0f, contact1 = cf[12 * 3 + 2] > 5.0f;
+    float r[T1_NREW];
+    {  // 0 action_smoothness
+      float t1s = 0.0f, t2s = 0.0f, t3s = 0.0f;
+      for (int j = 0; j < 12; ++j) {
+        const float d1 = (la[j] - a[j]) * 1.0f;
+        const float d2 = ((a[j] + lla[j]) - 2.0f * la[j]) * 1.0f;
+        t1s += d1 * d1;
+        t2s += d2 * d2;
+        t3s += fabsf(a[j] * 1.0f);
+      }
+      r[0] = (t1s + t2s) + 0.05f * t3s;
+    }
+    {  // 1 base_acc
+      const float* lrv = B.last_root_vel + n * 6;
+      float s = 0.0f;
+      for (int i = 0; i < 6; ++i) { const float d = lrv[i] - root[7 + i]; s += d * d; }
+      r[1] = expf(-sqrtf(s) * 3.0f);
+    }
+    {  // 2 base_height
+      const float mh = (f0[2] * ph.stance[0] + f1[2] * ph.stance[1]) / (ph.stance[0] + ph.stance[1]);
+      const float bh = root[2] - (mh - 0.05f);
+      r[2] = expf(-fabsf(bh - C.base_height_target) * 100.0f);
+    }
+    r[3] = norm3(cf[0], cf[1], cf[2]) > 0.1f ? 1.0f : 0.0f;  // 3 collision (penalised_contact_indices = base)
+    {  // 4 default_joint_pos
+      float jd[12], s = 0.0f;
+      for (int j = 0; j < 12; ++j) { jd[j] = dof[2 * j] - M.default_dof_pos[j]; s += jd[j] * jd[j]; }
+      float yr = norm3(jd[0], jd[1], jd[5]) + norm3(jd[6], jd[7], jd[11]);
+      yr = clampf(yr - 0.1f, 0.0f, 50.0f);
+      r[4] = expf(-yr * 100.0f) - 0.01f * sqrtf(s);
+    }
+    {  // 5 dof_acc, 6 dof_vel
+      const float* ldv = B.last_dof_vel + n * 12;
+      float s5 = 0.0f, s6 = 0.0f;
+      for (int j = 0; j < 12; ++j) {
+        const float d = (ldv[j] - dof[2 * j + 1]) / dtf;
+        s5 += d * d;
+        s6 += dof[2 * j + 1] * dof[2 * j + 1];
+      }
+      r[5] = s5;
+      r[6] = s6;
+    }
+    {  // 7 feet_air_time (mutates feet_air_time, last_contacts)
+      float sm0 = ph.stance[0], sm1 = ph.stance[1];
+      if (norm3(cmd[0], cmd[1], cmd[2]) < 0.05f) { sm0 = 1.0f; sm1 = 1.0f; }
+      uint8_t* lc = B.last_contacts + n * 2;
+      float* at = B.feet_air_time + n * 2;
+      const bool filt0 = contact0 || sm0 > 0.0f || lc[0];
+      const bool filt1 = contact1 || sm1 > 0.0f || lc[1];
+      lc[0] = contact0; lc[1] = contact1;
+      const bool first0 = at[0] > 0.0f && filt0, first1 = at[1] > 0.0f && filt1;
+      const float a0 = at[0] + dtf, a1 = at[1] + dtf;
+      const float air0 = clampf(a0, 0.0f, 0.5f) * (first0 ? 1.0f : 0.0f);
+      const float air1 = clampf(a1, 0.0f, 0.5f) * (first1 ? 1.0f : 0.0f);
+      at[0] = a0 * (filt0 ? 0.0f : 1.0f);
+      at[1] = a1 * (filt1 ? 0.0f : 1.0f);
+      r[7] = air0 + air1;
+    }
+    {  // 8 feet_clearance (mutates feet_height, last_feet_z)
+      float* fh = B.feet_height + n * 2;
+      float* lfz = B.last_feet_z + n * 2;
+      const float z0 = f0[2], z1 = f1[2];
+      const float h0 = fh[0] + (z0 - lfz[0]), h1 = fh[1] + (z1 - lfz[1]);
+      lfz[0] = z0; lfz[1] = z1;
+      const float sw0 = 1.0f - ph.stance[0], sw1 = 1.0f - ph.stance[1];
+      const float rp0 = (h0 > C.target_feet_height && h0 < C.target_feet_height_max) ? 1.0f : 0.0f;
+      const float rp1 = (h1 > C.target_feet_height && h1 < C.target_feet_height_max) ? 1.0f : 0.0f;
+      r[8] = rp0 * sw0 + rp1 * sw1;
+      fh[0] = h0 * (contact0 ? 0.0f : 1.0f);
+      fh[1] = h1 * (contact1 ? 0.0f : 1.0f);
+    }
+    {  // 9 feet_contact_forces
+      const float* c0 = cf + 6 * 3;
+      const float* c1 = cf + 12 * 3;
+      r[9] = clampf(norm3(c0[0], c0[1], c0[2]) - C.max_contact_force, 0.0f, 400.0f) +
+             clampf(norm3(c1[0], c1[1], c1[2]) - C.max_contact_force, 0.0f, 400.0f);
+    }
+    {  // 10 feet_contact_number
+      float sm0 = ph.stance[0], sm1 = ph.stance[1];
+      if (stand) { sm0 = 1.0f; sm1 = 1.0f; }
+      const float q0 = ((contact0 ? 1.0f : 0.0f) == sm0) ? 1.0f : -0.3f;
+      const float q1 = ((contact1 ? 1.0f : 0.0f) == sm1) ? 1.0f : -0.3f;
+      r[10] = (q0 + q1) / 2.0f;
+    }
+    {  // 11 feet_distance, 15 knee_distance
+      const float* k0 = rig + 4 * 13;
+      const float* k1 = rig + 10 * 13;
+      const float fd = norm2(f0[0] - f1[0], f0[1] - f1[1]);
+      const float kd = norm2(k0[0] - k1[0], k0[1] - k1[1]);
+      const float fmn = clampf(fd - C.foot_min_dist, -0.5f, 0.0f), fmx = clampf(fd - C.foot_max_dist, 0.0f, 0.5f);
+      const float kmn = clampf(kd - C.knee_min_dist, -0.5f, 0.0f), kmx = clampf(kd - C.knee_max_dist, 0.0f, 0.5f);
+      r[11] = (expf(-fabsf(fmn) * 100.0f) + expf(-fabsf(fmx) * 100.0f)) / 2.0f;
+      r[15] = (expf(-fabsf(kmn) * 100.0f) + expf(-fabsf(kmx) * 100.0f)) / 2.0f;
+    }
+    {  // 12 feet_rotation
+      const float rot = fe[1] * fe[1] + fe[4] * fe[4];
+      const float x = rot / 1.0f;
+      r[12] = 1.0f * expf(-(x * x));
+    }
+    {  // 13 foot_slip
+      const float s0 = sqrtf(norm2(f0[10], f0[11])), s1 = sqrtf(norm2(f1[10], f1[11]));
+      r[13] = s0 * (contact0 ? 1.0f : 0.0f) + s1 * (contact1 ? 1.0f : 0.0f);
+    }
+    {  // 14 joint_pos (uses ref_dof_pos from the previous compute_observations)
+      const float* ref = B.ref_dof_pos + n * 12;
+      float s = 0.0f;
+      for (int j = 0; j < 12; ++j) {
+        const float tgt = stand ? M.default_dof_pos[j] : ref[j];
+        const float d = dof[2 * j] - tgt;
+        s += d * d;
+      }
+      const float nr = sqrtf(s);
+      r[14] = stand ? 1.0f : expf(-2.0f * nr) - 0.2f * clampf(nr, 0.0f, 0.5f);
+    }
+    {  // 16 low_speed
+      const float sp = fabsf(blv[0]), cm = fabsf(cmd[0]);
+      const bool low = sp < 0.5f * cm, high = sp > 1.2f * cm, ok = !(low || high);
+      const bool mis = signf(blv[0]) != signf(cmd[0]);
+      float v = 0.0f;
+      if (low) v = -1.0f;
+      if (high) v = 0.0f;
+      if (ok) v = 1.2f;
+      if (mis) v = -2.0f;
+      r[16] = v * (fabsf(cmd[0]) > 0.05f ? 1.0f : 0.0f);
+    }
+    {  // 17 orientation
+      const float qm = expf(-(fabsf(be[0]) + fabsf(be[1])) * 10.0f);
+      const float o = expf(-norm2(pg[0], pg[1]) * 20.0f);
+      r[17] = (qm + o) / 2.0f;
+    }
+    {  // 18 stand_still
+      const int idx[8] = {0, 1, 2, 3, 5, 6, 7, 8};
+      const float w[10] = {2.0f, 2.0f, 1.0f, 1.0f, 1.0f, 2.0f, 2.0f, 1.0f, 1.0f, 1.0f};
+      float s = 0.0f;
+      for (int k = 0; k < 8; ++k) {
+        const float e = (dof[2 * idx[k]] - M.default_dof_pos[idx[k]]) * w[k];
+        s += e * e;
+      }
+      const float e8 = fe[1] * w[8], e9 = fe[4] * w[9];
+      s += e8 * e8;
+      s += e9 * e9;
+      r[18] = stand ? expf(-s) : 0.0f;
+    }
+    {  // 19 torques
+      const float* tq = B.torques + n * 12;
+      float s = 0.0f;
+      for (int j = 0; j < 12; ++j) s += tq[j] * tq[j];
+      r[19] = s;
+    }
+    {  // 20 track_vel_hard
+      const float le = norm2(cmd[0] - blv[0], cmd[1] - blv[1]);
+      const float ae = fabsf(cmd[2] - bav[2]);
+      r[20] = (expf(-le * 10.0f) + expf(-ae * 10.0f)) / 2.0f - 0.2f * (le + ae);
+    }
+    {  // 21 tracking_ang_vel
+      const float d = cmd[2] - bav[2];
+      r[21] = stand ? expf(-fabsf(d) * (C.tracking_sigma * 2.0f)) : expf(-(d * d) * C.tracking_sigma);
+    }
+    {  // 22 tracking_lin_vel
+      const float dx = cmd[0] - blv[0], dy = cmd[1] - blv[1];
+      r[22] = stand ? expf(-(fabsf(dx) + fabsf(dy)) * (C.tracking_sigma * 2.0f))
+                    : expf(-(dx * dx + dy * dy) * C.tracking_sigma);
+    }
+    {  // 23 vel_mismatch_exp
+      const float lm = expf(-(blv[2] * blv[2]) * 10.0f);
+      const float am = expf(-norm2(bav[0], bav[1]) * 5.0f);
+      r[23] = (lm + am) / 2.0f;
+    }
+    float rew = 0.0f;
+    for (int k = 0; k < T1_NREW; ++k) {
+      const float v = r[k] * C.reward_scales[k];
+      rew = rew + v;
+      const float s = B.episode_sums[(size_t)k * C.num_envs + n] + v;
+      B.episode_sums[(size_t)k * C.num_envs + n] = s;
+      contrib[k] = do_reset ? s : 0.0f;
+    }
+    if (C.only_positive_rewards) rew = fmaxf(rew, 0.0f);
+    B.rew_buf[n] = rew;
+  } else {
+    for (int k = 0; k < T1_NREW; ++k) contrib[k] = 0.0f;
+  }
+  // extras["episode"] means over reset envs: partial sums (finalised after post_b)
+  for (int k = 0; k < T1_NREW; ++k) wave_atomic_add(B.ep_accum + k, contrib[k]);
+  wave_atomic_add(B.ep_accum + 24, (live && do_reset) ? 1.0f : 0.0f);
+}
+
+// =====================================================================================================
+// reset_idx for one env (t1_dh_stand_env.py:483-559 + legged_robot.py:604-651, 732-783, 1076-1120, 1138-1158)
+// =====================================================================================================
+__device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B, const t1env_step_args& A,
+                          int n, uint32_t genv, uint32_t ctr, bool do_terrain) {
+  const uint32_t seed = C.seed;
+  if (do_terrain && C.terrain_curriculum) {  // _update_terrain_curriculum
+    const float* r = B.root_states + n * 13;
+    const float* o = B.env_origins + n * 3;
+    const float dist = norm2(r[0] - o[0], r[1] - o[1]);
+    const bool up = dist > C.env_length / 2.0f;
+    const float* cmd = B.commands + n * 4;
+    const bool down = (dist < norm2(cmd[0], cmd[1]) * (C.episode_length_s * 0.5f)) && !up;
+    int lv = B.terrain_levels[n] + (up ? 1 : 0) - (down ? 1 : 0);
+    const int rnd = rand_int(0, C.num_terrain_rows, seed, genv, ctr, SLOT_TERRAIN_LEVEL_RAND);
+    lv = lv >= C.num_terrain_rows ? rnd : (lv < 0 ? 0 : lv);
+    B.terrain_levels[n] = lv;
+    const float* to = B.terrain_origins + ((size_t)lv * C.num_terrain_cols + B.terrain_types[n]) * 3;
+    B.env_origins[n * 3 + 0] = to[0];
+    B.env_origins[n * 3 + 1] = to[1];
+    B.env_origins[n * 3 + 2] = to[2];
+  }
+  // _reset_dofs
+  for (int j = 0; j < 12; ++j) {
+    B.dof_state[n * 24 + 2 * j] =
+        M.default_dof_pos[j] + rand_float(-C.reset_dof_range, C.reset_dof_range, seed, genv, ctr, SLOT_RESET_DOF + j);
+    B.dof_state[n * 24 + 2 * j + 1] = 0.0f;
+  }
+  // _reset_root_states
+  float* r = B.root_states + n * 13;
+  for (int i = 0; i < 13; ++i) r[i] = M.base_init_state[i];
+  for (int i = 0; i < 3; ++i) r[i] += B.env_origins[n * 3 + i];
+  if (C.custom_origins) {
+    const float p3 = C.reset_xy_range;
+    r[0] += rand_float(-p3, p3, seed, genv, ctr, SLOT_RESET_ROOT_XY + 0);
+    r[1] += rand_float(-p3, p3, seed, genv, ctr, SLOT_RESET_ROOT_XY + 1);
+  }
+  // randomize_dof_props (torque_multi is redrawn every substep anyway; its reset draw has no effect)
+  for (int j = 0; j < 12; ++j) {
+    B.motor_offsets[n * 12 + j] =
+        rand_float(C.motor_offset_range[0], C.motor_offset_range[1], seed, genv, ctr, SLOT_DR_OFFSET + j);
+    B.kp[n * 12 + j] = rand_float(C.kp_mult_range[0], C.kp_mult_range[1], seed, genv, ctr, SLOT_DR_KP + j) * M.p_gains[j];
+    B.kd[n * 12 + j] = rand_float(C.kd_mult_range[0], C.kd_mult_range[1], seed, genv, ctr, SLOT_DR_KD + j) * M.d_gains[j];
+    B.coulomb[n * 12 + j] = rand_float(C.coulomb_range[0], C.coulomb_range[1], seed, genv, ctr, SLOT_DR_COULOMB + j);
+    B.viscous[n * 12 + j] = rand_float(C.viscous_range[0], C.viscous_range[1], seed, genv, ctr, SLOT_DR_VISCOUS + j);
+    B.armature[n * 12 + j] =
+        rand_float(C.armature_range[j][0], C.armature_range[j][1], seed, genv, ctr, SLOT_DR_ARMATURE + j);
+  }
+  // randomize_lag_props: zero the lag rings, redraw lag lengths
+  for (int i = 0; i < 48; ++i) B.act_hist[(size_t)n * 48 + i] = 0.0f;
+  for (int i = 0; i < 96; ++i) B.dof_hist[(size_t)n * 96 + i] = 0.0f;
+  for (int i = 0; i < 12; ++i) B.imu_hist[(size_t)n * 12 + i] = 0.0f;
+  B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_ACTION);
+  B.dof_lag_timestep[n] = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_DOF);
+  B.imu_lag_timestep[n] = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_IMU);
+  // buffers
+  for (int j = 0; j < 12; ++j) {
+    B.last_last_actions[n * 12 + j] = 0.0f;
+    B.actions[n * 12 + j] = 0.0f;
+    B.last_actions[n * 12 + j] = 0.0f;
+    B.last_dof_vel[n * 12 + j] = 0.0f;
+  }
+  for (int i = 0; i < 6; ++i) B.last_root_vel[n * 6 + i] = 0.0f;
+  B.feet_air_time[n * 2 + 0] = 0.0f;
+  B.feet_air_time[n * 2 + 1] = 0.0f;
+  B.episode_length_buf[n] = 0;
+  B.phase_length_buf[n] = 0;
+  B.reset_buf[n] = 1;
+  B.gait_start[n] = (float)rand_int(0, 2, seed, genv, ctr, SLOT_GAIT_START) * 0.5f;
+  // generate_gait_time (t1:109-124)
+  float g[3];
+  for (int i = 0; i < 3; ++i)
+    g[i] = rand_float(C.gait_time_range[i][0], C.gait_time_range[i][1], seed, genv, ctr, SLOT_GAIT_TIME + i);
+  const float s = (g[0] + g[1]) + g[2];
+  const float f = C.max_episode_length / s;
+  const float s0 = g[0] * f, s1 = g[1] * f;
+  B.gait_time[n * 3 + 0] = 0;
+  B.gait_time[n * 3 + 1] = (int32_t)(0.0f + s0);
+  B.gait_time[n * 3 + 2] = (int32_t)((0.0f + s0) + s1);
+  // episode sums are zeroed after the extras reduction; obs/critic history rows zeroed in the stack pass
+  for (int k = 0; k < T1_NREW; ++k) B.episode_sums[(size_t)k * C.num_envs + n] = 0.0f;
+  // base quantities of the reset env from the freshly written root state (t1:548-552)
+  base_quantities(B, n);
+}
+
+// =====================================================================================================
+// post-physics phase B: reset + observations (legged_robot.py:490-502, t1:368-481)
+// =====================================================================================================
+__global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
+                                                  t1env_buffers B, t1env_step_args A, uint8_t* __restrict__ hist_clear) {
+  const int n = blockIdx.x * BLOCK + threadIdx.x;
+  const t1env_config& C = *Cp;
+  if (n >= C.num_envs) return;
+  const DynModel& M = *Mp;
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  const uint32_t ctr = A.counter + 1u;
+  const bool do_reset = B.reset_buf[n] != 0;
+  const bool any_reset = B.ep_accum[24] > 0.0f;  // reset_idx runs only if some env resets (len(env_ids) > 0)
+  if (do_reset) {
+    reset_env(M, C, B, A, n, genv, ctr, true);
+    hist_clear[n] = 1;
+  }
+  if (any_reset) resample_commands(C, B, A, n, genv, ctr);
+  // ---- compute_observations
+  const float* cmd = B.commands + n * 4;
+  const bool stand = is_stand(C, cmd);
+  const float phase = get_phase(C, B, n, stand);
+  // compute_ref_state (t1:250-274)
+  const float sp = sinf(TWO_PI_F * phase);
+  const float cp = cosf(TWO_PI_F * phase);
+  float ref[12];
+  {
+    const float sl = sp > 0.0f ? 0.0f : sp;
+    const float sr = sp < 0.0f ? 0.0f : sp;
+    const float s1 = C.target_joint_pos_scale, s2 = 2.0f * C.target_joint_pos_scale;
+    for (int j = 0; j < 12; ++j) ref[j] = 0.0f;
+    ref[2] = sl * s1; ref[3] = -sl * s2; ref[4] = sl * s1;
+    ref[8] = -sr * s1; ref[9] = sr * s2; ref[10] = -sr * s1;
+    if (fabsf(sp) < 0.1f)
+      for (int j = 0; j < 12; ++j) ref[j] = 0.0f;
+    for (int j = 0; j < 12; ++j) {
+      ref[j] = ref[j] + M.default_dof_pos[j];
+      B.ref_dof_pos[n * 12 + j] = ref[j];
+    }
+  }
+  const Phase ph = gait_phase(phase);
+  const float* cf = B.contact_forces + (size_t)n * 39;
+  const float* dof = B.dof_state + (size_t)n * 24;
+  const float* act = B.actions + n * 12;
+  float* priv = B.priv_buf[A.obs_slot] + (size_t)n * (T1_NPRIV * T1_CHIST) + T1_NPRIV * (T1_CHIST - 1);
+  float* obs = B.obs_buf[A.obs_slot] + (size_t)n * (T1_NOBS * T1_HIST) + T1_NOBS * (T1_HIST - 1);
+  const float clipo = C.clip_obs;
+  float cin[5] = {sp, cp, cmd[0] * C.lin_vel_obs_scale, cmd[1] * C.lin_vel_obs_scale, cmd[2] * C.ang_vel_obs_scale};
+  {  // privileged frame (73)
+    int k = 0;
+    float v[T1_NPRIV];
+    for (int i = 0; i < 5; ++i) v[k++] = cin[i];
+    for (int j = 0; j < 12; ++j) v[k++] = (dof[2 * j] - M.default_dof_pos[j]) * C.dof_pos_obs_scale;
+    for (int j = 0; j < 12; ++j) v[k++] = dof[2 * j + 1] * C.dof_vel_obs_scale;
+    for (int j = 0; j < 12; ++j) v[k++] = act[j];
+    for (int j = 0; j < 12; ++j) v[k++] = dof[2 * j] - ref[j];
+    for (int i = 0; i < 3; ++i) v[k++] = B.base_lin_vel[n * 3 + i] * C.lin_vel_obs_scale;
+    for (int i = 0; i < 3; ++i) v[k++] = B.base_ang_vel[n * 3 + i] * C.ang_vel_obs_scale;
+    for (int i = 0; i < 3; ++i) v[k++] = B.base_euler_xyz[n * 3 + i] * C.quat_obs_scale;
+    v[k++] = B.ext_forces[n * 3 + 0] / (C.ext_force_max[0] + 0.1f);
+    v[k++] = B.ext_forces[n * 3 + 1] / (C.ext_force_max[0] + 0.1f);
+    for (int i = 0; i < 3; ++i) v[k++] = B.ext_torques[n * 3 + i] / (C.ext_torque_max + 0.1f);
+    v[k++] = B.friction[n];
+    v[k++] = B.body_mass[n] / 30.0f;
+    v[k++] = ph.stance[0];
+    v[k++] = ph.stance[1];
+    v[k++] = cf[6 * 3 + 2] > 5.0f ? 1.0f : 0.0f;
+    v[k++] = cf[12 * 3 + 2] > 5.0f ? 1.0f : 0.0f;
+    for (int i = 0; i < T1_NPRIV; ++i) priv[i] = clampf(v[i], -clipo, clipo);
+  }
+  {  // actor frame (47) from the lagged sensor rings + noise
+    const int dl = B.dof_lag_timestep[n], il = B.imu_lag_timestep[n];
+    const float* ld = B.dof_hist + ((size_t)n * 4 + ((A.counter - (uint32_t)(dl / 10)) & 3u)) * 24;
+    const float* li = B.imu_hist + ((size_t)n * 2 + ((A.counter - (uint32_t)(il / 10)) & 1u)) * 6;
+    float v[T1_NOBS];
+    int k = 0;
+    for (int i = 0; i < 5; ++i) v[k++] = cin[i];
+    for (int j = 0; j < 12; ++j) v[k++] = (ld[j] - M.default_dof_pos[j]) * C.dof_pos_obs_scale;
+    for (int j = 0; j < 12; ++j) v[k++] = ld[12 + j] * C.dof_vel_obs_scale;
+    for (int j = 0; j < 12; ++j) v[k++] = act[j];
+    for (int i = 0; i < 3; ++i) v[k++] = li[i] * C.ang_vel_obs_scale;
+    for (int i = 0; i < 3; ++i) v[k++] = li[3 + i] * C.quat_obs_scale;
+    for (int i = 0; i < T1_NOBS; ++i) {
+      const float u = uniform01(C.seed, genv, ctr, SLOT_OBS_NOISE + i);
+      const float nz = ((2.0f * u - 1.0f) * C.noise_vec[i]) * C.noise_level;
+      obs[i] = clampf(v[i] + nz, -clipo, clipo);
+    }
+  }
+  // last_* (legged_robot.py:496-502)
+  for (int j = 0; j < 12; ++j) {
+    B.last_last_actions[n * 12 + j] = B.last_actions[n * 12 + j];
+    B.last_actions[n * 12 + j] = act[j];
+    B.last_dof_vel[n * 12 + j] = dof[2 * j + 1];
+  }
+  for (int i = 0; i < 6; ++i) B.last_root_vel[n * 6 + i] = B.root_states[n * 13 + 7 + i];
+}
+
+// =====================================================================================================
+// history stack: out[n, :F*(H-1)] = clear[n] ? 0 : in[n, F:]  -- flat shift by F floats (the newest frame
+// was written by k_post_b).  One thread per 4 output floats; the shifted source is assembled from two
+// aligned 16-B loads (lane's own + neighbour via __shfl).  Block 0 also finalises the extras.
+// =====================================================================================================
+template <int F, int H>
+__device__ __forceinline__ void stack_rows(const float* __restrict__ in, float* __restrict__ out,
+                                           const uint8_t* __restrict__ clear, int64_t total, int64_t i4) {
+  constexpr int ROW = F * H;
+  const int64_t i = i4 * 4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  // source elements i+F .. i+F+3 (same row as output element when its column < ROW - F)
+  const int64_t s = i + F;
+  const int64_t sa = s & ~(int64_t)3;
+  const int rem = (int)(s - sa);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  if (sa + 3 < total) a = *reinterpret_cast<const float4*>(in + sa);
+  else { for (int k = 0; k < 4; ++k) if (sa + k < total) (&a.x)[k] = in[sa + k]; }
+  if (rem) {
+    if (sa + 7 < total) b = *reinterpret_cast<const float4*>(in + sa + 4);
+    else { for (int k = 0; k < 4; ++k) if (sa + 4 + k < total) (&b.x)[k] = in[sa + 4 + k]; }
+  }
+  float src[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  float o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t e = i + k;
+    if (e >= total) { o[k] = 0.f; continue; }
+    const int64_t row = e / ROW;
+    const int col = (int)(e - row * ROW);
+    if (col >= ROW - F) {  // newest frame: already written
+      o[k] = out[e];
+    } else {
+      o[k] = clear[row] ? 0.0f : src[rem + k];
+    }
+  }
+  if (i + 3 < total) {
+    *reinterpret_cast<float4*>(out + i) = make_float4(o[0], o[1], o[2], o[3]);
+  } else {
+    for (int k = 0; k < 4; ++k) if (i + k < total) out[i + k] = o[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_stack(const float* __restrict__ obs_in, float* __restrict__ obs_out,
+                                               const float* __restrict__ priv_in, float* __restrict__ priv_out,
+                                               const uint8_t* __restrict__ clear, int num_envs, int64_t n4_obs,
+                                               int64_t n4_priv) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot_obs = (int64_t)num_envs * T1_NOBS * T1_HIST;
+  const int64_t tot_priv = (int64_t)num_envs * T1_NPRIV * T1_CHIST;
+  if (tid < n4_obs) stack_rows<T1_NOBS, T1_HIST>(obs_in, obs_out, clear, tot_obs, tid);
+  else if (tid < n4_obs + n4_priv) stack_rows<T1_NPRIV, T1_CHIST>(priv_in, priv_out, clear, tot_priv, tid - n4_obs);
+}
+
+// extras finalisation + clear flags (runs after k_stack on the same stream)
+__global__ void k_finalize(t1env_buffers B, const t1env_config* __restrict__ Cp, uint8_t* __restrict__ hist_clear) {
+  const t1env_config& C = *Cp;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0) {
+    __shared__ float cnt;
+    if (threadIdx.x == 0) cnt = B.ep_accum[24];
+    __syncthreads();
+    if (threadIdx.x < T1_NREW && cnt > 0.0f) B.extras[threadIdx.x] = (B.ep_accum[threadIdx.x] / cnt) / C.episode_length_s;
+    if (threadIdx.x == 25 && cnt > 0.0f) B.extras[24] = B.ep_accum[25] / (float)C.num_envs;
+    __syncthreads();
+    if (threadIdx.x < 32) B.ep_accum[threadIdx.x] = 0.0f;
+  }
+  if (hist_clear && t < C.num_envs) hist_clear[t] = 0;
+}
+
+// terrain-level sum for extras["episode"]["terrain_level"] (only meaningful on reset steps)
+__global__ __launch_bounds__(256) void k_terrain_level_sum(t1env_buffers B, const t1env_config* __restrict__ Cp) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const t1env_config& C = *Cp;
+  const float v = (n < C.num_envs && C.terrain_curriculum && B.ep_accum[24] > 0.0f) ? (float)B.terrain_levels[n] : 0.0f;
+  wave_atomic_add(B.ep_accum + 25, v);
+}
+
+// creation-time state (see t1env_init in include/t1env.h)
+__global__ __launch_bounds__(BLOCK) void k_init(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
+                                                t1env_buffers B) {
+  const int n = blockIdx.x * BLOCK + threadIdx.x;
+  const t1env_config& C = *Cp;
+  if (n >= C.num_envs) return;
+  const DynModel& M = *Mp;
+  const uint32_t genv = (uint32_t)(C.env_offset + n), seed = C.seed, ctr = 0;
+  const float payload = C.dr_base_mass
+      ? rand_float(C.added_mass_range[0], C.added_mass_range[1], seed, genv, ctr, SLOT_PAYLOAD) : 0.0f;
+  B.body_mass[n] = M.mass[0] + payload;
+  for (int b = 0; b < 12; ++b)
+    B.link_mass_scale[n * 12 + b] = C.dr_link_mass
+        ? rand_float(C.link_mass_range[0], C.link_mass_range[1], seed, genv, ctr, SLOT_LINK_MASS + b) : 1.0f;
+  for (int k = 0; k < 3; ++k)
+    B.com_disp[n * 3 + k] = C.dr_com ? rand_float(C.com_range[k][0], C.com_range[k][1], seed, genv, ctr, SLOT_COM + k) : 0.0f;
+  if (C.dr_friction) {  // 256 buckets; env -> bucket id, bucket -> (friction, restitution)
+    const uint32_t bucket = (uint32_t)rand_int(0, 256, seed, genv, ctr, SLOT_FRICTION_BUCKET);
+    B.friction[n] = rand_float(C.friction_range[0], C.friction_range[1], seed, bucket, 0, SLOT_FRICTION_VALUE);
+    B.restitution[n] = rand_float(C.restitution_range[0], C.restitution_range[1], seed, bucket, 0, SLOT_RESTITUTION_VALUE);
+  } else {
+    B.friction[n] = 0.0f;
+    B.restitution[n] = 0.0f;
+  }
+  if (C.custom_origins) {
+    const int lv = rand_int(0, C.max_init_terrain_level + 1, seed, genv, ctr, SLOT_TERRAIN_LEVEL_INIT);
+    const int ty = (int)floorf((float)genv / ((float)C.num_envs_total / (float)C.num_terrain_cols));
+    B.terrain_levels[n] = lv;
+    B.terrain_types[n] = ty;
+    const float* to = B.terrain_origins + ((size_t)lv * C.num_terrain_cols + ty) * 3;
+    for (int k = 0; k < 3; ++k) B.env_origins[n * 3 + k] = to[k];
+  }
+  B.gait_start[n] = (float)rand_int(0, 2, seed, genv, ctr, SLOT_GAIT_START) * 0.5f;
+  B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_ACTION);
+  B.dof_lag_timestep[n] = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_DOF);
+  B.imu_lag_timestep[n] = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_IMU);
+  // start pose: origin + U(-1,1) xy jitter (legged_robot.py:1380-1383); DOF at the default pose
+  float* r = B.root_states + n * 13;
+  for (int i = 0; i < 13; ++i) r[i] = M.base_init_state[i];
+  for (int k = 0; k < 3; ++k) r[k] += B.env_origins[n * 3 + k];
+  r[0] += rand_float(-1.0f, 1.0f, seed, genv, ctr, SLOT_START_XY + 0);
+  r[1] += rand_float(-1.0f, 1.0f, seed, genv, ctr, SLOT_START_XY + 1);
+  for (int j = 0; j < 12; ++j) { B.dof_state[n * 24 + 2 * j] = M.default_dof_pos[j]; B.dof_state[n * 24 + 2 * j + 1] = 0.0f; }
+  for (int i = 0; i < 169; ++i) B.rigid_state[(size_t)n * 169 + i] = (i % 13 == 6) ? 1.0f : 0.0f;
+  for (int i = 0; i < 39; ++i) B.contact_forces[(size_t)n * 39 + i] = 0.0f;
+  for (int j = 0; j < 12; ++j) {  // gains are still zero when randomize_dof_props first runs
+    B.kp[n * 12 + j] = 0.0f; B.kd[n * 12 + j] = 0.0f; B.motor_offsets[n * 12 + j] = 0.0f;
+    B.coulomb[n * 12 + j] = 0.0f; B.viscous[n * 12 + j] = 0.0f; B.armature[n * 12 + j] = 0.0f;
+  }
+}
+
+// reset_idx(arange(N)) -- LeggedRobot.reset() (legged_robot.py:450-455)
+__global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
+                                                     t1env_buffers B, t1env_step_args A, uint8_t* __restrict__ hist_clear) {
+  const int n0 = blockIdx.x * BLOCK + threadIdx.x;
+  const t1env_config& C = *Cp;
+  const bool live = n0 < C.num_envs;
+  const int n = live ? n0 : C.num_envs - 1;
+  float contrib[T1_NREW];
+  for (int k = 0; k < T1_NREW; ++k) contrib[k] = live ? B.episode_sums[(size_t)k * C.num_envs + n] : 0.0f;
+  for (int k = 0; k < T1_NREW; ++k) wave_atomic_add(B.ep_accum + k, contrib[k]);
+  wave_atomic_add(B.ep_accum + 24, live ? 1.0f : 0.0f);
+  if (!live) return;
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  reset_env(*Mp, C, B, A, n, genv, A.counter, true);
+  resample_commands(C, B, A, n, genv, A.counter);
+  hist_clear[n] = 1;
+}
+
+// =====================================================================================================
+// C ABI
+// =====================================================================================================
+static int grid(int n, int b) { return (n + b - 1) / b; }
+
+extern "C" {
+
+const char* t1env_last_error(void) { return g_err; }
+const char* t1env_version(void) { return "t1env-hip 0.1 (gfx950)"; }
+
+int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_buffers* bufs, t1env** out) {
+  if (!model || !cfg || !bufs || !out) return fail(T1ENV_E_ARG, "t1env_create: null argument");
+  if (cfg->num_envs <= 0) return fail(T1ENV_E_SHAPE, "t1env_create: num_envs must be > 0");
+  if (cfg->decimation <= 0 || cfg->decimation > 64) return fail(T1ENV_E_ARG, "t1env_create: bad decimation");
+  if (model->n_contact > T1_MAXC) return fail(T1ENV_E_SHAPE, "t1env_create: too many contact points");
+  for (int i = 0; i < 3; ++i) {
+    if (cfg->lag_range[1] > 30 || cfg->dof_lag_range[1] > 30 || cfg->imu_lag_range[1] > 10 || cfg->lag_range[0] < 0 ||
+        cfg->dof_lag_range[0] < 0 || cfg->imu_lag_range[0] < 0)
+      return fail(T1ENV_E_ARG, "t1env_create: lag ranges must lie in [0,30] (dof/action) and [0,10] (imu)");
+  }
+  if (cfg->decimation != 10 && (cfg->lag_range[1] > 0 || cfg->dof_lag_range[1] > 0 || cfg->imu_lag_range[1] > 0))
+    return fail(T1ENV_E_ARG, "t1env_create: sensor/actuator lag rings assume decimation == 10");
+  DynModel dm;
+  memset(&dm, 0, sizeof(dm));
+  for (int b = 0; b < NB; ++b) {
+    int ax = -1;
+    float sg = 1.0f;
+    for (int k = 0; k < 3; ++k) {
+      const float v = model->joint_axis[b][k];
+      if (fabsf(fabsf(v) - 1.0f) < 1e-6f) { ax = k; sg = v > 0 ? 1.0f : -1.0f; }
+      else if (fabsf(v) > 1e-6f && b > 0) return fail(T1ENV_E_ARG, "t1env_create: joint axes must be +-x/y/z");
+    }
+    if (b > 0 && ax < 0) return fail(T1ENV_E_ARG, "t1env_create: missing joint axis");
+    dm.axis_idx[b] = ax < 0 ? 0 : ax;
+    dm.axis_sign[b] = sg;
+    for (int k = 0; k < 3; ++k) {
+      dm.joint_offset[b][k] = model->joint_offset[b][k];
+      dm.com[b][k] = model->com[b][k];
+    }
+    dm.mass[b] = model->mass[b];
+    for (int k = 0; k < 6; ++k) dm.inertia[b][k] = model->inertia[b][k];
+    dm.contact_start[b] = model->contact_start[b];
+    dm.contact_count[b] = model->contact_count[b];
+    if (b > 0 && model->parent[b] != (b == 1 || b == 7 ? 0 : b - 1))
+      return fail(T1ENV_E_ARG, "t1env_create: body order must be base, left leg chain, right leg chain");
+  }
+  for (int j = 0; j < ND; ++j) {
+    dm.q_lower[j] = model->q_lower[j]; dm.q_upper[j] = model->q_upper[j];
+    dm.vel_limit[j] = model->vel_limit[j]; dm.torque_limit[j] = model->torque_limit[j];
+    dm.default_dof_pos[j] = model->default_dof_pos[j]; dm.p_gains[j] = model->p_gains[j]; dm.d_gains[j] = model->d_gains[j];
+  }
+  for (int c = 0; c < model->n_contact; ++c)
+    for (int k = 0; k < 3; ++k) dm.contact_point[c][k] = model->contact_point[c][k];
+  dm.k_contact = model->k_contact; dm.d_contact = model->d_contact; dm.friction_vs = model->friction_vs;
+  dm.k_limit = model->k_limit; dm.d_limit = model->d_limit; dm.gravity = model->gravity;
+  dm.ground_friction = model->ground_friction; dm.ground_restitution = model->ground_restitution;
+  for (int i = 0; i < 13; ++i) dm.base_init_state[i] = model->base_init_state[i];
+
+  t1env* e = (t1env*)calloc(1, sizeof(t1env));
+  if (!e) return fail(T1ENV_E_STATE, "t1env_create: out of host memory");
+  e->cfg = *cfg;
+  e->buf = *bufs;
+  e->terrain = Terrain{nullptr, 0, 0, 0, 0.1f, 0.005f, 0.0f};
+  hipError_t err;
+  if ((err = hipMalloc(&e->d_model, sizeof(DynModel))) != hipSuccess ||
+      (err = hipMalloc(&e->d_cfg, sizeof(t1env_config))) != hipSuccess ||
+      (err = hipMalloc(&e->d_hist_clear, (size_t)cfg->num_envs)) != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "t1env_create: hipMalloc: %s", hipGetErrorString(err));
+    free(e);
+    return (int)err;
+  }
+  HIP_TRY(hipMemcpy(e->d_model, &dm, sizeof(DynModel), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_cfg, cfg, sizeof(t1env_config), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(e->d_hist_clear, 0, (size_t)cfg->num_envs));
+  HIP_TRY(hipMemset(e->buf.ep_accum, 0, 32 * sizeof(float)));
+  *out = e;
+  return 0;
+}
+
+int t1env_destroy(t1env* e) {
+  if (!e) return 0;
+  (void)hipFree(e->d_model);
+  (void)hipFree(e->d_cfg);
+  (void)hipFree(e->d_hist_clear);
+  free(e);
+  return 0;
+}
+
+int t1env_init(t1env* e, void* stream) {
+  if (!e) return fail(T1ENV_E_ARG, "t1env_init: null env");
+  const int N = e->cfg.num_envs;
+  hipLaunchKernelGGL(k_init, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, (hipStream_t)stream, e->d_model, e->d_cfg, e->buf);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int t1env_set_terrain(t1env* e, const int16_t* h, int32_t rows, int32_t cols, float hs, float vs, float border,
+                      int32_t mesh_type) {
+  if (!e) return fail(T1ENV_E_ARG, "t1env_set_terrain: null env");
+  if (mesh_type != 0 && (!h || rows < 2 || cols < 2)) return fail(T1ENV_E_SHAPE, "t1env_set_terrain: bad height field");
+  e->terrain = Terrain{h, rows, cols, mesh_type, hs, vs, border};
+  return 0;
+}
+
+static int launch_physics(t1env* e, const float* actions, const t1env_step_args* a, const t1env_injected* inj,
+                          hipStream_t s) {
+  const int N = e->cfg.num_envs;
+  t1env_injected none{};
+  if (inj)
+    hipLaunchKernelGGL(k_physics<true>, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
+                       e->terrain, actions, *a, *inj);
+  else
+    hipLaunchKernelGGL(k_physics<false>, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
+                       e->terrain, actions, *a, none);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_post_a, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int t1env_step_physics_and_rewards(t1env* e, const float* actions, const t1env_step_args* a, void* stream) {
+  if (!e || !actions || !a) return fail(T1ENV_E_ARG, "t1env_step_physics_and_rewards: null argument");
+  return launch_physics(e, actions, a, nullptr, (hipStream_t)stream);
+}
+
+int t1env_step_injected(t1env* e, const float* actions, const t1env_step_args* a, const t1env_injected* inj,
+                        void* stream) {
+  if (!e || !actions || !a || !inj || !inj->root || !inj->dof || !inj->rigid || !inj->contact)
+    return fail(T1ENV_E_ARG, "t1env_step_injected: null argument");
+  return launch_physics(e, actions, a, inj, (hipStream_t)stream);
+}
+
+int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* stream) {
+  if (!e || !a) return fail(T1ENV_E_ARG, "t1env_step_reset_and_observe: null argument");
+  if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
+  hipStream_t s = (hipStream_t)stream;
+  const int N = e->cfg.num_envs;
+  hipLaunchKernelGGL(k_post_b, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,
+                     e->d_hist_clear);
+  HIP_TRY(hipGetLastError());
+  if (e->cfg.terrain_curriculum) {
+    hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
+    HIP_TRY(hipGetLastError());
+  }
+  const int64_t n4o = ((int64_t)N * T1_NOBS * T1_HIST + 3) / 4;
+  const int64_t n4p = ((int64_t)N * T1_NPRIV * T1_CHIST + 3) / 4;
+  const int in = a->obs_slot ^ 1, outs = a->obs_slot;
+  hipLaunchKernelGGL(k_stack, dim3((unsigned)((n4o + n4p + 255) / 256)), dim3(256), 0, s, e->buf.obs_buf[in],
+                     e->buf.obs_buf[outs], e->buf.priv_buf[in], e->buf.priv_buf[outs], e->d_hist_clear, N, n4o, n4p);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_finalize, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg, e->d_hist_clear);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int t1env_step(t1env* e, const float* actions, const t1env_step_args* a, void* stream) {
+  int rc = t1env_step_physics_and_rewards(e, actions, a, stream);
+  if (rc) return rc;
+  return t1env_step_reset_and_observe(e, a, stream);
+}
+
+int t1env_reset_all(t1env* e, const t1env_step_args* a, void* stream) {
+  if (!e || !a) return fail(T1ENV_E_ARG, "t1env_reset_all: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int N = e->cfg.num_envs;
+  hipLaunchKernelGGL(k_reset_all, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,
+                     e->d_hist_clear);
+  HIP_TRY(hipGetLastError());
+  if (e->cfg.terrain_curriculum) {
+    hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
+    HIP_TRY(hipGetLastError());
+  }
+  // extras of the reset; history rows stay flagged (hist_clear) for the next stack pass
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg, (uint8_t*)nullptr);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"
