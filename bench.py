@@ -1,0 +1,174 @@
+"""Benchmark: env-steps/s of T1DHStandEnv.step() (the LeggedRobot.step() hot path) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--num-envs 8192] [--mesh trimesh]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[2], the metric's config): t1_dh_stand, 8192 envs per GPU, trimesh
+curriculum terrain (20 x 20 sub-terrains) + the full DHT1StandCfg domain randomisation, synthetic
+random-command rollouts: actions ~ N(0, 1) pre-generated on the device (policy inference excluded), the
+env's own gait scheduler draws the commands.  One step = one env.step(actions) for all envs on the rank
+(10 physics substeps + post-physics + 66-frame obs stack).  N > 1: envs shard by global env id across the
+ranks (weak scaling; the env step has no collective), timed region bracketed by barrier + synchronize,
+max over ranks.
+
+roofline: SURVEY.md §8(d) algorithmic bytes B_alg = 30,678 B per env-step over the step's GPU time (sum of
+the kernels' HIP-event durations on the env's stream inside the timed region), against the 8 TB/s HBM3E
+peak; per-kernel event times and each kernel's own algorithmic bytes are reported alongside.
+cpu_baseline: the build's CPU restatement (numpy oracle post-physics + OpenMP dynamics), rank 0, N = 1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+B_ALG = 30678          # algorithmic bytes per env-step (fp32, default t1 config)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+KERNELS = ["k_physics", "k_post_a", "k_post_b", "k_stack", "k_finalize"]
+# per-kernel algorithmic bytes per env (reads + writes it must do)
+KERNEL_BYTES = {
+    "k_physics": 4 * (13 + 24 + 12 + 48 + 12 * 6 + 13 + 3 + 3) + 4 * (13 + 24 + 169 + 39 + 12 + 12 + 12 + 24 + 6),
+    "k_post_a": 4 * (13 + 24 + 169 + 39 + 12 * 5 + 6 + 4 + 24 + 12 + 3 + 6 + 8) + 4 * (3 * 4 + 6 + 3 + 2 + 4 + 24 + 3 + 6),
+    "k_post_b": 4 * (24 + 13 + 12 * 2 + 3 * 3 + 39 + 24 + 6 + 8) + 4 * (47 + 73 + 12 * 4 + 6),
+    "k_stack": 4 * ((3102 - 47) + (219 - 73)) + 4 * (3102 + 219),
+    "k_finalize": 1,
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--num-envs", type=int, default=8192)
+    p.add_argument("--mesh", default="trimesh", choices=["plane", "heightfield", "trimesh"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-envs", type=int, default=256)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
+                   help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
+    return p.parse_args()
+
+
+def cpu_baseline(env, args):
+    """Bounded sample of the same workload on the host cores (the build's CPU restatement)."""
+    from oracle.cpu_env import CpuT1Env
+    terrain = None
+    if env.mesh_type in ("heightfield", "trimesh"):
+        tc = env.cfg.terrain
+        terrain = {"terrain_origins": env._terrain.env_origins, "height_samples": env._terrain.heightsamples,
+                   "horizontal_scale": tc.horizontal_scale, "vertical_scale": tc.vertical_scale,
+                   "border_size": tc.border_size, "num_envs_total": args.cpu_envs}
+    cpu = CpuT1Env(env._model, args.cpu_envs, seed=5, mesh_type=env.mesh_type, terrain=terrain)
+    cpu.reset()
+    rng = np.random.default_rng(0)
+    acts = rng.standard_normal((8, args.cpu_envs, 12)).astype(np.float32)
+    cpu.step(acts[0])
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        cpu.step(acts[n % 8])
+        n += 1
+    dt = time.perf_counter() - t0
+    try:
+        model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
+    except Exception:
+        model = "unknown"
+    return {"value": round(args.cpu_envs * n / dt, 1), "unit": "env-steps/s", "cores": cpu.threads(), "kind": "port",
+            "sample": f"{args.cpu_envs} envs x {n} steps ({dt:.1f} s), same cfg/terrain as the GPU run; "
+                      f"numpy oracle post-physics + OpenMP fp32 dynamics on {cpu.threads()} threads of {model}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    from ti5_isaacgym_amd import make_t1_env
+    N = args.num_envs
+    env = make_t1_env(num_envs=N, mesh_type=args.mesh, seed=5, device=str(dev), env_offset=rank * N,
+                      num_envs_total=N * world)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    pool = [torch.randn(N, 12, device=dev, generator=gen) for _ in range(8)]
+    env.reset()
+    for i in range(args.warmup):
+        env.step(pool[i % 8])
+    env.set_timing(True)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        env.step(pool[i % 8])
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kt = env.get_timing()
+    env.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ok = bool(torch.isfinite(env.root_states).all() and torch.isfinite(env.obs_buf).all())
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    steps = args.steps
+    value = N * world * steps / elapsed
+    gpu_ms = sum(kt[k]["ms"] for k in KERNELS) / steps
+    per_kernel = {}
+    for k in KERNELS:
+        ms = kt[k]["ms"] / max(1, kt[k]["launches"])
+        per_kernel[k] = {"avg_ms": round(ms, 5), "launches": kt[k]["launches"],
+                         "alg_bytes_per_launch": KERNEL_BYTES[k] * N,
+                         "alg_GBs": round(KERNEL_BYTES[k] * N / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
+    dom = max(KERNELS, key=lambda k: kt[k]["ms"])
+    achieved = B_ALG * N / (gpu_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("num_envs") == N and tj.get("mesh") == args.mesh:
+                traffic = tj.get("hbm_bytes_per_step")
+        except Exception:
+            traffic = None
+    line = {
+        "metric": "env-steps/sec at 8192 envs, t1_dh_stand, 1/2/4/8 MI355X; obs/reward parity",
+        "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"t1_dh_stand {N} envs/GPU, {args.mesh} curriculum terrain + full DR, "
+                               "random N(0,1) actions (policy excluded), 10 substeps/step",
+                   "num_envs_per_gpu": N, "global_envs": N * world, "mesh": args.mesh, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": "t1env_step (k_physics+k_post_a+k_post_b+k_stack+k_finalize)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "alg_bytes_per_env_step": B_ALG, "gpu_ms_per_step": round(gpu_ms, 4),
+                     "dominant_kernel": dom, "kernels": per_kernel},
+        "finite": ok,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(env, args)
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

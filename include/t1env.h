@@ -206,6 +206,11 @@ int t1env_step_physics_and_rewards(t1env* env, const float* actions, const t1env
 int t1env_step_reset_and_observe(t1env* env, const t1env_step_args* args, void* stream);
 int t1env_step_injected(t1env* env, const float* actions, const t1env_step_args* args, const t1env_injected* inj,
                         void* stream);
+/* Per-kernel timing with HIP events recorded around every launch (bench.py's live roofline).  Kernel ids:
+ * 0 k_physics, 1 k_post_a, 2 k_post_b, 3 k_stack, 4 k_finalize(+terrain-level sum). get_timing synchronises
+ * and returns the summed milliseconds and launch counts per kernel id since the last enable. */
+int t1env_set_timing(t1env* env, int32_t enable);
+int t1env_get_timing(t1env* env, double* ms /* [5] */, int32_t* launches /* [5] */);
 const char* t1env_last_error(void);
 const char* t1env_version(void);
 

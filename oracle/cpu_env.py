@@ -1,0 +1,55 @@
+"""CPU baseline env (TEST INFRASTRUCTURE / bench.py cpu_baseline leg only).
+
+The reference's own CPU path (Isaac Gym PhysX CPU + torch CPU) cannot run here or on the GPU box, so the
+CPU baseline is the build's restatement: the numpy oracle for PD + post-physics (oracle/t1_oracle.py)
+plus the dynamics header compiled for the host with OpenMP (oracle/dyn_cpu.cpp), fp32.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import build_cpu
+from .t1_oracle import T1Oracle
+
+
+class CpuT1Env:
+    def __init__(self, model, num_envs, seed=5, mesh_type="plane", terrain=None, fp64=False):
+        self.lib = C.CDLL(build_cpu.build())
+        self.model = model
+        self.o = T1Oracle(num_envs, seed=seed, mesh_type=mesh_type, terrain=terrain)
+        self.fp64 = int(fp64)
+        self.N = num_envs
+        if terrain is not None and mesh_type in ("heightfield", "trimesh"):
+            self.hf = np.ascontiguousarray(terrain["height_samples"], np.int16)
+            self.tparams = (self.hf.shape[0], self.hf.shape[1], terrain.get("horizontal_scale", 0.1),
+                            terrain.get("vertical_scale", 0.005), terrain.get("border_size", 25.0), 2)
+        else:
+            self.hf = np.zeros((2, 2), np.int16)
+            self.tparams = (2, 2, 0.1, 0.005, 0.0, 0)
+        self.rigid = np.zeros((num_envs, 13, 13), np.float32)
+        self.contact = np.zeros((num_envs, 13, 3), np.float32)
+
+    def threads(self):
+        return int(self.lib.t1dyn_num_threads())
+
+    def _physics(self, g, torques, o):
+        fp = C.POINTER(C.c_float)
+        f = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+        root, dof = f(o.root.copy()), f(o.dof.reshape(self.N, 24).copy())
+        args = [f(torques), f(o.body_mass), f(o.link_mass_scale), f(o.com_disp), f(o.armature), f(o.friction)]
+        ext = f(o.applied_force[:, 0, :]) if o.force_pending else None
+        rows, cols, hs, vs, border, mesh = self.tparams
+        rc = self.lib.t1dyn_substeps(
+            C.byref(self.model), self.N, self.fp64, root.ctypes.data_as(fp), dof.ctypes.data_as(fp),
+            *[a.ctypes.data_as(fp) for a in args], ext.ctypes.data_as(fp) if ext is not None else None,
+            C.c_float(0.001), 1, self.hf.ctypes.data_as(C.POINTER(C.c_int16)), rows, cols, C.c_float(hs),
+            C.c_float(vs), C.c_float(border), mesh, self.rigid.ctypes.data_as(fp), self.contact.ctypes.data_as(fp))
+        assert rc == 0
+        return root, dof.reshape(self.N, 12, 2), self.rigid.copy(), self.contact.copy()
+
+    def reset(self):
+        return self.o.reset(self._physics)
+
+    def step(self, actions):
+        return self.o.step(np.asarray(actions, np.float32), self._physics)

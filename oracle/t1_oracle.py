@@ -133,6 +133,9 @@ class T1Oracle:
         re_b = R.rand_float(0.0, 0.4, seed, np.arange(256), 0, R.SLOT_RESTITUTION_VALUE)
         self.friction = fr_b[bucket]
         self.restitution = re_b[bucket]
+        self.link_mass_scale = np.stack([R.rand_float(0.9, 1.1, seed, self.ids, 0, R.SLOT_LINK_MASS + b)
+                                         for b in range(12)], 1)
+        self.com_disp = np.stack([R.rand_float(-0.05, 0.05, seed, self.ids, 0, R.SLOT_COM + k) for k in range(3)], 1)
         # terrain origins (legged_robot.py:1477-1512)
         self.env_origins = np.zeros((N, 3), f32)
         if self.custom_origins:

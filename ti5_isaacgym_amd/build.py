@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "t1env.hip")
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("t1env.hip", "t1_dynamics.h", "t1_common.h", "t1env_post.h")] + \
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("t1env.hip", "t1_dynamics.h", "t1_common.h", "t1env_post.h", "t1_model_conv.h")] + \
     [os.path.join(os.path.dirname(HERE), "include", "t1env.h")]
 ARCH = os.environ.get("T1ENV_ARCH", "gfx950")
 

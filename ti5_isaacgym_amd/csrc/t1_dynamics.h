@@ -472,17 +472,17 @@ template <typename R> T1_HD void backsub_leg(const LegBlock<R>& lb, const R xb[6
 }
 
 // ---------------------------------------------------------------------------------------------------
-// one physics substep.  tau: joint torques; ext_f: world force at the base COM (apply_rigid_body_force
-// ENV_SPACE semantics); returns whether any contact was active.
+// Assemble and solve one substep: delta = change of u = [omega, v_O (spatial, about the fixed point O),
+// qd] over dt, including implicit contact / joint-limit terms.  tau: joint torques; ext_f: world force at
+// the base COM (apply_rigid_body_force_tensors ENV_SPACE semantics).
 // ---------------------------------------------------------------------------------------------------
 template <typename R>
-T1_HD void substep(const DynModel& M, const Terrain& T, const EnvParams<R>& P, EnvState<R>& s, const R tau[ND],
-                   V3<R> ext_f, R dt) {
+T1_HD void compute_delta(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s,
+                         const R tau[ND], V3<R> ext_f, R dt, R delta[6 + ND]) {
   M3<R> R0 = quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]);
   V3<R> base_abs = v3<R>(s.pos[0], s.pos[1], s.pos[2]);
   R V0[6] = {s.w[0], s.w[1], s.w[2], s.vo[0], s.vo[1], s.vo[2]};
   R A0[6] = {R(0), R(0), R(0), R(0), R(0), R(M.gravity)};  // fictitious base acceleration -g
-  // base body
   Sym6<R> Ac;
   R Icw[6];
   world_inertia(M, 0, R0, P.inertia_scale[0], Icw);
@@ -522,28 +522,31 @@ T1_HD void substep(const DynModel& M, const Terrain& T, const EnvParams<R>& P, E
 #pragma unroll
   for (int leg = 0; leg < 2; ++leg) eliminate_leg(lb[leg], Ac, rb);
   solve_base(Ac, rb);
-  R dq[2][NLEG];
 #pragma unroll
-  for (int leg = 0; leg < 2; ++leg) backsub_leg(lb[leg], rb, dq[leg]);
-  // velocity update (+ the omega x v term that turns the spatial base acceleration into the classical one)
-  V3<R> w_new = v3<R>(s.w[0] + rb[0], s.w[1] + rb[1], s.w[2] + rb[2]);
-  V3<R> vO_new = v3<R>(s.vo[0] + rb[3], s.vo[1] + rb[4], s.vo[2] + rb[5]);
+  for (int i = 0; i < 6; ++i) delta[i] = rb[i];
+#pragma unroll
+  for (int leg = 0; leg < 2; ++leg) backsub_leg(lb[leg], rb, delta + 6 + 6 * leg);
+}
+
+// Semi-implicit Euler with the solved velocity change (+ the omega x v term that turns the spatial base
+// acceleration into the classical acceleration of the base origin); joint speeds clamped like PhysX.
+template <typename R>
+T1_HD void integrate(const DynModel& M, EnvState<R>& s, const R delta[6 + ND], R dt) {
+  V3<R> w_new = v3<R>(s.w[0] + delta[0], s.w[1] + delta[1], s.w[2] + delta[2]);
+  V3<R> vO_new = v3<R>(s.vo[0] + delta[3], s.vo[1] + delta[4], s.vo[2] + delta[5]);
   V3<R> vb_new = vO_new + dt * cross(w_new, vO_new);
 #pragma unroll
-  for (int leg = 0; leg < 2; ++leg)
-#pragma unroll
-    for (int k = 0; k < NLEG; ++k) {
-      const int j = 6 * leg + k;
-      R v = s.qd[j] + dq[leg][k];
-      R vl = R(M.vel_limit[j]);
-      v = v > vl ? vl : (v < -vl ? -vl : v);
-      s.qd[j] = v;
-      s.q[j] += dt * v;
-    }
+  for (int j = 0; j < ND; ++j) {
+    R v = s.qd[j] + delta[6 + j];
+    R vl = R(M.vel_limit[j]);
+    v = v > vl ? vl : (v < -vl ? -vl : v);
+    s.qd[j] = v;
+    s.q[j] += dt * v;
+  }
   s.w[0] = w_new.x; s.w[1] = w_new.y; s.w[2] = w_new.z;
   s.vo[0] = vb_new.x; s.vo[1] = vb_new.y; s.vo[2] = vb_new.z;
   s.pos[0] += dt * vb_new.x; s.pos[1] += dt * vb_new.y; s.pos[2] += dt * vb_new.z;
-  // quaternion: q += 0.5 dt [w, 0] (x) q  (world-frame angular velocity)
+  // quaternion: q += 0.5 dt [w, 0] (x) q  (world-frame angular velocity), renormalised
   R qx = s.quat[0], qy = s.quat[1], qz = s.quat[2], qw = s.quat[3];
   R hx = R(0.5) * dt * w_new.x, hy = R(0.5) * dt * w_new.y, hz = R(0.5) * dt * w_new.z;
   R nx = qx + (hx * qw + hy * qz - hz * qy);
@@ -552,6 +555,14 @@ T1_HD void substep(const DynModel& M, const Terrain& T, const EnvParams<R>& P, E
   R nw = qw - (hx * qx + hy * qy + hz * qz);
   R inv = R(1) / sqrt(nx * nx + ny * ny + nz * nz + nw * nw);
   s.quat[0] = nx * inv; s.quat[1] = ny * inv; s.quat[2] = nz * inv; s.quat[3] = nw * inv;
+}
+
+template <typename R>
+T1_HD void substep(const DynModel& M, const Terrain& T, const EnvParams<R>& P, EnvState<R>& s, const R tau[ND],
+                   V3<R> ext_f, R dt) {
+  R delta[6 + ND];
+  compute_delta(M, T, P, s, tau, ext_f, dt, delta);
+  integrate(M, s, delta, dt);
 }
 
 // ---------------------------------------------------------------------------------------------------

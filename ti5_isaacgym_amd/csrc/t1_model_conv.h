@@ -1,0 +1,53 @@
+// t1_model_conv.h -- t1env_model (C ABI) -> DynModel (kernel layout); shared by the HIP library and the CPU
+// build of the dynamics (oracle/dyn_cpu.cpp).
+#pragma once
+#include <math.h>
+#include <string.h>
+
+#include "../../include/t1env.h"
+#include "t1_dynamics.h"
+
+namespace t1 {
+
+// returns nullptr on success, else a static error message
+inline const char* make_dyn_model(const t1env_model* model, DynModel* dm) {
+  memset(dm, 0, sizeof(*dm));
+  if (model->n_contact > T1_MAXC || model->n_contact > 48) return "too many contact points";
+  for (int b = 0; b < NB; ++b) {
+    int ax = -1;
+    float sg = 1.0f;
+    for (int k = 0; k < 3; ++k) {
+      const float v = model->joint_axis[b][k];
+      if (fabsf(fabsf(v) - 1.0f) < 1e-6f) { ax = k; sg = v > 0 ? 1.0f : -1.0f; }
+      else if (fabsf(v) > 1e-6f && b > 0) return "joint axes must be +-x/y/z";
+    }
+    if (b > 0 && ax < 0) return "missing joint axis";
+    if (b > 0 && model->parent[b] != (b == 1 || b == 7 ? 0 : b - 1))
+      return "body order must be base, left leg chain, right leg chain";
+    dm->axis_idx[b] = ax < 0 ? 0 : ax;
+    dm->axis_sign[b] = sg;
+    for (int k = 0; k < 3; ++k) {
+      dm->joint_offset[b][k] = model->joint_offset[b][k];
+      dm->com[b][k] = model->com[b][k];
+    }
+    dm->mass[b] = model->mass[b];
+    for (int k = 0; k < 6; ++k) dm->inertia[b][k] = model->inertia[b][k];
+    dm->contact_start[b] = model->contact_start[b];
+    dm->contact_count[b] = model->contact_count[b];
+  }
+  for (int j = 0; j < ND; ++j) {
+    dm->q_lower[j] = model->q_lower[j]; dm->q_upper[j] = model->q_upper[j];
+    dm->vel_limit[j] = model->vel_limit[j]; dm->torque_limit[j] = model->torque_limit[j];
+    dm->default_dof_pos[j] = model->default_dof_pos[j]; dm->p_gains[j] = model->p_gains[j];
+    dm->d_gains[j] = model->d_gains[j];
+  }
+  for (int c = 0; c < model->n_contact; ++c)
+    for (int k = 0; k < 3; ++k) dm->contact_point[c][k] = model->contact_point[c][k];
+  dm->k_contact = model->k_contact; dm->d_contact = model->d_contact; dm->friction_vs = model->friction_vs;
+  dm->k_limit = model->k_limit; dm->d_limit = model->d_limit; dm->gravity = model->gravity;
+  dm->ground_friction = model->ground_friction; dm->ground_restitution = model->ground_restitution;
+  for (int i = 0; i < 13; ++i) dm->base_init_state[i] = model->base_init_state[i];
+  return nullptr;
+}
+
+}  // namespace t1

@@ -17,6 +17,7 @@
 
 #include "../../include/t1env.h"
 #include "t1_dynamics.h"
+#include "t1_model_conv.h"
 
 using namespace t1;
 
@@ -40,8 +41,16 @@ constexpr int BLOCK = 64;  // one wave per workgroup: 8192 envs -> 128 workgroup
 
 }  // namespace
 
+constexpr int NKERN = 5;
+constexpr int MAX_TIMED = 1 << 14;
+
 struct t1env {
   t1env_config cfg;
+  int timing;
+  int n_timed;
+  int timed_kernel[MAX_TIMED];
+  hipEvent_t ev_start[MAX_TIMED], ev_stop[MAX_TIMED];
+  int n_events;  // events created so far (reused across enable cycles)
   t1env_buffers buf;
   DynModel* d_model;
   t1env_config* d_cfg;
@@ -896,6 +905,22 @@ __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict_
 // =====================================================================================================
 static int grid(int n, int b) { return (n + b - 1) / b; }
 
+// timing bracket around one launch: returns the slot (or -1 when timing is off / full)
+static int t_begin(t1env* e, int kid, hipStream_t s) {
+  if (!e->timing || e->n_timed >= MAX_TIMED) return -1;
+  const int i = e->n_timed++;
+  if (i >= e->n_events) {
+    if (hipEventCreate(&e->ev_start[i]) != hipSuccess || hipEventCreate(&e->ev_stop[i]) != hipSuccess) return -1;
+    e->n_events = i + 1;
+  }
+  e->timed_kernel[i] = kid;
+  (void)hipEventRecord(e->ev_start[i], s);
+  return i;
+}
+static void t_end(t1env* e, int i, hipStream_t s) {
+  if (i >= 0) (void)hipEventRecord(e->ev_stop[i], s);
+}
+
 extern "C" {
 
 const char* t1env_last_error(void) { return g_err; }
@@ -914,41 +939,7 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   if (cfg->decimation != 10 && (cfg->lag_range[1] > 0 || cfg->dof_lag_range[1] > 0 || cfg->imu_lag_range[1] > 0))
     return fail(T1ENV_E_ARG, "t1env_create: sensor/actuator lag rings assume decimation == 10");
   DynModel dm;
-  memset(&dm, 0, sizeof(dm));
-  for (int b = 0; b < NB; ++b) {
-    int ax = -1;
-    float sg = 1.0f;
-    for (int k = 0; k < 3; ++k) {
-      const float v = model->joint_axis[b][k];
-      if (fabsf(fabsf(v) - 1.0f) < 1e-6f) { ax = k; sg = v > 0 ? 1.0f : -1.0f; }
-      else if (fabsf(v) > 1e-6f && b > 0) return fail(T1ENV_E_ARG, "t1env_create: joint axes must be +-x/y/z");
-    }
-    if (b > 0 && ax < 0) return fail(T1ENV_E_ARG, "t1env_create: missing joint axis");
-    dm.axis_idx[b] = ax < 0 ? 0 : ax;
-    dm.axis_sign[b] = sg;
-    for (int k = 0; k < 3; ++k) {
-      dm.joint_offset[b][k] = model->joint_offset[b][k];
-      dm.com[b][k] = model->com[b][k];
-    }
-    dm.mass[b] = model->mass[b];
-    for (int k = 0; k < 6; ++k) dm.inertia[b][k] = model->inertia[b][k];
-    dm.contact_start[b] = model->contact_start[b];
-    dm.contact_count[b] = model->contact_count[b];
-    if (b > 0 && model->parent[b] != (b == 1 || b == 7 ? 0 : b - 1))
-      return fail(T1ENV_E_ARG, "t1env_create: body order must be base, left leg chain, right leg chain");
-  }
-  for (int j = 0; j < ND; ++j) {
-    dm.q_lower[j] = model->q_lower[j]; dm.q_upper[j] = model->q_upper[j];
-    dm.vel_limit[j] = model->vel_limit[j]; dm.torque_limit[j] = model->torque_limit[j];
-    dm.default_dof_pos[j] = model->default_dof_pos[j]; dm.p_gains[j] = model->p_gains[j]; dm.d_gains[j] = model->d_gains[j];
-  }
-  for (int c = 0; c < model->n_contact; ++c)
-    for (int k = 0; k < 3; ++k) dm.contact_point[c][k] = model->contact_point[c][k];
-  dm.k_contact = model->k_contact; dm.d_contact = model->d_contact; dm.friction_vs = model->friction_vs;
-  dm.k_limit = model->k_limit; dm.d_limit = model->d_limit; dm.gravity = model->gravity;
-  dm.ground_friction = model->ground_friction; dm.ground_restitution = model->ground_restitution;
-  for (int i = 0; i < 13; ++i) dm.base_init_state[i] = model->base_init_state[i];
-
+  if (const char* err = make_dyn_model(model, &dm)) return fail(T1ENV_E_ARG, err);
   t1env* e = (t1env*)calloc(1, sizeof(t1env));
   if (!e) return fail(T1ENV_E_STATE, "t1env_create: out of host memory");
   e->cfg = *cfg;
@@ -975,6 +966,10 @@ int t1env_destroy(t1env* e) {
   (void)hipFree(e->d_model);
   (void)hipFree(e->d_cfg);
   (void)hipFree(e->d_hist_clear);
+  for (int i = 0; i < e->n_events; ++i) {
+    (void)hipEventDestroy(e->ev_start[i]);
+    (void)hipEventDestroy(e->ev_stop[i]);
+  }
   free(e);
   return 0;
 }
@@ -999,14 +994,18 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
                           hipStream_t s) {
   const int N = e->cfg.num_envs;
   t1env_injected none{};
+  int t = t_begin(e, 0, s);
   if (inj)
     hipLaunchKernelGGL(k_physics<true>, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
                        e->terrain, actions, *a, *inj);
   else
     hipLaunchKernelGGL(k_physics<false>, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
                        e->terrain, actions, *a, none);
+  t_end(e, t, s);
   HIP_TRY(hipGetLastError());
+  t = t_begin(e, 1, s);
   hipLaunchKernelGGL(k_post_a, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a);
+  t_end(e, t, s);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -1028,20 +1027,26 @@ int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* strea
   if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
   hipStream_t s = (hipStream_t)stream;
   const int N = e->cfg.num_envs;
+  int t = t_begin(e, 2, s);
   hipLaunchKernelGGL(k_post_b, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,
                      e->d_hist_clear);
+  t_end(e, t, s);
   HIP_TRY(hipGetLastError());
+  const int64_t n4o = ((int64_t)N * T1_NOBS * T1_HIST + 3) / 4;
+  const int64_t n4p = ((int64_t)N * T1_NPRIV * T1_CHIST + 3) / 4;
+  const int in = a->obs_slot ^ 1, outs = a->obs_slot;
+  t = t_begin(e, 3, s);
+  hipLaunchKernelGGL(k_stack, dim3((unsigned)((n4o + n4p + 255) / 256)), dim3(256), 0, s, e->buf.obs_buf[in],
+                     e->buf.obs_buf[outs], e->buf.priv_buf[in], e->buf.priv_buf[outs], e->d_hist_clear, N, n4o, n4p);
+  t_end(e, t, s);
+  HIP_TRY(hipGetLastError());
+  t = t_begin(e, 4, s);
   if (e->cfg.terrain_curriculum) {
     hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
     HIP_TRY(hipGetLastError());
   }
-  const int64_t n4o = ((int64_t)N * T1_NOBS * T1_HIST + 3) / 4;
-  const int64_t n4p = ((int64_t)N * T1_NPRIV * T1_CHIST + 3) / 4;
-  const int in = a->obs_slot ^ 1, outs = a->obs_slot;
-  hipLaunchKernelGGL(k_stack, dim3((unsigned)((n4o + n4p + 255) / 256)), dim3(256), 0, s, e->buf.obs_buf[in],
-                     e->buf.obs_buf[outs], e->buf.priv_buf[in], e->buf.priv_buf[outs], e->d_hist_clear, N, n4o, n4p);
-  HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_finalize, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg, e->d_hist_clear);
+  t_end(e, t, s);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -1050,6 +1055,26 @@ int t1env_step(t1env* e, const float* actions, const t1env_step_args* a, void* s
   int rc = t1env_step_physics_and_rewards(e, actions, a, stream);
   if (rc) return rc;
   return t1env_step_reset_and_observe(e, a, stream);
+}
+
+int t1env_set_timing(t1env* e, int32_t enable) {
+  if (!e) return fail(T1ENV_E_ARG, "t1env_set_timing: null env");
+  e->timing = enable ? 1 : 0;
+  e->n_timed = 0;
+  return 0;
+}
+
+int t1env_get_timing(t1env* e, double* ms, int32_t* launches) {
+  if (!e || !ms || !launches) return fail(T1ENV_E_ARG, "t1env_get_timing: null argument");
+  for (int k = 0; k < NKERN; ++k) { ms[k] = 0.0; launches[k] = 0; }
+  if (e->n_timed > 0) HIP_TRY(hipEventSynchronize(e->ev_stop[e->n_timed - 1]));
+  for (int i = 0; i < e->n_timed; ++i) {
+    float t = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&t, e->ev_start[i], e->ev_stop[i]));
+    ms[e->timed_kernel[i]] += t;
+    launches[e->timed_kernel[i]] += 1;
+  }
+  return 0;
 }
 
 int t1env_reset_all(t1env* e, const t1env_step_args* a, void* stream) {
