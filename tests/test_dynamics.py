@@ -73,3 +73,120 @@ def test_accelerations_match_independent_formulation(dyn, model, seed):
     ref, M = Robot(tab, mass, isc, com, arm).accel(s["p"], s["quat"], s["w"], s["v"], s["q"], s["qd"], s["tau"])
     scale = np.abs(ref).max() + 1.0
     np.testing.assert_allclose(out, ref, atol=2e-5 * scale, rtol=1e-5)
+
+
+# ----------------------------------------------------------------------------------------------------
+# invariants on the full substep (contact + integration), fp64 host build
+# ----------------------------------------------------------------------------------------------------
+class Sim:
+    def __init__(self, dyn, m, n=1):
+        self.dyn, self.m, self.n = dyn, m, n
+        self.root = np.zeros((n, 13), np.float32)
+        self.root[:, 6] = 1.0
+        self.dof = np.zeros((n, 24), np.float32)
+        self.bm = np.full(n, m.mass[0], np.float32)
+        self.ls = np.ones((n, 12), np.float32)
+        self.cd = np.zeros((n, 3), np.float32)
+        self.arm = np.full((n, 12), 0.1, np.float32)
+        self.fr = np.full(n, 0.8, np.float32)
+        self.rigid = np.zeros((n, 13, 13), np.float32)
+        self.contact = np.zeros((n, 13, 3), np.float32)
+        self.hf = np.zeros((2, 2), np.int16)
+
+    def step(self, tau, nsub=1, dt=0.001):
+        fp = C.POINTER(C.c_float)
+        tau = np.ascontiguousarray(tau, np.float32).reshape(self.n, 12)
+        rc = self.dyn.t1dyn_substeps(C.byref(self.m), self.n, 1, self.root.ctypes.data_as(fp), self.dof.ctypes.data_as(fp),
+                                     tau.ctypes.data_as(fp), self.bm.ctypes.data_as(fp), self.ls.ctypes.data_as(fp),
+                                     self.cd.ctypes.data_as(fp), self.arm.ctypes.data_as(fp), self.fr.ctypes.data_as(fp),
+                                     None, C.c_float(dt), nsub, self.hf.ctypes.data_as(C.POINTER(C.c_int16)), 2, 2,
+                                     C.c_float(0.1), C.c_float(0.005), C.c_float(0.0), 0,
+                                     self.rigid.ctypes.data_as(fp), self.contact.ctypes.data_as(fp))
+        assert rc == 0
+
+    def momentum(self, masses):
+        return (masses[None, :, None] * self.rigid[:, :, 7:10]).sum(1)
+
+
+def test_free_fall_momentum(dyn, model):
+    """Airborne, zero torques: linear momentum changes at exactly M g; joints keep their initial speeds' energy."""
+    m, tab = model
+    s = Sim(dyn, m)
+    s.root[0, 2] = 50.0
+    rng = np.random.default_rng(0)
+    s.dof[0, 0::2] = [0, 0, -0.3, 0.6, -0.3, 0] * 2
+    s.dof[0, 1::2] = rng.normal(0, 1.0, 12)
+    s.root[0, 10:13] = rng.normal(0, 0.5, 3)
+    masses = np.array(tab["mass"], np.float32)
+    s.step(np.zeros(12), nsub=1)
+    p0 = s.momentum(masses)[0].astype(np.float64)
+    s.step(np.zeros(12), nsub=100)
+    p1 = s.momentum(masses)[0].astype(np.float64)
+    expect = p0 + np.array([0, 0, -9.81]) * masses.sum() * 0.1
+    np.testing.assert_allclose(p1, expect, atol=2e-3 * masses.sum())
+
+
+def test_energy_conserved_without_gravity(dyn, model):
+    m, tab = model
+    g0 = m.gravity
+    m.gravity = 0.0
+    try:
+        s = Sim(dyn, m)
+        s.root[0, 2] = 50.0
+        rng = np.random.default_rng(1)
+        s.dof[0, 0::2] = [0, 0, -0.3, 0.6, -0.3, 0] * 2
+        s.dof[0, 1::2] = rng.normal(0, 1.0, 12)
+        s.arm[:] = 0.0
+        masses = np.array(tab["mass"])
+        I_body = [np.array([[a, d, e], [d, b, f], [e, f, c]]) for a, b, c, d, e, f in tab["inertia"]]
+
+        def energy():
+            s.step(np.zeros(12), nsub=0)
+            E = 0.0
+            from oracle.dynamics_ref import quat_to_R
+            for b in range(13):
+                v = s.rigid[0, b, 7:10].astype(float)
+                w = s.rigid[0, b, 10:13].astype(float)
+                R = quat_to_R(s.rigid[0, b, 3:7].astype(float))
+                E += 0.5 * masses[b] * v @ v + 0.5 * w @ (R @ I_body[b] @ R.T) @ w
+            return E
+        e0 = energy()
+        s.step(np.zeros(12), nsub=200)
+        e1 = energy()
+        assert abs(e1 - e0) / e0 < 0.02, (e0, e1)
+    finally:
+        m.gravity = g0
+
+
+def test_stance_supports_weight_and_limits(dyn, model):
+    """Stiff PD stance on the plane: feet carry the weight (Newton), joints stay within limits (+ small
+    compliant overshoot), nothing penetrates more than a few mm."""
+    m, tab = model
+    s = Sim(dyn, m, n=1)
+    q0 = np.array([0, 0, -0.3, 0.6, -0.3, 0] * 2, np.float32)
+    s.root[0, 2] = 0.945
+    s.dof[0, 0::2] = q0
+    kp, kd = 800.0, 40.0
+    for _ in range(300):
+        q, qd = s.dof[0, 0::2], s.dof[0, 1::2]
+        s.step(kp * (q0 - q) - kd * qd, nsub=1)
+    total_mass = np.array(tab["mass"]).sum()
+    fz = s.contact[0, :, 2].sum()
+    assert abs(fz - total_mass * 9.81) < 0.1 * total_mass * 9.81, fz
+    assert s.contact[0, 0].sum() == 0.0
+    lo = np.array([m.q_lower[j] for j in range(12)])
+    hi = np.array([m.q_upper[j] for j in range(12)])
+    assert np.all(s.dof[0, 0::2] > lo - 0.02) and np.all(s.dof[0, 0::2] < hi + 0.02)
+    assert s.rigid[0, 6, 2] > 0.0 and s.rigid[0, 12, 2] > 0.0
+
+
+def test_joint_limit_holds_against_torque(dyn, model):
+    m, tab = model
+    s = Sim(dyn, m)
+    s.root[0, 2] = 50.0
+    s.dof[0, 0::2] = [0, 0, -0.3, 0.6, -0.3, 0] * 2
+    tau = np.zeros(12)
+    tau[3] = -150.0   # drive the left knee below its 0 rad lower limit
+    for _ in range(300):
+        s.step(tau, nsub=1)
+    assert s.dof[0, 6] > -0.02, s.dof[0, 6]
