@@ -17,28 +17,26 @@ template <typename R>
 void load(const DynModel& M, int n, const float* root, const float* dof, const float* body_mass,
           const float* link_scale, const float* com_disp, const float* armature, const float* friction,
           EnvParams<R>& P, EnvState<R>& s) {
-  P.mass[0] = body_mass[n];
-  P.inertia_scale[0] = P.mass[0] / R(M.mass[0]);
-  for (int b = 1; b < NB; ++b) { P.mass[b] = R(M.mass[b]) * link_scale[n * 12 + b - 1]; P.inertia_scale[b] = link_scale[n * 12 + b - 1]; }
-  for (int k = 0; k < 3; ++k) P.com_disp[k] = com_disp[n * 3 + k];
-  for (int j = 0; j < ND; ++j) P.armature[j] = armature[n * 12 + j];
-  P.friction = R(0.5) * (R(friction[n]) + R(M.ground_friction));
+  P.base.mass = body_mass[n];
+  P.base.inertia_scale = P.base.mass / R(M.mass[0]);
+  for (int k = 0; k < 3; ++k) P.base.com_disp[k] = com_disp[n * 3 + k];
+  P.base.friction = R(0.5) * (R(friction[n]) + R(M.ground_friction));
+  for (int j = 0; j < ND; ++j) {
+    LegParams<R>& L = P.leg[j / 6];
+    L.mass[j % 6] = R(M.mass[1 + j]) * link_scale[n * 12 + j];
+    L.inertia_scale[j % 6] = link_scale[n * 12 + j];
+    L.armature[j % 6] = armature[n * 12 + j];
+  }
   const float* r = root + (size_t)n * 13;
   for (int i = 0; i < 3; ++i) s.pos[i] = r[i];
   for (int i = 0; i < 4; ++i) s.quat[i] = r[3 + i];
   M3<R> R0 = quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]);
-  V3<R> c0 = mul(R0, v3<R>(R(M.com[0][0]) + P.com_disp[0], R(M.com[0][1]) + P.com_disp[1], R(M.com[0][2]) + P.com_disp[2]));
+  V3<R> c0 = base_com(M, P.base, R0);
   V3<R> w = v3<R>(r[10], r[11], r[12]);
   V3<R> vo = v3<R>(r[7], r[8], r[9]) - cross(w, c0);
   s.w[0] = w.x; s.w[1] = w.y; s.w[2] = w.z; s.vo[0] = vo.x; s.vo[1] = vo.y; s.vo[2] = vo.z;
   for (int j = 0; j < ND; ++j) { s.q[j] = dof[(size_t)n * 24 + 2 * j]; s.qd[j] = dof[(size_t)n * 24 + 2 * j + 1]; }
 }
-
-struct CpuWriter {
-  float* root; float* rigid; float* contact;
-  template <typename R> void rootw(const R* v) { for (int i = 0; i < 13; ++i) root[i] = (float)v[i]; }
-  template <typename R> void root_(const R* v) { rootw(v); }
-};
 
 template <typename R> struct Writer {
   float* rootp; float* rigidp; float* contactp;
@@ -67,7 +65,7 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
       substep(M, T, P, s, t, ef, R(dt));
     }
     Writer<R> W{root + (size_t)n * 13, rigid ? rigid + (size_t)n * 169 : nullptr, contact ? contact + (size_t)n * 39 : nullptr};
-    report(M, T, P, s, R(dt), W);
+    report(M, T, P, s, W);
     for (int j = 0; j < ND; ++j) { dof[(size_t)n * 24 + 2 * j] = (float)s.q[j]; dof[(size_t)n * 24 + 2 * j + 1] = (float)s.qd[j]; }
   }
   return 0;
@@ -94,10 +92,15 @@ int t1dyn_accel(const t1env_model* model, const double* mass, const double* iner
   if (make_dyn_model(model, &M)) return -1;
   Terrain T{nullptr, 0, 0, 0, 0.1f, 0.005f, 0.0f};
   EnvParams<double> P;
-  for (int b = 0; b < NB; ++b) { P.mass[b] = mass[b]; P.inertia_scale[b] = inertia_scale[b]; }
-  for (int k = 0; k < 3; ++k) P.com_disp[k] = com_disp[k];
-  for (int j = 0; j < ND; ++j) P.armature[j] = armature[j];
-  P.friction = 0.5;
+  P.base.mass = mass[0];
+  P.base.inertia_scale = inertia_scale[0];
+  for (int k = 0; k < 3; ++k) P.base.com_disp[k] = com_disp[k];
+  P.base.friction = 0.5;
+  for (int j = 0; j < ND; ++j) {
+    P.leg[j / 6].mass[j % 6] = mass[1 + j];
+    P.leg[j / 6].inertia_scale[j % 6] = inertia_scale[1 + j];
+    P.leg[j / 6].armature[j % 6] = armature[j];
+  }
   EnvState<double> s;
   for (int i = 0; i < 3; ++i) s.pos[i] = state[i];
   for (int i = 0; i < 4; ++i) s.quat[i] = state[3 + i];

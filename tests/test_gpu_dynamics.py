@@ -1,0 +1,77 @@
+"""k_dynamics (the HIP articulated-body solver + PD loop) against an independent host replica in fp64.
+
+PhysX itself cannot run anywhere here, so the simulator step is checked against the same algorithm run in
+double precision on the host (oracle/cpu_env.py: numpy oracle PD/post-physics + oracle/dyn_cpu.cpp fp64),
+from the same reset (same counter-RNG draws).  Contact dynamics amplify rounding chaotically over a
+trajectory, so the check is on the ONE-STEP error: before every env step the GPU env and a host fp32 replica
+are both set to the fp64 replica's state, all three advance one env step (10 substeps) with the same
+actions, and the GPU's distance from fp64 must stay within a small multiple of the host fp32 build's (plus
+an absolute floor) -- the GPU path adds nothing beyond single-precision rounding.  40 steps cover the drop,
+touchdown and stance phases (feet in contact from about step 17).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.cpu_env import CpuT1Env
+
+pytestmark = pytest.mark.gpu
+
+N, STEPS = 64, 40
+FLOOR = {"pos": 1e-5, "quat": 1e-5, "lin_vel": 1e-3, "ang_vel": 1e-3, "q": 1e-4, "qd": 1e-2}
+
+
+def _terrain_hook(cfg):
+    cfg.terrain.num_rows, cfg.terrain.num_cols, cfg.terrain.border_size = 6, 4, 5
+
+
+def _cpu_env(env, fp64):
+    terrain = None
+    if env.mesh_type in ("heightfield", "trimesh"):
+        tc = env.cfg.terrain
+        terrain = {"terrain_origins": env._terrain.env_origins, "height_samples": env._terrain.heightsamples,
+                   "horizontal_scale": tc.horizontal_scale, "vertical_scale": tc.vertical_scale,
+                   "border_size": tc.border_size, "num_envs_total": env.num_envs}
+    return CpuT1Env(env._model, env.num_envs, seed=5, mesh_type=env.mesh_type, terrain=terrain, fp64=fp64)
+
+
+def _state(root, dof):
+    return {"pos": root[:, :3], "quat": root[:, 3:7], "lin_vel": root[:, 7:10], "ang_vel": root[:, 10:13],
+            "q": dof[..., 0], "qd": dof[..., 1]}
+
+
+@pytest.mark.parametrize("mesh", ["plane", "trimesh"])
+def test_dynamics_one_step_matches_fp64_host(mesh):
+    from ti5_isaacgym_amd import make_t1_env
+    env = make_t1_env(num_envs=N, mesh_type=mesh, seed=5, device="cuda:0",
+                      cfg_hook=_terrain_hook if mesh != "plane" else None)
+    c64, c32 = _cpu_env(env, True), _cpu_env(env, False)
+    env.reset()
+    c64.reset()
+    c32.reset()
+    rng = np.random.default_rng(3)
+    worst = {}
+    contact_steps = 0
+    for t in range(STEPS):
+        a = (0.5 * rng.standard_normal((N, 12))).astype(np.float32)
+        root, dof = c64.o.root.copy(), c64.o.dof.copy()
+        env.root_states.copy_(torch.from_numpy(root))
+        env.dof_state.copy_(torch.from_numpy(dof.reshape(N * 12, 2)))
+        c32.o.root[:] = root
+        c32.o.dof[:] = dof
+        env.step(torch.from_numpy(a).to("cuda:0"))
+        c64.step(a)
+        c32.step(a)
+        same = env.reset_buf.cpu().numpy().astype(bool) == c64.o.reset_buf  # a differing reset is not physics
+        g = _state(env.root_states.cpu().numpy(), env.dof_state.view(N, 12, 2).cpu().numpy())
+        r64, r32 = _state(c64.o.root, c64.o.dof), _state(c32.o.root, c32.o.dof)
+        for k in g:
+            assert np.isfinite(g[k]).all(), f"{k} not finite at step {t}"
+            eg = float(np.abs(g[k] - r64[k])[same].max())
+            e32 = float(np.abs(r32[k] - r64[k])[same].max())
+            worst[k] = (max(worst.get(k, (0, 0))[0], eg), max(worst.get(k, (0, 0))[1], e32))
+            assert eg <= 20 * e32 + FLOOR[k], f"[{mesh} step {t}] {k}: |gpu-fp64| {eg:.3g} vs |cpu32-fp64| {e32:.3g}"
+        feet_f = env.contact_forces.view(N, 13, 3)[:, env.feet_indices].norm(dim=-1).cpu().numpy()
+        contact_steps += int((feet_f > 1).any())
+    assert contact_steps >= 10, "the run never reached stance; the check did not exercise contact"
+    print(mesh, {k: (f"{v[0]:.2e}", f"{v[1]:.2e}") for k, v in worst.items()})

@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libt1env_hip.so")
+LIB_PATH = os.environ.get("T1ENV_LIB") or os.path.join(HERE, "_lib", "libt1env_hip.so")  # override: A/B builds
 
 NB, ND, MAXC, NOBS, NPRIV, HIST, CHIST, NREW = 13, 12, 48, 47, 73, 66, 3, 24
 

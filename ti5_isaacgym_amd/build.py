@@ -14,16 +14,19 @@ DEPS = [os.path.join(HERE, "csrc", f) for f in ("t1env.hip", "t1_dynamics.h", "t
 ARCH = os.environ.get("T1ENV_ARCH", "gfx950")
 
 
-def build(force=False, extra=()):
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS):
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+def build(force=False, extra=(), out=None):
+    out = out or OUT
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in DEPS):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+    # -fno-slp-vectorize: the SLP pass packs scalar pairs of the dynamics into v_pk_* ops, which forces aligned
+    # register pairs and piles up v_mov shuffles; in k_dynamics that alone turned ~40 scratch ops into ~470.
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-o", OUT + ".tmp", SRC, *extra]
+           "-fno-slp-vectorize", "-o", out + ".tmp", SRC, *extra]
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -69,6 +69,29 @@ template <typename R> T1_HD R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b
 template <typename R> T1_HD V3<R> cross(V3<R> a, V3<R> b) {
   return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
+// fast reciprocal / square root: hardware v_rcp_f32 / v_sqrt_f32 (1 ulp) on the device, exact on the host
+T1_HD float rcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
+}
+T1_HD double rcp(double x) { return 1.0 / x; }
+T1_HD float fsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sqrtf(x);
+#else
+  return sqrtf(x);
+#endif
+}
+T1_HD double fsqrt(double x) { return sqrt(x); }
+// sin/cos of a joint angle.  The stock sincosf on purpose: a branch-free inlined Cody-Waite/minimax version
+// (and the hardware v_sin/v_cos) produced wrong dynamics in k_dynamics at -O3 although each was exact in
+// isolation, -O1 and a non-inlined call were correct -- tests/test_gpu_dynamics.py guards this.
+T1_HD void fsincos(float a, float* s, float* c) { sincosf(a, s, c); }
+T1_HD void fsincos(double a, double* s, double* c) { sincos(a, s, c); }
+
 // row-major 3x3
 template <typename R> struct M3 { R m[9]; };
 template <typename R> T1_HD V3<R> mul(const M3<R>& A, V3<R> v) {
@@ -83,10 +106,11 @@ template <typename R> T1_HD M3<R> quat_to_mat(R x, R y, R z, R w) {
   A.m[6] = 2 * (x * z - y * w);     A.m[7] = 2 * (y * z + x * w);     A.m[8] = 1 - 2 * (x * x + y * y);
   return A;
 }
-// A * Rot(axis, angle) for a unit coordinate axis (0=x,1=y,2=z): rotates two columns of A.
-template <typename R> T1_HD M3<R> mul_axis_rot(const M3<R>& A, int axis, R c, R s) {
+// A * Rot(axis, angle) for a unit coordinate axis (0=x,1=y,2=z): rotates two columns of A.  The axis is a
+// template parameter so every register index is static (a runtime column index would go to scratch).
+template <int AX, typename R> T1_HD M3<R> mul_axis_rot_t(const M3<R>& A, R c, R s) {
+  constexpr int i = (AX + 1) % 3, j = (AX + 2) % 3;  // e_i -> c e_i + s e_j ; e_j -> -s e_i + c e_j
   M3<R> B = A;
-  int i = (axis + 1) % 3, j = (axis + 2) % 3;  // Rot about axis: e_i -> c e_i + s e_j ; e_j -> -s e_i + c e_j
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
     R ai = A.m[3 * r + i], aj = A.m[3 * r + j];
@@ -95,21 +119,43 @@ template <typename R> T1_HD M3<R> mul_axis_rot(const M3<R>& A, int axis, R c, R 
   }
   return B;
 }
+template <typename R> T1_HD M3<R> mul_axis_rot(const M3<R>& A, int axis, R c, R s) {
+  // branch-free: with 0/1 weights ex, ey, ez for the axis, columns (i, j) = cyclic successors of the axis:
+  // for x: (y, z); y: (z, x); z: (x, y).  Column blends are exact (weights are 0 or 1).
+  const R ex = axis == 0 ? R(1) : R(0), ey = axis == 1 ? R(1) : R(0), ez = axis == 2 ? R(1) : R(0);
+  M3<R> B;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const R a0 = A.m[3 * r], a1 = A.m[3 * r + 1], a2 = A.m[3 * r + 2];
+    const R ai = ex * a1 + ey * a2 + ez * a0;  // column i
+    const R aj = ex * a2 + ey * a0 + ez * a1;  // column j
+    const R ni = c * ai + s * aj, nj = -s * ai + c * aj;
+    // write back: axis column unchanged, i -> ni, j -> nj
+    B.m[3 * r] = ex * a0 + ey * nj + ez * ni;
+    B.m[3 * r + 1] = ex * ni + ey * a1 + ez * nj;
+    B.m[3 * r + 2] = ex * nj + ey * ni + ez * a2;
+  }
+  return B;
+}
+// column of A selected without a runtime register index
+template <typename R> T1_HD V3<R> col_sel(const M3<R>& A, int c) {
+  return c == 0 ? V3<R>{A.m[0], A.m[3], A.m[6]} : (c == 1 ? V3<R>{A.m[1], A.m[4], A.m[7]} : V3<R>{A.m[2], A.m[5], A.m[8]});
+}
 // rotation matrix -> quaternion (x,y,z,w), Shepperd
 template <typename R> T1_HD void mat_to_quat(const M3<R>& A, R q[4]) {
   R t = A.m[0] + A.m[4] + A.m[8];
   if (t > 0) {
-    R s = sqrt(t + 1) * 2;
-    q[3] = R(0.25) * s; q[0] = (A.m[7] - A.m[5]) / s; q[1] = (A.m[2] - A.m[6]) / s; q[2] = (A.m[3] - A.m[1]) / s;
+    R s = fsqrt(t + 1) * 2, is = rcp(s);
+    q[3] = R(0.25) * s; q[0] = (A.m[7] - A.m[5]) * is; q[1] = (A.m[2] - A.m[6]) * is; q[2] = (A.m[3] - A.m[1]) * is;
   } else if (A.m[0] > A.m[4] && A.m[0] > A.m[8]) {
-    R s = sqrt(1 + A.m[0] - A.m[4] - A.m[8]) * 2;
-    q[3] = (A.m[7] - A.m[5]) / s; q[0] = R(0.25) * s; q[1] = (A.m[1] + A.m[3]) / s; q[2] = (A.m[2] + A.m[6]) / s;
+    R s = fsqrt(1 + A.m[0] - A.m[4] - A.m[8]) * 2, is = rcp(s);
+    q[3] = (A.m[7] - A.m[5]) * is; q[0] = R(0.25) * s; q[1] = (A.m[1] + A.m[3]) * is; q[2] = (A.m[2] + A.m[6]) * is;
   } else if (A.m[4] > A.m[8]) {
-    R s = sqrt(1 + A.m[4] - A.m[0] - A.m[8]) * 2;
-    q[3] = (A.m[2] - A.m[6]) / s; q[0] = (A.m[1] + A.m[3]) / s; q[1] = R(0.25) * s; q[2] = (A.m[5] + A.m[7]) / s;
+    R s = fsqrt(1 + A.m[4] - A.m[0] - A.m[8]) * 2, is = rcp(s);
+    q[3] = (A.m[2] - A.m[6]) * is; q[0] = (A.m[1] + A.m[3]) * is; q[1] = R(0.25) * s; q[2] = (A.m[5] + A.m[7]) * is;
   } else {
-    R s = sqrt(1 + A.m[8] - A.m[0] - A.m[4]) * 2;
-    q[3] = (A.m[3] - A.m[1]) / s; q[0] = (A.m[2] + A.m[6]) / s; q[1] = (A.m[5] + A.m[7]) / s; q[2] = R(0.25) * s;
+    R s = fsqrt(1 + A.m[8] - A.m[0] - A.m[4]) * 2, is = rcp(s);
+    q[3] = (A.m[3] - A.m[1]) * is; q[0] = (A.m[2] + A.m[6]) * is; q[1] = (A.m[5] + A.m[7]) * is; q[2] = R(0.25) * s;
   }
   if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
 }

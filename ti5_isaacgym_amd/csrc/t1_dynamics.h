@@ -18,6 +18,10 @@
 //     factorisation per substep solves everything (no contact iterations).
 //   * tree-sparse LTDL (Featherstone RBDA §6.5) over DOF order [base 0..5 | left leg | right leg]: each leg
 //     is eliminated into the 6x6 base block, the base block is factored densely, legs back-substitute.
+//     The leg work is written per leg (leg_assemble / eliminate_leg / backsub_leg) and the base block is the
+//     sum  base + contribution(left) + contribution(right)  in that order, so the GPU can run the two legs of
+//     an env on two waves that exchange a 27-float contribution, and the host build runs them in a loop --
+//     same arithmetic either way.
 //   * semi-implicit Euler; joint speeds clamped to the URDF velocity limits like PhysX max joint velocity.
 #pragma once
 #include "t1_common.h"
@@ -51,12 +55,16 @@ struct Terrain {
   float hscale, vscale, border;
 };
 
+template <typename R> struct BaseParams {
+  R mass, inertia_scale, com_disp[3];
+  R friction;  // combined shape/ground friction coefficient
+};
+template <typename R> struct LegParams {
+  R mass[NLEG], inertia_scale[NLEG], armature[NLEG];
+};
 template <typename R> struct EnvParams {
-  R mass[NB];
-  R inertia_scale[NB];
-  R com_disp[3];
-  R armature[ND];
-  R friction;
+  BaseParams<R> base;
+  LegParams<R> leg[2];
 };
 
 template <typename R> struct BodyState {  // per-body kinematics of one substep (world axes, about O)
@@ -133,38 +141,42 @@ template <typename R> T1_HD R dot6(const R a[6], const R b[6]) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// terrain query: height + unit normal at world (x, y)
+// terrain query: height + unit normal at world (x, y).  HF=false: the plane z=0.
 // ---------------------------------------------------------------------------------------------------
-template <typename R> T1_HD R terrain_height(const Terrain& T, R x, R y, V3<R>& n) {
-  if (T.type == 0) { n = v3<R>(0, 0, 1); return R(0); }
-  R fx = (x + R(T.border)) / R(T.hscale), fy = (y + R(T.border)) / R(T.hscale);
-  R ix = floor(fx), iy = floor(fy);
-  int i = (int)ix, j = (int)iy;
-  R u = fx - ix, v = fy - iy;
-  if (i < 0) { i = 0; u = 0; }
-  if (j < 0) { j = 0; v = 0; }
-  if (i > T.rows - 2) { i = T.rows - 2; u = 1; }
-  if (j > T.cols - 2) { j = T.cols - 2; v = 1; }
-  const int16_t* r0 = T.h + (size_t)i * T.cols + j;
-  R vs = R(T.vscale);
-  R h00 = vs * r0[0], h01 = vs * r0[1], h10 = vs * r0[T.cols], h11 = vs * r0[T.cols + 1];
-  R dhdu, dhdv, h;
-  if (u >= v) {  // triangle (i,j)-(i+1,j)-(i+1,j+1)
-    dhdu = h10 - h00; dhdv = h11 - h10; h = h00 + u * dhdu + v * dhdv;
-  } else {       // triangle (i,j)-(i+1,j+1)-(i,j+1)
-    dhdv = h01 - h00; dhdu = h11 - h01; h = h00 + v * dhdv + u * dhdu;
+template <bool HF, typename R> T1_HD R terrain_height(const Terrain& T, R x, R y, V3<R>& n) {
+  if constexpr (!HF) {
+    n = v3<R>(0, 0, 1);
+    return R(0);
+  } else {
+    const R ih = rcp(R(T.hscale));
+    R fx = (x + R(T.border)) * ih, fy = (y + R(T.border)) * ih;
+    R ix = floor(fx), iy = floor(fy);
+    int i = (int)ix, j = (int)iy;
+    R u = fx - ix, v = fy - iy;
+    if (i < 0) { i = 0; u = 0; }
+    if (j < 0) { j = 0; v = 0; }
+    if (i > T.rows - 2) { i = T.rows - 2; u = 1; }
+    if (j > T.cols - 2) { j = T.cols - 2; v = 1; }
+    const int16_t* r0 = T.h + (i * T.cols + j);
+    R vs = R(T.vscale);
+    R h00 = vs * r0[0], h01 = vs * r0[1], h10 = vs * r0[T.cols], h11 = vs * r0[T.cols + 1];
+    // triangle (i,j)-(i+1,j)-(i+1,j+1) if u >= v else (i,j)-(i+1,j+1)-(i,j+1)
+    const bool lo = u >= v;
+    R dhdu = lo ? h10 - h00 : h11 - h01;
+    R dhdv = lo ? h11 - h10 : h01 - h00;
+    R h = h00 + u * dhdu + v * dhdv;
+    R gx = dhdu * ih, gy = dhdv * ih;
+    R inv = rcp(fsqrt(R(1) + gx * gx + gy * gy));
+    n = v3<R>(-gx * inv, -gy * inv, inv);
+    return h;
   }
-  R gx = dhdu / R(T.hscale), gy = dhdv / R(T.hscale);
-  R inv = R(1) / sqrt(R(1) + gx * gx + gy * gy);
-  n = v3<R>(-gx * inv, -gy * inv, inv);
-  return h;
 }
 
 // ---------------------------------------------------------------------------------------------------
-// kinematics of one leg (bodies b0+1 .. b0+6), world axes about O
+// kinematics of one leg (bodies 1+6*leg .. 6+6*leg), world axes about O
 // ---------------------------------------------------------------------------------------------------
 template <typename R>
-T1_HD void leg_fk(const DynModel& M, int leg, const M3<R>& Rbase, const R q[ND], BodyState<R> B[NLEG]) {
+T1_HD void leg_fk(const DynModel& M, int leg, const M3<R>& Rbase, const R q[NLEG], BodyState<R> B[NLEG]) {
   M3<R> Rp = Rbase;
   V3<R> pp = v3<R>(0, 0, 0);
 #pragma unroll
@@ -172,8 +184,8 @@ T1_HD void leg_fk(const DynModel& M, int leg, const M3<R>& Rbase, const R q[ND],
     const int b = 1 + 6 * leg + k;
     V3<R> off = v3<R>(M.joint_offset[b][0], M.joint_offset[b][1], M.joint_offset[b][2]);
     V3<R> p = pp + mul(Rp, off);
-    R ang = R(M.axis_sign[b]) * q[6 * leg + k];
-    R s = sin(ang), c = cos(ang);
+    R s, c;
+    fsincos(R(M.axis_sign[b]) * q[k], &s, &c);
     M3<R> Rb = mul_axis_rot(Rp, M.axis_idx[b], c, s);
     B[k].Rot = Rb;
     B[k].p = p;
@@ -183,7 +195,10 @@ T1_HD void leg_fk(const DynModel& M, int leg, const M3<R>& Rbase, const R q[ND],
 }
 
 template <typename R> T1_HD void motion_subspace(const DynModel& M, int b, const BodyState<R>& B, R S[6]) {
-  V3<R> a = R(M.axis_sign[b]) * col(B.Rot, M.axis_idx[b]);
+  // a = Rot * (sign e_axis); the 0/+-1 weights are exact, and no register array is indexed at run time
+  const int ax = M.axis_idx[b];
+  const R sg = R(M.axis_sign[b]);
+  V3<R> a = mul(B.Rot, v3<R>(ax == 0 ? sg : R(0), ax == 1 ? sg : R(0), ax == 2 ? sg : R(0)));
   V3<R> l = cross(B.p, a);
   S[0] = a.x; S[1] = a.y; S[2] = a.z; S[3] = l.x; S[4] = l.y; S[5] = l.z;
 }
@@ -211,90 +226,119 @@ T1_HD void world_inertia(const DynModel& M, int b, const M3<R>& Rb, R scale, R o
 }
 
 // ---------------------------------------------------------------------------------------------------
-// contact of one body against the terrain: accumulates dt * J^T C J (6x6, about O) and the impulse wrench.
-// Per point: normal spring k*pen (+ implicit damping when approaching), regularised Coulomb friction as an
-// implicit tangential damper whose coefficient keeps |F_t| <= mu F_n (Stribeck speed friction_vs).
+// contact of one body's points [c_begin, c_end) against the terrain: accumulates dt * J^T C J (6x6, about
+// O) into A and subtracts the impulse wrench from g.  Per point: normal spring k*pen (+ implicit damping
+// when approaching), regularised Coulomb friction as an implicit tangential damper whose coefficient keeps
+// |F_t| <= mu F_n (Stribeck speed friction_vs).
 // ---------------------------------------------------------------------------------------------------
-template <typename R>
-T1_HD void body_contact(const DynModel& M, const Terrain& T, int b, const M3<R>& Rb, V3<R> pb, V3<R> base_abs,
-                        const R Vb[6], R mu, R dt, Sym6<R>& K, R w[6], bool& any) {
-  const int c0 = M.contact_start[b], nc = M.contact_count[b];
-  const R k = R(M.k_contact), d = R(M.d_contact);
-  for (int c = c0; c < c0 + nc; ++c) {
+template <bool HF, typename R>
+T1_HD void body_contact_t(const DynModel& M, const Terrain& T, int c_begin, int c_end, const M3<R>& Rb, V3<R> pb,
+                          V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
+  const R k = R(M.k_contact), d = R(M.d_contact), ivs = rcp(R(M.friction_vs));
+  for (int c = c_begin; c < c_end; ++c) {
     V3<R> r = v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]);
     V3<R> x = pb + mul(Rb, r);  // rel O
     V3<R> X = x + base_abs;
     V3<R> n;
-    R h = terrain_height(T, X.x, X.y, n);
+    R h = terrain_height<HF>(T, X.x, X.y, n);
     R pen = (h - X.z) * n.z;
     if (pen > R(0)) {
-      any = true;
       V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
       V3<R> vp = vo + cross(om, x);
       R vn = dot(n, vp);
       V3<R> vt = vp - vn * n;
-      R vtn = sqrt(dot(vt, vt));
+      R vtn = fsqrt(dot(vt, vt));
       R cn = vn < R(0) ? dt * k + d : R(0);
       R fn_est = k * pen + (vn < R(0) ? -d * vn : R(0));
-      R ct = mu * fn_est / (vtn > R(M.friction_vs) ? vtn : R(M.friction_vs));
+      R ct = mu * fn_est * (vtn > R(M.friction_vs) ? rcp(vtn) : ivs);
       // force at the current velocity (explicit part) f = k pen n - C vp, C = cn nn^T + ct (I - nn^T)
       V3<R> f = (k * pen - cn * vn) * n - ct * vt;
       V3<R> tq = cross(x, f);
-      w[0] += dt * tq.x; w[1] += dt * tq.y; w[2] += dt * tq.z;
-      w[3] += dt * f.x;  w[4] += dt * f.y;  w[5] += dt * f.z;
+      g[0] -= dt * tq.x; g[1] -= dt * tq.y; g[2] -= dt * tq.z;
+      g[3] -= dt * f.x;  g[4] -= dt * f.y;  g[5] -= dt * f.z;
       // C = ct I + (cn - ct) n n^T ; J^T C J = ct * sum_e w_e w_e^T + (cn - ct) w_n w_n^T, e over world axes
       V3<R> xn = cross(x, n);
       R wn[6] = {xn.x, xn.y, xn.z, n.x, n.y, n.z};
-      sym_rank1(K, dt * (cn - ct), wn);
+      sym_rank1(A, dt * (cn - ct), wn);
       R ex[6] = {R(0), x.z, -x.y, R(1), R(0), R(0)};   // [x cross e_x ; e_x]
       R ey[6] = {-x.z, R(0), x.x, R(0), R(1), R(0)};
       R ez[6] = {x.y, -x.x, R(0), R(0), R(0), R(1)};
-      sym_rank1(K, dt * ct, ex);
-      sym_rank1(K, dt * ct, ey);
-      sym_rank1(K, dt * ct, ez);
+      sym_rank1(A, dt * ct, ex);
+      sym_rank1(A, dt * ct, ey);
+      sym_rank1(A, dt * ct, ez);
     }
   }
 }
+template <typename R>
+T1_HD void body_contact(const DynModel& M, const Terrain& T, int c_begin, int c_end, const M3<R>& Rb, V3<R> pb,
+                        V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
+  if (T.type == 0) body_contact_t<false>(M, T, c_begin, c_end, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  else body_contact_t<true>(M, T, c_begin, c_end, Rb, pb, base_abs, Vb, mu, dt, A, g);
+}
 
 // contact force (world) a body receives at velocity Vb (used for the net-contact-force report)
-template <typename R>
-T1_HD V3<R> body_contact_force(const DynModel& M, const Terrain& T, int b, const M3<R>& Rb, V3<R> pb,
-                               V3<R> base_abs, const R Vb[6], R mu, R dt) {
+template <bool HF, typename R>
+T1_HD V3<R> body_contact_force_t(const DynModel& M, const Terrain& T, int b, const M3<R>& Rb, V3<R> pb,
+                                 V3<R> base_abs, const R Vb[6], R mu) {
   const int c0 = M.contact_start[b], nc = M.contact_count[b];
-  const R k = R(M.k_contact), d = R(M.d_contact);
+  const R k = R(M.k_contact), d = R(M.d_contact), ivs = rcp(R(M.friction_vs));
   V3<R> F = v3<R>(0, 0, 0);
   for (int c = c0; c < c0 + nc; ++c) {
     V3<R> r = v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]);
     V3<R> x = pb + mul(Rb, r);
     V3<R> X = x + base_abs;
     V3<R> n;
-    R h = terrain_height(T, X.x, X.y, n);
+    R h = terrain_height<HF>(T, X.x, X.y, n);
     R pen = (h - X.z) * n.z;
     if (pen > R(0)) {
       V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
       V3<R> vp = vo + cross(om, x);
       R vn = dot(n, vp);
       V3<R> vt = vp - vn * n;
-      R vtn = sqrt(dot(vt, vt));
+      R vtn = fsqrt(dot(vt, vt));
       R fn = k * pen - (vn < R(0) ? d * vn : R(0));
       fn = fn > R(0) ? fn : R(0);
-      R ct = mu * fn / (vtn > R(M.friction_vs) ? vtn : R(M.friction_vs));
+      R ct = mu * fn * (vtn > R(M.friction_vs) ? rcp(vtn) : ivs);
       F = F + fn * n - ct * vt;
     }
   }
   return F;
 }
+template <typename R>
+T1_HD V3<R> body_contact_force(const DynModel& M, const Terrain& T, int b, const M3<R>& Rb, V3<R> pb,
+                               V3<R> base_abs, const R Vb[6], R mu) {
+  return T.type == 0 ? body_contact_force_t<false>(M, T, b, Rb, pb, base_abs, Vb, mu)
+                     : body_contact_force_t<true>(M, T, b, Rb, pb, base_abs, Vb, mu);
+}
 
 // ---------------------------------------------------------------------------------------------------
 // Per-env state kept in registers across the decimation loop
 // ---------------------------------------------------------------------------------------------------
-template <typename R> struct EnvState {
+template <typename R> struct BaseState {
   R pos[3];   // base origin, world (absolute)
   R quat[4];  // xyzw
   R w[3];     // base angular velocity, world
   R vo[3];    // base origin velocity, world
+};
+template <typename R> struct EnvState : BaseState<R> {
   R q[ND], qd[ND];
 };
+
+// base quantities of one substep shared by both legs
+template <typename R> struct BaseFrame {
+  M3<R> R0;
+  V3<R> abs;  // O in world coordinates
+  R V0[6];    // base spatial velocity about O
+};
+template <typename R> T1_HD void base_frame(const BaseState<R>& s, BaseFrame<R>& F) {
+  F.R0 = quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]);
+  F.abs = v3<R>(s.pos[0], s.pos[1], s.pos[2]);
+  F.V0[0] = s.w[0]; F.V0[1] = s.w[1]; F.V0[2] = s.w[2];
+  F.V0[3] = s.vo[0]; F.V0[4] = s.vo[1]; F.V0[5] = s.vo[2];
+}
+template <typename R> T1_HD V3<R> base_com(const DynModel& M, const BaseParams<R>& P, const M3<R>& R0) {
+  return mul(R0, v3<R>(R(M.com[0][0]) + P.com_disp[0], R(M.com[0][1]) + P.com_disp[1], R(M.com[0][2]) + P.com_disp[2]));
+}
 
 // Leg block of the augmented system after assembly / elimination.
 template <typename R> struct LegBlock {
@@ -304,76 +348,121 @@ template <typename R> struct LegBlock {
 };
 
 // ---------------------------------------------------------------------------------------------------
-// assemble one leg: forward kinematics/velocity/bias, per-body inertia (+contact), backward composite
-// pass producing A(leg,leg), A(base,leg), rhs(leg) and the leg's contribution to the base composite.
+// base block: the base body's spatial inertia about O, its RNEA bias (gravity as the fictitious base
+// acceleration -g) and the external force at the base COM (apply_rigid_body_force_tensors ENV_SPACE).
 // ---------------------------------------------------------------------------------------------------
 template <typename R>
-T1_HD void assemble_leg(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s, int leg,
-                        const M3<R>& Rbase, V3<R> base_abs, const R V0[6], const R A0[6], const R tau[ND], R dt,
-                        LegBlock<R>& out, Sym6<R>& Ac_up, R gc_up[6], bool& any_contact) {
-  BodyState<R> B[NLEG];
-  leg_fk(M, leg, Rbase, s.q, B);
-  R S[NLEG][6], g[NLEG][6];
-  Sym6<R> Abody[NLEG];
-  R V[6], A[6];
+T1_HD void base_block(const DynModel& M, const BaseParams<R>& P, const BaseFrame<R>& F, V3<R> ext_f, R dt,
+                      Sym6<R>& Ac, R gc[6]) {
+  const R A0[6] = {R(0), R(0), R(0), R(0), R(0), R(M.gravity)};
+  R Icw[6];
+  world_inertia(M, 0, F.R0, P.inertia_scale, Icw);
+  V3<R> c0 = base_com(M, P, F.R0);
+  inertia_spatial(Ac, P.mass, c0, Icw);
+  R IA[6], IV[6], vf[6];
+  sym_mul(Ac, A0, IA);
+  sym_mul(Ac, F.V0, IV);
+  crf(F.V0, IV, vf);
+  V3<R> tq = cross(c0, ext_f);
+  R fe[6] = {tq.x, tq.y, tq.z, ext_f.x, ext_f.y, ext_f.z};
 #pragma unroll
-  for (int i = 0; i < 6; ++i) { V[i] = V0[i]; A[i] = A0[i]; }
+  for (int i = 0; i < 6; ++i) gc[i] = dt * (IA[i] + vf[i] - fe[i]);
+}
+
+// base-body contact points handled together with leg `leg` (the base's points are split between the legs so
+// that the two-wave GPU kernel does each point once)
+T1_HD void base_contact_range(const DynModel& M, int leg, int& c_begin, int& c_end) {
+  const int c0 = M.contact_start[0], nc = M.contact_count[0];
+  c_begin = c0 + (nc * leg) / 2;
+  c_end = c0 + (nc * (leg + 1)) / 2;
+}
+
+// spatial inertia about O (world axes) of leg body b at pose (Rk, pk)
+template <typename R>
+T1_HD void body_inertia(const DynModel& M, int b, R mass, R iscale, const M3<R>& Rk, V3<R> pk, Sym6<R>& I) {
+  R Icw[6];
+  world_inertia(M, b, Rk, iscale, Icw);
+  V3<R> c = pk + mul(Rk, v3<R>(M.com[b][0], M.com[b][1], M.com[b][2]));
+  inertia_spatial(I, mass, c, Icw);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// assemble one leg.  Forward pass (root to leaf): poses, velocities, velocity-product accelerations and the
+// RNEA bias g_k = dt (I_k a_k + v_k x* I_k v_k).  Backward pass (leaf to root): each body's pose and velocity
+// are rebuilt from its child (R_k = R_{k+1} Rot_{k+1}^T, p_k = p_{k+1} - R_k off_{k+1},
+// v_k = v_{k+1} - S_{k+1} qd_{k+1}), its inertia and contact stiffness join the composite, and column k of
+// the leg block is formed; the off-diagonal H(k, j>k) = S_k . (Ic_j S_j) reuses the stored coupling
+// columns.  Only g_k, the joint sin/cos and the leaf pose/velocity cross between the passes (66 floats),
+// which is what keeps a leg inside the register file.  Ac_up / gc_up accumulate the leg composite.
+// ---------------------------------------------------------------------------------------------------
+template <typename R>
+T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>& P, R mu, const BaseFrame<R>& F,
+                        const R q[NLEG], const R qd[NLEG], const R tau[NLEG], int leg, R dt, LegBlock<R>& out,
+                        Sym6<R>& Ac_up, R gc_up[6]) {
+  R sn[NLEG], cs[NLEG], g[NLEG][6];
+  M3<R> Rk = F.R0;
+  V3<R> pk = v3<R>(0, 0, 0);
+  R V[6], A[6], Sk[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { V[i] = F.V0[i]; A[i] = R(0); }
+  A[5] = R(M.gravity);
 #pragma unroll
   for (int k = 0; k < NLEG; ++k) {
-    const int b = 1 + 6 * leg + k, j = 6 * leg + k;
-    motion_subspace(M, b, B[k], S[k]);
+    const int b = 1 + 6 * leg + k;
+    pk = pk + mul(Rk, v3<R>(M.joint_offset[b][0], M.joint_offset[b][1], M.joint_offset[b][2]));
+    fsincos(R(M.axis_sign[b]) * q[k], &sn[k], &cs[k]);
+    Rk = mul_axis_rot(Rk, M.axis_idx[b], cs[k], sn[k]);
+    BodyState<R> Bk{Rk, pk};
+    motion_subspace(M, b, Bk, Sk);
     R vj[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) vj[i] = S[k][i] * s.qd[j];
+    for (int i = 0; i < 6; ++i) vj[i] = Sk[i] * qd[k];
 #pragma unroll
     for (int i = 0; i < 6; ++i) V[i] += vj[i];
     R cr[6];
-    crm(V, vj, cr);  // V_i x (S qd)
+    crm(V, vj, cr);  // V_k x (S qd)
 #pragma unroll
     for (int i = 0; i < 6; ++i) A[i] += cr[i];
-    // inertia about O
-    R Icw[6];
-    world_inertia(M, b, B[k].Rot, P.inertia_scale[b], Icw);
-    V3<R> c = B[k].p + mul(B[k].Rot, v3<R>(M.com[b][0], M.com[b][1], M.com[b][2]));
-    inertia_spatial(Abody[k], P.mass[b], c, Icw);
-    // RNEA body force f = I a + V x* (I V)
+    Sym6<R> I;
+    body_inertia(M, b, P.mass[k], P.inertia_scale[k], Rk, pk, I);
     R IA[6], IV[6], vf[6];
-    sym_mul(Abody[k], A, IA);
-    sym_mul(Abody[k], V, IV);
+    sym_mul(I, A, IA);
+    sym_mul(I, V, IV);
     crf(V, IV, vf);
 #pragma unroll
     for (int i = 0; i < 6; ++i) g[k][i] = dt * (IA[i] + vf[i]);
-    if (M.contact_count[b] > 0) {
-      R w[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
-      Sym6<R> K;
-      sym_zero(K);
-      bool any = false;
-      body_contact(M, T, b, B[k].Rot, B[k].p, base_abs, V, P.friction, dt, K, w, any);
-      if (any) {
-        any_contact = true;
-        sym_add(Abody[k], K);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) g[k][i] -= w[i];
-      }
-    }
   }
-  // backward: composites from the leaf up
   Sym6<R> Ac;
   sym_zero(Ac);
   R gc[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
 #pragma unroll
   for (int k = NLEG - 1; k >= 0; --k) {
-    const int j = 6 * leg + k;
-    sym_add(Ac, Abody[k]);
+    const int b = 1 + 6 * leg + k, j = 6 * leg + k;
+    if (k < NLEG - 1) {  // step up from child k+1 (Sk still holds S_{k+1})
+      const int bc = b + 1;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) V[i] -= Sk[i] * qd[k + 1];
+      Rk = mul_axis_rot(Rk, M.axis_idx[bc], cs[k + 1], -sn[k + 1]);
+      pk = pk - mul(Rk, v3<R>(M.joint_offset[bc][0], M.joint_offset[bc][1], M.joint_offset[bc][2]));
+    }
+    BodyState<R> Bk{Rk, pk};
+    motion_subspace(M, b, Bk, Sk);
+    {
+      Sym6<R> I;
+      body_inertia(M, b, P.mass[k], P.inertia_scale[k], Rk, pk, I);
+      sym_add(Ac, I);
+    }
+    const int c0 = M.contact_start[b], nc = M.contact_count[b];
+    if (nc > 0) body_contact(M, T, c0, c0 + nc, Rk, pk, F.abs, V, mu, dt, Ac, gc);
 #pragma unroll
     for (int i = 0; i < 6; ++i) gc[i] += g[k][i];
-    R F[6];
-    sym_mul(Ac, S[k], F);
+    R Fk[6];
+    sym_mul(Ac, Sk, Fk);
     // diagonal (+ armature + soft joint limit)
-    R Ajj = dot6(S[k], F) + P.armature[j];
-    R rj = dt * tau[j] - dot6(S[k], gc);
+    R Ajj = dot6(Sk, Fk) + P.armature[k];
+    R rj = dt * tau[k] - dot6(Sk, gc);
     R lo = R(M.q_lower[j]), hi = R(M.q_upper[j]);
-    R qj = s.q[j], qdj = s.qd[j];
+    R qj = q[k], qdj = qd[k];
     if (qj < lo) {
       R cl = qdj < R(0) ? dt * R(M.k_limit) + R(M.d_limit) : R(0);
       Ajj += dt * cl;
@@ -386,9 +475,12 @@ T1_HD void assemble_leg(const DynModel& M, const Terrain& T, const EnvParams<R>&
     out.L[sidx(k, k)] = Ajj;
     out.rhs[k] = rj;
 #pragma unroll
-    for (int i = 0; i < k; ++i) out.L[sidx(i, k)] = dot6(S[i], F);
+    for (int jj = k + 1; jj < NLEG; ++jj) {
+      R Fj[6] = {out.Bl[0][jj], out.Bl[1][jj], out.Bl[2][jj], out.Bl[3][jj], out.Bl[4][jj], out.Bl[5][jj]};
+      out.L[sidx(k, jj)] = dot6(Sk, Fj);
+    }
 #pragma unroll
-    for (int r = 0; r < 6; ++r) out.Bl[r][k] = F[r];
+    for (int r = 0; r < 6; ++r) out.Bl[r][k] = Fk[r];
   }
   sym_add(Ac_up, Ac);
 #pragma unroll
@@ -396,13 +488,13 @@ T1_HD void assemble_leg(const DynModel& M, const Terrain& T, const EnvParams<R>&
 }
 
 // Eliminate a leg's 6 DOF (leaf first) into the base block: Featherstone LTDL restricted to the path
-// [base 0..5, leg 0..5].  On return out.L/Bl hold the unit factor L (off-diagonal) and D (diagonal), Abb and
-// rhs_b hold the Schur-complement updates, and out.rhs holds the forward-substituted leg rhs.
+// [base 0..5, leg 0..5].  On return out.L/Bl hold the unit factor L (off-diagonal), L's diagonal holds
+// 1/D, Abb and rhs_b hold the Schur-complement updates, and out.rhs the forward-substituted leg rhs.
+// The Schur updates do not depend on Abb's value, so a leg can be eliminated into its own contribution.
 template <typename R> T1_HD void eliminate_leg(LegBlock<R>& lb, Sym6<R>& Abb, R rhs_b[6]) {
 #pragma unroll
   for (int k = NLEG - 1; k >= 0; --k) {
-    const R Dk = lb.L[sidx(k, k)];
-    const R inv = R(1) / Dk;
+    const R inv = rcp(lb.L[sidx(k, k)]);
     // ancestors of leg dof k: leg dofs i < k, then base dofs 5..0
     R a_leg[NLEG], a_base[6];
 #pragma unroll
@@ -428,6 +520,7 @@ template <typename R> T1_HD void eliminate_leg(LegBlock<R>& lb, Sym6<R>& Abb, R 
 #pragma unroll
     for (int r = 0; r < 6; ++r) rhs_b[r] -= a_base[r] * bk;
     // store the factor
+    lb.L[sidx(k, k)] = inv;
 #pragma unroll
     for (int i = 0; i < k; ++i) lb.L[sidx(i, k)] = a_leg[i];
 #pragma unroll
@@ -437,9 +530,11 @@ template <typename R> T1_HD void eliminate_leg(LegBlock<R>& lb, Sym6<R>& Abb, R 
 
 // dense LDL^T of the 6x6 base block with the same (leaf-first) convention and solve in place.
 template <typename R> T1_HD void solve_base(Sym6<R>& A, R b[6]) {
+  R invd[6];
 #pragma unroll
   for (int k = 5; k >= 0; --k) {
-    const R inv = R(1) / A.a[sidx(k, k)];
+    const R inv = rcp(A.a[sidx(k, k)]);
+    invd[k] = inv;
     R a[6];
 #pragma unroll
     for (int i = 0; i < k; ++i) a[i] = A.a[sidx(i, k)] * inv;
@@ -451,7 +546,7 @@ template <typename R> T1_HD void solve_base(Sym6<R>& A, R b[6]) {
     for (int i = 0; i < k; ++i) { b[i] -= a[i] * b[k]; A.a[sidx(i, k)] = a[i]; }
   }
 #pragma unroll
-  for (int k = 0; k < 6; ++k) b[k] /= A.a[sidx(k, k)];
+  for (int k = 0; k < 6; ++k) b[k] *= invd[k];
 #pragma unroll
   for (int k = 0; k < 6; ++k)
 #pragma unroll
@@ -462,7 +557,7 @@ template <typename R> T1_HD void solve_base(Sym6<R>& A, R b[6]) {
 template <typename R> T1_HD void backsub_leg(const LegBlock<R>& lb, const R xb[6], R x[NLEG]) {
 #pragma unroll
   for (int k = 0; k < NLEG; ++k) {
-    R v = lb.rhs[k] / lb.L[sidx(k, k)];
+    R v = lb.rhs[k] * lb.L[sidx(k, k)];
 #pragma unroll
     for (int r = 0; r < 6; ++r) v -= lb.Bl[r][k] * xb[r];
 #pragma unroll
@@ -471,78 +566,35 @@ template <typename R> T1_HD void backsub_leg(const LegBlock<R>& lb, const R xb[6
   }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// Assemble and solve one substep: delta = change of u = [omega, v_O (spatial, about the fixed point O),
-// qd] over dt, including implicit contact / joint-limit terms.  tau: joint torques; ext_f: world force at
-// the base COM (apply_rigid_body_force_tensors ENV_SPACE semantics).
-// ---------------------------------------------------------------------------------------------------
+// One leg's contribution to the base block: base-contact share + leg composite - Schur complement.
+// Returns the factored leg block (for backsub_leg) and (Ab, rb) to be summed into the base system.
 template <typename R>
-T1_HD void compute_delta(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s,
-                         const R tau[ND], V3<R> ext_f, R dt, R delta[6 + ND]) {
-  M3<R> R0 = quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]);
-  V3<R> base_abs = v3<R>(s.pos[0], s.pos[1], s.pos[2]);
-  R V0[6] = {s.w[0], s.w[1], s.w[2], s.vo[0], s.vo[1], s.vo[2]};
-  R A0[6] = {R(0), R(0), R(0), R(0), R(0), R(M.gravity)};  // fictitious base acceleration -g
-  Sym6<R> Ac;
-  R Icw[6];
-  world_inertia(M, 0, R0, P.inertia_scale[0], Icw);
-  V3<R> c0 = mul(R0, v3<R>(R(M.com[0][0]) + P.com_disp[0], R(M.com[0][1]) + P.com_disp[1],
-                           R(M.com[0][2]) + P.com_disp[2]));
-  inertia_spatial(Ac, P.mass[0], c0, Icw);
-  R gc[6];
-  {
-    R IA[6], IV[6], vf[6];
-    sym_mul(Ac, A0, IA);
-    sym_mul(Ac, V0, IV);
-    crf(V0, IV, vf);
-    V3<R> tq = cross(c0, ext_f);
-    R fe[6] = {tq.x, tq.y, tq.z, ext_f.x, ext_f.y, ext_f.z};
+T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParams<R>& PB, const LegParams<R>& PL,
+                            const BaseFrame<R>& F,
+                            const R q[NLEG], const R qd[NLEG], const R tau[NLEG], int leg, R dt,
+                            LegBlock<R>& lb, Sym6<R>& Ab, R rb[6]) {
+  sym_zero(Ab);
+  R g[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+  leg_assemble(M, T, PL, PB.friction, F, q, qd, tau, leg, dt, lb, Ab, g);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) gc[i] = dt * (IA[i] + vf[i] - fe[i]);
+  for (int i = 0; i < 6; ++i) rb[i] = -g[i];
+  eliminate_leg(lb, Ab, rb);
+  int cb, ce;
+  base_contact_range(M, leg, cb, ce);
+  if (ce > cb) {
+    R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+    body_contact(M, T, cb, ce, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rb[i] -= gw[i];
   }
-  bool any = false;
-  if (M.contact_count[0] > 0) {
-    R w[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
-    Sym6<R> K;
-    sym_zero(K);
-    bool a = false;
-    body_contact(M, T, 0, R0, v3<R>(0, 0, 0), base_abs, V0, P.friction, dt, K, w, a);
-    if (a) {
-      sym_add(Ac, K);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) gc[i] -= w[i];
-    }
-  }
-  LegBlock<R> lb[2];
-#pragma unroll
-  for (int leg = 0; leg < 2; ++leg) assemble_leg(M, T, P, s, leg, R0, base_abs, V0, A0, tau, dt, lb[leg], Ac, gc, any);
-  R rb[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) rb[i] = -gc[i];
-#pragma unroll
-  for (int leg = 0; leg < 2; ++leg) eliminate_leg(lb[leg], Ac, rb);
-  solve_base(Ac, rb);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) delta[i] = rb[i];
-#pragma unroll
-  for (int leg = 0; leg < 2; ++leg) backsub_leg(lb[leg], rb, delta + 6 + 6 * leg);
 }
 
-// Semi-implicit Euler with the solved velocity change (+ the omega x v term that turns the spatial base
-// acceleration into the classical acceleration of the base origin); joint speeds clamped like PhysX.
-template <typename R>
-T1_HD void integrate(const DynModel& M, EnvState<R>& s, const R delta[6 + ND], R dt) {
+// Semi-implicit Euler of the base with the solved velocity change (+ the omega x v term that turns the
+// spatial base acceleration into the classical acceleration of the base origin).
+template <typename R> T1_HD void integrate_base(BaseState<R>& s, const R delta[6], R dt) {
   V3<R> w_new = v3<R>(s.w[0] + delta[0], s.w[1] + delta[1], s.w[2] + delta[2]);
   V3<R> vO_new = v3<R>(s.vo[0] + delta[3], s.vo[1] + delta[4], s.vo[2] + delta[5]);
   V3<R> vb_new = vO_new + dt * cross(w_new, vO_new);
-#pragma unroll
-  for (int j = 0; j < ND; ++j) {
-    R v = s.qd[j] + delta[6 + j];
-    R vl = R(M.vel_limit[j]);
-    v = v > vl ? vl : (v < -vl ? -vl : v);
-    s.qd[j] = v;
-    s.q[j] += dt * v;
-  }
   s.w[0] = w_new.x; s.w[1] = w_new.y; s.w[2] = w_new.z;
   s.vo[0] = vb_new.x; s.vo[1] = vb_new.y; s.vo[2] = vb_new.z;
   s.pos[0] += dt * vb_new.x; s.pos[1] += dt * vb_new.y; s.pos[2] += dt * vb_new.z;
@@ -553,8 +605,48 @@ T1_HD void integrate(const DynModel& M, EnvState<R>& s, const R delta[6 + ND], R
   R ny = qy + (hy * qw + hz * qx - hx * qz);
   R nz = qz + (hz * qw + hx * qy - hy * qx);
   R nw = qw - (hx * qx + hy * qy + hz * qz);
-  R inv = R(1) / sqrt(nx * nx + ny * ny + nz * nz + nw * nw);
+  R inv = rcp(fsqrt(nx * nx + ny * ny + nz * nz + nw * nw));
   s.quat[0] = nx * inv; s.quat[1] = ny * inv; s.quat[2] = nz * inv; s.quat[3] = nw * inv;
+}
+// joint speeds clamped to the URDF velocity limit like PhysX max joint velocity
+template <typename R>
+T1_HD void integrate_leg(const DynModel& M, int leg, R q[NLEG], R qd[NLEG], const R delta[NLEG], R dt) {
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    R v = qd[k] + delta[k];
+    R vl = R(M.vel_limit[6 * leg + k]);
+    v = v > vl ? vl : (v < -vl ? -vl : v);
+    qd[k] = v;
+    q[k] += dt * v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Whole-env substep on one thread (host build / fp64 checks): delta = change of u = [omega, v_O (spatial,
+// about the fixed point O), qd] over dt, including implicit contact / joint-limit terms.
+// ---------------------------------------------------------------------------------------------------
+template <typename R>
+T1_HD void compute_delta(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s,
+                         const R tau[ND], V3<R> ext_f, R dt, R delta[6 + ND]) {
+  BaseFrame<R> F;
+  base_frame(s, F);
+  Sym6<R> Ac;
+  R gc[6];
+  base_block(M, P.base, F, ext_f, dt, Ac, gc);
+  R rb[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) rb[i] = -gc[i];
+  LegBlock<R> lb[2];
+  for (int leg = 0; leg < 2; ++leg) {
+    Sym6<R> Ab;
+    R r[6];
+    leg_contribution(M, T, P.base, P.leg[leg], F, s.q + 6 * leg, s.qd + 6 * leg, tau + 6 * leg, leg, dt, lb[leg], Ab, r);
+    sym_add(Ac, Ab);
+    for (int i = 0; i < 6; ++i) rb[i] += r[i];
+  }
+  solve_base(Ac, rb);
+  for (int i = 0; i < 6; ++i) delta[i] = rb[i];
+  for (int leg = 0; leg < 2; ++leg) backsub_leg(lb[leg], rb, delta + 6 + 6 * leg);
 }
 
 template <typename R>
@@ -562,7 +654,8 @@ T1_HD void substep(const DynModel& M, const Terrain& T, const EnvParams<R>& P, E
                    V3<R> ext_f, R dt) {
   R delta[6 + ND];
   compute_delta(M, T, P, s, tau, ext_f, dt, delta);
-  integrate(M, s, delta, dt);
+  integrate_base(s, delta, dt);
+  for (int leg = 0; leg < 2; ++leg) integrate_leg(M, leg, s.q + 6 * leg, s.qd + 6 * leg, delta + 6 + 6 * leg, dt);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -570,12 +663,9 @@ T1_HD void substep(const DynModel& M, const Terrain& T, const EnvParams<R>& P, E
 // Linear velocities are COM velocities (PhysX reports link COM velocity); positions are link frame origins.
 // ---------------------------------------------------------------------------------------------------
 template <typename R, typename Writer>
-T1_HD void report(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s, R dt, Writer& W) {
-  M3<R> R0 = quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]);
-  V3<R> base_abs = v3<R>(s.pos[0], s.pos[1], s.pos[2]);
-  R V0[6] = {s.w[0], s.w[1], s.w[2], s.vo[0], s.vo[1], s.vo[2]};
-  V3<R> c0 = mul(R0, v3<R>(R(M.com[0][0]) + P.com_disp[0], R(M.com[0][1]) + P.com_disp[1],
-                           R(M.com[0][2]) + P.com_disp[2]));
+T1_HD void report_base(const DynModel& M, const Terrain& T, const BaseParams<R>& P, const BaseState<R>& s,
+                       const BaseFrame<R>& F, Writer& W) {
+  V3<R> c0 = base_com(M, P, F.R0);
   V3<R> vcom = v3<R>(s.vo[0], s.vo[1], s.vo[2]) + cross(v3<R>(s.w[0], s.w[1], s.w[2]), c0);
   R body[13];
   body[0] = s.pos[0]; body[1] = s.pos[1]; body[2] = s.pos[2];
@@ -584,35 +674,41 @@ T1_HD void report(const DynModel& M, const Terrain& T, const EnvParams<R>& P, co
   body[10] = s.w[0]; body[11] = s.w[1]; body[12] = s.w[2];
   W.root(body);
   W.rigid(0, body);
-  V3<R> F0 = body_contact_force(M, T, 0, R0, v3<R>(0, 0, 0), base_abs, V0, P.friction, dt);
-  W.contact(0, F0);
+  W.contact(0, body_contact_force(M, T, 0, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, P.friction));
+}
+template <typename R, typename Writer>
+T1_HD void report_leg(const DynModel& M, const Terrain& T, R mu, const BaseFrame<R>& F, const R q[NLEG],
+                      const R qd[NLEG], int leg, Writer& W) {
+  BodyState<R> B[NLEG];
+  leg_fk(M, leg, F.R0, q, B);
+  R V[6];
 #pragma unroll
-  for (int leg = 0; leg < 2; ++leg) {
-    BodyState<R> B[NLEG];
-    leg_fk(M, leg, R0, s.q, B);
-    R V[6];
+  for (int i = 0; i < 6; ++i) V[i] = F.V0[i];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) V[i] = V0[i];
+  for (int k = 0; k < NLEG; ++k) {
+    const int b = 1 + 6 * leg + k;
+    R S[6];
+    motion_subspace(M, b, B[k], S);
 #pragma unroll
-    for (int k = 0; k < NLEG; ++k) {
-      const int b = 1 + 6 * leg + k;
-      R S[6];
-      motion_subspace(M, b, B[k], S);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) V[i] += S[i] * s.qd[6 * leg + k];
-      V3<R> c = B[k].p + mul(B[k].Rot, v3<R>(M.com[b][0], M.com[b][1], M.com[b][2]));
-      V3<R> om{V[0], V[1], V[2]};
-      V3<R> vc = v3<R>(V[3], V[4], V[5]) + cross(om, c);
-      R qb[4];
-      mat_to_quat(B[k].Rot, qb);
-      R out[13] = {B[k].p.x + base_abs.x, B[k].p.y + base_abs.y, B[k].p.z + base_abs.z, qb[0], qb[1], qb[2], qb[3],
-                   vc.x, vc.y, vc.z, om.x, om.y, om.z};
-      W.rigid(b, out);
-      V3<R> F = M.contact_count[b] > 0 ? body_contact_force(M, T, b, B[k].Rot, B[k].p, base_abs, V, P.friction, dt)
-                                       : v3<R>(0, 0, 0);
-      W.contact(b, F);
-    }
+    for (int i = 0; i < 6; ++i) V[i] += S[i] * qd[k];
+    V3<R> c = B[k].p + mul(B[k].Rot, v3<R>(M.com[b][0], M.com[b][1], M.com[b][2]));
+    V3<R> om{V[0], V[1], V[2]};
+    V3<R> vc = v3<R>(V[3], V[4], V[5]) + cross(om, c);
+    R qb[4];
+    mat_to_quat(B[k].Rot, qb);
+    R out[13] = {B[k].p.x + F.abs.x, B[k].p.y + F.abs.y, B[k].p.z + F.abs.z, qb[0], qb[1], qb[2], qb[3],
+                 vc.x, vc.y, vc.z, om.x, om.y, om.z};
+    W.rigid(b, out);
+    W.contact(b, M.contact_count[b] > 0 ? body_contact_force(M, T, b, B[k].Rot, B[k].p, F.abs, V, mu)
+                                        : v3<R>(0, 0, 0));
   }
+}
+template <typename R, typename Writer>
+T1_HD void report(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s, Writer& W) {
+  BaseFrame<R> F;
+  base_frame(s, F);
+  report_base(M, T, P.base, s, F, W);
+  for (int leg = 0; leg < 2; ++leg) report_leg(M, T, P.base.friction, F, s.q + 6 * leg, s.qd + 6 * leg, leg, W);
 }
 
 }  // namespace t1

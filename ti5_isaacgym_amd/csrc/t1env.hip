@@ -80,39 +80,38 @@ struct DevWriter {
   }
 };
 
-__device__ __forceinline__ void load_params(const DynModel& M, const t1env_buffers& B, int n, EnvParams<float>& P,
-                                            float ground_friction) {
-  P.mass[0] = B.body_mass[n];
-  P.inertia_scale[0] = P.mass[0] / M.mass[0];
-#pragma unroll
-  for (int b = 1; b < NB; ++b) {
-    const float s = B.link_mass_scale[n * 12 + (b - 1)];
-    P.mass[b] = M.mass[b] * s;
-    P.inertia_scale[b] = s;
-  }
+// per-env base parameters; PhysX combines shape and ground friction by averaging (third-party semantics,
+// unpinned)
+__device__ __forceinline__ void load_base_params(const DynModel& M, const t1env_buffers& B, int n,
+                                                 BaseParams<float>& P) {
+  P.mass = B.body_mass[n];
+  P.inertia_scale = P.mass / M.mass[0];
 #pragma unroll
   for (int i = 0; i < 3; ++i) P.com_disp[i] = B.com_disp[n * 3 + i];
-#pragma unroll
-  for (int j = 0; j < ND; ++j) P.armature[j] = B.armature[n * 12 + j];
-  // PhysX combines shape and ground friction by averaging (third-party semantics, unpinned)
-  P.friction = 0.5f * (B.friction[n] + ground_friction);
+  P.friction = 0.5f * (B.friction[n] + M.ground_friction);
 }
-
-// root state (COM velocity) -> internal state (base-origin velocity)
-__device__ __forceinline__ void load_state(const DynModel& M, const EnvParams<float>& P, const float* root,
-                                           const float* dof, EnvState<float>& s) {
+__device__ __forceinline__ void load_leg_params(const DynModel& M, const t1env_buffers& B, int n, int j0,
+                                                LegParams<float>& P) {
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    const float s = B.link_mass_scale[n * 12 + j0 + k];
+    P.mass[k] = M.mass[1 + j0 + k] * s;
+    P.inertia_scale[k] = s;
+    P.armature[k] = B.armature[n * 12 + j0 + k];
+  }
+}
+// root state (COM velocity) -> internal base state (base-origin velocity)
+__device__ __forceinline__ void load_base_state(const DynModel& M, const BaseParams<float>& P, const float* root,
+                                                BaseState<float>& s) {
 #pragma unroll
   for (int i = 0; i < 3; ++i) s.pos[i] = root[i];
 #pragma unroll
   for (int i = 0; i < 4; ++i) s.quat[i] = root[3 + i];
-  M3<float> R0 = quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]);
-  V3<float> c0 = mul(R0, v3<float>(M.com[0][0] + P.com_disp[0], M.com[0][1] + P.com_disp[1], M.com[0][2] + P.com_disp[2]));
+  V3<float> c0 = base_com(M, P, quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]));
   V3<float> w = v3<float>(root[10], root[11], root[12]);
   V3<float> vo = v3<float>(root[7], root[8], root[9]) - cross(w, c0);
   s.w[0] = w.x; s.w[1] = w.y; s.w[2] = w.z;
   s.vo[0] = vo.x; s.vo[1] = vo.y; s.vo[2] = vo.z;
-#pragma unroll
-  for (int j = 0; j < ND; ++j) { s.q[j] = dof[2 * j]; s.qd[j] = dof[2 * j + 1]; }
 }
 
 #pragma clang fp contract(off)
@@ -120,23 +119,26 @@ __device__ __forceinline__ void load_state(const DynModel& M, const EnvParams<fl
 
 // PD torque of one substep (legged_robot.py:1019-1074): lagged action, randomized gains, viscous +
 // Coulomb friction, torque multiplier redrawn every substep, clip to 0.85 * effort.
+// Joints j0 .. j0+NJ-1 (NJ = 12: whole env; NJ = 6: one leg of the two-wave kernel).
+template <int NJ>
 __device__ __forceinline__ void pd_torques(const DynModel& M, const t1env_config& C, const t1env_buffers& B, int n,
-                                           uint32_t genv, uint32_t ctr, int sub, int lag, const float q[12],
-                                           const float qd[12], float tau[12]) {
+                                           uint32_t genv, uint32_t ctr, int sub, int lag, int j0, const float q[NJ],
+                                           const float qd[NJ], float tau[NJ]) {
   const int d = lag > sub ? (lag - sub + 9) / 10 : 0;
   const float* la = B.act_hist + ((size_t)n * 4 + ((ctr - (uint32_t)d) & 3u)) * 12;
 #pragma unroll
-  for (int j = 0; j < 12; ++j) {
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int j = j0 + jj;
     const float kp = B.kp[n * 12 + j], kd = B.kd[n * 12 + j];
-    float t = kp * (((la[j] + M.default_dof_pos[j]) - q[j]) + B.motor_offsets[n * 12 + j]);
-    t = t - kd * qd[j];
-    t = t - B.viscous[n * 12 + j] * qd[j];
-    t = t - B.coulomb[n * 12 + j] * signf(qd[j]);
+    float t = kp * (((la[j] + M.default_dof_pos[j]) - q[jj]) + B.motor_offsets[n * 12 + j]);
+    t = t - kd * qd[jj];
+    t = t - B.viscous[n * 12 + j] * qd[jj];
+    t = t - B.coulomb[n * 12 + j] * signf(qd[jj]);
     const float tm = rand_float(C.torque_mult_range[0], C.torque_mult_range[1], C.seed, genv, ctr,
                                 SLOT_TORQUE_MULT + sub * 12 + j);
     t = t * tm;
     const float lim = M.torque_limit[j];
-    tau[j] = fminf(fmaxf(t, -lim), lim);
+    tau[jj] = fminf(fmaxf(t, -lim), lim);
   }
 }
 
@@ -148,17 +150,133 @@ __device__ __forceinline__ void capture_imu(const float quat[4], const float w_w
   dst[3] = e[0]; dst[4] = e[1]; dst[5] = e[2];
 }
 
-template <bool INJECTED>
-__global__ __launch_bounds__(BLOCK) void k_physics(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
-                                                   t1env_buffers B, Terrain T, const float* __restrict__ actions,
-                                                   t1env_step_args A, t1env_injected inj) {
+// ---------------------------------------------------------------------------------------------------
+// k_dynamics: the decimation loop with the articulated-body solver.  A workgroup owns 64 envs and runs
+// them on two waves: wave 0 handles every env's left leg, wave 1 the right leg (the leg index is
+// wave-uniform, so all model reads are scalar loads).  Per substep each wave eliminates its leg into a
+// 27-float base-block contribution (t1_dynamics.h leg_contribution), the two contributions meet in LDS
+// (double-buffered by substep parity -> one barrier per substep), and both waves solve the 6x6 base system
+// redundantly, so the base state stays bit-identical in both without further exchange.
+// ---------------------------------------------------------------------------------------------------
+constexpr int DYN_ENVS = 64;
+constexpr int DYN_BLOCK = 2 * DYN_ENVS;
+constexpr int XCH = 27;  // Sym6 (21) + rhs (6)
+
+__global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restrict__ Mp,
+                                                        const t1env_config* __restrict__ Cp, t1env_buffers B,
+                                                        Terrain T, const float* __restrict__ actions,
+                                                        t1env_step_args A) {
+  __shared__ float xch[2][2][XCH][DYN_ENVS];  // [substep parity][leg][value][env]
+  const t1env_config& C = *Cp;
+  const DynModel& M = *Mp;
+  const int leg = __builtin_amdgcn_readfirstlane((int)threadIdx.x / DYN_ENVS);
+  const int lane = threadIdx.x % DYN_ENVS;
+  const int N = C.num_envs;
+  const bool active = (int)(blockIdx.x * DYN_ENVS) + lane < N;
+  const int n = active ? blockIdx.x * DYN_ENVS + lane : N - 1;  // inactive lanes shadow a valid env, never store
+  const int j0 = 6 * leg;
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  const uint32_t ctr = A.counter;
+  // actions = clip(actions); push the scaled action into this step's history slot
+  if (active) {
+    float* slot = B.act_hist + ((size_t)n * 4 + (ctr & 3u)) * 12;
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      const float a = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
+      B.actions[n * 12 + j0 + k] = a;
+      slot[j0 + k] = a * C.action_scale;
+    }
+  }
+  const int lag = B.lag_timestep[n];
+  const int s_dof = 9 - B.dof_lag_timestep[n] % 10, s_imu = 9 - B.imu_lag_timestep[n] % 10;
+  float* dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
+  float* imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 6;
+  const float dt = C.sim_dt;
+  BaseParams<float> PB;
+  LegParams<float> PL;
+  load_base_params(M, B, n, PB);
+  load_leg_params(M, B, n, j0, PL);
+  BaseState<float> sb;
+  load_base_state(M, PB, B.root_states + (size_t)n * 13, sb);
+  float q[NLEG], qd[NLEG], tau[NLEG];
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
+    qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
+  }
+  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
+  for (int sub = 0; sub < C.decimation; ++sub) {
+    // re-derive the model pointer each substep so the ~200 model scalars are re-read (scalar cache hits)
+    // instead of being hoisted out of the loop and spilled
+    const DynModel* Ml = Mp;
+    asm volatile("" : "+s"(Ml));
+    const DynModel& M = *Ml;
+    pd_torques<NLEG>(M, C, B, n, genv, ctr, sub, lag, j0, q, qd, tau);
+    BaseFrame<float> F;
+    base_frame(sb, F);
+    LegBlock<float> lb;
+    {
+      Sym6<float> Ab;
+      float rb[6];
+      leg_contribution(M, T, PB, PL, F, q, qd, tau, leg, dt, lb, Ab, rb);
+      float* X = &xch[sub & 1][leg][0][lane];
+#pragma unroll
+      for (int i = 0; i < 21; ++i) X[i * DYN_ENVS] = Ab.a[i];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) X[(21 + i) * DYN_ENVS] = rb[i];
+    }
+    Sym6<float> Ac;
+    float r[6];
+    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r[i] = -r[i];
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const float* Y = &xch[sub & 1][l][0][lane];
+#pragma unroll
+      for (int i = 0; i < 21; ++i) Ac.a[i] += Y[i * DYN_ENVS];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) r[i] += Y[(21 + i) * DYN_ENVS];
+    }
+    solve_base(Ac, r);
+    float dq[NLEG];
+    backsub_leg(lb, r, dq);
+    integrate_base(sb, r, dt);
+    integrate_leg(M, leg, q, qd, dq, dt);
+    if (active && sub == s_dof) {
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { dof_dst[j0 + k] = q[k]; dof_dst[12 + j0 + k] = qd[k]; }
+    }
+    if (active && leg == 0 && sub == s_imu) capture_imu(sb.quat, sb.w, imu_dst);
+  }
+  if (!active) return;
+  BaseFrame<float> F;
+  base_frame(sb, F);
+  DevWriter W{B.root_states + (size_t)n * 13, B.rigid_state + (size_t)n * 169, B.contact_forces + (size_t)n * 39};
+  if (leg == 0) report_base(M, T, PB, sb, F, W);
+  report_leg(M, T, PB.friction, F, q, qd, leg, W);
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
+    B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
+    B.torques[n * 12 + j0 + k] = tau[k];
+  }
+}
+
+// k_physics_injected: the same decimation loop with the physics states supplied by the caller (golden
+// parity harness: the reference ran on identical injected states), so PD / lag / sensor capture are checked
+// bit-for-bit without a simulator in the loop.
+__global__ __launch_bounds__(BLOCK) void k_physics_injected(const DynModel* __restrict__ Mp,
+                                                            const t1env_config* __restrict__ Cp, t1env_buffers B,
+                                                            const float* __restrict__ actions, t1env_step_args A,
+                                                            t1env_injected inj) {
   const int n = blockIdx.x * BLOCK + threadIdx.x;
   const t1env_config& C = *Cp;
   if (n >= C.num_envs) return;
   const DynModel& M = *Mp;
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   const uint32_t ctr = A.counter;
-  // actions = clip(actions); push the scaled action into this step's history slot
   float* slot = B.act_hist + ((size_t)n * 4 + (ctr & 3u)) * 12;
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
@@ -167,63 +285,37 @@ __global__ __launch_bounds__(BLOCK) void k_physics(const DynModel* __restrict__ 
     slot[j] = a * C.action_scale;
   }
   const int lag = B.lag_timestep[n];
-  const int dlag = B.dof_lag_timestep[n], ilag = B.imu_lag_timestep[n];
-  const int s_dof = 9 - dlag % 10, s_imu = 9 - ilag % 10;
+  const int s_dof = 9 - B.dof_lag_timestep[n] % 10, s_imu = 9 - B.imu_lag_timestep[n] % 10;
   float* dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
   float* imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 6;
-  const float dt = C.sim_dt;
+  const int N = C.num_envs;
   float tau[12];
-  if constexpr (!INJECTED) {
-    EnvParams<float> P;
-    load_params(M, B, n, P, M.ground_friction);
-    EnvState<float> s;
-    load_state(M, P, B.root_states + (size_t)n * 13, B.dof_state + (size_t)n * 24, s);
-    V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
-    for (int sub = 0; sub < C.decimation; ++sub) {
-      pd_torques(M, C, B, n, genv, ctr, sub, lag, s.q, s.qd, tau);
-      substep(M, T, P, s, tau, sub == 0 ? ef : v3<float>(0, 0, 0), dt);
-      if (sub == s_dof) {
+  for (int sub = 0; sub < C.decimation; ++sub) {
+    float q[12], qd[12];
 #pragma unroll
-        for (int j = 0; j < 12; ++j) { dof_dst[j] = s.q[j]; dof_dst[12 + j] = s.qd[j]; }
-      }
-      if (sub == s_imu) capture_imu(s.quat, s.w, imu_dst);
+    for (int j = 0; j < 12; ++j) { q[j] = B.dof_state[n * 24 + 2 * j]; qd[j] = B.dof_state[n * 24 + 2 * j + 1]; }
+    pd_torques<12>(M, C, B, n, genv, ctr, sub, lag, 0, q, qd, tau);
+    if (inj.torque_log) {
+#pragma unroll
+      for (int j = 0; j < 12; ++j) inj.torque_log[((size_t)sub * N + n) * 12 + j] = tau[j];
     }
-    DevWriter W{B.root_states + (size_t)n * 13, B.rigid_state + (size_t)n * 169, B.contact_forces + (size_t)n * 39};
-    report(M, T, P, s, dt, W);
+    const float* r = inj.root + ((size_t)sub * N + n) * 13;
+    const float* d = inj.dof + ((size_t)sub * N + n) * 24;
 #pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      B.dof_state[n * 24 + 2 * j] = s.q[j];
-      B.dof_state[n * 24 + 2 * j + 1] = s.qd[j];
+    for (int i = 0; i < 13; ++i) B.root_states[n * 13 + i] = r[i];
+#pragma unroll
+    for (int i = 0; i < 24; ++i) B.dof_state[n * 24 + i] = d[i];
+    if (sub == s_dof) {
+#pragma unroll
+      for (int j = 0; j < 12; ++j) { dof_dst[j] = d[2 * j]; dof_dst[12 + j] = d[2 * j + 1]; }
     }
-  } else {
-    const int N = C.num_envs;
-    for (int sub = 0; sub < C.decimation; ++sub) {
-      float q[12], qd[12];
-#pragma unroll
-      for (int j = 0; j < 12; ++j) { q[j] = B.dof_state[n * 24 + 2 * j]; qd[j] = B.dof_state[n * 24 + 2 * j + 1]; }
-      pd_torques(M, C, B, n, genv, ctr, sub, lag, q, qd, tau);
-      if (inj.torque_log) {
-#pragma unroll
-        for (int j = 0; j < 12; ++j) inj.torque_log[((size_t)sub * N + n) * 12 + j] = tau[j];
-      }
-      const float* r = inj.root + ((size_t)sub * N + n) * 13;
-      const float* d = inj.dof + ((size_t)sub * N + n) * 24;
-#pragma unroll
-      for (int i = 0; i < 13; ++i) B.root_states[n * 13 + i] = r[i];
-#pragma unroll
-      for (int i = 0; i < 24; ++i) B.dof_state[n * 24 + i] = d[i];
-      if (sub == s_dof) {
-#pragma unroll
-        for (int j = 0; j < 12; ++j) { dof_dst[j] = d[2 * j]; dof_dst[12 + j] = d[2 * j + 1]; }
-      }
-      if (sub == s_imu) {
-        float quat[4] = {r[3], r[4], r[5], r[6]}, w[3] = {r[10], r[11], r[12]};
-        capture_imu(quat, w, imu_dst);
-      }
+    if (sub == s_imu) {
+      float quat[4] = {r[3], r[4], r[5], r[6]}, w[3] = {r[10], r[11], r[12]};
+      capture_imu(quat, w, imu_dst);
     }
-    for (int i = 0; i < 169; ++i) B.rigid_state[(size_t)n * 169 + i] = inj.rigid[(size_t)n * 169 + i];
-    for (int i = 0; i < 39; ++i) B.contact_forces[(size_t)n * 39 + i] = inj.contact[(size_t)n * 39 + i];
   }
+  for (int i = 0; i < 169; ++i) B.rigid_state[(size_t)n * 169 + i] = inj.rigid[(size_t)n * 169 + i];
+  for (int i = 0; i < 39; ++i) B.contact_forces[(size_t)n * 39 + i] = inj.contact[(size_t)n * 39 + i];
 #pragma unroll
   for (int j = 0; j < 12; ++j) B.torques[n * 12 + j] = tau[j];
 }
@@ -993,14 +1085,13 @@ int t1env_set_terrain(t1env* e, const int16_t* h, int32_t rows, int32_t cols, fl
 static int launch_physics(t1env* e, const float* actions, const t1env_step_args* a, const t1env_injected* inj,
                           hipStream_t s) {
   const int N = e->cfg.num_envs;
-  t1env_injected none{};
   int t = t_begin(e, 0, s);
   if (inj)
-    hipLaunchKernelGGL(k_physics<true>, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
-                       e->terrain, actions, *a, *inj);
+    hipLaunchKernelGGL(k_physics_injected, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
+                       actions, *a, *inj);
   else
-    hipLaunchKernelGGL(k_physics<false>, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
-                       e->terrain, actions, *a, none);
+    hipLaunchKernelGGL(k_dynamics, dim3(grid(N, DYN_ENVS)), dim3(DYN_BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
+                       e->terrain, actions, *a);
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
   t = t_begin(e, 1, s);

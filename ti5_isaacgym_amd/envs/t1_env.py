@@ -45,6 +45,59 @@ def _ptr(t):
     return t.data_ptr()
 
 
+def build_model(cfg, urdf_path=None):
+    """LeggedRobotCfg + URDF -> (t1env_model ctypes struct, model table, default pose, kp, kd).
+
+    Mirrors _create_envs / _process_dof_props / _init_buffers (legged_robot.py:225-234, 1171-1262): dof
+    limits scaled by cfg.safety, PD gains by substring match of the dof names."""
+    tab = load_model(urdf_path)
+    m = _lib.Model()
+    for b in range(13):
+        for k in range(3):
+            m.joint_offset[b][k] = tab["joint_offset"][b][k]
+            m.joint_axis[b][k] = tab["joint_axis"][b][k]
+            m.com[b][k] = tab["com"][b][k]
+        m.parent[b] = tab["parent"][b]
+        m.mass[b] = tab["mass"][b]
+        for k in range(6):
+            m.inertia[b][k] = tab["inertia"][b][k]
+        m.contact_start[b] = tab["contact_start"][b]
+        m.contact_count[b] = tab["contact_count"][b]
+    lim = np.asarray(tab["limits"])
+    default = np.array([cfg.init_state.default_joint_angles[n] for n in tab["dof_names"]], np.float32)
+    kp = np.zeros(12, np.float32)
+    kd = np.zeros(12, np.float32)
+    for i, n in enumerate(tab["dof_names"]):   # substring match, legged_robot.py:225-234
+        for key in cfg.control.stiffness:
+            if key in n:
+                kp[i] = cfg.control.stiffness[key]
+                kd[i] = cfg.control.damping[key]
+    safety = getattr(cfg, "safety", None)
+    pos_k = safety.pos_limit if safety else 1.0
+    vel_k = safety.vel_limit if safety else 1.0
+    tq_k = safety.torque_limit if safety else 1.0
+    for j in range(12):
+        m.q_lower[j], m.q_upper[j] = lim[j, 0] * pos_k, lim[j, 1] * pos_k
+        m.vel_limit[j] = lim[j, 3] * vel_k
+        m.torque_limit[j] = np.float32(lim[j, 2]) * np.float32(tq_k)
+        m.default_dof_pos[j], m.p_gains[j], m.d_gains[j] = default[j], kp[j], kd[j]
+    pts = tab["contact_point"]
+    m.n_contact = len(pts)
+    for c, p in enumerate(pts):
+        for k in range(3):
+            m.contact_point[c][k] = p[k]
+    for k, v in SOLVER.items():
+        setattr(m, k, v)
+    m.gravity = -float(cfg.sim.gravity[2]) if hasattr(cfg.sim, "gravity") else 9.81
+    m.ground_friction = cfg.terrain.static_friction
+    m.ground_restitution = cfg.terrain.restitution
+    init = list(cfg.init_state.pos) + list(cfg.init_state.rot) + list(cfg.init_state.lin_vel) + \
+        list(cfg.init_state.ang_vel)
+    for i in range(13):
+        m.base_init_state[i] = init[i]
+    return m, tab, default, kp, kd
+
+
 class T1DHStandEnv(VecEnv):
     def __init__(self, cfg, sim_params=None, physics_engine=None, sim_device="cuda:0", headless=True,
                  env_offset=0, num_envs_total=None, urdf_path=None):
@@ -160,55 +213,11 @@ class T1DHStandEnv(VecEnv):
 
     def _build_model(self, urdf_path):
         cfg = self.cfg
-        tab = load_model(urdf_path)
-        m = _lib.Model()
-        for b in range(13):
-            for k in range(3):
-                m.joint_offset[b][k] = tab["joint_offset"][b][k]
-                m.joint_axis[b][k] = tab["joint_axis"][b][k]
-                m.com[b][k] = tab["com"][b][k]
-            m.parent[b] = tab["parent"][b]
-            m.mass[b] = tab["mass"][b]
-            for k in range(6):
-                m.inertia[b][k] = tab["inertia"][b][k]
-            m.contact_start[b] = tab["contact_start"][b]
-            m.contact_count[b] = tab["contact_count"][b]
+        m, tab, default, kp, kd = build_model(cfg, urdf_path)
         self.dof_names = tab["dof_names"]
         self.body_names = tab["body_names"]
         self.num_dof = self.num_dofs = 12
         self.num_bodies = 13
-        lim = np.asarray(tab["limits"])
-        default = np.array([cfg.init_state.default_joint_angles[n] for n in self.dof_names], np.float32)
-        kp = np.zeros(12, np.float32)
-        kd = np.zeros(12, np.float32)
-        for i, n in enumerate(self.dof_names):   # substring match, legged_robot.py:225-234
-            for key in cfg.control.stiffness:
-                if key in n:
-                    kp[i] = cfg.control.stiffness[key]
-                    kd[i] = cfg.control.damping[key]
-        safety = getattr(cfg, "safety", None)
-        pos_k = safety.pos_limit if safety else 1.0
-        vel_k = safety.vel_limit if safety else 1.0
-        tq_k = safety.torque_limit if safety else 1.0
-        for j in range(12):
-            m.q_lower[j], m.q_upper[j] = lim[j, 0] * pos_k, lim[j, 1] * pos_k
-            m.vel_limit[j] = lim[j, 3] * vel_k
-            m.torque_limit[j] = np.float32(lim[j, 2]) * np.float32(tq_k)
-            m.default_dof_pos[j], m.p_gains[j], m.d_gains[j] = default[j], kp[j], kd[j]
-        pts = tab["contact_point"]
-        m.n_contact = len(pts)
-        for c, p in enumerate(pts):
-            for k in range(3):
-                m.contact_point[c][k] = p[k]
-        for k, v in SOLVER.items():
-            setattr(m, k, v)
-        m.gravity = -float(cfg.sim.gravity[2]) if hasattr(cfg.sim, "gravity") else 9.81
-        m.ground_friction = cfg.terrain.static_friction
-        m.ground_restitution = cfg.terrain.restitution
-        init = list(cfg.init_state.pos) + list(cfg.init_state.rot) + list(cfg.init_state.lin_vel) + \
-            list(cfg.init_state.ang_vel)
-        for i in range(13):
-            m.base_init_state[i] = init[i]
         d = self.device
         self.default_dof_pos = torch.tensor(default, device=d).unsqueeze(0)
         self.default_joint_pd_target = self.default_dof_pos.clone()
