@@ -109,9 +109,12 @@ class T1Oracle:
     """Numpy mirror of T1DHStandEnv's state and step.  ``physics(g, torques, st)`` must return
     (root (N,13), dof (N,12,2), rigid (N,13,13), contact (N,13,3)) after global substep g."""
 
-    def __init__(self, num_envs, seed=5, mesh_type="plane", terrain=None, env_offset=0):
+    def __init__(self, num_envs, seed=5, mesh_type="plane", terrain=None, env_offset=0, reduce_fn=None):
+        """reduce_fn: sharded runs only -- (sum, count) -> (sum, count) over all ranks, so the command
+        curriculum sees the same mean as an unsharded run."""
         N = num_envs
         self.N, self.seed, self.env_offset = N, int(seed), int(env_offset)
+        self.reduce_fn = reduce_fn
         self.ids = np.arange(N, dtype=np.int64) + env_offset
         self.mesh_type = mesh_type
         self.curriculum = mesh_type in ("heightfield", "trimesh")   # legged_robot.py:104-105
@@ -538,17 +541,27 @@ class T1Oracle:
         return np.exp(-np.square(rot / f32(1)))
 
     # ---------------------------------------------------------------- reset (t1:483-559)
+    def _widen_commands(self):
+        cr = self.command_ranges["lin_vel_x"]
+        cr[0] = float(np.clip(cr[0] - 0.25, -1.5 / 2, 0.0))
+        cr[1] = float(np.clip(cr[1] + 0.5, 0.0, 1.5))
+
     def reset_idx(self, env_ids):
+        curriculum_step = self.common_step_counter % MAX_EPISODE_LEN == 0
+        if self.reduce_fn is not None and curriculum_step:
+            # sharded: every rank takes part, also with no local resets (the mean is over all ranks' resets)
+            s, c = self.reduce_fn(float(np.sum(self.episode_sums["tracking_lin_vel"][env_ids], dtype=np.float64)),
+                                  float(len(env_ids)))
+            if c > 0 and s / c / MAX_EPISODE_LEN > 0.8 * self.reward_scales["tracking_lin_vel"]:
+                self._widen_commands()
         if len(env_ids) == 0:
             return
         if self.curriculum:
             self._update_terrain_curriculum(env_ids)
-        if self.common_step_counter % MAX_EPISODE_LEN == 0:      # command curriculum (legged_robot.py:1160-1169)
+        if self.reduce_fn is None and curriculum_step:      # command curriculum (legged_robot.py:1160-1169)
             if np.mean(self.episode_sums["tracking_lin_vel"][env_ids]) / MAX_EPISODE_LEN > \
                     0.8 * self.reward_scales["tracking_lin_vel"]:
-                cr = self.command_ranges["lin_vel_x"]
-                cr[0] = float(np.clip(cr[0] - 0.25, -1.5 / 2, 0.0))
-                cr[1] = float(np.clip(cr[1] + 0.5, 0.0, 1.5))
+                self._widen_commands()
         n = len(env_ids)
         # _reset_dofs (legged_robot.py:1076-1090)
         self.dof[env_ids, :, 0] = Q0 + np.stack([self._rf(-0.1, 0.1, env_ids, R.SLOT_RESET_DOF + j)

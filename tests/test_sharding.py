@@ -1,0 +1,118 @@
+"""Multi-GPU semantics on CPU: sharding the envs over ranks must reproduce the unsharded run.
+
+Rank r owns global envs [r·N, (r+1)·N) (t1env_config.env_offset = r·N, num_envs_total = world·N).  Every
+random draw is keyed by the global env id, terrain types use the global id, and the one cross-env quantity
+of the step -- the command-curriculum mean -- is all-reduced.  Two gloo ranks run their shard of the oracle
+(the CPU restatement the HIP path is pinned to) on injected physics, through a curriculum step with
+time-outs, and the gathered results must equal a single-process run over all envs exactly.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+sys.path.insert(0, HERE)
+
+N_PER_RANK, WORLD, STEPS, SEED, SYNTH_SEED = 12, 2, 5, 5, 11
+KEYS = ("obs", "priv", "rew", "reset", "time_out", "root", "commands", "episode_length", "env_origins",
+        "terrain_levels", "torques", "gait_time")
+
+
+def _terrain(n_total):
+    from ti5_isaacgym_amd.envs.configs import DHT1StandCfg
+    from ti5_isaacgym_amd.utils.terrain import Terrain
+    cfg = DHT1StandCfg().terrain
+    cfg.mesh_type = "trimesh"
+    cfg.num_rows, cfg.num_cols, cfg.border_size = 6, 4, 5
+    t = Terrain(cfg, n_total)
+    return {"terrain_origins": t.env_origins, "height_samples": t.heightsamples, "num_envs_total": n_total}
+
+
+def _run(n, env_offset, n_total, reduce_fn=None):
+    import synth
+    from oracle.t1_oracle import T1Oracle
+    o = T1Oracle(n, seed=SEED, mesh_type="trimesh", terrain=_terrain(n_total), env_offset=env_offset,
+                 reduce_fn=reduce_fn)
+
+    def physics(g, torques, env):
+        return synth.state(SYNTH_SEED, n, g, np.asarray(env.env_origins), env_offset=env_offset)
+
+    o.reset(physics)
+    ids = np.arange(n) + env_offset
+    # reach a command-curriculum step (counter % 2400 == 0) on step 3, with every 5th env timing out there
+    # and the tracking sums high enough to widen the command range
+    o.common_step_counter = 2400 - 3
+    o.episode_length_buf[ids % 5 == 0] = 2398
+    # rank 0's resetting envs track well (1.35x the 0.8 threshold scale), rank 1's poorly (0.63x): only the
+    # mean over ALL ranks (1.06x) widens the range, so a missing all-reduce desynchronises the ranks
+    good = np.where(ids < N_PER_RANK, 1.35, 0.63)
+    o.episode_sums["tracking_lin_vel"][:] = (2400 * good * o.reward_scales["tracking_lin_vel"]).astype(np.float32)
+    acts = np.random.default_rng(7).standard_normal((STEPS, n_total, 12)).astype(np.float32)
+    outs = []
+    for t in range(STEPS):
+        o.step(acts[t, env_offset:env_offset + n], physics)
+        outs.append({"obs": o.obs_buf.copy(), "priv": o.priv_buf.copy(), "rew": o.rew_buf.copy(),
+                     "reset": o.reset_buf.copy(), "time_out": o.time_out_buf.copy(), "root": o.root.copy(),
+                     "commands": o.commands.copy(), "episode_length": o.episode_length_buf.copy(),
+                     "env_origins": o.env_origins.copy(), "terrain_levels": o.terrain_levels.copy(),
+                     "torques": np.stack(o.torque_log), "gait_time": o.gait_time.copy(),
+                     "max_command_x": np.float64(o.command_ranges["lin_vel_x"][1])})
+    return outs
+
+
+def _worker(rank, port, out_dir):
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+
+    def reduce_fn(s, c):
+        t = torch.tensor([s, c], dtype=torch.float64)
+        dist.all_reduce(t)
+        return float(t[0]), float(t[1])
+
+    outs = _run(N_PER_RANK, rank * N_PER_RANK, WORLD * N_PER_RANK, reduce_fn)
+    gathered = {}
+    for t, o in enumerate(outs):
+        for k, v in o.items():
+            arr = torch.from_numpy(np.ascontiguousarray(v).reshape(-1).astype(np.float64))
+            lst = [torch.zeros_like(arr) for _ in range(WORLD)]
+            dist.all_gather(lst, arr)
+            for r, x in enumerate(lst):
+                gathered[f"{t}/{k}/{r}"] = x.numpy()
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "sharded.npz"), **gathered)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_shards_match_unsharded(tmp_path):
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    z = np.load(os.path.join(tmp_path, "sharded.npz"))
+    sharded = [{k: [z[f"{t}/{k}/{r}"] for r in range(WORLD)] for k in KEYS + ("max_command_x",)}
+               for t in range(STEPS)]
+    full = _run(WORLD * N_PER_RANK, 0, WORLD * N_PER_RANK)
+    widened = False
+    for t in range(STEPS):
+        ref = full[t]
+        for k in KEYS:
+            per_rank = [p.reshape((-1,) + np.asarray(ref[k]).shape[1:]) if k != "torques" else
+                        p.reshape(10, N_PER_RANK, 12) for p in sharded[t][k]]
+            got = np.concatenate(per_rank, axis=1 if k == "torques" else 0)
+            np.testing.assert_array_equal(got, np.asarray(ref[k], dtype=np.float64), err_msg=f"{k} step {t}")
+        for r in range(WORLD):
+            assert float(sharded[t]["max_command_x"][r][0]) == ref["max_command_x"], f"max_command_x rank {r}"
+        widened |= ref["max_command_x"] > 0.5
+    assert widened, "the run never reached the command-curriculum widening it is meant to exercise"
+    assert any(full[t]["time_out"].any() for t in range(STEPS))

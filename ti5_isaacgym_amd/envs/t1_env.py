@@ -442,7 +442,17 @@ class T1DHStandEnv(VecEnv):
 
     def _command_curriculum(self, sums, count):
         """update_command_curriculum (legged_robot.py:1160-1169), evaluated on the host once per episode length."""
-        if not self.cfg.commands.curriculum or "tracking_lin_vel" not in self.reward_scales or count <= 0:
+        if not self.cfg.commands.curriculum or "tracking_lin_vel" not in self.reward_scales:
+            return
+        if torch.distributed.is_available() and torch.distributed.is_initialized() and \
+                torch.distributed.get_world_size() > 1:
+            # sharded envs: the mean runs over every rank's resetting envs (SURVEY §8e), so all ranks keep
+            # identical command ranges; every rank calls this at the same step counter
+            dev = self.device if torch.distributed.get_backend() == "nccl" else torch.device("cpu")
+            t = torch.tensor([sums, count], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t)
+            sums, count = float(t[0]), float(t[1])
+        if count <= 0:
             return
         if sums / count / self.max_episode_length > 0.8 * self.reward_scales["tracking_lin_vel"]:
             r = self.command_ranges["lin_vel_x"]
