@@ -7,9 +7,13 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "t1env.hip")
+CSRC = os.path.join(HERE, "csrc")
+# translation unit -> optimisation level.  k_dynamics is built at -O1: at -O2/-O3 the optimiser produced wrong
+# dynamics for it (caught by tests/test_gpu_dynamics.py) and -O1 is also the fastest build of it.
+UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1")]
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("t1env.hip", "t1_dynamics.h", "t1_common.h", "t1env_post.h", "t1_model_conv.h")] + \
+DEPS = [os.path.join(CSRC, f) for f in ("t1env.hip", "t1env_dynamics.hip", "t1_dynamics.h", "t1_common.h", "t1env_post.h",
+                                       "t1_model_conv.h", "t1env_device.h", "t1env_internal.h")] + \
     [os.path.join(os.path.dirname(HERE), "include", "t1env.h")]
 ARCH = os.environ.get("T1ENV_ARCH", "gfx950")
 
@@ -22,9 +26,13 @@ def build(force=False, extra=(), out=None):
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     # -fno-slp-vectorize: the SLP pass packs scalar pairs of the dynamics into v_pk_* ops, which forces aligned
     # register pairs and piles up v_mov shuffles; in k_dynamics that alone turned ~40 scratch ops into ~470.
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-fno-slp-vectorize", "-o", out + ".tmp", SRC, *extra]
-    subprocess.run(cmd, check=True)
+    common = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result", "-fno-slp-vectorize", *extra]
+    objs = []
+    for src, opt in UNITS:
+        obj = os.path.join(os.path.dirname(out), os.path.splitext(src)[0] + ".o")
+        subprocess.run([hipcc, opt, *common, "-c", "-o", obj, os.path.join(CSRC, src)], check=True)
+        objs.append(obj)
+    subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs], check=True)
     os.replace(out + ".tmp", out)
     return out
 

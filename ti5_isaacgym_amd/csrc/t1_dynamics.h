@@ -24,6 +24,8 @@
 //     same arithmetic either way.
 //   * semi-implicit Euler; joint speeds clamped to the URDF velocity limits like PhysX max joint velocity.
 #pragma once
+#include <type_traits>
+
 #include "t1_common.h"
 
 namespace t1 {
@@ -231,42 +233,74 @@ T1_HD void world_inertia(const DynModel& M, int b, const M3<R>& Rb, R scale, R o
 // when approaching), regularised Coulomb friction as an implicit tangential damper whose coefficient keeps
 // |F_t| <= mu F_n (Stribeck speed friction_vs).
 // ---------------------------------------------------------------------------------------------------
+template <typename R>
+T1_HD void contact_point(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[6], R mu, R dt, Sym6<R>& A,
+                         R g[6]) {
+  const R k = R(M.k_contact), d = R(M.d_contact);
+  V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
+  V3<R> vp = vo + cross(om, x);
+  R vn = dot(n, vp);
+  V3<R> vt = vp - vn * n;
+  R vtn = fsqrt(dot(vt, vt));
+  R cn = vn < R(0) ? dt * k + d : R(0);
+  R fn_est = k * pen + (vn < R(0) ? -d * vn : R(0));
+  R ct = mu * fn_est * rcp(vtn > R(M.friction_vs) ? vtn : R(M.friction_vs));
+  // force at the current velocity (explicit part) f = k pen n - C vp, C = cn nn^T + ct (I - nn^T)
+  V3<R> f = (k * pen - cn * vn) * n - ct * vt;
+  V3<R> tq = cross(x, f);
+  g[0] -= dt * tq.x; g[1] -= dt * tq.y; g[2] -= dt * tq.z;
+  g[3] -= dt * f.x;  g[4] -= dt * f.y;  g[5] -= dt * f.z;
+  // C = ct I + (cn - ct) n n^T ; J^T C J = ct * sum_e w_e w_e^T + (cn - ct) w_n w_n^T, e over world axes
+  V3<R> xn = cross(x, n);
+  R wn[6] = {xn.x, xn.y, xn.z, n.x, n.y, n.z};
+  sym_rank1(A, dt * (cn - ct), wn);
+  R ex[6] = {R(0), x.z, -x.y, R(1), R(0), R(0)};   // [x cross e_x ; e_x]
+  R ey[6] = {-x.z, R(0), x.x, R(0), R(1), R(0)};
+  R ez[6] = {x.y, -x.x, R(0), R(0), R(0), R(1)};
+  sym_rank1(A, dt * ct, ex);
+  sym_rank1(A, dt * ct, ey);
+  sym_rank1(A, dt * ct, ez);
+}
+
+// NP points known at compile time: phase 1 transforms every point and queries the terrain with no branch
+// in between, so all coordinate (scalar) and height-field (vector) loads issue together and the body pays
+// one memory latency instead of one per point; phase 2 runs the contact math for the points in contact.
+template <bool HF, int NP, typename R>
+T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb,
+                           V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
+  constexpr int CH = NP < 4 ? NP : 4;  // points in flight per batch (bounds the live registers)
+  static_assert(NP % CH == 0, "contact points per body must be a multiple of the batch");
+#pragma unroll
+  for (int c0 = 0; c0 < NP; c0 += CH) {
+    V3<R> xs[CH], ns[CH];
+    R pens[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = c_begin + c0 + i;
+      xs[i] = pb + mul(Rb, v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]));
+      V3<R> X = xs[i] + base_abs;
+      R h = terrain_height<HF>(T, X.x, X.y, ns[i]);
+      pens[i] = (h - X.z) * ns[i].z;
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      if (pens[i] > R(0)) contact_point(M, xs[i], ns[i], pens[i], Vb, mu, dt, A, g);
+  }
+}
+
 template <bool HF, typename R>
 T1_HD void body_contact_t(const DynModel& M, const Terrain& T, int c_begin, int c_end, const M3<R>& Rb, V3<R> pb,
                           V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
-  const R k = R(M.k_contact), d = R(M.d_contact), ivs = rcp(R(M.friction_vs));
+  // the T1 model: 8 points per contact body (base box split 4 + 4 between the legs)
+  if (c_end - c_begin == 8) return body_contact_np<HF, 8>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  if (c_end - c_begin == 4) return body_contact_np<HF, 4>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
   for (int c = c_begin; c < c_end; ++c) {
-    V3<R> r = v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]);
-    V3<R> x = pb + mul(Rb, r);  // rel O
+    V3<R> x = pb + mul(Rb, v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]));
     V3<R> X = x + base_abs;
     V3<R> n;
     R h = terrain_height<HF>(T, X.x, X.y, n);
     R pen = (h - X.z) * n.z;
-    if (pen > R(0)) {
-      V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
-      V3<R> vp = vo + cross(om, x);
-      R vn = dot(n, vp);
-      V3<R> vt = vp - vn * n;
-      R vtn = fsqrt(dot(vt, vt));
-      R cn = vn < R(0) ? dt * k + d : R(0);
-      R fn_est = k * pen + (vn < R(0) ? -d * vn : R(0));
-      R ct = mu * fn_est * (vtn > R(M.friction_vs) ? rcp(vtn) : ivs);
-      // force at the current velocity (explicit part) f = k pen n - C vp, C = cn nn^T + ct (I - nn^T)
-      V3<R> f = (k * pen - cn * vn) * n - ct * vt;
-      V3<R> tq = cross(x, f);
-      g[0] -= dt * tq.x; g[1] -= dt * tq.y; g[2] -= dt * tq.z;
-      g[3] -= dt * f.x;  g[4] -= dt * f.y;  g[5] -= dt * f.z;
-      // C = ct I + (cn - ct) n n^T ; J^T C J = ct * sum_e w_e w_e^T + (cn - ct) w_n w_n^T, e over world axes
-      V3<R> xn = cross(x, n);
-      R wn[6] = {xn.x, xn.y, xn.z, n.x, n.y, n.z};
-      sym_rank1(A, dt * (cn - ct), wn);
-      R ex[6] = {R(0), x.z, -x.y, R(1), R(0), R(0)};   // [x cross e_x ; e_x]
-      R ey[6] = {-x.z, R(0), x.x, R(0), R(1), R(0)};
-      R ez[6] = {x.y, -x.x, R(0), R(0), R(0), R(1)};
-      sym_rank1(A, dt * ct, ex);
-      sym_rank1(A, dt * ct, ey);
-      sym_rank1(A, dt * ct, ez);
-    }
+    if (pen > R(0)) contact_point(M, x, n, pen, Vb, mu, dt, A, g);
   }
 }
 template <typename R>
@@ -395,7 +429,23 @@ T1_HD void body_inertia(const DynModel& M, int b, R mass, R iscale, const M3<R>&
 // columns.  Only g_k, the joint sin/cos and the leaf pose/velocity cross between the passes (66 floats),
 // which is what keeps a leg inside the register file.  Ac_up / gc_up accumulate the leg composite.
 // ---------------------------------------------------------------------------------------------------
-template <typename R>
+// Contact layout known at compile time: CM = bit mask of the leg bodies (k = 0..5) that carry NPC contact
+// points each (the T1: shank k=3 and foot k=5, 8 points each; base box 8 points = 4 per leg).  CM < 0: read
+// the layout from the model at run time (host build, other robots).  The GPU kernel requires the T1 layout
+// (t1_model_conv.h checks it) so every contact loop is fully unrolled with its loads batched.
+constexpr int T1_LEG_CONTACT_MASK = (1 << 3) | (1 << 5);
+constexpr int T1_POINTS_PER_BODY = 8;
+
+template <int NP, typename R>
+T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb,
+                              V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
+  if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+}
+
+template <int K> using kconst = std::integral_constant<int, K>;
+
+template <int CM, typename R>
 T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>& P, R mu, const BaseFrame<R>& F,
                         const R q[NLEG], const R qd[NLEG], const R tau[NLEG], int leg, R dt, LegBlock<R>& out,
                         Sym6<R>& Ac_up, R gc_up[6]) {
@@ -435,10 +485,11 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
   Sym6<R> Ac;
   sym_zero(Ac);
   R gc[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
-#pragma unroll
-  for (int k = NLEG - 1; k >= 0; --k) {
+  // one instantiation per body (leaf first): every array index below is a compile-time constant
+  auto step = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
     const int b = 1 + 6 * leg + k, j = 6 * leg + k;
-    if (k < NLEG - 1) {  // step up from child k+1 (Sk still holds S_{k+1})
+    if constexpr (k < NLEG - 1) {  // step up from child k+1 (Sk still holds S_{k+1})
       const int bc = b + 1;
 #pragma unroll
       for (int i = 0; i < 6; ++i) V[i] -= Sk[i] * qd[k + 1];
@@ -452,8 +503,13 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
       body_inertia(M, b, P.mass[k], P.inertia_scale[k], Rk, pk, I);
       sym_add(Ac, I);
     }
-    const int c0 = M.contact_start[b], nc = M.contact_count[b];
-    if (nc > 0) body_contact(M, T, c0, c0 + nc, Rk, pk, F.abs, V, mu, dt, Ac, gc);
+    if constexpr (CM >= 0) {
+      if constexpr ((CM >> k) & 1)
+        body_contact_fixed<T1_POINTS_PER_BODY>(M, T, M.contact_start[b], Rk, pk, F.abs, V, mu, dt, Ac, gc);
+    } else {
+      const int c0 = M.contact_start[b], nc = M.contact_count[b];
+      if (nc > 0) body_contact(M, T, c0, c0 + nc, Rk, pk, F.abs, V, mu, dt, Ac, gc);
+    }
 #pragma unroll
     for (int i = 0; i < 6; ++i) gc[i] += g[k][i];
     R Fk[6];
@@ -481,7 +537,14 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
     }
 #pragma unroll
     for (int r = 0; r < 6; ++r) out.Bl[r][k] = Fk[r];
-  }
+  };
+  static_assert(NLEG == 6, "backward pass is written out for 6-DOF legs");
+  step(kconst<5>{});
+  step(kconst<4>{});
+  step(kconst<3>{});
+  step(kconst<2>{});
+  step(kconst<1>{});
+  step(kconst<0>{});
   sym_add(Ac_up, Ac);
 #pragma unroll
   for (int i = 0; i < 6; ++i) gc_up[i] += gc[i];
@@ -568,25 +631,26 @@ template <typename R> T1_HD void backsub_leg(const LegBlock<R>& lb, const R xb[6
 
 // One leg's contribution to the base block: base-contact share + leg composite - Schur complement.
 // Returns the factored leg block (for backsub_leg) and (Ab, rb) to be summed into the base system.
-template <typename R>
+template <int CM = -1, typename R>
 T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParams<R>& PB, const LegParams<R>& PL,
-                            const BaseFrame<R>& F,
-                            const R q[NLEG], const R qd[NLEG], const R tau[NLEG], int leg, R dt,
-                            LegBlock<R>& lb, Sym6<R>& Ab, R rb[6]) {
+                            const BaseFrame<R>& F, const R q[NLEG], const R qd[NLEG], const R tau[NLEG], int leg,
+                            R dt, LegBlock<R>& lb, Sym6<R>& Ab, R rb[6]) {
   sym_zero(Ab);
   R g[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
-  leg_assemble(M, T, PL, PB.friction, F, q, qd, tau, leg, dt, lb, Ab, g);
+  leg_assemble<CM>(M, T, PL, PB.friction, F, q, qd, tau, leg, dt, lb, Ab, g);
 #pragma unroll
   for (int i = 0; i < 6; ++i) rb[i] = -g[i];
   eliminate_leg(lb, Ab, rb);
   int cb, ce;
   base_contact_range(M, leg, cb, ce);
-  if (ce > cb) {
-    R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
-    body_contact(M, T, cb, ce, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) rb[i] -= gw[i];
+  R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+  if constexpr (CM >= 0) {
+    body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, cb, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
+  } else {
+    if (ce > cb) body_contact(M, T, cb, ce, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
   }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) rb[i] -= gw[i];
 }
 
 // Semi-implicit Euler of the base with the solved velocity change (+ the omega x v term that turns the

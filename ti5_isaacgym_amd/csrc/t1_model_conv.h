@@ -50,4 +50,17 @@ inline const char* make_dyn_model(const t1env_model* model, DynModel* dm) {
   return nullptr;
 }
 
+// The HIP kernel compiles the T1 contact layout in (t1_dynamics.h T1_LEG_CONTACT_MASK): base box and, on each
+// leg, the shank (k=3) and the foot (k=5) with T1_POINTS_PER_BODY points each; no points elsewhere.
+inline const char* check_fixed_contact_layout(const DynModel& dm) {
+  if (dm.contact_count[0] != T1_POINTS_PER_BODY) return "base must carry 8 contact points";
+  for (int leg = 0; leg < 2; ++leg)
+    for (int k = 0; k < NLEG; ++k) {
+      const bool has = (T1_LEG_CONTACT_MASK >> k) & 1;
+      if (dm.contact_count[1 + 6 * leg + k] != (has ? T1_POINTS_PER_BODY : 0))
+        return "leg contact points must be 8 on the shank and the foot and none elsewhere";
+    }
+  return nullptr;
+}
+
 }  // namespace t1

@@ -18,6 +18,8 @@
 #include "../../include/t1env.h"
 #include "t1_dynamics.h"
 #include "t1_model_conv.h"
+#include "t1env_device.h"
+#include "t1env_internal.h"
 
 using namespace t1;
 
@@ -57,212 +59,6 @@ struct t1env {
   Terrain terrain;
   uint8_t* d_hist_clear;  // (N,) history rows to zero in the next stack pass (reset_idx)
 };
-
-// =====================================================================================================
-// physics: decimation loop (legged_robot.py:399-434)
-// =====================================================================================================
-struct DevWriter {
-  float* rootp;
-  float* rigidp;
-  float* contactp;
-  __device__ void root(const float* v) {
-#pragma unroll
-    for (int i = 0; i < 13; ++i) rootp[i] = v[i];
-  }
-  __device__ void rigid(int b, const float* v) {
-#pragma unroll
-    for (int i = 0; i < 13; ++i) rigidp[b * 13 + i] = v[i];
-  }
-  __device__ void contact(int b, V3<float> f) {
-    contactp[b * 3 + 0] = f.x;
-    contactp[b * 3 + 1] = f.y;
-    contactp[b * 3 + 2] = f.z;
-  }
-};
-
-// per-env base parameters; PhysX combines shape and ground friction by averaging (third-party semantics,
-// unpinned)
-__device__ __forceinline__ void load_base_params(const DynModel& M, const t1env_buffers& B, int n,
-                                                 BaseParams<float>& P) {
-  P.mass = B.body_mass[n];
-  P.inertia_scale = P.mass / M.mass[0];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) P.com_disp[i] = B.com_disp[n * 3 + i];
-  P.friction = 0.5f * (B.friction[n] + M.ground_friction);
-}
-__device__ __forceinline__ void load_leg_params(const DynModel& M, const t1env_buffers& B, int n, int j0,
-                                                LegParams<float>& P) {
-#pragma unroll
-  for (int k = 0; k < NLEG; ++k) {
-    const float s = B.link_mass_scale[n * 12 + j0 + k];
-    P.mass[k] = M.mass[1 + j0 + k] * s;
-    P.inertia_scale[k] = s;
-    P.armature[k] = B.armature[n * 12 + j0 + k];
-  }
-}
-// root state (COM velocity) -> internal base state (base-origin velocity)
-__device__ __forceinline__ void load_base_state(const DynModel& M, const BaseParams<float>& P, const float* root,
-                                                BaseState<float>& s) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i) s.pos[i] = root[i];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) s.quat[i] = root[3 + i];
-  V3<float> c0 = base_com(M, P, quat_to_mat(s.quat[0], s.quat[1], s.quat[2], s.quat[3]));
-  V3<float> w = v3<float>(root[10], root[11], root[12]);
-  V3<float> vo = v3<float>(root[7], root[8], root[9]) - cross(w, c0);
-  s.w[0] = w.x; s.w[1] = w.y; s.w[2] = w.z;
-  s.vo[0] = vo.x; s.vo[1] = vo.y; s.vo[2] = vo.z;
-}
-
-#pragma clang fp contract(off)
-#include "t1env_post.h"
-
-// PD torque of one substep (legged_robot.py:1019-1074): lagged action, randomized gains, viscous +
-// Coulomb friction, torque multiplier redrawn every substep, clip to 0.85 * effort.
-// Joints j0 .. j0+NJ-1 (NJ = 12: whole env; NJ = 6: one leg of the two-wave kernel).
-template <int NJ>
-__device__ __forceinline__ void pd_torques(const DynModel& M, const t1env_config& C, const t1env_buffers& B, int n,
-                                           uint32_t genv, uint32_t ctr, int sub, int lag, int j0, const float q[NJ],
-                                           const float qd[NJ], float tau[NJ]) {
-  const int d = lag > sub ? (lag - sub + 9) / 10 : 0;
-  const float* la = B.act_hist + ((size_t)n * 4 + ((ctr - (uint32_t)d) & 3u)) * 12;
-#pragma unroll
-  for (int jj = 0; jj < NJ; ++jj) {
-    const int j = j0 + jj;
-    const float kp = B.kp[n * 12 + j], kd = B.kd[n * 12 + j];
-    float t = kp * (((la[j] + M.default_dof_pos[j]) - q[jj]) + B.motor_offsets[n * 12 + j]);
-    t = t - kd * qd[jj];
-    t = t - B.viscous[n * 12 + j] * qd[jj];
-    t = t - B.coulomb[n * 12 + j] * signf(qd[jj]);
-    const float tm = rand_float(C.torque_mult_range[0], C.torque_mult_range[1], C.seed, genv, ctr,
-                                SLOT_TORQUE_MULT + sub * 12 + j);
-    t = t * tm;
-    const float lim = M.torque_limit[j];
-    tau[jj] = fminf(fmaxf(t, -lim), lim);
-  }
-}
-
-__device__ __forceinline__ void capture_imu(const float quat[4], const float w_world[3], float* dst) {
-  float av[3], e[3];
-  quat_rotate_inverse(quat, w_world, av);
-  euler_xyz(quat, e);
-  dst[0] = av[0]; dst[1] = av[1]; dst[2] = av[2];
-  dst[3] = e[0]; dst[4] = e[1]; dst[5] = e[2];
-}
-
-// ---------------------------------------------------------------------------------------------------
-// k_dynamics: the decimation loop with the articulated-body solver.  A workgroup owns 64 envs and runs
-// them on two waves: wave 0 handles every env's left leg, wave 1 the right leg (the leg index is
-// wave-uniform, so all model reads are scalar loads).  Per substep each wave eliminates its leg into a
-// 27-float base-block contribution (t1_dynamics.h leg_contribution), the two contributions meet in LDS
-// (double-buffered by substep parity -> one barrier per substep), and both waves solve the 6x6 base system
-// redundantly, so the base state stays bit-identical in both without further exchange.
-// ---------------------------------------------------------------------------------------------------
-constexpr int DYN_ENVS = 64;
-constexpr int DYN_BLOCK = 2 * DYN_ENVS;
-constexpr int XCH = 27;  // Sym6 (21) + rhs (6)
-
-__global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restrict__ Mp,
-                                                        const t1env_config* __restrict__ Cp, t1env_buffers B,
-                                                        Terrain T, const float* __restrict__ actions,
-                                                        t1env_step_args A) {
-  __shared__ float xch[2][2][XCH][DYN_ENVS];  // [substep parity][leg][value][env]
-  const t1env_config& C = *Cp;
-  const DynModel& M = *Mp;
-  const int leg = __builtin_amdgcn_readfirstlane((int)threadIdx.x / DYN_ENVS);
-  const int lane = threadIdx.x % DYN_ENVS;
-  const int N = C.num_envs;
-  const bool active = (int)(blockIdx.x * DYN_ENVS) + lane < N;
-  const int n = active ? blockIdx.x * DYN_ENVS + lane : N - 1;  // inactive lanes shadow a valid env, never store
-  const int j0 = 6 * leg;
-  const uint32_t genv = (uint32_t)(C.env_offset + n);
-  const uint32_t ctr = A.counter;
-  // actions = clip(actions); push the scaled action into this step's history slot
-  if (active) {
-    float* slot = B.act_hist + ((size_t)n * 4 + (ctr & 3u)) * 12;
-#pragma unroll
-    for (int k = 0; k < NLEG; ++k) {
-      const float a = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
-      B.actions[n * 12 + j0 + k] = a;
-      slot[j0 + k] = a * C.action_scale;
-    }
-  }
-  const int lag = B.lag_timestep[n];
-  const int s_dof = 9 - B.dof_lag_timestep[n] % 10, s_imu = 9 - B.imu_lag_timestep[n] % 10;
-  float* dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
-  float* imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 6;
-  const float dt = C.sim_dt;
-  BaseParams<float> PB;
-  LegParams<float> PL;
-  load_base_params(M, B, n, PB);
-  load_leg_params(M, B, n, j0, PL);
-  BaseState<float> sb;
-  load_base_state(M, PB, B.root_states + (size_t)n * 13, sb);
-  float q[NLEG], qd[NLEG], tau[NLEG];
-#pragma unroll
-  for (int k = 0; k < NLEG; ++k) {
-    q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
-    qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
-  }
-  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
-  for (int sub = 0; sub < C.decimation; ++sub) {
-    // re-derive the model pointer each substep so the ~200 model scalars are re-read (scalar cache hits)
-    // instead of being hoisted out of the loop and spilled
-    const DynModel* Ml = Mp;
-    asm volatile("" : "+s"(Ml));
-    const DynModel& M = *Ml;
-    pd_torques<NLEG>(M, C, B, n, genv, ctr, sub, lag, j0, q, qd, tau);
-    BaseFrame<float> F;
-    base_frame(sb, F);
-    LegBlock<float> lb;
-    {
-      Sym6<float> Ab;
-      float rb[6];
-      leg_contribution(M, T, PB, PL, F, q, qd, tau, leg, dt, lb, Ab, rb);
-      float* X = &xch[sub & 1][leg][0][lane];
-#pragma unroll
-      for (int i = 0; i < 21; ++i) X[i * DYN_ENVS] = Ab.a[i];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) X[(21 + i) * DYN_ENVS] = rb[i];
-    }
-    Sym6<float> Ac;
-    float r[6];
-    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) r[i] = -r[i];
-    __syncthreads();
-#pragma unroll
-    for (int l = 0; l < 2; ++l) {
-      const float* Y = &xch[sub & 1][l][0][lane];
-#pragma unroll
-      for (int i = 0; i < 21; ++i) Ac.a[i] += Y[i * DYN_ENVS];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) r[i] += Y[(21 + i) * DYN_ENVS];
-    }
-    solve_base(Ac, r);
-    float dq[NLEG];
-    backsub_leg(lb, r, dq);
-    integrate_base(sb, r, dt);
-    integrate_leg(M, leg, q, qd, dq, dt);
-    if (active && sub == s_dof) {
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) { dof_dst[j0 + k] = q[k]; dof_dst[12 + j0 + k] = qd[k]; }
-    }
-    if (active && leg == 0 && sub == s_imu) capture_imu(sb.quat, sb.w, imu_dst);
-  }
-  if (!active) return;
-  BaseFrame<float> F;
-  base_frame(sb, F);
-  DevWriter W{B.root_states + (size_t)n * 13, B.rigid_state + (size_t)n * 169, B.contact_forces + (size_t)n * 39};
-  if (leg == 0) report_base(M, T, PB, sb, F, W);
-  report_leg(M, T, PB.friction, F, q, qd, leg, W);
-#pragma unroll
-  for (int k = 0; k < NLEG; ++k) {
-    B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
-    B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
-    B.torques[n * 12 + j0 + k] = tau[k];
-  }
-}
 
 // k_physics_injected: the same decimation loop with the physics states supplied by the caller (golden
 // parity harness: the reference ran on identical injected states), so PD / lag / sensor capture are checked
@@ -1032,6 +828,7 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
     return fail(T1ENV_E_ARG, "t1env_create: sensor/actuator lag rings assume decimation == 10");
   DynModel dm;
   if (const char* err = make_dyn_model(model, &dm)) return fail(T1ENV_E_ARG, err);
+  if (const char* err = check_fixed_contact_layout(dm)) return fail(T1ENV_E_ARG, err);
   t1env* e = (t1env*)calloc(1, sizeof(t1env));
   if (!e) return fail(T1ENV_E_STATE, "t1env_create: out of host memory");
   e->cfg = *cfg;
@@ -1090,8 +887,7 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
     hipLaunchKernelGGL(k_physics_injected, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
                        actions, *a, *inj);
   else
-    hipLaunchKernelGGL(k_dynamics, dim3(grid(N, DYN_ENVS)), dim3(DYN_BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
-                       e->terrain, actions, *a);
+    HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, N, s));
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
   t = t_begin(e, 1, s);

@@ -1,0 +1,11 @@
+// t1env_internal.h -- entry points shared between the library's translation units (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/t1env.h"
+#include "t1_dynamics.h"
+
+// k_dynamics launch (t1env_dynamics.hip); returns a hipError_t
+int t1_launch_dynamics(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B,
+                       const t1::Terrain& T, const float* actions, const t1env_step_args& A, int num_envs,
+                       hipStream_t s);
