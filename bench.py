@@ -12,9 +12,11 @@ env's own gait scheduler draws the commands.  One step = one env.step(actions) f
 ranks (weak scaling; the env step has no collective), timed region bracketed by barrier + synchronize,
 max over ranks.
 
-roofline: SURVEY.md §8(d) algorithmic bytes B_alg = 30,678 B per env-step over the step's GPU time (sum of
-the kernels' HIP-event durations on the env's stream inside the timed region), against the 8 TB/s HBM3E
-peak; per-kernel event times and each kernel's own algorithmic bytes are reported alongside.
+roofline: SURVEY.md §8(d): achieved = env_steps_per_s x B_alg (30,678 algorithmic bytes per env-step) against
+the 8 TB/s HBM3E peak; `traffic` = PMC-measured HBM bytes per step (profiles/traffic_*.json, tools/
+pmc_traffic.py).  Per-kernel durations are measured live with HIP events around each launch on every
+--time-every'th timed step (event records cost host time, so not on every step), with each kernel's own
+algorithmic bytes; the dominant kernel is k_dynamics (VALU-bound).
 cpu_baseline: the build's CPU restatement (numpy oracle post-physics + OpenMP dynamics), rank 0, N = 1 only.
 """
 import argparse
@@ -31,13 +33,13 @@ sys.path.insert(0, REPO)
 
 B_ALG = 30678          # algorithmic bytes per env-step (fp32, default t1 config)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-KERNELS = ["k_physics", "k_post_a", "k_post_b", "k_stack", "k_finalize"]
-# per-kernel algorithmic bytes per env (reads + writes it must do; DESIGN.md §rooflines)
+KERNELS = ["k_dynamics", "k_post_a", "k_post_b", "k_shift", "k_finalize"]
+# per-kernel algorithmic bytes per env (reads + writes it must do; DESIGN.md §3)
 KERNEL_BYTES = {
-    "k_physics": 4 * (13 + 24 + 12 + 48 + 12 * 6 + 13 + 3 + 3) + 4 * (13 + 24 + 169 + 39 + 12 + 12 + 12 + 24 + 6),
+    "k_dynamics": 4 * (13 + 24 + 12 + 48 + 12 * 6 + 13 + 3 + 3) + 4 * (13 + 24 + 169 + 39 + 12 + 12 + 12 + 24 + 6),
     "k_post_a": 4 * (13 + 24 + 169 + 39 + 12 * 5 + 6 + 4 + 24 + 12 + 3 + 6 + 8) + 4 * (3 * 4 + 6 + 3 + 2 + 4 + 24 + 3 + 6),
     "k_post_b": 4 * (24 + 13 + 12 * 2 + 3 * 3 + 39 + 24 + 6 + 8) + 4 * (47 + 73 + 12 * 4 + 6),
-    "k_stack": 4 * ((3102 - 47) + (219 - 73)) + 4 * (3102 + 219),
+    "k_shift": 2 * 4 * ((3102 - 47) + (219 - 73)),
     "k_finalize": 1,
 }
 
@@ -50,6 +52,9 @@ def parse():
     p.add_argument("--num-envs", type=int, default=8192)
     p.add_argument("--mesh", default="trimesh", choices=["plane", "heightfield", "trimesh"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--time-every", type=int, default=8,
+                   help="record per-kernel HIP events on every k-th timed step (event records cost host time; "
+                        "0 = never, 1 = every step)")
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
@@ -104,7 +109,6 @@ def main():
     env.reset()
     for i in range(args.warmup):
         env.step(pool[i % 8])
-    env.set_timing(True)
 
     def barrier():
         if world > 1:
@@ -113,7 +117,10 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
+    te = args.time_every
     for i in range(args.steps):
+        if te:
+            env.set_timing(i % te == 0, reset=False)  # sampled live per-kernel timing inside the timed region
         env.step(pool[i % 8])
     torch.cuda.synchronize(dev)
     barrier()
@@ -131,15 +138,18 @@ def main():
         return
     steps = args.steps
     value = N * world * steps / elapsed
-    gpu_ms = sum(kt[k]["ms"] for k in KERNELS) / steps
+    # live per-kernel HIP-event timing on the sampled steps (k_shift runs on the side stream, overlapping)
     per_kernel = {}
     for k in KERNELS:
         ms = kt[k]["ms"] / max(1, kt[k]["launches"])
-        per_kernel[k] = {"avg_ms": round(ms, 5), "launches": kt[k]["launches"],
+        per_kernel[k] = {"avg_ms": round(ms, 5), "timed_launches": kt[k]["launches"],
                          "alg_bytes_per_launch": KERNEL_BYTES[k] * N,
                          "alg_GBs": round(KERNEL_BYTES[k] * N / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
     dom = max(KERNELS, key=lambda k: kt[k]["ms"])
-    achieved = B_ALG * N / (gpu_ms * 1e-3) / 1e9
+    step_span_ms = kt["step"]["ms"] / kt["step"]["launches"] if kt["step"]["launches"] else None
+    # roofline.achieved = env_steps_per_s x B_alg (the env step is the unit of work; on one GPU
+    # the rank's steps/s)
+    achieved = value / world * B_ALG / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -156,10 +166,11 @@ def main():
         "config": {"workload": f"t1_dh_stand {N} envs/GPU, {args.mesh} curriculum terrain + full DR, "
                                "random N(0,1) actions (policy excluded), 10 substeps/step",
                    "num_envs_per_gpu": N, "global_envs": N * world, "mesh": args.mesh, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": "t1env_step (k_physics+k_post_a+k_post_b+k_stack+k_finalize)",
+        "roofline": {"bound": "hbm", "kernel": "t1env_step (k_dynamics || k_shift, k_post_a, k_post_b, k_finalize)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes_per_env_step": B_ALG, "gpu_ms_per_step": round(gpu_ms, 4),
+                     "alg_bytes_per_step": B_ALG * N, "alg_bytes_per_env_step": B_ALG,
+                     "step_span_ms_timed": round(step_span_ms, 4) if step_span_ms else None,
                      "dominant_kernel": dom, "kernels": per_kernel},
         "finite": ok,
     }

@@ -199,18 +199,24 @@ int t1env_reset_all(t1env* env, const t1env_step_args* args, void* stream);
 /* Phase A of post-physics ends with the per-env reset decision; curriculum steps (counter+1) % 2400 == 0
  * need the host to read ep_accum between the phases, so the step is exposed in two halves:
  *   t1env_step_physics_and_rewards  -> physics, post_a (callback, termination, rewards, extras reduction)
- *   t1env_step_reset_and_observe    -> post_b (reset_idx of flagged envs, observations, history stack)
+ *   t1env_step_reset_and_observe    -> post_b (reset_idx of flagged envs, observations, newest history frame)
+ * The 65 older history frames are shifted by a kernel the library forks onto an internal stream at the start
+ * of phase A and joins before post_b (it reads only the previous step's buffer).
  * t1env_step() runs both back to back (no host sync). */
 int t1env_step(t1env* env, const float* actions, const t1env_step_args* args, void* stream);
 int t1env_step_physics_and_rewards(t1env* env, const float* actions, const t1env_step_args* args, void* stream);
 int t1env_step_reset_and_observe(t1env* env, const t1env_step_args* args, void* stream);
 int t1env_step_injected(t1env* env, const float* actions, const t1env_step_args* args, const t1env_injected* inj,
                         void* stream);
-/* Per-kernel timing with HIP events recorded around every launch (bench.py's live roofline).  Kernel ids:
- * 0 k_physics, 1 k_post_a, 2 k_post_b, 3 k_stack, 4 k_finalize(+terrain-level sum). get_timing synchronises
- * and returns the summed milliseconds and launch counts per kernel id since the last enable. */
+/* Per-kernel timing with HIP events recorded around every launch (bench.py's live roofline).  Ids:
+ * 0 k_dynamics (or the injected-physics kernel), 1 k_post_a, 2 k_post_b, 3 k_shift (internal side stream,
+ * overlapping 0-1), 4 k_finalize(+terrain-level sum), 5 the whole step (phase A start .. phase B end on the
+ * caller's stream).  get_timing synchronises and returns summed milliseconds and launch counts per id since
+ * the last enable. */
+#define T1ENV_NTIMERS 6
+/* enable: bit 0 = record events from now on; bit 1 = keep (do not clear) the events recorded so far */
 int t1env_set_timing(t1env* env, int32_t enable);
-int t1env_get_timing(t1env* env, double* ms /* [5] */, int32_t* launches /* [5] */);
+int t1env_get_timing(t1env* env, double* ms /* [T1ENV_NTIMERS] */, int32_t* launches /* [T1ENV_NTIMERS] */);
 const char* t1env_last_error(void);
 const char* t1env_version(void);
 

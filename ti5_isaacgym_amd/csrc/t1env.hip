@@ -7,8 +7,11 @@
 //                episode sums, per-step extras reduction (legged_robot.py:458-489, 509-517, 654-680)
 //   k_post_b   : masked reset_idx, compute_observations -> newest obs/priv frame, last_* bookkeeping
 //                (legged_robot.py:490-502, t1_dh_stand_env.py:368-559)
-//   k_stack    : 66-frame / 3-frame history shift into the ping-pong output buffers, thread per 4 floats,
-//                fully coalesced (the HBM-dominant part: ~24 KB per env per step)
+//   k_shift    : 65 older frames of the 66-frame (and 3-frame critic) history shifted into the ping-pong
+//                output buffer, thread per 4 floats, fully coalesced (the HBM-dominant part: ~26 KB per env
+//                per step).  It does not depend on this step's physics, so it runs on an internal side stream
+//                concurrently with k_dynamics (which leaves half the CUs idle at 8192 envs); k_post_b joins it
+//                before writing the newest frame and zeroing the history rows of reset envs.
 // See include/t1env.h for the ABI and DESIGN.md for layouts and rooflines.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -43,7 +46,7 @@ constexpr int BLOCK = 64;  // one wave per workgroup: 8192 envs -> 128 workgroup
 
 }  // namespace
 
-constexpr int NKERN = 5;
+constexpr int NKERN = 6;  // 0 physics, 1 post_a, 2 post_b, 3 shift (side stream), 4 finalize, 5 whole step
 constexpr int MAX_TIMED = 1 << 14;
 
 struct t1env {
@@ -57,7 +60,10 @@ struct t1env {
   DynModel* d_model;
   t1env_config* d_cfg;
   Terrain terrain;
-  uint8_t* d_hist_clear;  // (N,) history rows to zero in the next stack pass (reset_idx)
+  hipStream_t side;       // history shift, forked from the caller's stream at the start of each step
+  hipEvent_t ev_fork, ev_join;
+  int shift_pending;      // a shift was forked in phase A and not yet joined
+  int step_timer;         // timing slot of the current step span (phase A start .. phase B end)
 };
 
 // k_physics_injected: the same decimation loop with the physics states supplied by the caller (golden
@@ -547,20 +553,13 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
 // =====================================================================================================
 // post-physics phase B: reset + observations (legged_robot.py:490-502, t1:368-481)
 // =====================================================================================================
-__global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
-                                                  t1env_buffers B, t1env_step_args A, uint8_t* __restrict__ hist_clear) {
-  const int n = blockIdx.x * BLOCK + threadIdx.x;
-  const t1env_config& C = *Cp;
-  if (n >= C.num_envs) return;
-  const DynModel& M = *Mp;
+__device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                           const t1env_step_args& A, int n) {
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   const uint32_t ctr = A.counter + 1u;
   const bool do_reset = B.reset_buf[n] != 0;
   const bool any_reset = B.ep_accum[24] > 0.0f;  // reset_idx runs only if some env resets (len(env_ids) > 0)
-  if (do_reset) {
-    reset_env(M, C, B, A, n, genv, ctr, true);
-    hist_clear[n] = 1;
-  }
+  if (do_reset) reset_env(M, C, B, A, n, genv, ctr, true);
   if (any_reset) resample_commands(C, B, A, n, genv, ctr);
   // ---- compute_observations
   const float* cmd = B.commands + n * 4;
@@ -641,18 +640,37 @@ __global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ M
   for (int i = 0; i < 6; ++i) B.last_root_vel[n * 6 + i] = B.root_states[n * 13 + 7 + i];
 }
 
+__global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
+                                                  t1env_buffers B, t1env_step_args A) {
+  const int n = blockIdx.x * BLOCK + threadIdx.x;
+  const t1env_config& C = *Cp;
+  const bool live = n < C.num_envs;
+  const bool do_reset = live && B.reset_buf[n] != 0;
+  if (live) post_b_env(*Mp, C, B, A, n);
+  // reset_idx zeroes the obs / critic history of the reset envs (t1:548-558): k_shift wrote the 65 (2) older
+  // frames of every row, so the wave zeroes those of its reset envs here, one row at a time, coalesced
+  uint64_t m = __ballot(do_reset);
+  while (m) {
+    const int l = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    const size_t row = (size_t)blockIdx.x * BLOCK + l;
+    float* o = B.obs_buf[A.obs_slot] + row * (T1_NOBS * T1_HIST);
+    for (int c = threadIdx.x; c < T1_NOBS * (T1_HIST - 1); c += BLOCK) o[c] = 0.0f;
+    float* p = B.priv_buf[A.obs_slot] + row * (T1_NPRIV * T1_CHIST);
+    for (int c = threadIdx.x; c < T1_NPRIV * (T1_CHIST - 1); c += BLOCK) p[c] = 0.0f;
+  }
+}
+
 // =====================================================================================================
-// history stack: out[n, :F*(H-1)] = clear[n] ? 0 : in[n, F:]  -- flat shift by F floats (the newest frame
-// was written by k_post_b).  One thread per 4 output floats; the shifted source is assembled from two
-// aligned 16-B loads (lane's own + neighbour via __shfl).  Block 0 also finalises the extras.
+// history shift: out[n, :F*(H-1)] = in[n, F:]  -- a flat shift by F floats of every row; the newest frame
+// (columns >= F*(H-1)) is left to k_post_b, which also zeroes the older frames of reset envs.  One thread per
+// 4 output floats; the shifted source is assembled from two aligned 16-B loads.
 // =====================================================================================================
 template <int F, int H>
-__device__ __forceinline__ void stack_rows(const float* __restrict__ in, float* __restrict__ out,
-                                           const uint8_t* __restrict__ clear, int64_t total, int64_t i4) {
+__device__ __forceinline__ void shift_rows(const float* __restrict__ in, float* __restrict__ out, int64_t total,
+                                           int64_t i4) {
   constexpr int ROW = F * H;
   const int64_t i = i4 * 4;
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  // source elements i+F .. i+F+3 (same row as output element when its column < ROW - F)
   const int64_t s = i + F;
   const int64_t sa = s & ~(int64_t)3;
   const int rem = (int)(s - sa);
@@ -663,43 +681,37 @@ __device__ __forceinline__ void stack_rows(const float* __restrict__ in, float* 
     if (sa + 7 < total) b = *reinterpret_cast<const float4*>(in + sa + 4);
     else { for (int k = 0; k < 4; ++k) if (sa + 4 + k < total) (&b.x)[k] = in[sa + 4 + k]; }
   }
-  float src[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  float o[4];
+  const float src[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  // the 4 outputs are all older-frame columns of one row unless the chunk touches a row's newest frame
+  const int64_t row0 = i / ROW;
+  const int col0 = (int)(i - row0 * ROW);
+  if (col0 + 3 < ROW - F && i + 3 < total) {
+    *reinterpret_cast<float4*>(out + i) = make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]);
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t e = i + k;
-    if (e >= total) { o[k] = 0.f; continue; }
+    if (e >= total) break;
     const int64_t row = e / ROW;
-    const int col = (int)(e - row * ROW);
-    if (col >= ROW - F) {  // newest frame: already written
-      o[k] = out[e];
-    } else {
-      o[k] = clear[row] ? 0.0f : src[rem + k];
-    }
-  }
-  if (i + 3 < total) {
-    *reinterpret_cast<float4*>(out + i) = make_float4(o[0], o[1], o[2], o[3]);
-  } else {
-    for (int k = 0; k < 4; ++k) if (i + k < total) out[i + k] = o[k];
+    if ((int)(e - row * ROW) < ROW - F) out[e] = src[rem + k];
   }
 }
 
-__global__ __launch_bounds__(256) void k_stack(const float* __restrict__ obs_in, float* __restrict__ obs_out,
+__global__ __launch_bounds__(256) void k_shift(const float* __restrict__ obs_in, float* __restrict__ obs_out,
                                                const float* __restrict__ priv_in, float* __restrict__ priv_out,
-                                               const uint8_t* __restrict__ clear, int num_envs, int64_t n4_obs,
-                                               int64_t n4_priv) {
+                                               int num_envs, int64_t n4_obs, int64_t n4_priv) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t tot_obs = (int64_t)num_envs * T1_NOBS * T1_HIST;
   const int64_t tot_priv = (int64_t)num_envs * T1_NPRIV * T1_CHIST;
-  if (tid < n4_obs) stack_rows<T1_NOBS, T1_HIST>(obs_in, obs_out, clear, tot_obs, tid);
-  else if (tid < n4_obs + n4_priv) stack_rows<T1_NPRIV, T1_CHIST>(priv_in, priv_out, clear, tot_priv, tid - n4_obs);
+  if (tid < n4_obs) shift_rows<T1_NOBS, T1_HIST>(obs_in, obs_out, tot_obs, tid);
+  else if (tid < n4_obs + n4_priv) shift_rows<T1_NPRIV, T1_CHIST>(priv_in, priv_out, tot_priv, tid - n4_obs);
 }
 
-// extras finalisation + clear flags (runs after k_stack on the same stream)
-__global__ void k_finalize(t1env_buffers B, const t1env_config* __restrict__ Cp, uint8_t* __restrict__ hist_clear) {
+// extras finalisation (one block)
+__global__ void k_finalize(t1env_buffers B, const t1env_config* __restrict__ Cp) {
   const t1env_config& C = *Cp;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0) {
+  {
     __shared__ float cnt;
     if (threadIdx.x == 0) cnt = B.ep_accum[24];
     __syncthreads();
@@ -708,7 +720,6 @@ __global__ void k_finalize(t1env_buffers B, const t1env_config* __restrict__ Cp,
     __syncthreads();
     if (threadIdx.x < 32) B.ep_accum[threadIdx.x] = 0.0f;
   }
-  if (hist_clear && t < C.num_envs) hist_clear[t] = 0;
 }
 
 // terrain-level sum for extras["episode"]["terrain_level"] (only meaningful on reset steps)
@@ -772,7 +783,7 @@ __global__ __launch_bounds__(BLOCK) void k_init(const DynModel* __restrict__ Mp,
 
 // reset_idx(arange(N)) -- LeggedRobot.reset() (legged_robot.py:450-455)
 __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
-                                                     t1env_buffers B, t1env_step_args A, uint8_t* __restrict__ hist_clear) {
+                                                     t1env_buffers B, t1env_step_args A) {
   const int n0 = blockIdx.x * BLOCK + threadIdx.x;
   const t1env_config& C = *Cp;
   const bool live = n0 < C.num_envs;
@@ -785,7 +796,6 @@ __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict_
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   reset_env(*Mp, C, B, A, n, genv, A.counter, true);
   resample_commands(C, B, A, n, genv, A.counter);
-  hist_clear[n] = 1;
 }
 
 // =====================================================================================================
@@ -837,14 +847,15 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   hipError_t err;
   if ((err = hipMalloc(&e->d_model, sizeof(DynModel))) != hipSuccess ||
       (err = hipMalloc(&e->d_cfg, sizeof(t1env_config))) != hipSuccess ||
-      (err = hipMalloc(&e->d_hist_clear, (size_t)cfg->num_envs)) != hipSuccess) {
+      (err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking)) != hipSuccess ||
+      (err = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+      (err = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "t1env_create: hipMalloc: %s", hipGetErrorString(err));
     free(e);
     return (int)err;
   }
   HIP_TRY(hipMemcpy(e->d_model, &dm, sizeof(DynModel), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_cfg, cfg, sizeof(t1env_config), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(e->d_hist_clear, 0, (size_t)cfg->num_envs));
   HIP_TRY(hipMemset(e->buf.ep_accum, 0, 32 * sizeof(float)));
   *out = e;
   return 0;
@@ -854,7 +865,10 @@ int t1env_destroy(t1env* e) {
   if (!e) return 0;
   (void)hipFree(e->d_model);
   (void)hipFree(e->d_cfg);
-  (void)hipFree(e->d_hist_clear);
+  if (e->side) (void)hipStreamSynchronize(e->side);
+  if (e->side) (void)hipStreamDestroy(e->side);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   for (int i = 0; i < e->n_events; ++i) {
     (void)hipEventDestroy(e->ev_start[i]);
     (void)hipEventDestroy(e->ev_stop[i]);
@@ -879,9 +893,30 @@ int t1env_set_terrain(t1env* e, const int16_t* h, int32_t rows, int32_t cols, fl
   return 0;
 }
 
+// fork the history shift of this step onto the side stream (it reads only the previous step's buffer)
+static int fork_shift(t1env* e, const t1env_step_args* a, hipStream_t s) {
+  if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
+  const int N = e->cfg.num_envs;
+  const int64_t n4o = ((int64_t)N * T1_NOBS * T1_HIST + 3) / 4;
+  const int64_t n4p = ((int64_t)N * T1_NPRIV * T1_CHIST + 3) / 4;
+  const int in = a->obs_slot ^ 1, outs = a->obs_slot;
+  HIP_TRY(hipEventRecord(e->ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+  const int t = t_begin(e, 3, e->side);
+  hipLaunchKernelGGL(k_shift, dim3((unsigned)((n4o + n4p + 255) / 256)), dim3(256), 0, e->side, e->buf.obs_buf[in],
+                     e->buf.obs_buf[outs], e->buf.priv_buf[in], e->buf.priv_buf[outs], N, n4o, n4p);
+  t_end(e, t, e->side);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(e->ev_join, e->side));
+  e->shift_pending = 1;
+  return 0;
+}
+
 static int launch_physics(t1env* e, const float* actions, const t1env_step_args* a, const t1env_injected* inj,
                           hipStream_t s) {
   const int N = e->cfg.num_envs;
+  e->step_timer = t_begin(e, 5, s);
+  if (int rc = fork_shift(e, a, s)) return rc;
   int t = t_begin(e, 0, s);
   if (inj)
     hipLaunchKernelGGL(k_physics_injected, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
@@ -914,17 +949,14 @@ int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* strea
   if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
   hipStream_t s = (hipStream_t)stream;
   const int N = e->cfg.num_envs;
+  if (!e->shift_pending) {  // phase B without phase A on this env: shift now, in order
+    e->step_timer = -1;
+    if (int rc = fork_shift(e, a, s)) return rc;
+  }
+  HIP_TRY(hipStreamWaitEvent(s, e->ev_join, 0));
+  e->shift_pending = 0;
   int t = t_begin(e, 2, s);
-  hipLaunchKernelGGL(k_post_b, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,
-                     e->d_hist_clear);
-  t_end(e, t, s);
-  HIP_TRY(hipGetLastError());
-  const int64_t n4o = ((int64_t)N * T1_NOBS * T1_HIST + 3) / 4;
-  const int64_t n4p = ((int64_t)N * T1_NPRIV * T1_CHIST + 3) / 4;
-  const int in = a->obs_slot ^ 1, outs = a->obs_slot;
-  t = t_begin(e, 3, s);
-  hipLaunchKernelGGL(k_stack, dim3((unsigned)((n4o + n4p + 255) / 256)), dim3(256), 0, s, e->buf.obs_buf[in],
-                     e->buf.obs_buf[outs], e->buf.priv_buf[in], e->buf.priv_buf[outs], e->d_hist_clear, N, n4o, n4p);
+  hipLaunchKernelGGL(k_post_b, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a);
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
   t = t_begin(e, 4, s);
@@ -932,9 +964,11 @@ int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* strea
     hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
     HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_finalize, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg, e->d_hist_clear);
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg);
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
+  t_end(e, e->step_timer, s);
+  e->step_timer = -1;
   return 0;
 }
 
@@ -946,8 +980,8 @@ int t1env_step(t1env* e, const float* actions, const t1env_step_args* a, void* s
 
 int t1env_set_timing(t1env* e, int32_t enable) {
   if (!e) return fail(T1ENV_E_ARG, "t1env_set_timing: null env");
-  e->timing = enable ? 1 : 0;
-  e->n_timed = 0;
+  e->timing = (enable & 1) ? 1 : 0;
+  if (!(enable & 2)) e->n_timed = 0;  // bit 1: keep the events recorded so far (sampled timing)
   return 0;
 }
 
@@ -968,16 +1002,19 @@ int t1env_reset_all(t1env* e, const t1env_step_args* a, void* stream) {
   if (!e || !a) return fail(T1ENV_E_ARG, "t1env_reset_all: null argument");
   hipStream_t s = (hipStream_t)stream;
   const int N = e->cfg.num_envs;
-  hipLaunchKernelGGL(k_reset_all, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,
-                     e->d_hist_clear);
+  hipLaunchKernelGGL(k_reset_all, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a);
   HIP_TRY(hipGetLastError());
   if (e->cfg.terrain_curriculum) {
     hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
     HIP_TRY(hipGetLastError());
   }
-  // extras of the reset; history rows stay flagged (hist_clear) for the next stack pass
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg, (uint8_t*)nullptr);
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg);
   HIP_TRY(hipGetLastError());
+  // every history row restarts from zeros: clear both ping-pong buffers (the next step shifts from either)
+  for (int k = 0; k < 2; ++k) {
+    HIP_TRY(hipMemsetAsync(e->buf.obs_buf[k], 0, sizeof(float) * (size_t)N * T1_NOBS * T1_HIST, s));
+    HIP_TRY(hipMemsetAsync(e->buf.priv_buf[k], 0, sizeof(float) * (size_t)N * T1_NPRIV * T1_CHIST, s));
+  }
   return 0;
 }
 

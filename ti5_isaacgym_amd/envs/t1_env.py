@@ -517,15 +517,16 @@ class T1DHStandEnv(VecEnv):
         obs, priv, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
         return obs, priv
 
-    def set_timing(self, enable=True):
-        """Record HIP events around every kernel launch (bench.py's live per-kernel timing)."""
-        _lib.check(self._lib.t1env_set_timing(self._handle, int(enable)), "t1env_set_timing")
+    def set_timing(self, enable=True, reset=True):
+        """Record HIP events around every kernel launch (bench.py's live per-kernel timing).  reset=False keeps
+        the events recorded so far (bench.py samples every k-th step)."""
+        _lib.check(self._lib.t1env_set_timing(self._handle, int(enable) | (0 if reset else 2)), "t1env_set_timing")
 
     def get_timing(self):
-        ms = (_lib.C.c_double * 5)()
-        n = (_lib.C.c_int32 * 5)()
+        names = ["k_dynamics", "k_post_a", "k_post_b", "k_shift", "k_finalize", "step"]
+        ms = (_lib.C.c_double * len(names))()
+        n = (_lib.C.c_int32 * len(names))()
         _lib.check(self._lib.t1env_get_timing(self._handle, ms, n), "t1env_get_timing")
-        names = ["k_physics", "k_post_a", "k_post_b", "k_stack", "k_finalize"]
         return {k: {"ms": ms[i], "launches": n[i]} for i, k in enumerate(names)}
 
     def render(self, sync_frame_time=True):
