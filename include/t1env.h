@@ -42,6 +42,8 @@ extern "C" {
 #define T1_CHIST 3        /* c_frame_stack */
 #define T1_NREW 24        /* active reward terms, alphabetical order */
 
+#define T1ENV_EXTRAS_RING 64  /* steps an extras["episode"] view stays valid (the runner logs every 24) */
+
 #define T1ENV_E_ARG (-1)
 #define T1ENV_E_SHAPE (-2)
 #define T1ENV_E_STATE (-3)
@@ -160,7 +162,9 @@ typedef struct t1env_buffers {
   int32_t* terrain_levels;  /* (N,) */
   int32_t* terrain_types;   /* (N,) */
   float* terrain_origins;   /* (rows, cols, 3) */
-  float* extras;            /* (32,) episode extras: [0,24) rew_<name> means, [24] terrain level mean */
+  float* extras;            /* (T1ENV_EXTRAS_RING, 32) ring of extras["episode"]: [0,24) rew_<name> means, [24]
+                               terrain level mean.  A step with args.counter = c writes slot (c+1) % RING
+                               (t1env_reset_all: c % RING); a step without resets carries the previous slot */
   float* ep_accum;          /* (32,) per-step reduction scratch: [0,24) sums over reset envs, [24] count,
                                [25] terrain level sum; zeroed by the library */
 } t1env_buffers;
@@ -209,9 +213,9 @@ int t1env_step_reset_and_observe(t1env* env, const t1env_step_args* args, void* 
 int t1env_step_injected(t1env* env, const float* actions, const t1env_step_args* args, const t1env_injected* inj,
                         void* stream);
 /* Per-kernel timing with HIP events recorded around every launch (bench.py's live roofline).  Ids:
- * 0 k_dynamics (or the injected-physics kernel), 1 k_post_a, 2 k_post_b, 3 k_shift (internal side stream,
- * overlapping 0-1), 4 k_finalize(+terrain-level sum), 5 the whole step (phase A start .. phase B end on the
- * caller's stream).  get_timing synchronises and returns summed milliseconds and launch counts per id since
+ * 0 k_dynamics (or the injected-physics kernel), 1 k_post_a, 2 k_post_b (its last block also finalises the
+ * extras), 3 k_shift (internal side stream, overlapping 0-1), 4 unused, 5 the whole step (phase A start ..
+ * phase B end on the caller's stream).  get_timing synchronises and returns summed milliseconds and launch counts per id since
  * the last enable. */
 #define T1ENV_NTIMERS 6
 /* enable: bit 0 = record events from now on; bit 1 = keep (do not clear) the events recorded so far */

@@ -64,6 +64,7 @@ struct t1env {
   hipEvent_t ev_fork, ev_join;
   int shift_pending;      // a shift was forked in phase A and not yet joined
   int step_timer;         // timing slot of the current step span (phase A start .. phase B end)
+  unsigned* d_done;       // k_post_b block-completion counter (its last block finalises the extras)
 };
 
 // k_physics_injected: the same decimation loop with the physics states supplied by the caller (golden
@@ -203,6 +204,27 @@ __device__ __forceinline__ void wave_atomic_add(float* dst, float v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   if ((threadIdx.x & 63) == 0 && v != 0.0f) atomicAdd(dst, v);
 }
+
+// extras["episode"] of one step (legged_robot.py:560-569 via reset_idx): means over the envs reset this step
+// into ring slot `slot`; a step without resets keeps the previous values, like the reference's extras dict.
+// Run by one wave after every env's contribution to ep_accum is complete; zeroes ep_accum.
+__device__ __forceinline__ void finalize_extras(const t1env_buffers& B, const t1env_config& C, int slot) {
+  const int t = threadIdx.x & 63;
+  const float cnt = atomicAdd(B.ep_accum + 24, 0.0f);  // device-scope read of the other blocks' atomics
+  float* ex = B.extras + (size_t)slot * 32;
+  const float* prev = B.extras + (size_t)((slot + T1ENV_EXTRAS_RING - 1) % T1ENV_EXTRAS_RING) * 32;
+  if (t < 32) {
+    float v = prev[t];
+    if (cnt > 0.0f) {
+      if (t < T1_NREW) v = (atomicAdd(B.ep_accum + t, 0.0f) / cnt) / C.episode_length_s;
+      else if (t == 24) v = atomicAdd(B.ep_accum + 25, 0.0f) / (float)C.num_envs;
+    }
+    ex[t] = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (t < 32) B.ep_accum[t] = 0.0f;
+}
+
 
 // =====================================================================================================
 // post-physics phase A: callback, termination, rewards (legged_robot.py:469-489)
@@ -641,12 +663,15 @@ __device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config
 }
 
 __global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
-                                                  t1env_buffers B, t1env_step_args A) {
+                                                  t1env_buffers B, t1env_step_args A, unsigned* __restrict__ done) {
   const int n = blockIdx.x * BLOCK + threadIdx.x;
   const t1env_config& C = *Cp;
   const bool live = n < C.num_envs;
   const bool do_reset = live && B.reset_buf[n] != 0;
+  const bool any_reset = B.ep_accum[24] > 0.0f;
   if (live) post_b_env(*Mp, C, B, A, n);
+  // extras["episode"]["terrain_level"] = mean level over all envs after this step's resets (legged_robot.py:1158)
+  if (C.terrain_curriculum && any_reset) wave_atomic_add(B.ep_accum + 25, live ? (float)B.terrain_levels[n] : 0.0f);
   // reset_idx zeroes the obs / critic history of the reset envs (t1:548-558): k_shift wrote the 65 (2) older
   // frames of every row, so the wave zeroes those of its reset envs here, one row at a time, coalesced
   uint64_t m = __ballot(do_reset);
@@ -658,6 +683,16 @@ __global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ M
     for (int c = threadIdx.x; c < T1_NOBS * (T1_HIST - 1); c += BLOCK) o[c] = 0.0f;
     float* p = B.priv_buf[A.obs_slot] + row * (T1_NPRIV * T1_CHIST);
     for (int c = threadIdx.x; c < T1_NPRIV * (T1_CHIST - 1); c += BLOCK) p[c] = 0.0f;
+  }
+  // the last block to finish finalises the step's extras (no separate launch)
+  __threadfence();
+  unsigned prev = 0;
+  if (threadIdx.x == 0) prev = atomicAdd(done, 1u);
+  prev = __shfl(prev, 0, 64);
+  if (prev == gridDim.x - 1) {
+    __threadfence();
+    finalize_extras(B, C, (int)((A.counter + 1u) % T1ENV_EXTRAS_RING));
+    if (threadIdx.x == 0) *done = 0u;
   }
 }
 
@@ -708,18 +743,9 @@ __global__ __launch_bounds__(256) void k_shift(const float* __restrict__ obs_in,
   else if (tid < n4_obs + n4_priv) shift_rows<T1_NPRIV, T1_CHIST>(priv_in, priv_out, tot_priv, tid - n4_obs);
 }
 
-// extras finalisation (one block)
-__global__ void k_finalize(t1env_buffers B, const t1env_config* __restrict__ Cp) {
-  const t1env_config& C = *Cp;
-  {
-    __shared__ float cnt;
-    if (threadIdx.x == 0) cnt = B.ep_accum[24];
-    __syncthreads();
-    if (threadIdx.x < T1_NREW && cnt > 0.0f) B.extras[threadIdx.x] = (B.ep_accum[threadIdx.x] / cnt) / C.episode_length_s;
-    if (threadIdx.x == 25 && cnt > 0.0f) B.extras[24] = B.ep_accum[25] / (float)C.num_envs;
-    __syncthreads();
-    if (threadIdx.x < 32) B.ep_accum[threadIdx.x] = 0.0f;
-  }
+// extras finalisation for t1env_reset_all (one wave)
+__global__ void k_finalize(t1env_buffers B, const t1env_config* __restrict__ Cp, int slot) {
+  finalize_extras(B, *Cp, slot);
 }
 
 // terrain-level sum for extras["episode"]["terrain_level"] (only meaningful on reset steps)
@@ -849,7 +875,8 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
       (err = hipMalloc(&e->d_cfg, sizeof(t1env_config))) != hipSuccess ||
       (err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking)) != hipSuccess ||
       (err = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming)) != hipSuccess ||
-      (err = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess) {
+      (err = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess ||
+      (err = hipMalloc(&e->d_done, sizeof(unsigned))) != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "t1env_create: hipMalloc: %s", hipGetErrorString(err));
     free(e);
     return (int)err;
@@ -857,6 +884,7 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   HIP_TRY(hipMemcpy(e->d_model, &dm, sizeof(DynModel), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_cfg, cfg, sizeof(t1env_config), hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(e->buf.ep_accum, 0, 32 * sizeof(float)));
+  HIP_TRY(hipMemset(e->d_done, 0, sizeof(unsigned)));
   *out = e;
   return 0;
 }
@@ -865,6 +893,7 @@ int t1env_destroy(t1env* e) {
   if (!e) return 0;
   (void)hipFree(e->d_model);
   (void)hipFree(e->d_cfg);
+  (void)hipFree(e->d_done);
   if (e->side) (void)hipStreamSynchronize(e->side);
   if (e->side) (void)hipStreamDestroy(e->side);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -956,15 +985,8 @@ int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* strea
   HIP_TRY(hipStreamWaitEvent(s, e->ev_join, 0));
   e->shift_pending = 0;
   int t = t_begin(e, 2, s);
-  hipLaunchKernelGGL(k_post_b, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a);
-  t_end(e, t, s);
-  HIP_TRY(hipGetLastError());
-  t = t_begin(e, 4, s);
-  if (e->cfg.terrain_curriculum) {
-    hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
-    HIP_TRY(hipGetLastError());
-  }
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg);
+  hipLaunchKernelGGL(k_post_b, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,
+                     e->d_done);
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
   t_end(e, e->step_timer, s);
@@ -1008,7 +1030,7 @@ int t1env_reset_all(t1env* e, const t1env_step_args* a, void* stream) {
     hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
     HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg);
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg, (int)(a->counter % T1ENV_EXTRAS_RING));
   HIP_TRY(hipGetLastError());
   // every history row restarts from zeros: clear both ping-pong buffers (the next step shifts from either)
   for (int k = 0; k < 2; ++k) {

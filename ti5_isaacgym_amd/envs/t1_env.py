@@ -12,7 +12,7 @@ stream and returns without a host sync (the only syncs: the command curriculum c
 steps, and ``reset()``).  Differences in buffer semantics vs the reference (documented in DESIGN.md):
   * obs/priv are two ping-pong buffers; the tensor returned by step k stays valid through step k+1
     (the reference allocates a fresh tensor per step; DHPPO only keeps one step back).
-  * extras["episode"] values are 0-d device tensors cloned per step.
+  * extras["episode"] values are 0-d views into a 64-step ring the library writes (no per-step copy).
 """
 import math
 
@@ -33,6 +33,7 @@ REWARD_NAMES = sorted(["action_smoothness", "base_acc", "base_height", "collisio
 GAIT_KINDS = {"walk_omnidirectional": 0, "stand": 1, "walk_sagittal": 2, "walk_lateral": 3, "rotate": 4}
 
 # Solver constants of the compliant contact / soft limit model (PhysX TGS is unpinned).
+EXTRAS_RING = 64  # include/t1env.h T1ENV_EXTRAS_RING
 SOLVER = dict(k_contact=1.0e5, d_contact=1.5e3, friction_vs=0.01, k_limit=2.0e4, d_limit=200.0, gravity=9.81)
 
 
@@ -164,6 +165,7 @@ class T1DHStandEnv(VecEnv):
                                              2 if self.mesh_type == "trimesh" else 1), "t1env_set_terrain")
         _lib.check(lib.t1env_init(handle, self._stream()), "t1env_init")
         self.extras = {}
+        self._ep_dicts = None
         self._slot = 0
         self.init_done = True
 
@@ -203,7 +205,7 @@ class T1DHStandEnv(VecEnv):
         self._act_hist, self._dof_hist, self._imu_hist = z(N, 4, 12), z(N, 4, 24), z(N, 2, 6)
         self.terrain_levels, self.terrain_types = z(N, dtype=i32), z(N, dtype=i32)
         self.terrain_origins = z(1, 1, 3)
-        self._extras_buf = torch.full((32,), float("nan"), device=d)
+        self._extras_ring = torch.full((EXTRAS_RING, 32), float("nan"), device=d)
         self._ep_accum = z(32)
         # views mirroring the reference's attribute names
         self.dof_pos = self.dof_state.view(N, 12, 2)[..., 0]
@@ -373,7 +375,7 @@ class T1DHStandEnv(VecEnv):
             "dof_lag_timestep": self.dof_lag_timestep, "imu_lag_timestep": self.imu_lag_timestep,
             "act_hist": self._act_hist, "dof_hist": self._dof_hist, "imu_hist": self._imu_hist,
             "env_origins": self.env_origins, "terrain_levels": self.terrain_levels, "terrain_types": self.terrain_types,
-            "terrain_origins": self.terrain_origins, "extras": self._extras_buf, "ep_accum": self._ep_accum,
+            "terrain_origins": self.terrain_origins, "extras": self._extras_ring, "ep_accum": self._ep_accum,
         }
         types = dict(_lib.BUFFER_FIELDS)
         for name, t in m.items():
@@ -488,14 +490,21 @@ class T1DHStandEnv(VecEnv):
             _lib.check(lib.t1env_step_reset_and_observe(h, _lib.C.byref(a), s), "t1env_step_reset_and_observe")
         self.common_step_counter += 1
         self._slot ^= 1
-        self._fill_extras()
+        self._fill_extras(self.common_step_counter % EXTRAS_RING)
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
 
-    def _fill_extras(self):
-        ex = self._extras_buf.clone()
-        ep = {"rew_" + k: ex[REWARD_NAMES.index(k)] for k in self.reward_names}
-        if self.mesh_type == "trimesh":
-            ep["terrain_level"] = ex[24]
+    def _fill_extras(self, slot):
+        """extras["episode"] for the ring slot the library just wrote (0-d views, valid for EXTRAS_RING steps --
+        the runner logs every num_steps_per_env = 24); the dicts are built once, a step only picks one."""
+        if self._ep_dicts is None:
+            self._ep_dicts = []
+            for r in range(EXTRAS_RING):
+                ex = self._extras_ring[r]
+                ep = {"rew_" + k: ex[REWARD_NAMES.index(k)] for k in self.reward_names}
+                if self.mesh_type == "trimesh":
+                    ep["terrain_level"] = ex[24]
+                self._ep_dicts.append(ep)
+        ep = self._ep_dicts[slot]
         if self.cfg.commands.curriculum:
             ep["max_command_x"] = self.command_ranges["lin_vel_x"][1]
         self.extras["episode"] = ep
@@ -509,7 +518,7 @@ class T1DHStandEnv(VecEnv):
             self._command_curriculum(float(self.episode_sums["tracking_lin_vel"].sum()), float(self.num_envs))
         a = self._args(self.common_step_counter)
         _lib.check(self._lib.t1env_reset_all(self._handle, _lib.C.byref(a), self._stream()), "t1env_reset_all")
-        self._fill_extras()
+        self._fill_extras(self.common_step_counter % EXTRAS_RING)
 
     def reset(self):
         """LeggedRobot.reset (legged_robot.py:450-455)."""
