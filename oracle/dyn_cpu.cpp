@@ -52,7 +52,7 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
                   float border, int mesh, float* rigid, float* contact) {
   DynModel M;
   if (make_dyn_model(model, &M)) return -1;
-  Terrain T{hf, rows, cols, mesh, hs, vs, border};
+  Terrain T = make_terrain(hf, rows, cols, mesh, hs, vs, border);
 #pragma omp parallel for schedule(static)
   for (int n = 0; n < N; ++n) {
     EnvParams<R> P;
@@ -90,7 +90,7 @@ int t1dyn_accel(const t1env_model* model, const double* mass, const double* iner
                 const double* armature, const double* state /* 3+4+3+3+12+12 */, const double* tau, double* udot) {
   DynModel M;
   if (make_dyn_model(model, &M)) return -1;
-  Terrain T{nullptr, 0, 0, 0, 0.1f, 0.005f, 0.0f};
+  Terrain T = make_terrain(nullptr, 0, 0, 0, 0.1f, 0.005f, 0.0f);
   EnvParams<double> P;
   P.base.mass = mass[0];
   P.base.inertia_scale = inertia_scale[0];

@@ -44,6 +44,7 @@ struct DynModel {
   float default_dof_pos[ND], p_gains[ND], d_gains[ND];
   int32_t contact_start[NB], contact_count[NB];
   float contact_point[48][3];
+  float contact_radius[NB];  // max distance of a body's contact points from its frame origin
   float k_contact, d_contact, friction_vs, k_limit, d_limit, gravity;
   float ground_friction, ground_restitution;
   float base_init_state[13];
@@ -55,7 +56,17 @@ struct Terrain {
   const int16_t* h;  // (rows, cols), rows along x
   int32_t rows, cols, type;
   float hscale, vscale, border;
+  float inv_hscale;  // 1 / hscale
+  // coarse bound: hmax[ci][cj] = highest sample within K cells of coarse cell (ci, cj) (K * cell >= every
+  // contact radius), raw units; lets a contact body far above the ground skip its point queries exactly.
+  const int16_t* hmax;  // (hm_rows, hm_cols) or null (no bound: always query)
+  int32_t hm_rows, hm_cols;
+  float hm_inv_cell;    // 1 / coarse cell size [1/m]
 };
+inline Terrain make_terrain(const int16_t* h, int32_t rows, int32_t cols, int32_t type, float hscale, float vscale,
+                            float border) {
+  return Terrain{h, rows, cols, type, hscale, vscale, border, 1.0f / hscale, nullptr, 0, 0, 0.0f};
+}
 
 template <typename R> struct BaseParams {
   R mass, inertia_scale, com_disp[3];
@@ -143,14 +154,15 @@ template <typename R> T1_HD R dot6(const R a[6], const R b[6]) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// terrain query: height + unit normal at world (x, y).  HF=false: the plane z=0.
+// terrain query at world (x, y): height h and slope (gx, gy) = dh/dx, dh/dy; the unit normal
+// (-gx, -gy, 1) / |.| is formed only for points in contact (terrain_normal).  HF=false: the plane z=0.
 // ---------------------------------------------------------------------------------------------------
-template <bool HF, typename R> T1_HD R terrain_height(const Terrain& T, R x, R y, V3<R>& n) {
+template <bool HF, typename R> T1_HD R terrain_height(const Terrain& T, R x, R y, R& gx, R& gy) {
   if constexpr (!HF) {
-    n = v3<R>(0, 0, 1);
+    gx = gy = R(0);
     return R(0);
   } else {
-    const R ih = rcp(R(T.hscale));
+    const R ih = R(T.inv_hscale);
     R fx = (x + R(T.border)) * ih, fy = (y + R(T.border)) * ih;
     R ix = floor(fx), iy = floor(fy);
     int i = (int)ix, j = (int)iy;
@@ -166,12 +178,24 @@ template <bool HF, typename R> T1_HD R terrain_height(const Terrain& T, R x, R y
     const bool lo = u >= v;
     R dhdu = lo ? h10 - h00 : h11 - h01;
     R dhdv = lo ? h11 - h10 : h01 - h00;
-    R h = h00 + u * dhdu + v * dhdv;
-    R gx = dhdu * ih, gy = dhdv * ih;
-    R inv = rcp(fsqrt(R(1) + gx * gx + gy * gy));
-    n = v3<R>(-gx * inv, -gy * inv, inv);
-    return h;
+    gx = dhdu * ih;
+    gy = dhdv * ih;
+    return h00 + u * dhdu + v * dhdv;
   }
+}
+template <bool HF, typename R> T1_HD V3<R> terrain_normal(R gx, R gy) {
+  if constexpr (!HF) {
+    return v3<R>(0, 0, 1);
+  } else {
+    R inv = rcp(fsqrt(R(1) + gx * gx + gy * gy));
+    return v3<R>(-gx * inv, -gy * inv, inv);
+  }
+}
+template <bool HF, typename R> T1_HD R terrain_height(const Terrain& T, R x, R y, V3<R>& n) {
+  R gx, gy;
+  R h = terrain_height<HF>(T, x, y, gx, gy);
+  n = terrain_normal<HF>(gx, gy);
+  return h;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -233,9 +257,33 @@ T1_HD void world_inertia(const DynModel& M, int b, const M3<R>& Rb, R scale, R o
 // when approaching), regularised Coulomb friction as an implicit tangential damper whose coefficient keeps
 // |F_t| <= mu F_n (Stribeck speed friction_vs).
 // ---------------------------------------------------------------------------------------------------
+// Sum over a body's contact points of c * sum_e w_e w_e^T with w_e = [x cross e ; e] over the world axes e:
+// that is the spatial inertia of point masses c at x, [[ |x|^2 I - x x^T, [x]x ], [[x]x^T, I]] * c, so the
+// friction stiffness accumulates as 10 moments per body instead of three 6x6 rank-1 updates per point.
+template <typename R> struct PointMoments {
+  R m, hx, hy, hz, sxx, syy, szz, sxy, sxz, syz;
+};
+template <typename R> T1_HD void moments_zero(PointMoments<R>& P) {
+  P.m = P.hx = P.hy = P.hz = P.sxx = P.syy = P.szz = P.sxy = P.sxz = P.syz = R(0);
+}
+template <typename R> T1_HD void moments_add(PointMoments<R>& P, R c, V3<R> x) {
+  const R cx = c * x.x, cy = c * x.y, cz = c * x.z;
+  P.m += c; P.hx += cx; P.hy += cy; P.hz += cz;
+  P.sxx += cx * x.x; P.syy += cy * x.y; P.szz += cz * x.z;
+  P.sxy += cx * x.y; P.sxz += cx * x.z; P.syz += cy * x.z;
+}
+template <typename R> T1_HD void moments_flush(const PointMoments<R>& P, Sym6<R>& A) {
+  A.a[sidx(0, 0)] += P.syy + P.szz; A.a[sidx(1, 1)] += P.sxx + P.szz; A.a[sidx(2, 2)] += P.sxx + P.syy;
+  A.a[sidx(0, 1)] -= P.sxy; A.a[sidx(0, 2)] -= P.sxz; A.a[sidx(1, 2)] -= P.syz;
+  A.a[sidx(0, 4)] -= P.hz; A.a[sidx(0, 5)] += P.hy;
+  A.a[sidx(1, 3)] += P.hz; A.a[sidx(1, 5)] -= P.hx;
+  A.a[sidx(2, 3)] -= P.hy; A.a[sidx(2, 4)] += P.hx;
+  A.a[sidx(3, 3)] += P.m; A.a[sidx(4, 4)] += P.m; A.a[sidx(5, 5)] += P.m;
+}
+
 template <typename R>
 T1_HD void contact_point(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[6], R mu, R dt, Sym6<R>& A,
-                         R g[6]) {
+                         R g[6], PointMoments<R>& fric) {
   const R k = R(M.k_contact), d = R(M.d_contact);
   V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
   V3<R> vp = vo + cross(om, x);
@@ -254,38 +302,41 @@ T1_HD void contact_point(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[
   V3<R> xn = cross(x, n);
   R wn[6] = {xn.x, xn.y, xn.z, n.x, n.y, n.z};
   sym_rank1(A, dt * (cn - ct), wn);
-  R ex[6] = {R(0), x.z, -x.y, R(1), R(0), R(0)};   // [x cross e_x ; e_x]
-  R ey[6] = {-x.z, R(0), x.x, R(0), R(1), R(0)};
-  R ez[6] = {x.y, -x.x, R(0), R(0), R(0), R(1)};
-  sym_rank1(A, dt * ct, ex);
-  sym_rank1(A, dt * ct, ey);
-  sym_rank1(A, dt * ct, ez);
+  moments_add(fric, dt * ct, x);
 }
 
 // NP points known at compile time: phase 1 transforms every point and queries the terrain with no branch
 // in between, so all coordinate (scalar) and height-field (vector) loads issue together and the body pays
 // one memory latency instead of one per point; phase 2 runs the contact math for the points in contact.
+#ifndef T1_CONTACT_BATCH
+#define T1_CONTACT_BATCH 4
+#endif
 template <bool HF, int NP, typename R>
 T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb,
                            V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
-  constexpr int CH = NP < 4 ? NP : 4;  // points in flight per batch (bounds the live registers)
+  constexpr int CH = NP < T1_CONTACT_BATCH ? NP : T1_CONTACT_BATCH;  // points in flight (bounds live registers)
   static_assert(NP % CH == 0, "contact points per body must be a multiple of the batch");
+  PointMoments<R> fric;
+  moments_zero(fric);
 #pragma unroll
   for (int c0 = 0; c0 < NP; c0 += CH) {
-    V3<R> xs[CH], ns[CH];
-    R pens[CH];
+    V3<R> xs[CH];
+    R dz[CH], gxs[CH], gys[CH];
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int c = c_begin + c0 + i;
       xs[i] = pb + mul(Rb, v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]));
       V3<R> X = xs[i] + base_abs;
-      R h = terrain_height<HF>(T, X.x, X.y, ns[i]);
-      pens[i] = (h - X.z) * ns[i].z;
+      dz[i] = terrain_height<HF>(T, X.x, X.y, gxs[i], gys[i]) - X.z;
     }
 #pragma unroll
     for (int i = 0; i < CH; ++i)
-      if (pens[i] > R(0)) contact_point(M, xs[i], ns[i], pens[i], Vb, mu, dt, A, g);
+      if (dz[i] > R(0)) {  // below the surface (the normal's z is positive)
+        const V3<R> n = terrain_normal<HF>(gxs[i], gys[i]);
+        contact_point(M, xs[i], n, dz[i] * n.z, Vb, mu, dt, A, g, fric);
+      }
   }
+  moments_flush(fric, A);
 }
 
 template <bool HF, typename R>
@@ -294,14 +345,17 @@ T1_HD void body_contact_t(const DynModel& M, const Terrain& T, int c_begin, int 
   // the T1 model: 8 points per contact body (base box split 4 + 4 between the legs)
   if (c_end - c_begin == 8) return body_contact_np<HF, 8>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
   if (c_end - c_begin == 4) return body_contact_np<HF, 4>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  PointMoments<R> fric;
+  moments_zero(fric);
   for (int c = c_begin; c < c_end; ++c) {
     V3<R> x = pb + mul(Rb, v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]));
     V3<R> X = x + base_abs;
     V3<R> n;
     R h = terrain_height<HF>(T, X.x, X.y, n);
     R pen = (h - X.z) * n.z;
-    if (pen > R(0)) contact_point(M, x, n, pen, Vb, mu, dt, A, g);
+    if (pen > R(0)) contact_point(M, x, n, pen, Vb, mu, dt, A, g, fric);
   }
+  moments_flush(fric, A);
 }
 template <typename R>
 T1_HD void body_contact(const DynModel& M, const Terrain& T, int c_begin, int c_end, const M3<R>& Rb, V3<R> pb,
@@ -436,11 +490,31 @@ T1_HD void body_inertia(const DynModel& M, int b, R mass, R iscale, const M3<R>&
 constexpr int T1_LEG_CONTACT_MASK = (1 << 3) | (1 << 5);
 constexpr int T1_POINTS_PER_BODY = 8;
 
+// true when every point within `radius` of world position W is certainly above the terrain (no contact
+// possible): exact -- the trimesh interpolation never exceeds its vertices, and hmax covers the radius.
+template <bool HF, typename R> T1_HD bool above_terrain(const Terrain& T, V3<R> W, R radius) {
+  if constexpr (!HF) {
+    return W.z - radius > R(0);
+  } else {
+    if (!T.hmax) return false;
+    int ci = (int)floor((W.x + R(T.border)) * R(T.hm_inv_cell));
+    int cj = (int)floor((W.y + R(T.border)) * R(T.hm_inv_cell));
+    ci = ci < 0 ? 0 : (ci > T.hm_rows - 1 ? T.hm_rows - 1 : ci);
+    cj = cj < 0 ? 0 : (cj > T.hm_cols - 1 ? T.hm_cols - 1 : cj);
+    return W.z - radius > R(T.vscale) * R(T.hmax[ci * T.hm_cols + cj]);
+  }
+}
+
 template <int NP, typename R>
-T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb,
+T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, int b, int c_begin, const M3<R>& Rb, V3<R> pb,
                               V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
-  if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
-  else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  const V3<R> W = pb + base_abs;
+  const R rad = R(M.contact_radius[b]);
+  if (T.type == 0) {
+    if (!above_terrain<false>(T, W, rad)) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  } else {
+    if (!above_terrain<true>(T, W, rad)) body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  }
 }
 
 template <int K> using kconst = std::integral_constant<int, K>;
@@ -505,7 +579,7 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
     }
     if constexpr (CM >= 0) {
       if constexpr ((CM >> k) & 1)
-        body_contact_fixed<T1_POINTS_PER_BODY>(M, T, M.contact_start[b], Rk, pk, F.abs, V, mu, dt, Ac, gc);
+        body_contact_fixed<T1_POINTS_PER_BODY>(M, T, b, M.contact_start[b], Rk, pk, F.abs, V, mu, dt, Ac, gc);
     } else {
       const int c0 = M.contact_start[b], nc = M.contact_count[b];
       if (nc > 0) body_contact(M, T, c0, c0 + nc, Rk, pk, F.abs, V, mu, dt, Ac, gc);
@@ -645,7 +719,7 @@ T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParam
   base_contact_range(M, leg, cb, ce);
   R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
   if constexpr (CM >= 0) {
-    body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, cb, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
+    body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, 0, cb, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
   } else {
     if (ce > cb) body_contact(M, T, cb, ce, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
   }

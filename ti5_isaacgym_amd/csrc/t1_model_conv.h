@@ -13,6 +13,10 @@ namespace t1 {
 inline const char* make_dyn_model(const t1env_model* model, DynModel* dm) {
   memset(dm, 0, sizeof(*dm));
   if (model->n_contact > T1_MAXC || model->n_contact > 48) return "too many contact points";
+  for (int b = 0; b < NB; ++b)
+    if (model->contact_count[b] < 0 || model->contact_start[b] < 0 ||
+        model->contact_start[b] + model->contact_count[b] > model->n_contact)
+      return "contact_start/contact_count out of range";
   for (int b = 0; b < NB; ++b) {
     int ax = -1;
     float sg = 1.0f;
@@ -43,6 +47,15 @@ inline const char* make_dyn_model(const t1env_model* model, DynModel* dm) {
   }
   for (int c = 0; c < model->n_contact; ++c)
     for (int k = 0; k < 3; ++k) dm->contact_point[c][k] = model->contact_point[c][k];
+  for (int b = 0; b < NB; ++b) {
+    float r2 = 0.0f;
+    for (int c = dm->contact_start[b]; c < dm->contact_start[b] + dm->contact_count[b]; ++c) {
+      const float* p = dm->contact_point[c];
+      const float d = p[0] * p[0] + p[1] * p[1] + p[2] * p[2];
+      r2 = d > r2 ? d : r2;
+    }
+    dm->contact_radius[b] = sqrtf(r2) * 1.0001f + 1e-6f;  // rounded up: the bound must be conservative
+  }
   dm->k_contact = model->k_contact; dm->d_contact = model->d_contact; dm->friction_vs = model->friction_vs;
   dm->k_limit = model->k_limit; dm->d_limit = model->d_limit; dm->gravity = model->gravity;
   dm->ground_friction = model->ground_friction; dm->ground_restitution = model->ground_restitution;

@@ -65,6 +65,8 @@ struct t1env {
   int shift_pending;      // a shift was forked in phase A and not yet joined
   int step_timer;         // timing slot of the current step span (phase A start .. phase B end)
   unsigned* d_done;       // k_post_b block-completion counter (its last block finalises the extras)
+  int16_t* d_hmax;        // coarse terrain height bound (Terrain::hmax), built by t1env_set_terrain
+  float max_contact_radius;
 };
 
 // k_physics_injected: the same decimation loop with the physics states supplied by the caller (golden
@@ -824,6 +826,22 @@ __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict_
   resample_commands(C, B, A, n, genv, A.counter);
 }
 
+// coarse height bound: out[ci][cj] = max height sample of rows [(ci-K)c, (ci+K+1)c] x cols [(cj-K)c, (cj+K+1)c]
+// (clamped), c = HMAX_CELL -- every triangle a point within K cells of coarse cell (ci, cj) can fall on.
+constexpr int HMAX_CELL = 3;
+__global__ void k_hmax(const int16_t* __restrict__ h, int rows, int cols, int16_t* __restrict__ out, int hr, int hc,
+                       int K) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hr * hc) return;
+  const int ci = t / hc, cj = t % hc;
+  const int r0 = max(0, (ci - K) * HMAX_CELL), r1 = min(rows - 1, (ci + K + 1) * HMAX_CELL);
+  const int c0 = max(0, (cj - K) * HMAX_CELL), c1 = min(cols - 1, (cj + K + 1) * HMAX_CELL);
+  int m = -32768;
+  for (int r = r0; r <= r1; ++r)
+    for (int c = c0; c <= c1; ++c) m = max(m, (int)h[(size_t)r * cols + c]);
+  out[t] = (int16_t)m;
+}
+
 // =====================================================================================================
 // C ABI
 // =====================================================================================================
@@ -869,7 +887,7 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   if (!e) return fail(T1ENV_E_STATE, "t1env_create: out of host memory");
   e->cfg = *cfg;
   e->buf = *bufs;
-  e->terrain = Terrain{nullptr, 0, 0, 0, 0.1f, 0.005f, 0.0f};
+  e->terrain = make_terrain(nullptr, 0, 0, 0, 0.1f, 0.005f, 0.0f);
   hipError_t err;
   if ((err = hipMalloc(&e->d_model, sizeof(DynModel))) != hipSuccess ||
       (err = hipMalloc(&e->d_cfg, sizeof(t1env_config))) != hipSuccess ||
@@ -885,6 +903,7 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   HIP_TRY(hipMemcpy(e->d_cfg, cfg, sizeof(t1env_config), hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(e->buf.ep_accum, 0, 32 * sizeof(float)));
   HIP_TRY(hipMemset(e->d_done, 0, sizeof(unsigned)));
+  for (int b = 0; b < NB; ++b) e->max_contact_radius = fmaxf(e->max_contact_radius, dm.contact_radius[b]);
   *out = e;
   return 0;
 }
@@ -894,6 +913,7 @@ int t1env_destroy(t1env* e) {
   (void)hipFree(e->d_model);
   (void)hipFree(e->d_cfg);
   (void)hipFree(e->d_done);
+  if (e->d_hmax) (void)hipFree(e->d_hmax);
   if (e->side) (void)hipStreamSynchronize(e->side);
   if (e->side) (void)hipStreamDestroy(e->side);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -918,7 +938,24 @@ int t1env_set_terrain(t1env* e, const int16_t* h, int32_t rows, int32_t cols, fl
                       int32_t mesh_type) {
   if (!e) return fail(T1ENV_E_ARG, "t1env_set_terrain: null env");
   if (mesh_type != 0 && (!h || rows < 2 || cols < 2)) return fail(T1ENV_E_SHAPE, "t1env_set_terrain: bad height field");
-  e->terrain = Terrain{h, rows, cols, mesh_type, hs, vs, border};
+  e->terrain = make_terrain(h, rows, cols, mesh_type, hs, vs, border);
+  if (e->d_hmax) {
+    (void)hipFree(e->d_hmax);
+    e->d_hmax = nullptr;
+  }
+  if (mesh_type != 0) {
+    // coarse cells of HMAX_CELL samples; window K cells each side with K * cell >= every contact radius
+    const int hr = (rows + HMAX_CELL - 1) / HMAX_CELL, hc = (cols + HMAX_CELL - 1) / HMAX_CELL;
+    const int K = (int)ceilf(e->max_contact_radius / (HMAX_CELL * hs));
+    HIP_TRY(hipMalloc(&e->d_hmax, sizeof(int16_t) * (size_t)hr * hc));
+    hipLaunchKernelGGL(k_hmax, dim3(grid(hr * hc, 256)), dim3(256), 0, 0, h, rows, cols, e->d_hmax, hr, hc, K);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(0));
+    e->terrain.hmax = e->d_hmax;
+    e->terrain.hm_rows = hr;
+    e->terrain.hm_cols = hc;
+    e->terrain.hm_inv_cell = 1.0f / (HMAX_CELL * hs);
+  }
   return 0;
 }
 
