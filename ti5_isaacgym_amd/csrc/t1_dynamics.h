@@ -32,6 +32,17 @@ namespace t1 {
 
 constexpr int NB = 13, ND = 12, NLEG = 6;
 
+// Contact layout known at compile time: CM = bit mask of the leg bodies (k = 0..5) that carry NPC contact
+// points each (the T1: shank k=3 and foot k=5, 8 points each; base box 8 points = 4 per leg).  CM < 0: read
+// the layout from the model at run time (host build, other robots).  The GPU kernel requires the T1 layout
+// (t1_model_conv.h checks it) so every contact loop is fully unrolled with its loads batched.
+constexpr int T1_LEG_CONTACT_MASK = (1 << 3) | (1 << 5);
+constexpr int T1_POINTS_PER_BODY = 8;
+// joint axis of leg joint k (0 = x, 1 = y, 2 = z): hip yaw z, hip roll x, hip pitch y, knee y, ankle pitch y,
+// ankle roll x -- compiled in with the fixed layout (checked at create) so rotations use static indices
+constexpr int T1_LEG_AXIS[NLEG] = {2, 0, 1, 1, 1, 0};
+
+
 // Model in the form the kernels consume (built from t1env_model at create time).
 struct DynModel {
   float joint_offset[NB][3];
@@ -198,6 +209,35 @@ template <bool HF, typename R> T1_HD R terrain_height(const Terrain& T, R x, R y
   return h;
 }
 
+// Highest terrain a body whose frame origin is at world (x, y) can touch with points within its contact radius
+// (hmax covers every contact radius): a body with origin height - radius above it cannot be in contact.
+// Exact -- the trimesh interpolation never exceeds its vertices.  Split from the test so the load can be
+// issued early and consumed later.  No bound (always query): +inf.
+// The raw bound sample (height-field units) is returned so the load's consumer -- and its wait -- stays where
+// the bound is tested (bound_height).
+template <bool HF, typename R> T1_HD int32_t terrain_bound_raw(const Terrain& T, R x, R y) {
+  if constexpr (!HF) {
+    return 0;
+  } else {
+    if (!T.hmax) return 0x7fffffff;
+    int ci = (int)floor((x + R(T.border)) * R(T.hm_inv_cell));
+    int cj = (int)floor((y + R(T.border)) * R(T.hm_inv_cell));
+    ci = ci < 0 ? 0 : (ci > T.hm_rows - 1 ? T.hm_rows - 1 : ci);
+    cj = cj < 0 ? 0 : (cj > T.hm_cols - 1 ? T.hm_cols - 1 : cj);
+    return T.hmax[ci * T.hm_cols + cj];
+  }
+}
+template <typename R> T1_HD R bound_height(const Terrain& T, int32_t raw) {
+  return raw == 0x7fffffff ? R(INFINITY) : R(T.vscale) * R(raw);
+}
+template <bool HF, typename R> T1_HD R terrain_bound(const Terrain& T, R x, R y) {
+  return bound_height<R>(T, terrain_bound_raw<HF>(T, x, y));
+}
+template <typename R> T1_HD int32_t terrain_bound_raw_any(const Terrain& T, R x, R y) {
+  return T.type == 0 ? terrain_bound_raw<false>(T, x, y) : terrain_bound_raw<true>(T, x, y);
+}
+
+
 // ---------------------------------------------------------------------------------------------------
 // kinematics of one leg (bodies 1+6*leg .. 6+6*leg), world axes about O
 // ---------------------------------------------------------------------------------------------------
@@ -309,7 +349,7 @@ T1_HD void contact_point(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[
 // in between, so all coordinate (scalar) and height-field (vector) loads issue together and the body pays
 // one memory latency instead of one per point; phase 2 runs the contact math for the points in contact.
 #ifndef T1_CONTACT_BATCH
-#define T1_CONTACT_BATCH 4
+#define T1_CONTACT_BATCH 8
 #endif
 template <bool HF, int NP, typename R>
 T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb,
@@ -365,12 +405,45 @@ T1_HD void body_contact(const DynModel& M, const Terrain& T, int c_begin, int c_
 }
 
 // contact force (world) a body receives at velocity Vb (used for the net-contact-force report)
+template <typename R>
+T1_HD V3<R> point_contact_force(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[6], R mu) {
+  const R k = R(M.k_contact), d = R(M.d_contact);
+  V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
+  V3<R> vp = vo + cross(om, x);
+  R vn = dot(n, vp);
+  V3<R> vt = vp - vn * n;
+  R vtn = fsqrt(dot(vt, vt));
+  R fn = k * pen - (vn < R(0) ? d * vn : R(0));
+  fn = fn > R(0) ? fn : R(0);
+  R ct = mu * fn * rcp(vtn > R(M.friction_vs) ? vtn : R(M.friction_vs));
+  return fn * n - ct * vt;
+}
 template <bool HF, typename R>
 T1_HD V3<R> body_contact_force_t(const DynModel& M, const Terrain& T, int b, const M3<R>& Rb, V3<R> pb,
                                  V3<R> base_abs, const R Vb[6], R mu) {
   const int c0 = M.contact_start[b], nc = M.contact_count[b];
-  const R k = R(M.k_contact), d = R(M.d_contact), ivs = rcp(R(M.friction_vs));
   V3<R> F = v3<R>(0, 0, 0);
+  const V3<R> W = pb + base_abs;
+  if (W.z - R(M.contact_radius[b]) > terrain_bound<HF>(T, W.x, W.y)) return F;
+  if (nc == T1_POINTS_PER_BODY) {  // batched: all queries of the body in flight together
+    constexpr int NP = T1_POINTS_PER_BODY;
+    V3<R> xs[NP];
+    R dz[NP], gxs[NP], gys[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int c = c0 + i;
+      xs[i] = pb + mul(Rb, v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]));
+      V3<R> X = xs[i] + base_abs;
+      dz[i] = terrain_height<HF>(T, X.x, X.y, gxs[i], gys[i]) - X.z;
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+      if (dz[i] > R(0)) {
+        const V3<R> n = terrain_normal<HF>(gxs[i], gys[i]);
+        F = F + point_contact_force(M, xs[i], n, dz[i] * n.z, Vb, mu);
+      }
+    return F;
+  }
   for (int c = c0; c < c0 + nc; ++c) {
     V3<R> r = v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]);
     V3<R> x = pb + mul(Rb, r);
@@ -378,17 +451,7 @@ T1_HD V3<R> body_contact_force_t(const DynModel& M, const Terrain& T, int b, con
     V3<R> n;
     R h = terrain_height<HF>(T, X.x, X.y, n);
     R pen = (h - X.z) * n.z;
-    if (pen > R(0)) {
-      V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
-      V3<R> vp = vo + cross(om, x);
-      R vn = dot(n, vp);
-      V3<R> vt = vp - vn * n;
-      R vtn = fsqrt(dot(vt, vt));
-      R fn = k * pen - (vn < R(0) ? d * vn : R(0));
-      fn = fn > R(0) ? fn : R(0);
-      R ct = mu * fn * (vtn > R(M.friction_vs) ? rcp(vtn) : ivs);
-      F = F + fn * n - ct * vt;
-    }
+    if (pen > R(0)) F = F + point_contact_force(M, x, n, pen, Vb, mu);
   }
   return F;
 }
@@ -483,38 +546,32 @@ T1_HD void body_inertia(const DynModel& M, int b, R mass, R iscale, const M3<R>&
 // columns.  Only g_k, the joint sin/cos and the leaf pose/velocity cross between the passes (66 floats),
 // which is what keeps a leg inside the register file.  Ac_up / gc_up accumulate the leg composite.
 // ---------------------------------------------------------------------------------------------------
-// Contact layout known at compile time: CM = bit mask of the leg bodies (k = 0..5) that carry NPC contact
-// points each (the T1: shank k=3 and foot k=5, 8 points each; base box 8 points = 4 per leg).  CM < 0: read
-// the layout from the model at run time (host build, other robots).  The GPU kernel requires the T1 layout
-// (t1_model_conv.h checks it) so every contact loop is fully unrolled with its loads batched.
-constexpr int T1_LEG_CONTACT_MASK = (1 << 3) | (1 << 5);
-constexpr int T1_POINTS_PER_BODY = 8;
-
-// true when every point within `radius` of world position W is certainly above the terrain (no contact
-// possible): exact -- the trimesh interpolation never exceeds its vertices, and hmax covers the radius.
-template <bool HF, typename R> T1_HD bool above_terrain(const Terrain& T, V3<R> W, R radius) {
-  if constexpr (!HF) {
-    return W.z - radius > R(0);
+// joint rotation / motion subspace with the axis known at compile time (AX >= 0) or read from the model
+template <int AX, typename R> T1_HD M3<R> joint_rot(const DynModel& M, int b, const M3<R>& A, R c, R s) {
+  if constexpr (AX >= 0) return mul_axis_rot_t<AX>(A, c, s);
+  else return mul_axis_rot(A, M.axis_idx[b], c, s);
+}
+template <int AX, typename R> T1_HD void joint_subspace(const DynModel& M, int b, const M3<R>& Rb, V3<R> p, R S[6]) {
+  if constexpr (AX >= 0) {
+    const R sg = R(M.axis_sign[b]);
+    const V3<R> a = v3<R>(sg * Rb.m[AX], sg * Rb.m[3 + AX], sg * Rb.m[6 + AX]);
+    const V3<R> l = cross(p, a);
+    S[0] = a.x; S[1] = a.y; S[2] = a.z; S[3] = l.x; S[4] = l.y; S[5] = l.z;
   } else {
-    if (!T.hmax) return false;
-    int ci = (int)floor((W.x + R(T.border)) * R(T.hm_inv_cell));
-    int cj = (int)floor((W.y + R(T.border)) * R(T.hm_inv_cell));
-    ci = ci < 0 ? 0 : (ci > T.hm_rows - 1 ? T.hm_rows - 1 : ci);
-    cj = cj < 0 ? 0 : (cj > T.hm_cols - 1 ? T.hm_cols - 1 : cj);
-    return W.z - radius > R(T.vscale) * R(T.hmax[ci * T.hm_cols + cj]);
+    BodyState<R> Bk{Rb, p};
+    motion_subspace(M, b, Bk, S);
   }
 }
 
+// contact of a body with NP points; `lowest` = its origin height minus its contact radius, `bound` = the
+// terrain_bound at its origin (fetched earlier): skipped when the body cannot reach the terrain
 template <int NP, typename R>
-T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, int b, int c_begin, const M3<R>& Rb, V3<R> pb,
-                              V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
-  const V3<R> W = pb + base_abs;
-  const R rad = R(M.contact_radius[b]);
-  if (T.type == 0) {
-    if (!above_terrain<false>(T, W, rad)) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
-  } else {
-    if (!above_terrain<true>(T, W, rad)) body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
-  }
+T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, R lowest, int32_t bound_raw, int c_begin,
+                              const M3<R>& Rb, V3<R> pb, V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A,
+                              R g[6]) {
+  if (lowest > bound_height<R>(T, bound_raw)) return;
+  if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
 }
 
 template <int K> using kconst = std::integral_constant<int, K>;
@@ -527,17 +584,23 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
   M3<R> Rk = F.R0;
   V3<R> pk = v3<R>(0, 0, 0);
   R V[6], A[6], Sk[6];
+  R lowest[NLEG];  // contact bodies (fixed layout): origin height - radius, and the terrain bound sample
+  int32_t bound[NLEG];  // fetched in the forward pass, tested in the backward pass
 #pragma unroll
   for (int i = 0; i < 6; ++i) { V[i] = F.V0[i]; A[i] = R(0); }
   A[5] = R(M.gravity);
-#pragma unroll
-  for (int k = 0; k < NLEG; ++k) {
+  auto fwd = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int AX = CM >= 0 ? T1_LEG_AXIS[k] : -1;
     const int b = 1 + 6 * leg + k;
     pk = pk + mul(Rk, v3<R>(M.joint_offset[b][0], M.joint_offset[b][1], M.joint_offset[b][2]));
     fsincos(R(M.axis_sign[b]) * q[k], &sn[k], &cs[k]);
-    Rk = mul_axis_rot(Rk, M.axis_idx[b], cs[k], sn[k]);
-    BodyState<R> Bk{Rk, pk};
-    motion_subspace(M, b, Bk, Sk);
+    Rk = joint_rot<AX>(M, b, Rk, cs[k], sn[k]);
+    if constexpr (CM >= 0 && ((CM >> k) & 1)) {
+      lowest[k] = pk.z + F.abs.z - R(M.contact_radius[b]);
+      bound[k] = terrain_bound_raw_any(T, pk.x + F.abs.x, pk.y + F.abs.y);
+    }
+    joint_subspace<AX>(M, b, Rk, pk, Sk);
     R vj[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) vj[i] = Sk[i] * qd[k];
@@ -555,7 +618,13 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
     crf(V, IV, vf);
 #pragma unroll
     for (int i = 0; i < 6; ++i) g[k][i] = dt * (IA[i] + vf[i]);
-  }
+  };
+  fwd(kconst<0>{});
+  fwd(kconst<1>{});
+  fwd(kconst<2>{});
+  fwd(kconst<3>{});
+  fwd(kconst<4>{});
+  fwd(kconst<5>{});
   Sym6<R> Ac;
   sym_zero(Ac);
   R gc[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
@@ -564,14 +633,14 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
     constexpr int k = decltype(kc)::value;
     const int b = 1 + 6 * leg + k, j = 6 * leg + k;
     if constexpr (k < NLEG - 1) {  // step up from child k+1 (Sk still holds S_{k+1})
+      constexpr int AXC = CM >= 0 ? T1_LEG_AXIS[k + 1] : -1;
       const int bc = b + 1;
 #pragma unroll
       for (int i = 0; i < 6; ++i) V[i] -= Sk[i] * qd[k + 1];
-      Rk = mul_axis_rot(Rk, M.axis_idx[bc], cs[k + 1], -sn[k + 1]);
+      Rk = joint_rot<AXC>(M, bc, Rk, cs[k + 1], -sn[k + 1]);
       pk = pk - mul(Rk, v3<R>(M.joint_offset[bc][0], M.joint_offset[bc][1], M.joint_offset[bc][2]));
     }
-    BodyState<R> Bk{Rk, pk};
-    motion_subspace(M, b, Bk, Sk);
+    joint_subspace<(CM >= 0 ? T1_LEG_AXIS[k] : -1)>(M, b, Rk, pk, Sk);
     {
       Sym6<R> I;
       body_inertia(M, b, P.mass[k], P.inertia_scale[k], Rk, pk, I);
@@ -579,7 +648,8 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
     }
     if constexpr (CM >= 0) {
       if constexpr ((CM >> k) & 1)
-        body_contact_fixed<T1_POINTS_PER_BODY>(M, T, b, M.contact_start[b], Rk, pk, F.abs, V, mu, dt, Ac, gc);
+        body_contact_fixed<T1_POINTS_PER_BODY>(M, T, lowest[k], bound[k], M.contact_start[b], Rk, pk, F.abs, V, mu,
+                                               dt, Ac, gc);
     } else {
       const int c0 = M.contact_start[b], nc = M.contact_count[b];
       if (nc > 0) body_contact(M, T, c0, c0 + nc, Rk, pk, F.abs, V, mu, dt, Ac, gc);
@@ -711,6 +781,7 @@ T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParam
                             R dt, LegBlock<R>& lb, Sym6<R>& Ab, R rb[6]) {
   sym_zero(Ab);
   R g[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+  const int32_t base_bound = CM >= 0 ? terrain_bound_raw_any(T, F.abs.x, F.abs.y) : 0;  // tested after the leg pass
   leg_assemble<CM>(M, T, PL, PB.friction, F, q, qd, tau, leg, dt, lb, Ab, g);
 #pragma unroll
   for (int i = 0; i < 6; ++i) rb[i] = -g[i];
@@ -719,7 +790,8 @@ T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParam
   base_contact_range(M, leg, cb, ce);
   R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
   if constexpr (CM >= 0) {
-    body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, 0, cb, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
+    body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - R(M.contact_radius[0]), base_bound, cb, F.R0,
+                                               v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
   } else {
     if (ce > cb) body_contact(M, T, cb, ce, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
   }

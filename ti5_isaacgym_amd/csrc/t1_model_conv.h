@@ -63,10 +63,13 @@ inline const char* make_dyn_model(const t1env_model* model, DynModel* dm) {
   return nullptr;
 }
 
-// The HIP kernel compiles the T1 contact layout in (t1_dynamics.h T1_LEG_CONTACT_MASK): base box and, on each
-// leg, the shank (k=3) and the foot (k=5) with T1_POINTS_PER_BODY points each; no points elsewhere.
+// The HIP kernel compiles the T1 layout in (t1_dynamics.h): joint axes T1_LEG_AXIS, and contact points on the
+// base box and, on each leg, the shank (k=3) and the foot (k=5), T1_POINTS_PER_BODY each; none elsewhere.
 inline const char* check_fixed_contact_layout(const DynModel& dm) {
   if (dm.contact_count[0] != T1_POINTS_PER_BODY) return "base must carry 8 contact points";
+  for (int leg = 0; leg < 2; ++leg)
+    for (int k = 0; k < NLEG; ++k)
+      if (dm.axis_idx[1 + 6 * leg + k] != T1_LEG_AXIS[k]) return "leg joint axes must be z, x, y, y, y, x (T1)";
   for (int leg = 0; leg < 2; ++leg)
     for (int k = 0; k < NLEG; ++k) {
       const bool has = (T1_LEG_CONTACT_MASK >> k) & 1;
