@@ -9,11 +9,13 @@ no CPU fallback.
 import copy
 
 from .envs.configs import BaseConfig, DHT1StandCfg, DHT1StandCfgPPO, LeggedRobotCfg, LeggedRobotCfgPPO
+from .algo import ActorCriticDH, DHOnPolicyRunner, DHPPO, RolloutStorage
 from .envs.t1_env import T1DHStandEnv
 from .utils.helpers import class_to_dict, get_args, set_seed, update_class_from_dict
 from .utils.task_registry import task_registry
 
 task_registry.register("t1_dh_stand", T1DHStandEnv, DHT1StandCfg(), DHT1StandCfgPPO())
+task_registry.register_runner("DHOnPolicyRunner", DHOnPolicyRunner)
 
 
 def make_t1_env(num_envs=4096, mesh_type=None, seed=5, device="cuda:0", env_offset=0, num_envs_total=None,

@@ -1,0 +1,130 @@
+"""DHPPO: PPO with the state-estimator auxiliary loss (reference humanoid/algo/ppo/dh_ppo.py:13-205).
+
+Same constructor arguments, API (``init_storage``, ``act``, ``process_env_step``, ``compute_returns``,
+``update``) and losses as the reference:
+  loss = clipped surrogate + value_loss_coef * clipped value loss - entropy_coef * entropy
+         + MSE(state_estimator(short history), privileged base linear velocity [lin_vel_idx : +3]).
+Additions for data-parallel training over RCCL (distributed.py): one bucketed gradient all-reduce between
+backward() and clip_grad_norm_, the KL mean all-reduced before the adaptive learning-rate decision, and
+rank-0 weights broadcast at start.  Losses are accumulated on the device and read once per update.
+"""
+import torch
+import torch.nn as nn
+import torch.optim as optim
+
+from . import distributed as dist_util
+from .dh_policy import ActorCriticDH
+from .rollout import RolloutStorage
+
+
+class DHPPO:
+    actor_critic: ActorCriticDH
+
+    def __init__(self, actor_critic, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998,
+                 lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
+                 lin_vel_idx=45, use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu"):
+        self.device = device
+        self.desired_kl, self.schedule, self.learning_rate = desired_kl, schedule, learning_rate
+        self.actor_critic = actor_critic
+        self.actor_critic.to(self.device)
+        self.storage = None
+        self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=learning_rate)
+        # created (and checkpointed) like the reference's; its separate step is disabled there as well
+        self.state_estimator_optimizer = optim.Adam(self.actor_critic.state_estimator.parameters(), lr=learning_rate)
+        self.transition = RolloutStorage.Transition()
+        self.clip_param, self.num_learning_epochs, self.num_mini_batches = clip_param, num_learning_epochs, num_mini_batches
+        self.value_loss_coef, self.entropy_coef = value_loss_coef, entropy_coef
+        self.gamma, self.lam, self.max_grad_norm = gamma, lam, max_grad_norm
+        self.use_clipped_value_loss = use_clipped_value_loss
+        self.num_short_obs = self.actor_critic.num_short_obs
+        self.lin_vel_idx = lin_vel_idx
+        self.grads = dist_util.GradientBucket(self.actor_critic.parameters())
+        self.grads.broadcast_params_()
+
+    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
+        self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
+                                      action_shape, None, self.device)
+
+    def test_mode(self):
+        self.actor_critic.test()
+
+    def train_mode(self):
+        self.actor_critic.train()
+
+    def act(self, obs, critic_obs):
+        ac, t = self.actor_critic, self.transition
+        t.actions = ac.act(obs).detach()
+        t.values = ac.evaluate(critic_obs).detach()
+        t.actions_log_prob = ac.get_actions_log_prob(t.actions).detach()
+        t.action_mean = ac.action_mean.detach()
+        t.action_sigma = ac.action_std.detach()
+        t.observations = obs  # recorded before env.step(); the env's obs buffer of this step stays valid
+        t.critic_observations = critic_obs
+        return t.actions
+
+    def process_env_step(self, rewards, dones, infos):
+        t = self.transition
+        t.rewards = rewards.clone()
+        t.dones = dones
+        if "time_outs" in infos:  # bootstrap on time-outs
+            t.rewards += self.gamma * torch.squeeze(t.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
+        self.storage.add_transitions(t)
+        t.clear()
+        self.actor_critic.reset(dones)
+
+    def compute_returns(self, last_critic_obs):
+        last_values = self.actor_critic.evaluate(last_critic_obs).detach()
+        self.storage.compute_returns(last_values, self.gamma, self.lam)
+
+    def _adapt_lr(self, mu, sigma, old_mu, old_sigma):
+        with torch.inference_mode():
+            kl = torch.sum(torch.log(sigma / old_sigma + 1.0e-5)
+                           + (torch.square(old_sigma) + torch.square(old_mu - mu)) / (2.0 * torch.square(sigma)) - 0.5,
+                           axis=-1)
+            kl_mean = dist_util.all_reduce_mean_(torch.mean(kl).reshape(1))[0]
+            kl_mean = float(kl_mean)
+        if kl_mean > self.desired_kl * 2.0:
+            self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+        elif 0.0 < kl_mean < self.desired_kl / 2.0:
+            self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+        for g in self.optimizer.param_groups:
+            g["lr"] = self.learning_rate
+
+    def update(self):
+        ac = self.actor_critic
+        sums = torch.zeros(3, device=self.device)  # value, surrogate, state-estimator losses
+        mse = nn.MSELoss()
+        gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        for (obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b,
+             hid_b, masks_b) in gen:
+            ac.act(obs_b, masks=masks_b, hidden_states=hid_b[0])
+            est_lin_vel = ac.state_estimator(obs_b[:, -self.num_short_obs:])
+            ref_lin_vel = critic_b[:, self.lin_vel_idx:self.lin_vel_idx + 3].clone()
+            logp_b = ac.get_actions_log_prob(actions_b)
+            value_b = ac.evaluate(critic_b, masks=masks_b, hidden_states=hid_b[1])
+            mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
+            if self.desired_kl is not None and self.schedule == "adaptive":
+                self._adapt_lr(mu_b, sigma_b, old_mu_b, old_sigma_b)
+            # clipped surrogate
+            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+            adv = torch.squeeze(adv_b)
+            surrogate_loss = torch.max(-adv * ratio,
+                                       -adv * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)).mean()
+            # value loss
+            if self.use_clipped_value_loss:
+                v_clip = target_values_b + (value_b - target_values_b).clamp(-self.clip_param, self.clip_param)
+                value_loss = torch.max((value_b - returns_b).pow(2), (v_clip - returns_b).pow(2)).mean()
+            else:
+                value_loss = (returns_b - value_b).pow(2).mean()
+            se_loss = mse(est_lin_vel, ref_lin_vel)
+            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean() + se_loss
+            self.optimizer.zero_grad()
+            loss.backward()
+            self.grads.all_reduce_()
+            nn.utils.clip_grad_norm_(ac.parameters(), self.max_grad_norm)
+            self.optimizer.step()
+            sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), se_loss.detach()])
+        n = self.num_learning_epochs * self.num_mini_batches
+        self.storage.clear()
+        mv, ms, mse_ = (sums / n).tolist()
+        return mv, ms, mse_
