@@ -33,14 +33,13 @@ sys.path.insert(0, REPO)
 
 B_ALG = 30678          # algorithmic bytes per env-step (fp32, default t1 config)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-KERNELS = ["k_dynamics", "k_post_a", "k_post_b", "k_shift", "k_finalize"]
+KERNELS = ["k_dynamics", "k_post_a", "k_post_b", "k_shift"]
 # per-kernel algorithmic bytes per env (reads + writes it must do)
 KERNEL_BYTES = {
     "k_dynamics": 4 * (13 + 24 + 12 + 48 + 12 * 6 + 13 + 3 + 3) + 4 * (13 + 24 + 169 + 39 + 12 + 12 + 12 + 24 + 6),
     "k_post_a": 4 * (13 + 24 + 169 + 39 + 12 * 5 + 6 + 4 + 24 + 12 + 3 + 6 + 8) + 4 * (3 * 4 + 6 + 3 + 2 + 4 + 24 + 3 + 6),
     "k_post_b": 4 * (24 + 13 + 12 * 2 + 3 * 3 + 39 + 24 + 6 + 8) + 4 * (47 + 73 + 12 * 4 + 6),
     "k_shift": 2 * 4 * ((3102 - 47) + (219 - 73)),
-    "k_finalize": 1,
 }
 
 

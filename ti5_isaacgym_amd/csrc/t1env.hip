@@ -735,14 +735,19 @@ __device__ __forceinline__ void shift_rows(const float* __restrict__ in, float* 
   }
 }
 
+// grid-stride over the float4 chunks: a bounded grid (SHIFT_BLOCKS) streams the history at HBM rate while
+// leaving CUs for k_dynamics, whose waves each need a whole SIMD register file
+constexpr int SHIFT_BLOCKS = 1024;
 __global__ __launch_bounds__(256) void k_shift(const float* __restrict__ obs_in, float* __restrict__ obs_out,
                                                const float* __restrict__ priv_in, float* __restrict__ priv_out,
                                                int num_envs, int64_t n4_obs, int64_t n4_priv) {
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t tot_obs = (int64_t)num_envs * T1_NOBS * T1_HIST;
   const int64_t tot_priv = (int64_t)num_envs * T1_NPRIV * T1_CHIST;
-  if (tid < n4_obs) shift_rows<T1_NOBS, T1_HIST>(obs_in, obs_out, tot_obs, tid);
-  else if (tid < n4_obs + n4_priv) shift_rows<T1_NPRIV, T1_CHIST>(priv_in, priv_out, tot_priv, tid - n4_obs);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < n4_obs + n4_priv; tid += stride) {
+    if (tid < n4_obs) shift_rows<T1_NOBS, T1_HIST>(obs_in, obs_out, tot_obs, tid);
+    else shift_rows<T1_NPRIV, T1_CHIST>(priv_in, priv_out, tot_priv, tid - n4_obs);
+  }
 }
 
 // extras finalisation for t1env_reset_all (one wave)
@@ -959,17 +964,25 @@ int t1env_set_terrain(t1env* e, const int16_t* h, int32_t rows, int32_t cols, fl
   return 0;
 }
 
-// fork the history shift of this step onto the side stream (it reads only the previous step's buffer)
+// fork the history shift of this step onto the side stream (it reads only the previous step's buffer).  The
+// fork point is recorded on the caller's stream first (mark_fork); the shift itself is enqueued after
+// k_dynamics so the dynamics workgroups claim their CUs first.
+static int mark_fork(t1env* e, hipStream_t s) {
+  HIP_TRY(hipEventRecord(e->ev_fork, s));
+  return 0;
+}
 static int fork_shift(t1env* e, const t1env_step_args* a, hipStream_t s) {
   if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
   const int N = e->cfg.num_envs;
   const int64_t n4o = ((int64_t)N * T1_NOBS * T1_HIST + 3) / 4;
   const int64_t n4p = ((int64_t)N * T1_NPRIV * T1_CHIST + 3) / 4;
   const int in = a->obs_slot ^ 1, outs = a->obs_slot;
-  HIP_TRY(hipEventRecord(e->ev_fork, s));
+  (void)s;
   HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fork, 0));
   const int t = t_begin(e, 3, e->side);
-  hipLaunchKernelGGL(k_shift, dim3((unsigned)((n4o + n4p + 255) / 256)), dim3(256), 0, e->side, e->buf.obs_buf[in],
+  const int64_t blocks = (n4o + n4p + 255) / 256;
+  hipLaunchKernelGGL(k_shift, dim3((unsigned)(blocks < SHIFT_BLOCKS ? blocks : SHIFT_BLOCKS)), dim3(256), 0, e->side,
+                     e->buf.obs_buf[in],
                      e->buf.obs_buf[outs], e->buf.priv_buf[in], e->buf.priv_buf[outs], N, n4o, n4p);
   t_end(e, t, e->side);
   HIP_TRY(hipGetLastError());
@@ -982,7 +995,7 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
                           hipStream_t s) {
   const int N = e->cfg.num_envs;
   e->step_timer = t_begin(e, 5, s);
-  if (int rc = fork_shift(e, a, s)) return rc;
+  if (int rc = mark_fork(e, s)) return rc;
   int t = t_begin(e, 0, s);
   if (inj)
     hipLaunchKernelGGL(k_physics_injected, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
@@ -991,6 +1004,7 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
     HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, N, s));
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
+  if (int rc = fork_shift(e, a, s)) return rc;
   t = t_begin(e, 1, s);
   hipLaunchKernelGGL(k_post_a, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a);
   t_end(e, t, s);
@@ -1017,6 +1031,7 @@ int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* strea
   const int N = e->cfg.num_envs;
   if (!e->shift_pending) {  // phase B without phase A on this env: shift now, in order
     e->step_timer = -1;
+    if (int rc = mark_fork(e, s)) return rc;
     if (int rc = fork_shift(e, a, s)) return rc;
   }
   HIP_TRY(hipStreamWaitEvent(s, e->ev_join, 0));
