@@ -204,8 +204,9 @@ int t1env_reset_all(t1env* env, const t1env_step_args* args, void* stream);
  * need the host to read ep_accum between the phases, so the step is exposed in two halves:
  *   t1env_step_physics_and_rewards  -> physics, post_a (callback, termination, rewards, extras reduction)
  *   t1env_step_reset_and_observe    -> post_b (reset_idx of flagged envs, observations, newest history frame)
- * The 65 older history frames are shifted by a kernel the library forks onto an internal stream at the start
- * of phase A and joins before post_b (it reads only the previous step's buffer).
+ * The 65 older history frames are shifted by extra workgroups of phase A's dynamics launch (it reads only the
+ * previous step's buffer, so it overlaps the dynamics on the CUs they leave idle); post_b follows in stream
+ * order.  Everything runs on the caller's stream: no internal streams or events.
  * t1env_step() runs both back to back (no host sync). */
 int t1env_step(t1env* env, const float* actions, const t1env_step_args* args, void* stream);
 int t1env_step_physics_and_rewards(t1env* env, const float* actions, const t1env_step_args* args, void* stream);
@@ -213,9 +214,9 @@ int t1env_step_reset_and_observe(t1env* env, const t1env_step_args* args, void* 
 int t1env_step_injected(t1env* env, const float* actions, const t1env_step_args* args, const t1env_injected* inj,
                         void* stream);
 /* Per-kernel timing with HIP events recorded around every launch (bench.py's live roofline).  Ids:
- * 0 k_dynamics (or the injected-physics kernel), 1 k_post_a, 2 k_post_b (its last block also finalises the
- * extras), 3 k_shift (internal side stream, overlapping 0-1), 4 unused, 5 the whole step (phase A start ..
- * phase B end on the caller's stream).  get_timing synchronises and returns summed milliseconds and launch counts per id since
+ * 0 k_dynamics incl. its history-shift workgroups (or the injected-physics kernel), 1 k_post_a, 2 k_post_b (its
+ * last block also finalises the extras), 3 stand-alone k_shift (injected physics or phase B without phase A),
+ * 4 unused, 5 the whole step (phase A start .. phase B end).  get_timing synchronises and returns summed milliseconds and launch counts per id since
  * the last enable. */
 #define T1ENV_NTIMERS 6
 /* enable: bit 0 = record events from now on; bit 1 = keep (do not clear) the events recorded so far */

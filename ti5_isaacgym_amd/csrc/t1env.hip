@@ -7,11 +7,11 @@
 //                episode sums, per-step extras reduction (legged_robot.py:458-489, 509-517, 654-680)
 //   k_post_b   : masked reset_idx, compute_observations -> newest obs/priv frame, last_* bookkeeping
 //                (legged_robot.py:490-502, t1_dh_stand_env.py:368-559)
-//   k_shift    : 65 older frames of the 66-frame (and 3-frame critic) history shifted into the ping-pong
-//                output buffer, thread per 4 floats, fully coalesced (the HBM-dominant part: ~26 KB per env
-//                per step).  It does not depend on this step's physics, so it runs on an internal side stream
-//                concurrently with k_dynamics (which leaves half the CUs idle at 8192 envs); k_post_b joins it
-//                before writing the newest frame and zeroing the history rows of reset envs.
+//   shift      : 65 older frames of the 66-frame (and 3-frame critic) history shifted into the ping-pong
+//                output buffer, lane per 4 floats, fully coalesced (the HBM-dominant part: ~26 KB per env
+//                per step).  It does not depend on this step's physics, so it runs as extra workgroups of the
+//                k_dynamics launch on the CUs the dynamics leaves idle (t1env_dynamics.hip); k_post_b, next
+//                on the stream, writes the newest frame and zeroes the history rows of reset envs.
 // See include/t1env.h for the ABI and DESIGN.md for layouts and rooflines.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -46,7 +46,12 @@ constexpr int BLOCK = 64;  // one wave per workgroup: 8192 envs -> 128 workgroup
 
 }  // namespace
 
-constexpr int NKERN = 6;  // 0 physics, 1 post_a, 2 post_b, 3 shift (side stream), 4 finalize, 5 whole step
+constexpr int NKERN = 6;  // 0 physics (+ shift), 1 post_a, 2 post_b, 3 shift alone, 4 unused, 5 whole step
+constexpr int SHIFT_BLOCKS = 1024;       // grid of the stand-alone k_shift (256 threads)
+// history-shift workgroups appended to k_dynamics (128 threads).  A k_dynamics wave holds a whole SIMD's
+// registers (1 wave/SIMD, 2 workgroups/CU), so the default fills exactly the workgroup slots the dynamics
+// leaves free: 2 * CUs - dynamics workgroups (384 at 8192 envs on 256 CUs), at least MIN_SHIFT_BLOCKS.
+constexpr int MIN_SHIFT_BLOCKS = 64;
 constexpr int MAX_TIMED = 1 << 14;
 
 struct t1env {
@@ -60,9 +65,8 @@ struct t1env {
   DynModel* d_model;
   t1env_config* d_cfg;
   Terrain terrain;
-  hipStream_t side;       // history shift, forked from the caller's stream at the start of each step
-  hipEvent_t ev_fork, ev_join;
-  int shift_pending;      // a shift was forked in phase A and not yet joined
+  int shift_blocks;       // see MIN_SHIFT_BLOCKS; T1ENV_SHIFT_BLOCKS in the environment overrides (tuning)
+  int shift_pending;      // phase A enqueued this step's history shift (phase B alone must run it)
   int step_timer;         // timing slot of the current step span (phase A start .. phase B end)
   unsigned* d_done;       // k_post_b block-completion counter (its last block finalises the extras)
   int16_t* d_hmax;        // coarse terrain height bound (Terrain::hmax), built by t1env_set_terrain
@@ -698,56 +702,10 @@ __global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ M
   }
 }
 
-// =====================================================================================================
-// history shift: out[n, :F*(H-1)] = in[n, F:]  -- a flat shift by F floats of every row; the newest frame
-// (columns >= F*(H-1)) is left to k_post_b, which also zeroes the older frames of reset envs.  One thread per
-// 4 output floats; the shifted source is assembled from two aligned 16-B loads.
-// =====================================================================================================
-template <int F, int H>
-__device__ __forceinline__ void shift_rows(const float* __restrict__ in, float* __restrict__ out, int64_t total,
-                                           int64_t i4) {
-  constexpr int ROW = F * H;
-  const int64_t i = i4 * 4;
-  const int64_t s = i + F;
-  const int64_t sa = s & ~(int64_t)3;
-  const int rem = (int)(s - sa);
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-  if (sa + 3 < total) a = *reinterpret_cast<const float4*>(in + sa);
-  else { for (int k = 0; k < 4; ++k) if (sa + k < total) (&a.x)[k] = in[sa + k]; }
-  if (rem) {
-    if (sa + 7 < total) b = *reinterpret_cast<const float4*>(in + sa + 4);
-    else { for (int k = 0; k < 4; ++k) if (sa + 4 + k < total) (&b.x)[k] = in[sa + 4 + k]; }
-  }
-  const float src[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  // the 4 outputs are all older-frame columns of one row unless the chunk touches a row's newest frame
-  const int64_t row0 = i / ROW;
-  const int col0 = (int)(i - row0 * ROW);
-  if (col0 + 3 < ROW - F && i + 3 < total) {
-    *reinterpret_cast<float4*>(out + i) = make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]);
-    return;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t e = i + k;
-    if (e >= total) break;
-    const int64_t row = e / ROW;
-    if ((int)(e - row * ROW) < ROW - F) out[e] = src[rem + k];
-  }
-}
-
-// grid-stride over the float4 chunks: a bounded grid (SHIFT_BLOCKS) streams the history at HBM rate while
-// leaving CUs for k_dynamics, whose waves each need a whole SIMD register file
-constexpr int SHIFT_BLOCKS = 1024;
-__global__ __launch_bounds__(256) void k_shift(const float* __restrict__ obs_in, float* __restrict__ obs_out,
-                                               const float* __restrict__ priv_in, float* __restrict__ priv_out,
-                                               int num_envs, int64_t n4_obs, int64_t n4_priv) {
-  const int64_t tot_obs = (int64_t)num_envs * T1_NOBS * T1_HIST;
-  const int64_t tot_priv = (int64_t)num_envs * T1_NPRIV * T1_CHIST;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < n4_obs + n4_priv; tid += stride) {
-    if (tid < n4_obs) shift_rows<T1_NOBS, T1_HIST>(obs_in, obs_out, tot_obs, tid);
-    else shift_rows<T1_NPRIV, T1_CHIST>(priv_in, priv_out, tot_priv, tid - n4_obs);
-  }
+// history shift for the paths that do not run k_dynamics (injected physics, phase B alone): the same
+// shift_history as k_dynamics' tail workgroups, as its own launch on the caller's stream
+__global__ __launch_bounds__(256) void k_shift(ShiftArgs S) {
+  shift_history(S, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
 }
 
 // extras finalisation for t1env_reset_all (one wave)
@@ -896,9 +854,6 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   hipError_t err;
   if ((err = hipMalloc(&e->d_model, sizeof(DynModel))) != hipSuccess ||
       (err = hipMalloc(&e->d_cfg, sizeof(t1env_config))) != hipSuccess ||
-      (err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking)) != hipSuccess ||
-      (err = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming)) != hipSuccess ||
-      (err = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess ||
       (err = hipMalloc(&e->d_done, sizeof(unsigned))) != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "t1env_create: hipMalloc: %s", hipGetErrorString(err));
     free(e);
@@ -908,6 +863,15 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   HIP_TRY(hipMemcpy(e->d_cfg, cfg, sizeof(t1env_config), hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(e->buf.ep_accum, 0, 32 * sizeof(float)));
   HIP_TRY(hipMemset(e->d_done, 0, sizeof(unsigned)));
+  {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+        hipSuccess) cus = 256;
+    const int free_slots = 2 * cus - (cfg->num_envs + 63) / 64;
+    e->shift_blocks = free_slots > MIN_SHIFT_BLOCKS ? free_slots : MIN_SHIFT_BLOCKS;
+    if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))
+      if (atoi(sb) > 0) e->shift_blocks = atoi(sb);
+  }
   for (int b = 0; b < NB; ++b) e->max_contact_radius = fmaxf(e->max_contact_radius, dm.contact_radius[b]);
   *out = e;
   return 0;
@@ -919,10 +883,6 @@ int t1env_destroy(t1env* e) {
   (void)hipFree(e->d_cfg);
   (void)hipFree(e->d_done);
   if (e->d_hmax) (void)hipFree(e->d_hmax);
-  if (e->side) (void)hipStreamSynchronize(e->side);
-  if (e->side) (void)hipStreamDestroy(e->side);
-  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   for (int i = 0; i < e->n_events; ++i) {
     (void)hipEventDestroy(e->ev_start[i]);
     (void)hipEventDestroy(e->ev_stop[i]);
@@ -964,47 +924,40 @@ int t1env_set_terrain(t1env* e, const int16_t* h, int32_t rows, int32_t cols, fl
   return 0;
 }
 
-// fork the history shift of this step onto the side stream (it reads only the previous step's buffer).  The
-// fork point is recorded on the caller's stream first (mark_fork); the shift itself is enqueued after
-// k_dynamics so the dynamics workgroups claim their CUs first.
-static int mark_fork(t1env* e, hipStream_t s) {
-  HIP_TRY(hipEventRecord(e->ev_fork, s));
-  return 0;
+static ShiftArgs shift_args(const t1env* e, const t1env_step_args* a) {
+  const int64_t N = e->cfg.num_envs;
+  const int in = a->obs_slot ^ 1, out = a->obs_slot;
+  return ShiftArgs{e->buf.obs_buf[in], e->buf.obs_buf[out], e->buf.priv_buf[in], e->buf.priv_buf[out],
+                   N * T1_NOBS * T1_HIST, N * T1_NPRIV * T1_CHIST};
 }
-static int fork_shift(t1env* e, const t1env_step_args* a, hipStream_t s) {
-  if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
-  const int N = e->cfg.num_envs;
-  const int64_t n4o = ((int64_t)N * T1_NOBS * T1_HIST + 3) / 4;
-  const int64_t n4p = ((int64_t)N * T1_NPRIV * T1_CHIST + 3) / 4;
-  const int in = a->obs_slot ^ 1, outs = a->obs_slot;
-  (void)s;
-  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fork, 0));
-  const int t = t_begin(e, 3, e->side);
-  const int64_t blocks = (n4o + n4p + 255) / 256;
-  hipLaunchKernelGGL(k_shift, dim3((unsigned)(blocks < SHIFT_BLOCKS ? blocks : SHIFT_BLOCKS)), dim3(256), 0, e->side,
-                     e->buf.obs_buf[in],
-                     e->buf.obs_buf[outs], e->buf.priv_buf[in], e->buf.priv_buf[outs], N, n4o, n4p);
-  t_end(e, t, e->side);
+
+// the history shift as its own launch, in stream order (paths without k_dynamics)
+static int launch_shift(t1env* e, const t1env_step_args* a, hipStream_t s) {
+  const int t = t_begin(e, 3, s);
+  hipLaunchKernelGGL(k_shift, dim3(SHIFT_BLOCKS), dim3(256), 0, s, shift_args(e, a));
+  t_end(e, t, s);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(e->ev_join, e->side));
-  e->shift_pending = 1;
   return 0;
 }
 
 static int launch_physics(t1env* e, const float* actions, const t1env_step_args* a, const t1env_injected* inj,
                           hipStream_t s) {
+  if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
   const int N = e->cfg.num_envs;
   e->step_timer = t_begin(e, 5, s);
-  if (int rc = mark_fork(e, s)) return rc;
   int t = t_begin(e, 0, s);
   if (inj)
     hipLaunchKernelGGL(k_physics_injected, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
                        actions, *a, *inj);
   else
-    HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, N, s));
+    HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, N,
+                                           shift_args(e, a), e->shift_blocks, s));
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
-  if (int rc = fork_shift(e, a, s)) return rc;
+  if (inj) {
+    if (int rc = launch_shift(e, a, s)) return rc;
+  }
+  e->shift_pending = 1;
   t = t_begin(e, 1, s);
   hipLaunchKernelGGL(k_post_a, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a);
   t_end(e, t, s);
@@ -1031,10 +984,8 @@ int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* strea
   const int N = e->cfg.num_envs;
   if (!e->shift_pending) {  // phase B without phase A on this env: shift now, in order
     e->step_timer = -1;
-    if (int rc = mark_fork(e, s)) return rc;
-    if (int rc = fork_shift(e, a, s)) return rc;
+    if (int rc = launch_shift(e, a, s)) return rc;
   }
-  HIP_TRY(hipStreamWaitEvent(s, e->ev_join, 0));
   e->shift_pending = 0;
   int t = t_begin(e, 2, s);
   hipLaunchKernelGGL(k_post_b, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,

@@ -102,4 +102,81 @@ __device__ __forceinline__ void capture_imu(const float quat[4], const float w_w
   dst[3] = e[0]; dst[4] = e[1]; dst[5] = e[2];
 }
 
+
+// =====================================================================================================
+// history shift: out[n, :F*(H-1)] = in[n, F:] -- a flat shift by F floats of every row of the 66-frame obs
+// and 3-frame critic history; the newest frame (columns >= F*(H-1)) is left to k_post_b, which also zeroes
+// the older frames of reset envs.  One lane per 4 output floats, the shifted source assembled from two
+// aligned 16-B loads.  SHIFT_UNROLL chunks per lane are loaded before any is stored (all loads are
+// unconditional, clamped in bounds), so a lane keeps 8 x 16 B in flight: the shift reaches HBM rate with a
+// few hundred workgroups, which is what k_dynamics' tail workgroups can field (each of its waves holds 240
+// VGPRs).  It reads only the previous step's buffer, so it overlaps the dynamics inside one launch.
+// =====================================================================================================
+struct ShiftArgs {
+  const float* obs_in;
+  float* obs_out;
+  const float* priv_in;
+  float* priv_out;
+  int64_t total_obs, total_priv;  // floats
+};
+constexpr int SHIFT_UNROLL = 4;
+
+template <int F, int H>
+__device__ __forceinline__ void shift_store(float* __restrict__ out, int64_t total, int64_t i, const float4 a,
+                                            const float4 b, int rem) {
+  constexpr int ROW = F * H;
+  const float src[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const int64_t row0 = i / ROW;
+  const int col0 = (int)(i - row0 * ROW);
+  // the 4 outputs are all older-frame columns of one row unless the chunk touches a row's newest frame
+  if (col0 + 3 < ROW - F && i + 3 < total) {
+    *reinterpret_cast<float4*>(out + i) = make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t e = i + k;
+    if (e >= total) break;
+    const int64_t row = e / ROW;
+    if ((int)(e - row * ROW) < ROW - F) out[e] = src[rem + k];
+  }
+}
+
+template <int F, int H>
+__device__ __forceinline__ void shift_range(const float* __restrict__ in, float* __restrict__ out, int64_t total,
+                                            int64_t t0, int64_t stride) {
+  const int64_t n4 = (total + 3) / 4;
+  for (int64_t base = t0; base < n4; base += SHIFT_UNROLL * stride) {
+    float4 a[SHIFT_UNROLL], b[SHIFT_UNROLL];
+#pragma unroll
+    for (int u = 0; u < SHIFT_UNROLL; ++u) {
+      const int64_t sa = ((base + u * stride) * 4 + F) & ~(int64_t)3;
+      const int64_t sc = sa + 8 <= total ? sa : (total - 8) & ~(int64_t)3;  // tail: aligned in-bounds dummy
+      a[u] = *reinterpret_cast<const float4*>(in + sc);
+      b[u] = *reinterpret_cast<const float4*>(in + sc + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < SHIFT_UNROLL; ++u) {
+      const int64_t i4 = base + u * stride;
+      if (i4 >= n4) break;
+      const int64_t i = i4 * 4, s = i + F, sa = s & ~(int64_t)3;
+      float4 x = a[u], y = b[u];
+      if (sa + 8 > total) {  // the last chunks of the buffer: element loads, zero past the end
+        float t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = sa + k < total ? in[sa + k] : 0.0f;
+        x = make_float4(t[0], t[1], t[2], t[3]);
+        y = make_float4(t[4], t[5], t[6], t[7]);
+      }
+      shift_store<F, H>(out, total, i, x, y, (int)(s - sa));
+    }
+  }
+}
+
+// lane `t0` of `stride` lanes: the obs history, then the critic history
+__device__ __forceinline__ void shift_history(const ShiftArgs& S, int64_t t0, int64_t stride) {
+  shift_range<T1_NOBS, T1_HIST>(S.obs_in, S.obs_out, S.total_obs, t0, stride);
+  shift_range<T1_NPRIV, T1_CHIST>(S.priv_in, S.priv_out, S.total_priv, t0, stride);
+}
+
 }  // namespace t1

@@ -16,6 +16,12 @@ using namespace t1;
 // 27-float base-block contribution (t1_dynamics.h leg_contribution), the two contributions meet in LDS
 // (double-buffered by substep parity -> one barrier per substep), and both waves solve the 6x6 base system
 // redundantly, so the base state stays bit-identical in both without further exchange.
+//
+// Workgroups past the dynamics grid (blockIdx >= dyn_blocks) run the history shift instead
+// (t1env_device.h shift_history).  The dynamics waves fill at most half the CUs at 8192 envs, so the
+// HBM-bound shift streams on the rest of the chip inside the same launch -- no second stream, no
+// cross-stream events on the step path.  The dynamics workgroups have the lower ids, so they are dispatched
+// first.
 // ---------------------------------------------------------------------------------------------------
 constexpr int DYN_ENVS = 64;
 constexpr int DYN_BLOCK = 2 * DYN_ENVS;
@@ -27,8 +33,13 @@ template <bool HF>
 __global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restrict__ Mp,
                                                         const t1env_config* __restrict__ Cp, t1env_buffers B,
                                                         Terrain Tin, const float* __restrict__ actions,
-                                                        t1env_step_args A) {
+                                                        t1env_step_args A, ShiftArgs S, int dyn_blocks) {
   __shared__ float xch[2][2][XCH][DYN_ENVS];  // [substep parity][leg][value][env]
+  if ((int)blockIdx.x >= dyn_blocks) {
+    const int64_t stride = (int64_t)(gridDim.x - dyn_blocks) * DYN_BLOCK;
+    shift_history(S, (int64_t)(blockIdx.x - dyn_blocks) * DYN_BLOCK + threadIdx.x, stride);
+    return;
+  }
   Terrain T = Tin;
   T.type = HF ? 2 : 0;
   const t1env_config& C = *Cp;
@@ -124,11 +135,13 @@ __global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restri
 }
 
 int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
-                       const float* actions, const t1env_step_args& A, int num_envs, hipStream_t s) {
-  const dim3 grid((num_envs + DYN_ENVS - 1) / DYN_ENVS), block(DYN_BLOCK);
+                       const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
+                       int shift_blocks, hipStream_t s) {
+  const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
+  const dim3 grid(dyn_blocks + shift_blocks), block(DYN_BLOCK);
   if (T.type == 0)
-    hipLaunchKernelGGL(k_dynamics<false>, grid, block, 0, s, d_model, d_cfg, B, T, actions, A);
+    hipLaunchKernelGGL(k_dynamics<false>, grid, block, 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks);
   else
-    hipLaunchKernelGGL(k_dynamics<true>, grid, block, 0, s, d_model, d_cfg, B, T, actions, A);
+    hipLaunchKernelGGL(k_dynamics<true>, grid, block, 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks);
   return (int)hipGetLastError();
 }

@@ -5,7 +5,10 @@
 #include "../../include/t1env.h"
 #include "t1_dynamics.h"
 
-// k_dynamics launch (t1env_dynamics.hip); returns a hipError_t
+#include "t1env_device.h"
+
+// k_dynamics launch (t1env_dynamics.hip) with `shift_blocks` extra workgroups running the history shift S
+// (shift_blocks >= 1); returns a hipError_t
 int t1_launch_dynamics(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B,
                        const t1::Terrain& T, const float* actions, const t1env_step_args& A, int num_envs,
-                       hipStream_t s);
+                       const t1::ShiftArgs& S, int shift_blocks, hipStream_t s);

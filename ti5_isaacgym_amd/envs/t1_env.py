@@ -532,7 +532,7 @@ class T1DHStandEnv(VecEnv):
         _lib.check(self._lib.t1env_set_timing(self._handle, int(enable) | (0 if reset else 2)), "t1env_set_timing")
 
     def get_timing(self):
-        names = ["k_dynamics", "k_post_a", "k_post_b", "k_shift", "k_finalize", "step"]
+        names = ["k_dynamics", "k_post_a", "k_post_b", "k_shift", "unused", "step"]  # include/t1env.h timers
         ms = (_lib.C.c_double * len(names))()
         n = (_lib.C.c_int32 * len(names))()
         _lib.check(self._lib.t1env_get_timing(self._handle, ms, n), "t1env_get_timing")
