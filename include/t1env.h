@@ -213,6 +213,11 @@ int t1env_step_physics_and_rewards(t1env* env, const float* actions, const t1env
 int t1env_step_reset_and_observe(t1env* env, const t1env_step_args* args, void* stream);
 int t1env_step_injected(t1env* env, const float* actions, const t1env_step_args* args, const t1env_injected* inj,
                         void* stream);
+/* t1env_step runs the whole step as ONE launch by default (fused): the history shift and post-physics ride in
+ * the dynamics kernel (post-physics in its epilogue).  enable = 0 makes t1env_step run the split sequence
+ * (physics_and_rewards + reset_and_observe) instead; both give the same buffers.  The split entry points are
+ * unaffected (they are what command-curriculum steps use). */
+int t1env_set_fused(t1env* env, int32_t enable);
 /* Per-kernel timing with HIP events recorded around every launch (bench.py's live roofline).  Ids:
  * 0 k_dynamics incl. its history-shift workgroups (or the injected-physics kernel), 1 k_post_a, 2 k_post_b (its
  * last block also finalises the extras), 3 stand-alone k_shift (injected physics or phase B without phase A),

@@ -85,7 +85,7 @@ class Injected(C.Structure):
 
 EXPORTS = ["t1env_create", "t1env_destroy", "t1env_init", "t1env_set_terrain", "t1env_reset_all", "t1env_step",
            "t1env_step_physics_and_rewards", "t1env_step_reset_and_observe", "t1env_step_injected",
-           "t1env_set_timing", "t1env_get_timing", "t1env_last_error", "t1env_version"]
+           "t1env_set_fused", "t1env_set_timing", "t1env_get_timing", "t1env_last_error", "t1env_version"]
 
 _lib = None
 
@@ -110,6 +110,7 @@ def load():
         "t1env_step_physics_and_rewards": ([vp, vp, P(StepArgs), vp], C.c_int),
         "t1env_step_reset_and_observe": ([vp, P(StepArgs), vp], C.c_int),
         "t1env_step_injected": ([vp, vp, P(StepArgs), P(Injected), vp], C.c_int),
+        "t1env_set_fused": ([vp, i32], C.c_int),
         "t1env_set_timing": ([vp, i32], C.c_int),
         "t1env_get_timing": ([vp, C.POINTER(C.c_double), i32p], C.c_int),
         "t1env_last_error": ([], C.c_char_p),

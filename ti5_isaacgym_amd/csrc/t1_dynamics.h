@@ -28,6 +28,11 @@
 
 #include "t1_common.h"
 
+// phase profiling hook (t1env_dynamics.hip built with -DT1_PHASE_PROF); compiled out otherwise
+#ifndef T1_PROF_MARK
+#define T1_PROF_MARK(i) ((void)0)
+#endif
+
 namespace t1 {
 
 constexpr int NB = 13, ND = 12, NLEG = 6;
@@ -625,6 +630,7 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
   fwd(kconst<3>{});
   fwd(kconst<4>{});
   fwd(kconst<5>{});
+  T1_PROF_MARK(1);
   Sym6<R> Ac;
   sym_zero(Ac);
   R gc[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
@@ -647,9 +653,12 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
       sym_add(Ac, I);
     }
     if constexpr (CM >= 0) {
-      if constexpr ((CM >> k) & 1)
+      if constexpr ((CM >> k) & 1) {
+        T1_PROF_MARK(2);
         body_contact_fixed<T1_POINTS_PER_BODY>(M, T, lowest[k], bound[k], M.contact_start[b], Rk, pk, F.abs, V, mu,
                                                dt, Ac, gc);
+        T1_PROF_MARK(3);
+      }
     } else {
       const int c0 = M.contact_start[b], nc = M.contact_count[b];
       if (nc > 0) body_contact(M, T, c0, c0 + nc, Rk, pk, F.abs, V, mu, dt, Ac, gc);
@@ -783,9 +792,11 @@ T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParam
   R g[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
   const int32_t base_bound = CM >= 0 ? terrain_bound_raw_any(T, F.abs.x, F.abs.y) : 0;  // tested after the leg pass
   leg_assemble<CM>(M, T, PL, PB.friction, F, q, qd, tau, leg, dt, lb, Ab, g);
+  T1_PROF_MARK(2);
 #pragma unroll
   for (int i = 0; i < 6; ++i) rb[i] = -g[i];
   eliminate_leg(lb, Ab, rb);
+  T1_PROF_MARK(4);
   int cb, ce;
   base_contact_range(M, leg, cb, ce);
   R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
@@ -797,6 +808,7 @@ T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParam
   }
 #pragma unroll
   for (int i = 0; i < 6; ++i) rb[i] -= gw[i];
+  T1_PROF_MARK(5);
 }
 
 // Semi-implicit Euler of the base with the solved velocity change (+ the omega x v term that turns the

@@ -121,7 +121,25 @@ struct ShiftArgs {
 };
 constexpr int SHIFT_UNROLL = 4;
 
-template <int F, int H>
+// Stores of the shift.  SC1 = the agent-coherent flavour (global_store ... sc1): the line leaves the XCD's L2
+// and the store is visible to every XCD once it completes, so a later handoff needs only s_waitcnt, not an L2
+// write-back (MI355X_MICROARCH.md, inter-workgroup visibility).  The fused step uses it for the rows whose
+// reset zeroing may run on another XCD.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <bool SC1> __device__ __forceinline__ void store4(float* p, float4 v) {
+  if constexpr (SC1) {
+    const f32x4 x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(x) : "memory");
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
+template <bool SC1> __device__ __forceinline__ void store1(float* p, float v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+template <int F, int H, bool SC1>
 __device__ __forceinline__ void shift_store(float* __restrict__ out, int64_t total, int64_t i, const float4 a,
                                             const float4 b, int rem) {
   constexpr int ROW = F * H;
@@ -130,7 +148,7 @@ __device__ __forceinline__ void shift_store(float* __restrict__ out, int64_t tot
   const int col0 = (int)(i - row0 * ROW);
   // the 4 outputs are all older-frame columns of one row unless the chunk touches a row's newest frame
   if (col0 + 3 < ROW - F && i + 3 < total) {
-    *reinterpret_cast<float4*>(out + i) = make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]);
+    store4<SC1>(out + i, make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]));
     return;
   }
 #pragma unroll
@@ -138,15 +156,15 @@ __device__ __forceinline__ void shift_store(float* __restrict__ out, int64_t tot
     const int64_t e = i + k;
     if (e >= total) break;
     const int64_t row = e / ROW;
-    if ((int)(e - row * ROW) < ROW - F) out[e] = src[rem + k];
+    if ((int)(e - row * ROW) < ROW - F) store1<SC1>(out + e, src[rem + k]);
   }
 }
 
-template <int F, int H>
+// chunks [lo4, hi4) of one history buffer, lane t0 of `stride` lanes
+template <int F, int H, bool SC1 = false>
 __device__ __forceinline__ void shift_range(const float* __restrict__ in, float* __restrict__ out, int64_t total,
-                                            int64_t t0, int64_t stride) {
-  const int64_t n4 = (total + 3) / 4;
-  for (int64_t base = t0; base < n4; base += SHIFT_UNROLL * stride) {
+                                            int64_t lo4, int64_t hi4, int64_t t0, int64_t stride) {
+  for (int64_t base = lo4 + t0; base < hi4; base += SHIFT_UNROLL * stride) {
     float4 a[SHIFT_UNROLL], b[SHIFT_UNROLL];
 #pragma unroll
     for (int u = 0; u < SHIFT_UNROLL; ++u) {
@@ -158,7 +176,7 @@ __device__ __forceinline__ void shift_range(const float* __restrict__ in, float*
 #pragma unroll
     for (int u = 0; u < SHIFT_UNROLL; ++u) {
       const int64_t i4 = base + u * stride;
-      if (i4 >= n4) break;
+      if (i4 >= hi4) break;
       const int64_t i = i4 * 4, s = i + F, sa = s & ~(int64_t)3;
       float4 x = a[u], y = b[u];
       if (sa + 8 > total) {  // the last chunks of the buffer: element loads, zero past the end
@@ -168,15 +186,37 @@ __device__ __forceinline__ void shift_range(const float* __restrict__ in, float*
         x = make_float4(t[0], t[1], t[2], t[3]);
         y = make_float4(t[4], t[5], t[6], t[7]);
       }
-      shift_store<F, H>(out, total, i, x, y, (int)(s - sa));
+      shift_store<F, H, SC1>(out, total, i, x, y, (int)(s - sa));
     }
   }
 }
 
 // lane `t0` of `stride` lanes: the obs history, then the critic history
 __device__ __forceinline__ void shift_history(const ShiftArgs& S, int64_t t0, int64_t stride) {
-  shift_range<T1_NOBS, T1_HIST>(S.obs_in, S.obs_out, S.total_obs, t0, stride);
-  shift_range<T1_NPRIV, T1_CHIST>(S.priv_in, S.priv_out, S.total_priv, t0, stride);
+  shift_range<T1_NOBS, T1_HIST>(S.obs_in, S.obs_out, S.total_obs, 0, (S.total_obs + 3) / 4, t0, stride);
+  shift_range<T1_NPRIV, T1_CHIST>(S.priv_in, S.priv_out, S.total_priv, 0, (S.total_priv + 3) / 4, t0, stride);
+}
+
+// the rows [r0, r1) of both histories (r0 a multiple of 4, so both row ranges start on a 16-B chunk), with
+// agent-coherent (sc1) stores
+__device__ __forceinline__ void shift_rows_range_sc1(const ShiftArgs& S, int64_t r0, int64_t r1, int64_t t0,
+                                                 int64_t stride) {
+  constexpr int64_t RO = T1_NOBS * T1_HIST, RP = T1_NPRIV * T1_CHIST;
+  const int64_t n4o = (S.total_obs + 3) / 4, n4p = (S.total_priv + 3) / 4;
+  const int64_t ho = (r1 * RO + 3) / 4, hp = (r1 * RP + 3) / 4;
+  shift_range<T1_NOBS, T1_HIST, true>(S.obs_in, S.obs_out, S.total_obs, r0 * RO / 4, ho < n4o ? ho : n4o, t0,
+                                      stride);
+  shift_range<T1_NPRIV, T1_CHIST, true>(S.priv_in, S.priv_out, S.total_priv, r0 * RP / 4, hp < n4p ? hp : n4p, t0,
+                                        stride);
+}
+
+// reset_idx clears the obs / critic history deques of a reset env (t1_dh_stand_env.py:548-558): the 65 (2)
+// older frames of `row` in the freshly shifted output, lane t0 of `stride` lanes
+__device__ __forceinline__ void zero_history_row(const ShiftArgs& S, int64_t row, int t0, int stride) {
+  float* o = S.obs_out + row * (T1_NOBS * T1_HIST);
+  for (int c = t0; c < T1_NOBS * (T1_HIST - 1); c += stride) o[c] = 0.0f;
+  float* p = S.priv_out + row * (T1_NPRIV * T1_CHIST);
+  for (int c = t0; c < T1_NPRIV * (T1_CHIST - 1); c += stride) p[c] = 0.0f;
 }
 
 }  // namespace t1

@@ -7,8 +7,15 @@
 
 #include "t1env_device.h"
 
+// state of the fused step (k_dynamics with post-physics in its epilogue, t1env_dynamics.hip)
+struct FusedArgs {
+  unsigned* done;                  // dynamics-workgroup completion counter (the last one finalises the extras)
+  uint32_t* unit_state;            // per shift unit: epoch-tagged handoff word (reset mask inside)
+  uint32_t epoch;                  // launch number (unique per fused step)
+};
+
 // k_dynamics launch (t1env_dynamics.hip) with `shift_blocks` extra workgroups running the history shift S
-// (shift_blocks >= 1); returns a hipError_t
+// (shift_blocks >= 1); fused != nullptr: the whole step (post-physics in the epilogue).  Returns a hipError_t.
 int t1_launch_dynamics(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B,
                        const t1::Terrain& T, const float* actions, const t1env_step_args& A, int num_envs,
-                       const t1::ShiftArgs& S, int shift_blocks, hipStream_t s);
+                       const t1::ShiftArgs& S, int shift_blocks, const FusedArgs* fused, hipStream_t s);

@@ -526,6 +526,10 @@ class T1DHStandEnv(VecEnv):
         obs, priv, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
         return obs, priv
 
+    def set_fused(self, enable=True):
+        """t1env_step as one fused launch (default) or the split kernel sequence (same results; tests)."""
+        _lib.check(self._lib.t1env_set_fused(self._handle, int(bool(enable))), "t1env_set_fused")
+
     def set_timing(self, enable=True, reset=True):
         """Record HIP events around every kernel launch (bench.py's live per-kernel timing).  reset=False keeps
         the events recorded so far (bench.py samples every k-th step)."""

@@ -1,0 +1,73 @@
+"""Dev probe: where k_dynamics spends its time, per substep phase (shader-clock deltas inside the kernel).
+
+    python tools/prof_dynamics_phases.py --build      # here: builds _lib/libt1env_hip_prof.so (-DT1_PHASE_PROF)
+    python tools/prof_dynamics_phases.py [--mesh trimesh] [--num-envs 8192]   # on the GPU box
+
+Lane 0 of every dynamics wave accumulates clock64() deltas between the T1_PROF_MARK points of
+t1env_dynamics.hip / t1_dynamics.h.  Reported per wave (0 = left leg, 1 = right leg) as the share of the
+wave's cycles and as microseconds scaled to the measured kernel time.  The marks cost a few instructions
+each, so the profiled kernel is slightly slower than the product one.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF_LIB = os.path.join(REPO, "ti5_isaacgym_amd", "_lib", "libt1env_hip_prof.so")
+BUCKETS = ["pd_torque+base_frame", "leg forward pass", "leg backward (no contact)", "leg contacts",
+           "leg elimination", "base-box contacts", "LDS write + base block", "substep tail / loop",
+           "barrier wait", "base solve + backsub + integrate", "prologue loads", "report (outputs)",
+           "epilogue barrier", "post_a (fused)", "post_b (fused)", "handoff + zeroing + finalize"]
+NB = len(BUCKETS)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--build", action="store_true")
+    p.add_argument("--mesh", default="trimesh")
+    p.add_argument("--num-envs", type=int, default=8192)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--split", action="store_true", help="time the split path (k_dynamics without epilogue)")
+    a = p.parse_args()
+    sys.path.insert(0, REPO)
+    if a.build:
+        from ti5_isaacgym_amd import build
+        print(build.build(force=True, extra=["-DT1_PHASE_PROF"], out=PROF_LIB))
+        return
+    os.environ["T1ENV_LIB"] = PROF_LIB
+    import torch
+    from ti5_isaacgym_amd import make_t1_env
+    env = make_t1_env(num_envs=a.num_envs, mesh_type=a.mesh, seed=5, device="cuda:0")
+    env.set_fused(not a.split)
+    lib = ctypes.CDLL(PROF_LIB)
+    buf = (ctypes.c_ulonglong * (2 * NB))()
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    acts = [torch.randn(a.num_envs, 12, device="cuda:0", generator=g) for _ in range(8)]
+    for i in range(50):
+        env.step(acts[i % 8])
+    torch.cuda.synchronize()
+    assert lib.t1env_debug_phase_cycles(buf, 1) == 0
+    env.set_timing(True)
+    for i in range(a.steps):
+        env.step(acts[i % 8])
+    torch.cuda.synchronize()
+    t = env.get_timing()
+    env.set_timing(False)
+    assert lib.t1env_debug_phase_cycles(buf, 0) == 0
+    kern_us = t["k_dynamics"]["ms"] / max(1, t["k_dynamics"]["launches"]) * 1e3
+    waves = (a.num_envs + 63) // 64
+    print(f"k_dynamics {kern_us:.1f} us/launch (events), {a.mesh}, {a.num_envs} envs, {a.steps} steps, "
+          f"{'split' if a.split else 'fused'}")
+    for w in range(2):
+        cyc = [buf[w * NB + i] / (waves * a.steps) for i in range(NB)]
+        tot = sum(cyc)
+        print(f"wave {w} ({'left' if w == 0 else 'right'} leg): {tot:.0f} cycles/launch")
+        for name, c in sorted(zip(BUCKETS, cyc), key=lambda x: -x[1]):
+            if c > 0:
+                print(f"   {name:34s} {c:10.0f} cyc  {100 * c / tot:5.1f}%  ~{kern_us * c / tot:6.1f} us")
+
+
+if __name__ == "__main__":
+    main()
