@@ -157,7 +157,7 @@ typedef struct t1env_buffers {
   int32_t* imu_lag_timestep;/* (N,) */
   float* act_hist;          /* (N,4,12) scaled actions of the last 4 env steps (ring by step) */
   float* dof_hist;          /* (N,4,24) lagged (q, qd) samples, ring by step */
-  float* imu_hist;          /* (N,2,6) lagged (ang vel, euler) samples, ring by step */
+  float* imu_hist;          /* (N,2,8) lagged IMU samples (raw base quat xyzw, world ang vel, pad), ring by step */
   float* env_origins;       /* (N,3) */
   int32_t* terrain_levels;  /* (N,) */
   int32_t* terrain_types;   /* (N,) */

@@ -811,6 +811,174 @@ T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParam
   T1_PROF_MARK(5);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Leg assembly split for the 4-wave kernel (t1env_dynamics.hip k_dyn4): the leg wave runs the articulated-
+// body passes without contact (leg_forward_nc, leg_backward_nc) while a helper wave computes the contact terms
+// of the leg's contact bodies from the poses the forward pass publishes; leg_apply_contacts then folds them
+// in.  Exact algebra, in world axes about O: the composite of body k is Ic_k = Ic0_k + Cs_k with
+// Cs_k = sum over contact bodies c >= k of C_c (C_c = dt J^T C J of body c's points, c_c its impulse wrench,
+// cs_k likewise), so every quantity of the backward pass is its contact-free value plus a linear term:
+//   F_k = F0_k + Cs_k S_k,   D_k = D0_k + S_k.Cs_k S_k,   H(k,j) = H0(k,j) + S_k.Cs_j S_j  (j > k),
+//   r_k = r0_k + dt tau_k - S_k.cs_k,   leg composite += sum_c C_c, bias += sum_c c_c.
+// Same system as leg_assemble up to fp32 summation order (tests/test_gpu_dynamics.py bounds both).
+// ---------------------------------------------------------------------------------------------------
+template <typename R> struct LegPass {
+  R sn[NLEG], cs[NLEG], g[NLEG][6];  // joint sin/cos, RNEA bias per body
+  M3<R> Rk;                           // leaf pose after the forward pass
+  V3<R> pk;
+  R S[NLEG][6];                       // motion subspaces, filled by the backward pass
+};
+
+// forward pass (root to leaf) without contact; pub(kconst<k>, R_k, p_k, V_k) is called for every contact
+// body k of the CM mask
+template <int CM, typename R, typename Pub>
+T1_HD void leg_forward_nc(const DynModel& M, const LegParams<R>& P, const BaseFrame<R>& F, const R q[NLEG],
+                          const R qd[NLEG], int leg, R dt, LegPass<R>& st, Pub&& pub) {
+  M3<R> Rk = F.R0;
+  V3<R> pk = v3<R>(0, 0, 0);
+  R V[6], A[6], Sk[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { V[i] = F.V0[i]; A[i] = R(0); }
+  A[5] = R(M.gravity);
+  auto fwd = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int AX = T1_LEG_AXIS[k];
+    const int b = 1 + 6 * leg + k;
+    pk = pk + mul(Rk, v3<R>(M.joint_offset[b][0], M.joint_offset[b][1], M.joint_offset[b][2]));
+    fsincos(R(M.axis_sign[b]) * q[k], &st.sn[k], &st.cs[k]);
+    Rk = joint_rot<AX>(M, b, Rk, st.cs[k], st.sn[k]);
+    joint_subspace<AX>(M, b, Rk, pk, Sk);
+    R vj[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) vj[i] = Sk[i] * qd[k];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) V[i] += vj[i];
+    R cr[6];
+    crm(V, vj, cr);  // V_k x (S qd)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) A[i] += cr[i];
+    if constexpr ((CM >> k) & 1) pub(kc, Rk, pk, V);
+    Sym6<R> I;
+    body_inertia(M, b, P.mass[k], P.inertia_scale[k], Rk, pk, I);
+    R IA[6], IV[6], vf[6];
+    sym_mul(I, A, IA);
+    sym_mul(I, V, IV);
+    crf(V, IV, vf);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) st.g[k][i] = dt * (IA[i] + vf[i]);
+  };
+  fwd(kconst<0>{});
+  fwd(kconst<1>{});
+  fwd(kconst<2>{});
+  fwd(kconst<3>{});
+  fwd(kconst<4>{});
+  fwd(kconst<5>{});
+  st.Rk = Rk;
+  st.pk = pk;
+}
+
+// backward pass (leaf to root) without contact and without the joint torque: D0, H0, F0 = Bl, r0 and the
+// contact-free leg composite; stores each S_k for leg_apply_contacts
+template <typename R>
+T1_HD void leg_backward_nc(const DynModel& M, const LegParams<R>& P, const R q[NLEG], const R qd[NLEG], int leg,
+                           R dt, LegPass<R>& st, LegBlock<R>& out, Sym6<R>& Ac_up, R gc_up[6]) {
+  M3<R> Rk = st.Rk;
+  V3<R> pk = st.pk;
+  Sym6<R> Ac;
+  sym_zero(Ac);
+  R gc[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+  auto step = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int b = 1 + 6 * leg + k, j = 6 * leg + k;
+    if constexpr (k < NLEG - 1) {  // step up from child k+1
+      constexpr int AXC = T1_LEG_AXIS[k + 1];
+      const int bc = b + 1;
+      Rk = joint_rot<AXC>(M, bc, Rk, st.cs[k + 1], -st.sn[k + 1]);
+      pk = pk - mul(Rk, v3<R>(M.joint_offset[bc][0], M.joint_offset[bc][1], M.joint_offset[bc][2]));
+    }
+    R* Sk = st.S[k];
+    joint_subspace<T1_LEG_AXIS[k]>(M, b, Rk, pk, Sk);
+    {
+      Sym6<R> I;
+      body_inertia(M, b, P.mass[k], P.inertia_scale[k], Rk, pk, I);
+      sym_add(Ac, I);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) gc[i] += st.g[k][i];
+    R Fk[6];
+    sym_mul(Ac, Sk, Fk);
+    R Ajj = dot6(Sk, Fk) + P.armature[k];
+    R rj = -dot6(Sk, gc);
+    const R lo = R(M.q_lower[j]), hi = R(M.q_upper[j]);
+    const R qj = q[k], qdj = qd[k];
+    if (qj < lo) {
+      const R cl = qdj < R(0) ? dt * R(M.k_limit) + R(M.d_limit) : R(0);
+      Ajj += dt * cl;
+      rj += dt * (R(M.k_limit) * (lo - qj) - cl * qdj);
+    } else if (qj > hi) {
+      const R cl = qdj > R(0) ? dt * R(M.k_limit) + R(M.d_limit) : R(0);
+      Ajj += dt * cl;
+      rj += dt * (R(M.k_limit) * (hi - qj) - cl * qdj);
+    }
+    out.L[sidx(k, k)] = Ajj;
+    out.rhs[k] = rj;
+#pragma unroll
+    for (int jj = k + 1; jj < NLEG; ++jj) {
+      R Fj[6] = {out.Bl[0][jj], out.Bl[1][jj], out.Bl[2][jj], out.Bl[3][jj], out.Bl[4][jj], out.Bl[5][jj]};
+      out.L[sidx(k, jj)] = dot6(Sk, Fj);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) out.Bl[r][k] = Fk[r];
+  };
+  step(kconst<5>{});
+  step(kconst<4>{});
+  step(kconst<3>{});
+  step(kconst<2>{});
+  step(kconst<1>{});
+  step(kconst<0>{});
+  sym_add(Ac_up, Ac);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) gc_up[i] += gc[i];
+}
+
+// fold the contact terms of contact bodies K0 < K1 (C0/c0, C1/c1) and the joint torques into the contact-free
+// backward-pass result (see above)
+template <int K0, int K1, typename R>
+T1_HD void leg_apply_contacts(const Sym6<R>& C0, const R c0[6], const Sym6<R>& C1, const R c1[6],
+                              const R tau[NLEG], R dt, const LegPass<R>& st, LegBlock<R>& out, Sym6<R>& Ac_up,
+                              R gc_up[6]) {
+  static_assert(0 <= K0 && K0 < K1 && K1 < NLEG, "contact bodies K0 < K1 of the leg");
+  Sym6<R> Cs = C0;
+  sym_add(Cs, C1);
+  R cs[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) cs[i] = c0[i] + c1[i];
+  R u[NLEG][6];  // Cs_k S_k
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    if (k <= K0) sym_mul(Cs, st.S[k], u[k]);
+    else if (k <= K1) sym_mul(C1, st.S[k], u[k]);
+    else
+#pragma unroll
+      for (int i = 0; i < 6; ++i) u[k][i] = R(0);
+  }
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    const R sc = k <= K0 ? dot6(st.S[k], cs) : (k <= K1 ? dot6(st.S[k], c1) : R(0));
+    out.L[sidx(k, k)] += dot6(st.S[k], u[k]);
+    out.rhs[k] += dt * tau[k] - sc;
+#pragma unroll
+    for (int jj = k + 1; jj < NLEG; ++jj) out.L[sidx(k, jj)] += dot6(st.S[k], u[jj]);
+  }
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k)
+#pragma unroll
+    for (int r = 0; r < 6; ++r) out.Bl[r][k] += u[k][r];
+  sym_add(Ac_up, Cs);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) gc_up[i] += cs[i];
+}
+
 // Semi-implicit Euler of the base with the solved velocity change (+ the omega x v term that turns the
 // spatial base acceleration into the classical acceleration of the base origin).
 template <typename R> T1_HD void integrate_base(BaseState<R>& s, const R delta[6], R dt) {

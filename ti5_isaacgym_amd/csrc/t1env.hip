@@ -50,10 +50,6 @@ constexpr int BLOCK = 64;  // one wave per workgroup: 8192 envs -> 128 workgroup
 
 constexpr int NKERN = 6;  // 0 physics (+ shift), 1 post_a, 2 post_b, 3 shift alone, 4 unused, 5 whole step
 constexpr int SHIFT_BLOCKS = 1024;       // grid of the stand-alone k_shift (256 threads)
-// history-shift workgroups appended to k_dynamics (128 threads).  A k_dynamics wave holds a whole SIMD's
-// registers (1 wave/SIMD, 2 workgroups/CU), so the default fills exactly the workgroup slots the dynamics
-// leaves free: 2 * CUs - dynamics workgroups (384 at 8192 envs on 256 CUs), at least MIN_SHIFT_BLOCKS.
-constexpr int MIN_SHIFT_BLOCKS = 64;
 constexpr int MAX_TIMED = 1 << 14;
 
 struct t1env {
@@ -67,7 +63,7 @@ struct t1env {
   DynModel* d_model;
   t1env_config* d_cfg;
   Terrain terrain;
-  int shift_blocks;       // see MIN_SHIFT_BLOCKS; T1ENV_SHIFT_BLOCKS in the environment overrides (tuning)
+  DynLaunch dyn;          // dynamics kernel shape (T1ENV_DYN_WAVES / T1ENV_SHIFT_BLOCKS override; tuning)
   int shift_pending;      // phase A enqueued this step's history shift (phase B alone must run it)
   int fused;              // t1env_step runs the single fused launch (t1env_set_fused; default on)
   uint32_t epoch;         // fused launches so far (tags the shift-unit handoff words)
@@ -101,7 +97,7 @@ __global__ __launch_bounds__(BLOCK) void k_physics_injected(const DynModel* __re
   const int lag = B.lag_timestep[n];
   const int s_dof = 9 - B.dof_lag_timestep[n] % 10, s_imu = 9 - B.imu_lag_timestep[n] % 10;
   float* dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
-  float* imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 6;
+  float* imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
   const int N = C.num_envs;
   float tau[12];
   for (int sub = 0; sub < C.decimation; ++sub) {
@@ -344,10 +340,13 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
         hipSuccess) cus = 256;
-    const int free_slots = 2 * cus - (cfg->num_envs + 63) / 64;
-    e->shift_blocks = free_slots > MIN_SHIFT_BLOCKS ? free_slots : MIN_SHIFT_BLOCKS;
+    e->dyn.cus = cus;
+    e->dyn.waves = t1_dyn_waves_default();
+    if (const char* w = getenv("T1ENV_DYN_WAVES"))
+      if (atoi(w) == 2 || atoi(w) == 4) e->dyn.waves = atoi(w);
+    e->dyn.shift_blocks = 0;
     if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))
-      if (atoi(sb) > 0) e->shift_blocks = atoi(sb);
+      if (atoi(sb) > 0) e->dyn.shift_blocks = atoi(sb);
   }
   for (int b = 0; b < NB; ++b) e->max_contact_radius = fmaxf(e->max_contact_radius, dm.contact_radius[b]);
   *out = e;
@@ -429,7 +428,7 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
                        actions, *a, *inj);
   else
     HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, N,
-                                           shift_args(e, a), e->shift_blocks, nullptr, s));
+                                           shift_args(e, a), e->dyn, nullptr, s));
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
   if (inj) {
@@ -482,7 +481,7 @@ static int launch_fused(t1env* e, const float* actions, const t1env_step_args* a
   const int t = t_begin(e, 0, s);
   const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch};
   HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, e->cfg.num_envs,
-                                         shift_args(e, a), e->shift_blocks, &FA, s));
+                                         shift_args(e, a), e->dyn, &FA, s));
   t_end(e, t, s);
   t_end(e, e->step_timer, s);
   e->step_timer = -1;

@@ -94,12 +94,67 @@ __device__ __forceinline__ void pd_torques(const DynModel& M, const t1env_config
   }
 }
 
+// IMU lag ring entry: the raw base quaternion and world angular velocity of the captured substep (8 floats).
+// The derived sample (base-frame angular velocity, euler angles: t1_dh_stand_env.py:398-404) is formed once
+// per step where the observation reads it (imu_sample), not in the substep loop: lanes capture at
+// different substeps, so in the loop the wave would evaluate it on most substeps.
+// The per-env PD constants of one leg (randomized gains, motor offsets, viscous / Coulomb friction) and the
+// 4-step action ring, staged in LDS once per env step ([value][joint][env]: conflict-free rows), so the
+// substep loop reads LDS instead of re-gathering ~36 scattered rows from global memory every substep.
+template <int LANES> struct PdStage {
+  float kp[NLEG][LANES], kd[NLEG][LANES], off[NLEG][LANES], visc[NLEG][LANES], coul[NLEG][LANES];
+  float act[4][NLEG][LANES];
+};
+template <int LANES>
+__device__ __forceinline__ void pd_stage(const t1env_buffers& B, int n, int j0, int lane, PdStage<LANES>& P) {
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    const int j = j0 + k;
+    P.kp[k][lane] = B.kp[n * 12 + j];
+    P.kd[k][lane] = B.kd[n * 12 + j];
+    P.off[k][lane] = B.motor_offsets[n * 12 + j];
+    P.visc[k][lane] = B.viscous[n * 12 + j];
+    P.coul[k][lane] = B.coulomb[n * 12 + j];
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) P.act[s][k][lane] = B.act_hist[((size_t)n * 4 + s) * 12 + j0 + k];
+}
+// pd_torques<NLEG> with the constants from a PdStage (same arithmetic, same order)
+template <int LANES>
+__device__ __forceinline__ void pd_torques_staged(const DynModel& M, const t1env_config& C, const PdStage<LANES>& P,
+                                                  int lane, uint32_t genv, uint32_t ctr, int sub, int lag, int j0,
+                                                  const float q[NLEG], const float qd[NLEG], float tau[NLEG]) {
+  const int d = lag > sub ? (lag - sub + 9) / 10 : 0;
+  const int slot = (int)((ctr - (uint32_t)d) & 3u);
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    const int j = j0 + k;
+    const float kp = P.kp[k][lane], kd = P.kd[k][lane];
+    float t = kp * (((P.act[slot][k][lane] + M.default_dof_pos[j]) - q[k]) + P.off[k][lane]);
+    t = t - kd * qd[k];
+    t = t - P.visc[k][lane] * qd[k];
+    t = t - P.coul[k][lane] * signf(qd[k]);
+    const float tm = rand_float(C.torque_mult_range[0], C.torque_mult_range[1], C.seed, genv, ctr,
+                                SLOT_TORQUE_MULT + sub * 12 + j);
+    t = t * tm;
+    const float lim = M.torque_limit[j];
+    tau[k] = fminf(fmaxf(t, -lim), lim);
+  }
+}
+
 __device__ __forceinline__ void capture_imu(const float quat[4], const float w_world[3], float* dst) {
+  dst[0] = quat[0]; dst[1] = quat[1]; dst[2] = quat[2]; dst[3] = quat[3];
+  dst[4] = w_world[0]; dst[5] = w_world[1]; dst[6] = w_world[2]; dst[7] = 0.0f;
+}
+__device__ __forceinline__ void imu_sample(const float raw[8], float out[6]) {
+  const float quat[4] = {raw[0], raw[1], raw[2], raw[3]}, w[3] = {raw[4], raw[5], raw[6]};
   float av[3], e[3];
-  quat_rotate_inverse(quat, w_world, av);
+  quat_rotate_inverse(quat, w, av);
   euler_xyz(quat, e);
-  dst[0] = av[0]; dst[1] = av[1]; dst[2] = av[2];
-  dst[3] = e[0]; dst[4] = e[1]; dst[5] = e[2];
+  out[0] = av[0]; out[1] = av[1]; out[2] = av[2];
+  out[3] = e[0]; out[4] = e[1]; out[5] = e[2];
 }
 
 

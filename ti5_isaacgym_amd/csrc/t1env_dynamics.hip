@@ -1,15 +1,16 @@
-// t1env_dynamics.hip -- k_dynamics, the decimation loop with the articulated-body solver (legged_robot.py:
-// 399-434 + Isaac Gym simulate()).  Its own translation unit because it is compiled at -O1 (build.py): at
-// -O2/-O3 the optimiser produced wrong dynamics for this kernel (GPU one-step error far above fp32 against
-// the host fp64 replica, tests/test_gpu_dynamics.py) while -O1 is both correct and faster (no scratch).
+// t1env_dynamics.hip -- the env step's main launch: the decimation loop with the articulated-body solver
+// (legged_robot.py:399-434 + Isaac Gym simulate()), the history shift, and in the fused step post-physics.
+// Its own translation unit because it is compiled at -O1 (build.py): at -O2/-O3 the optimiser produced wrong
+// dynamics for this kernel (GPU one-step error far above fp32 against the host fp64 replica,
+// tests/test_gpu_dynamics.py) while -O1 is both correct and faster (no scratch).
 #include <hip/hip_runtime.h>
 
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py): lane 0 of every dynamics wave accumulates shader-clock
 // deltas between T1_PROF_MARK points into per-phase buckets; never part of the product build.
 #ifdef T1_PHASE_PROF
-constexpr int T1_NPROF = 16;
-__device__ unsigned long long g_t1_prof[2][T1_NPROF];
-__shared__ unsigned long long t1_prof_acc[2][T1_NPROF + 1];  // [wave][bucket], last = previous mark
+constexpr int T1_NPROF = 16, T1_PROF_WAVES = 4;
+__device__ unsigned long long g_t1_prof[T1_PROF_WAVES][T1_NPROF];
+__shared__ unsigned long long t1_prof_acc[T1_PROF_WAVES][T1_NPROF + 1];  // [wave][bucket], last = previous mark
 __device__ __forceinline__ void t1_prof_mark(int i) {
   const int w = threadIdx.x / 64;
   if ((threadIdx.x & 63) == 0) {
@@ -18,7 +19,24 @@ __device__ __forceinline__ void t1_prof_mark(int i) {
     t1_prof_acc[w][T1_NPROF] = now;
   }
 }
+__device__ __forceinline__ void t1_prof_begin() {
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    for (int i = 0; i < T1_NPROF; ++i) t1_prof_acc[w][i] = 0;
+    t1_prof_acc[w][T1_NPROF] = clock64();
+  }
+}
+__device__ __forceinline__ void t1_prof_end() {
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < T1_NPROF; ++i) atomicAdd(&g_t1_prof[w][i], t1_prof_acc[w][i]);
+}
 #define T1_PROF_MARK(i) t1_prof_mark(i)
+#define T1_PROF_BEGIN() t1_prof_begin()
+#define T1_PROF_END() t1_prof_end()
+#else
+#define T1_PROF_BEGIN() ((void)0)
+#define T1_PROF_END() ((void)0)
 #endif
 
 #include "t1env_device.h"
@@ -28,20 +46,24 @@ __device__ __forceinline__ void t1_prof_mark(int i) {
 using namespace t1;
 
 // ---------------------------------------------------------------------------------------------------
-// k_dynamics: the decimation loop with the articulated-body solver.  A workgroup owns 64 envs and runs
-// them on two waves: wave 0 handles every env's left leg, wave 1 the right leg (the leg index is
-// wave-uniform, so all model reads are scalar loads).  Per substep each wave eliminates its leg into a
-// 27-float base-block contribution (t1_dynamics.h leg_contribution), the two contributions meet in LDS
-// (double-buffered by substep parity -> one barrier per substep), and both waves solve the 6x6 base system
-// redundantly, so the base state stays bit-identical in both without further exchange.
+// Two kernels share the launch layout: ceil(N/64) dynamics workgroups of 64 envs, then history-shift
+// workgroups (blockIdx >= dyn_blocks, t1env_device.h).  The dynamics fill at most half the CUs at 8192 envs,
+// so the HBM-bound shift streams on the rest of the chip inside the same launch -- no second stream, no
+// cross-stream events on the step path.
 //
-// Workgroups past the dynamics grid (blockIdx >= dyn_blocks) run the history shift instead
-// (t1env_device.h shift_history).  The dynamics waves fill at most half the CUs at 8192 envs, so the
-// HBM-bound shift streams on the rest of the chip inside the same launch -- no second stream, no
-// cross-stream events on the step path.  The dynamics workgroups have the lower ids, so they are dispatched
-// first.
+//   k_dynamics (2 waves / 64 envs): wave 0 runs every env's left leg, wave 1 the right leg (the leg index is
+//     wave-uniform, so model reads are scalar loads).  Per substep each wave eliminates its leg into a
+//     27-float base-block contribution (t1_dynamics.h leg_contribution), the two contributions meet in LDS
+//     (double-buffered by substep parity -> one barrier per substep), and both waves solve the 6x6 base system
+//     redundantly, so the base state stays bit-identical in both without further exchange.
+//   k_dyn4 (4 waves / 64 envs, the default): waves 0/1 are the leg waves as above, but run the articulated-
+//     body passes without contact (leg_forward_nc / leg_backward_nc); waves 2/3 are their contact helpers:
+//     from the poses the leg wave publishes after its forward pass they compute the shank / foot contact
+//     terms while the leg wave runs its backward pass, then the base-box contact terms while the leg wave
+//     folds the contact terms in (leg_apply_contacts) and eliminates.  Three barriers per substep; all four
+//     SIMDs of the CU work on the same 64 envs (+34 % env-steps/s over k_dynamics at 8192 envs).
 //
-// FUSED (t1env_step on every step that needs no host decision between the phases): the whole env step is this
+// FUSED (t1env_step on every step that needs no host decision between the phases): the whole env step is
 // one launch.  After its dynamics, wave 0 of each dynamics workgroup runs post-physics for its 64 envs
 // (t1env_postphys.h post_a_env + post_b_env: rewards, termination, reset_idx, observations, newest history
 // frame), and the last dynamics workgroup to finish finalises the extras.  Two things had to change for that:
@@ -50,16 +72,17 @@ using namespace t1;
 //     env needs only its own reset flag;
 //   * zeroing the history rows of reset envs must follow the shift of those rows, which other workgroups do
 //     concurrently.  The shift is cut into units of SHIFT_UNIT rows, and each unit has a handoff word
-//     (epoch-tagged): the shift workgroup sets bit 0 once the unit is shifted and written back, the dynamics
-//     workgroup sets bit 1 together with the unit's 8-bit reset mask.  Whoever sets the second bit zeroes the
-//     unit's reset rows.  Nobody waits for anybody, so no dispatch order or residency is assumed.
-//     The shift writes these rows with agent-coherent sc1 stores (t1env_device.h store4), so once they have
-//     completed (s_waitcnt) no dirty copy is left in any L2 and the zeros, written later by either party, land
-//     last -- placement-independent, and without an L2 write-back fence (buffer_wbl2 per unit cost the
-//     concurrently running dynamics ~8 %).
+//     (epoch-tagged): the shift workgroup sets bit 0 once the unit is shifted, the dynamics workgroup sets
+//     bit 1 together with the unit's 8-bit reset mask.  Whoever sets the second bit zeroes the unit's reset
+//     rows.  Nobody waits for anybody, so no dispatch order or residency is assumed.  The shift writes these
+//     rows with agent-coherent sc1 stores (t1env_device.h store4), so once they have completed (s_waitcnt) no
+//     dirty copy is left in any L2 and the zeros, written later by either party, land last --
+//     placement-independent, and without an L2 write-back fence (buffer_wbl2 per unit cost the concurrently
+//     running dynamics ~8 %).
 // ---------------------------------------------------------------------------------------------------
 constexpr int DYN_ENVS = 64;
 constexpr int DYN_BLOCK = 2 * DYN_ENVS;
+constexpr int D4_BLOCK = 4 * DYN_ENVS;
 constexpr int XCH = 27;  // Sym6 (21) + rhs (6)
 constexpr int SHIFT_UNIT = 8;  // rows per shift/zeroing unit (a multiple of 4: unit boundaries are 16-B aligned)
 static_assert(DYN_ENVS % SHIFT_UNIT == 0, "a dynamics workgroup owns whole shift units");
@@ -90,6 +113,132 @@ __device__ __forceinline__ void zero_unit_resets(const ShiftArgs& S, int u, uint
   }
 }
 
+// A history-shift workgroup (j of nsw) of BS threads; `words` is LDS scratch of >= BS uint32.
+template <bool FUSED, int BS>
+__device__ __forceinline__ void shift_workgroup(const ShiftArgs& S, const FusedArgs& FA, int N, int j, int nsw,
+                                                uint32_t* words) {
+  if constexpr (!FUSED) {
+    shift_history(S, (int64_t)j * BS + threadIdx.x, (int64_t)nsw * BS);
+  } else {
+    const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
+    for (int u = j; u < units; u += nsw) {
+      const int64_t r0 = (int64_t)u * SHIFT_UNIT, r1 = r0 + SHIFT_UNIT < N ? r0 + SHIFT_UNIT : N;
+      shift_rows_range_sc1(S, r0, r1, threadIdx.x, BS);
+    }
+    // every lane's sc1 stores complete (visible at agent scope) before any handoff
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    const int mine = units > j ? (units - j + nsw - 1) / nsw : 0;  // units of this workgroup
+    for (int k0 = 0; k0 < mine; k0 += BS) {
+      const int k = k0 + (int)threadIdx.x;
+      if (k < mine) words[threadIdx.x] = unit_handoff(FA.unit_state + j + k * nsw, FA.epoch, HANDOFF_SHIFT);
+      __syncthreads();
+      const int cnt = mine - k0 < BS ? mine - k0 : BS;
+      for (int i = 0; i < cnt; ++i)
+        if (handoff_complete(words[i])) zero_unit_resets(S, j + (k0 + i) * nsw, words[i], threadIdx.x, BS);
+      __syncthreads();
+    }
+  }
+}
+
+// The fused step's post-physics for one dynamics workgroup's 64 envs, run by one whole wave after the
+// dynamics outputs of the workgroup are in memory (t1env_postphys.h: the same code as k_post_a / k_post_b),
+// then the reset-row handoff and the extras finalisation.
+__device__ __forceinline__ void fused_epilogue(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                               const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
+                                               int dyn_blocks, int lane) {
+  const int N = C.num_envs;
+  const int n0 = blockIdx.x * DYN_ENVS + lane;
+  const bool active = n0 < N;
+  const int n = active ? n0 : N - 1;
+  const bool do_reset = post_a_env(M, C, B, A, n0);
+  T1_PROF_MARK(13);
+  if (active) post_b_env(M, C, B, A, n, do_reset, do_reset);
+  T1_PROF_MARK(14);
+  if (C.terrain_curriculum) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
+  // ---- reset rows: hand off each of the workgroup's shift units with its 8-bit reset mask
+  const unsigned long long m = __ballot(do_reset && active);
+  const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
+  const int u = blockIdx.x * (DYN_ENVS / SHIFT_UNIT) + lane;
+  uint32_t w = 0;
+  if (lane < DYN_ENVS / SHIFT_UNIT && u < units)
+    w = unit_handoff(FA.unit_state + u, FA.epoch, HANDOFF_DYN | ((uint32_t)(m >> (lane * SHIFT_UNIT)) & 0xffu) << 2);
+  uint64_t todo = __ballot(handoff_complete(w));
+  while (todo) {
+    const int l = __ffsll((unsigned long long)todo) - 1;
+    todo &= todo - 1;
+    zero_unit_resets(S, blockIdx.x * (DYN_ENVS / SHIFT_UNIT) + l, __shfl(w, l, 64), lane, DYN_ENVS);
+  }
+  // ---- the last dynamics workgroup to finish finalises the step's extras.  Only atomics cross workgroups
+  // here (the ep_accum sums and this counter; agent-scope atomics are performed past the L2s), so waiting for
+  // this wave's atomics to complete orders them before the increment; the finaliser reads ep_accum through
+  // atomics as well.
+  __builtin_amdgcn_s_waitcnt(0);
+  unsigned prev = 0;
+  if (lane == 0) prev = __hip_atomic_fetch_add(FA.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  prev = __shfl(prev, 0, 64);
+  if (prev == (unsigned)dyn_blocks - 1u) {
+    finalize_extras(B, C, (int)((A.counter + 1u) % T1ENV_EXTRAS_RING));
+    if (lane == 0) __hip_atomic_store(FA.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  T1_PROF_MARK(15);
+}
+
+// per-leg setup shared by both kernels: clipped actions into the step's action slot, sensor-lag capture
+// slots, per-env parameters, base state and the leg's joint state
+struct LegSetup {
+  int lag, s_dof, s_imu;
+  float* dof_dst;
+  float* imu_dst;
+};
+__device__ __forceinline__ LegSetup leg_setup(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                              const float* __restrict__ actions, uint32_t ctr, int n, bool active,
+                                              int j0, BaseParams<float>& PB, LegParams<float>& PL,
+                                              BaseState<float>& sb, float q[NLEG], float qd[NLEG]) {
+  if (active) {  // actions = clip(actions); push the scaled action into this step's history slot
+    float* slot = B.act_hist + ((size_t)n * 4 + (ctr & 3u)) * 12;
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      const float a = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
+      B.actions[n * 12 + j0 + k] = a;
+      slot[j0 + k] = a * C.action_scale;
+    }
+  }
+  LegSetup L;
+  L.lag = B.lag_timestep[n];
+  L.s_dof = 9 - B.dof_lag_timestep[n] % 10;
+  L.s_imu = 9 - B.imu_lag_timestep[n] % 10;
+  L.dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
+  L.imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
+  load_base_params(M, B, n, PB);
+  load_leg_params(M, B, n, j0, PL);
+  load_base_state(M, PB, B.root_states + (size_t)n * 13, sb);
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
+    qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
+  }
+  return L;
+}
+
+// the step's outputs of one leg wave (Gym-shaped root / rigid / contact / dof / torque buffers)
+__device__ __forceinline__ void leg_report(const DynModel& M, const Terrain& T, const t1env_buffers& B,
+                                           const BaseParams<float>& PB, const BaseState<float>& sb,
+                                           const float q[NLEG], const float qd[NLEG], const float tau[NLEG], int n,
+                                           int leg, int j0) {
+  BaseFrame<float> F;
+  base_frame(sb, F);
+  DevWriter W{B.root_states + (size_t)n * 13, B.rigid_state + (size_t)n * 169, B.contact_forces + (size_t)n * 39};
+  if (leg == 0) report_base(M, T, PB, sb, F, W);
+  report_leg(M, T, PB.friction, F, q, qd, leg, W);
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
+    B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
+    B.torques[n * 12 + j0 + k] = tau[k];
+  }
+}
+
 // HF: height-field terrain (mesh heightfield/trimesh) or plane; one instantiation each so the contact code
 // of the other terrain kind is folded away (it is uniform per launch).
 template <bool HF, bool FUSED>
@@ -100,31 +249,8 @@ __global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restri
                                                         FusedArgs FA) {
   __shared__ float xch[2][2][XCH][DYN_ENVS];  // [substep parity][leg][value][env]
   if ((int)blockIdx.x >= dyn_blocks) {
-    const int j = blockIdx.x - dyn_blocks, nsw = gridDim.x - dyn_blocks;
-    if constexpr (!FUSED) {
-      shift_history(S, (int64_t)j * DYN_BLOCK + threadIdx.x, (int64_t)nsw * DYN_BLOCK);
-    } else {
-      const int N = Cp->num_envs;
-      const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
-      uint32_t* words = reinterpret_cast<uint32_t*>(&xch[0][0][0][0]);  // LDS: handoff results of this WG
-      for (int u = j; u < units; u += nsw) {
-        const int64_t r0 = (int64_t)u * SHIFT_UNIT, r1 = r0 + SHIFT_UNIT < N ? r0 + SHIFT_UNIT : N;
-        shift_rows_range_sc1(S, r0, r1, threadIdx.x, DYN_BLOCK);
-      }
-      // every lane's sc1 stores complete (visible at agent scope) before any handoff
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-      const int mine = units > j ? (units - j + nsw - 1) / nsw : 0;  // units of this workgroup
-      for (int k0 = 0; k0 < mine; k0 += DYN_BLOCK) {
-        const int k = k0 + (int)threadIdx.x;
-        if (k < mine) words[threadIdx.x] = unit_handoff(FA.unit_state + j + k * nsw, FA.epoch, HANDOFF_SHIFT);
-        __syncthreads();
-        const int cnt = mine - k0 < DYN_BLOCK ? mine - k0 : DYN_BLOCK;
-        for (int i = 0; i < cnt; ++i)
-          if (handoff_complete(words[i])) zero_unit_resets(S, j + (k0 + i) * nsw, words[i], threadIdx.x, DYN_BLOCK);
-        __syncthreads();
-      }
-    }
+    shift_workgroup<FUSED, DYN_BLOCK>(S, FA, Cp->num_envs, blockIdx.x - dyn_blocks, gridDim.x - dyn_blocks,
+                                      reinterpret_cast<uint32_t*>(&xch[0][0][0][0]));
     return;
   }
   Terrain T = Tin;
@@ -132,12 +258,7 @@ __global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restri
   const t1env_config& C = *Cp;
   const DynModel& M = *Mp;
   const int leg = __builtin_amdgcn_readfirstlane((int)threadIdx.x / DYN_ENVS);
-#ifdef T1_PHASE_PROF
-  if ((threadIdx.x & 63) == 0) {
-    for (int i = 0; i < T1_NPROF; ++i) t1_prof_acc[leg][i] = 0;
-    t1_prof_acc[leg][T1_NPROF] = clock64();
-  }
-#endif
+  T1_PROF_BEGIN();
   const int lane = threadIdx.x % DYN_ENVS;
   const int N = C.num_envs;
   const bool active = (int)(blockIdx.x * DYN_ENVS) + lane < N;
@@ -145,38 +266,17 @@ __global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restri
   const int j0 = 6 * leg;
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   const uint32_t ctr = A.counter;
-  // actions = clip(actions); push the scaled action into this step's history slot
-  if (active) {
-    float* slot = B.act_hist + ((size_t)n * 4 + (ctr & 3u)) * 12;
-#pragma unroll
-    for (int k = 0; k < NLEG; ++k) {
-      const float a = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
-      B.actions[n * 12 + j0 + k] = a;
-      slot[j0 + k] = a * C.action_scale;
-    }
-  }
-  const int lag = B.lag_timestep[n];
-  const int s_dof = 9 - B.dof_lag_timestep[n] % 10, s_imu = 9 - B.imu_lag_timestep[n] % 10;
-  float* dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
-  float* imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 6;
   const float dt = C.sim_dt;
   BaseParams<float> PB;
   LegParams<float> PL;
-  load_base_params(M, B, n, PB);
-  load_leg_params(M, B, n, j0, PL);
   BaseState<float> sb;
-  load_base_state(M, PB, B.root_states + (size_t)n * 13, sb);
   float q[NLEG], qd[NLEG], tau[NLEG];
-#pragma unroll
-  for (int k = 0; k < NLEG; ++k) {
-    q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
-    qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
-  }
+  const LegSetup L = leg_setup(M, C, B, actions, ctr, n, active, j0, PB, PL, sb, q, qd);
   const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
   T1_PROF_MARK(10);
   for (int sub = 0; sub < C.decimation; ++sub) {
     T1_PROF_MARK(7);
-    pd_torques<NLEG>(M, C, B, n, genv, ctr, sub, lag, j0, q, qd, tau);
+    pd_torques<NLEG>(M, C, B, n, genv, ctr, sub, L.lag, j0, q, qd, tau);
     BaseFrame<float> F;
     base_frame(sb, F);
     T1_PROF_MARK(0);
@@ -213,101 +313,307 @@ __global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restri
     integrate_base(sb, r, dt);
     integrate_leg(M, leg, q, qd, dq, dt);
     T1_PROF_MARK(9);
-    if (active && sub == s_dof) {
+    if (active && sub == L.s_dof) {
 #pragma unroll
-      for (int k = 0; k < NLEG; ++k) { dof_dst[j0 + k] = q[k]; dof_dst[12 + j0 + k] = qd[k]; }
+      for (int k = 0; k < NLEG; ++k) { L.dof_dst[j0 + k] = q[k]; L.dof_dst[12 + j0 + k] = qd[k]; }
     }
-    if (active && leg == 0 && sub == s_imu) capture_imu(sb.quat, sb.w, imu_dst);
+    if (active && leg == 0 && sub == L.s_imu) capture_imu(sb.quat, sb.w, L.imu_dst);
   }
   T1_PROF_MARK(7);
-  if (active) {
-    BaseFrame<float> F;
-    base_frame(sb, F);
-    DevWriter W{B.root_states + (size_t)n * 13, B.rigid_state + (size_t)n * 169, B.contact_forces + (size_t)n * 39};
-    if (leg == 0) report_base(M, T, PB, sb, F, W);
-    report_leg(M, T, PB.friction, F, q, qd, leg, W);
-#pragma unroll
-    for (int k = 0; k < NLEG; ++k) {
-      B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
-      B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
-      B.torques[n * 12 + j0 + k] = tau[k];
-    }
-  }
+  if (active) leg_report(M, T, B, PB, sb, q, qd, tau, n, leg, j0);
   T1_PROF_MARK(11);
   if constexpr (FUSED) {
     __syncthreads();  // both legs' outputs are in memory (same workgroup: visible after the barrier)
     T1_PROF_MARK(12);
-#ifdef T1_PHASE_PROF
-    if (leg != 0 && (threadIdx.x & 63) == 0)
-      for (int i = 0; i < T1_NPROF; ++i) atomicAdd(&g_t1_prof[leg][i], t1_prof_acc[leg][i]);
-#endif
-    if (leg != 0) return;
-    // ---- post-physics of the workgroup's 64 envs on wave 0 (t1env_postphys.h; same code as k_post_a/b)
-    const int n0 = blockIdx.x * DYN_ENVS + lane;
-    const bool do_reset = post_a_env(M, C, B, A, n0);
-    T1_PROF_MARK(13);
-    if (active) post_b_env(M, C, B, A, n, do_reset, do_reset);
-    T1_PROF_MARK(14);
-    if (C.terrain_curriculum) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
-    // ---- reset rows: hand off each of the workgroup's shift units with its 8-bit reset mask
-    const unsigned long long m = __ballot(do_reset && active);
-    const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
-    const int u = blockIdx.x * (DYN_ENVS / SHIFT_UNIT) + lane;
-    uint32_t w = 0;
-    if (lane < DYN_ENVS / SHIFT_UNIT && u < units)
-      w = unit_handoff(FA.unit_state + u, FA.epoch,
-                       HANDOFF_DYN | ((uint32_t)(m >> (lane * SHIFT_UNIT)) & 0xffu) << 2);
-    uint64_t todo = __ballot(handoff_complete(w));
-    while (todo) {
-      const int l = __ffsll((unsigned long long)todo) - 1;
-      todo &= todo - 1;
-      zero_unit_resets(S, blockIdx.x * (DYN_ENVS / SHIFT_UNIT) + l, __shfl(w, l, 64), lane, DYN_ENVS);
-    }
-    // ---- the last dynamics workgroup to finish finalises the step's extras.  Only atomics cross workgroups
-    // here (the ep_accum sums and this counter; agent-scope atomics are performed past the L2s), so waiting for
-    // this wave's atomics to complete orders them before the increment; the finaliser reads ep_accum through
-    // atomics as well.
-    __builtin_amdgcn_s_waitcnt(0);
-    unsigned prev = 0;
-    if (lane == 0) prev = __hip_atomic_fetch_add(FA.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prev = __shfl(prev, 0, 64);
-    if (prev == (unsigned)dyn_blocks - 1u) {
-      finalize_extras(B, C, (int)((A.counter + 1u) % T1ENV_EXTRAS_RING));
-      if (lane == 0) __hip_atomic_store(FA.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    T1_PROF_MARK(15);
+    if (leg == 0) fused_epilogue(M, C, B, A, S, FA, dyn_blocks, lane);
   }
-#ifdef T1_PHASE_PROF
-  if ((threadIdx.x & 63) == 0 && (!FUSED || leg == 0))
-    for (int i = 0; i < T1_NPROF; ++i) atomicAdd(&g_t1_prof[leg][i], t1_prof_acc[leg][i]);
-#endif
+  T1_PROF_END();
 }
+
+// ---------------------------------------------------------------------------------------------------
+// k_dyn4: 4 waves per 64 envs (see the top of the file).  Per substep, leg wave | contact helper wave:
+//   forward pass, publishing the base frame and the shank / foot poses       |
+//   S1 -------------------------------------------------------------------------------------------------
+//   PD torques, backward pass without contact                                 | shank + foot contact terms
+//   S2 -------------------------------------------------------------------------------------------------
+//   contact terms folded in (leg_apply_contacts), elimination, base block     | base-box contact terms
+//   S3 -------------------------------------------------------------------------------------------------
+//   base solve (4 contributions), back-substitution, integration             | (waits for the next poses)
+// The leg wave stages its PD constants and the action ring in LDS once per step, and captures the lagged
+// sensor samples into LDS (written to the rings once after the loop): in the loop it touches global memory
+// only for the terrain.
+// LDS per workgroup (floats, [value][env]: every access is a conflict-free row):
+//   pose[leg] (POSE_N): base frame R0 (9) abs (3) V0 (6), then shank / foot R (9) p (3) V (6)
+//   ct[leg]   (CT_N):   shank C (21) c (6), foot C (21) c (6)
+//   xch[4]:             base-block contributions: legs 0, 1 (leg waves), base-box contacts 0, 1 (helpers)
+// Each region is written and read in disjoint barrier intervals (pose: written before S1, read S1..S3;
+// ct: written S1..S2, read S2..S3; xch: written S2..S3, read after S3, rewritten after the next S2).
+// ---------------------------------------------------------------------------------------------------
+constexpr int POSE_F = 18, POSE_B = 18, POSE_N = POSE_F + 2 * POSE_B;
+constexpr int CT_N = 2 * XCH;
+constexpr int CAP_N = 2 * NLEG + 8;  // dof capture (q, qd of the leg), IMU capture (raw, leg 0)
+constexpr int K_SHANK = 3, K_FOOT = 5;
+static_assert(T1_LEG_CONTACT_MASK == ((1 << K_SHANK) | (1 << K_FOOT)), "k_dyn4 assumes shank + foot contact bodies");
+
+struct Dyn4Lds {
+  float pose[2][POSE_N][DYN_ENVS];
+  float ct[2][CT_N][DYN_ENVS];
+  float xch[4][XCH][DYN_ENVS];
+  PdStage<DYN_ENVS> pd[2];
+  float cap[2][CAP_N][DYN_ENVS];
+};
+
+__device__ __forceinline__ void lds_put_m3(float (*dst)[DYN_ENVS], int lane, const M3<float>& R) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) dst[i][lane] = R.m[i];
+}
+__device__ __forceinline__ M3<float> lds_get_m3(const float (*src)[DYN_ENVS], int lane) {
+  M3<float> R;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R.m[i] = src[i][lane];
+  return R;
+}
+__device__ __forceinline__ void lds_put_sym(float (*dst)[DYN_ENVS], int lane, const Sym6<float>& A, const float g[6]) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) dst[i][lane] = A.a[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) dst[21 + i][lane] = g[i];
+}
+__device__ __forceinline__ void lds_get_sym(const float (*src)[DYN_ENVS], int lane, Sym6<float>& A, float g[6]) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) A.a[i] = src[i][lane];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) g[i] = src[21 + i][lane];
+}
+
+// contact terms (Sym6 + wrench) of a leg contact body from its published pose
+__device__ __forceinline__ void body_terms(const DynModel& M, const Terrain& T, const float (*P)[DYN_ENVS], int lane,
+                                           int b, V3<float> abs, float mu, float dt, float (*dst)[DYN_ENVS]) {
+  Sym6<float> Cc;
+  float cc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  sym_zero(Cc);
+  const M3<float> Rb = lds_get_m3(P, lane);
+  const V3<float> pb = v3<float>(P[9][lane], P[10][lane], P[11][lane]);
+  float Vb[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) Vb[i] = P[12 + i][lane];
+  const int32_t bound = terrain_bound_raw_any(T, pb.x + abs.x, pb.y + abs.y);
+  body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pb.z + abs.z - M.contact_radius[b], bound, M.contact_start[b], Rb, pb,
+                                         abs, Vb, mu, dt, Cc, cc);
+  lds_put_sym(dst, lane, Cc, cc);
+}
+
+template <bool HF, bool FUSED>
+__global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
+                                                   t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
+                                                   t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA) {
+  __shared__ Dyn4Lds lds;
+  if ((int)blockIdx.x >= dyn_blocks) {
+    shift_workgroup<FUSED, D4_BLOCK>(S, FA, Cp->num_envs, blockIdx.x - dyn_blocks, gridDim.x - dyn_blocks,
+                                     reinterpret_cast<uint32_t*>(&lds.xch[0][0][0]));
+    return;
+  }
+  Terrain T = Tin;
+  T.type = HF ? 2 : 0;
+  const t1env_config& C = *Cp;
+  const DynModel& M = *Mp;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / DYN_ENVS);
+  const int leg = wave & 1;
+  const bool helper = wave >= 2;
+  T1_PROF_BEGIN();
+  const int lane = threadIdx.x % DYN_ENVS;
+  const int N = C.num_envs;
+  const bool active = (int)(blockIdx.x * DYN_ENVS) + lane < N;
+  const int n = active ? blockIdx.x * DYN_ENVS + lane : N - 1;  // inactive lanes shadow a valid env, never store
+  const float dt = C.sim_dt;
+  if (helper) {
+    // ---------------- contact helper of leg `leg`
+    const float mu = 0.5f * (B.friction[n] + M.ground_friction);
+    int cb, ce;
+    base_contact_range(M, leg, cb, ce);
+    const float (*P)[DYN_ENVS] = lds.pose[leg];
+    T1_PROF_MARK(10);
+    for (int sub = 0; sub < C.decimation; ++sub) {
+      T1_PROF_MARK(7);
+      __syncthreads();  // S1: poses of this substep published
+      T1_PROF_MARK(8);
+      const V3<float> abs = v3<float>(P[9][lane], P[10][lane], P[11][lane]);
+      body_terms(M, T, P + POSE_F, lane, 1 + 6 * leg + K_SHANK, abs, mu, dt, lds.ct[leg]);
+      body_terms(M, T, P + POSE_F + POSE_B, lane, 1 + 6 * leg + K_FOOT, abs, mu, dt, lds.ct[leg] + XCH);
+      T1_PROF_MARK(3);
+      __syncthreads();  // S2: contact terms published
+      T1_PROF_MARK(11);
+      {  // base-box contact share of this leg, straight into the base system
+        BaseFrame<float> F;
+        F.R0 = lds_get_m3(P, lane);
+        F.abs = abs;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) F.V0[i] = P[12 + i][lane];
+        Sym6<float> Cb;
+        float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        sym_zero(Cb);
+        const int32_t bound = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
+        body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - M.contact_radius[0], bound, cb, F.R0,
+                                                   v3<float>(0, 0, 0), F.abs, F.V0, mu, dt, Cb, gw);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) gw[i] = -gw[i];
+        lds_put_sym(lds.xch[2 + leg], lane, Cb, gw);
+      }
+      T1_PROF_MARK(5);
+      __syncthreads();  // S3: base system complete
+      T1_PROF_MARK(12);
+    }
+    if constexpr (FUSED) __syncthreads();  // the epilogue barrier
+    T1_PROF_END();
+    return;
+  }
+  // ---------------- leg wave
+  const int j0 = 6 * leg;
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  const uint32_t ctr = A.counter;
+  BaseParams<float> PB;
+  LegParams<float> PL;
+  BaseState<float> sb;
+  float q[NLEG], qd[NLEG], tau[NLEG];
+  const LegSetup L = leg_setup(M, C, B, actions, ctr, n, active, j0, PB, PL, sb, q, qd);
+  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
+  PdStage<DYN_ENVS>& PD = lds.pd[leg];
+  pd_stage(B, n, j0, lane, PD);  // this step's action slot was written by leg_setup (same lane)
+  float (*P)[DYN_ENVS] = lds.pose[leg];
+  float (*CAP)[DYN_ENVS] = lds.cap[leg];
+  T1_PROF_MARK(10);
+  for (int sub = 0; sub < C.decimation; ++sub) {
+    T1_PROF_MARK(7);
+    BaseFrame<float> F;
+    base_frame(sb, F);
+    lds_put_m3(P, lane, F.R0);
+    P[9][lane] = F.abs.x; P[10][lane] = F.abs.y; P[11][lane] = F.abs.z;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) P[12 + i][lane] = F.V0[i];
+    LegPass<float> st;
+    leg_forward_nc<T1_LEG_CONTACT_MASK>(M, PL, F, q, qd, leg, dt, st,
+                                        [&](auto kc, const M3<float>& Rk, V3<float> pk, const float* V) {
+                                          constexpr int k = decltype(kc)::value;
+                                          float (*D)[DYN_ENVS] = P + POSE_F + (k == K_FOOT ? POSE_B : 0);
+                                          lds_put_m3(D, lane, Rk);
+                                          D[9][lane] = pk.x; D[10][lane] = pk.y; D[11][lane] = pk.z;
+#pragma unroll
+                                          for (int i = 0; i < 6; ++i) D[12 + i][lane] = V[i];
+                                        });
+    T1_PROF_MARK(1);
+    __syncthreads();  // S1
+    T1_PROF_MARK(8);
+    pd_torques_staged(M, C, PD, lane, genv, ctr, sub, L.lag, j0, q, qd, tau);
+    T1_PROF_MARK(0);
+    LegBlock<float> lb;
+    Sym6<float> Ab;
+    float g6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    sym_zero(Ab);
+    leg_backward_nc(M, PL, q, qd, leg, dt, st, lb, Ab, g6);
+    T1_PROF_MARK(2);
+    __syncthreads();  // S2
+    T1_PROF_MARK(11);
+    {
+      Sym6<float> Csh, Cft;
+      float csh[6], cft[6];
+      lds_get_sym(lds.ct[leg], lane, Csh, csh);
+      lds_get_sym(lds.ct[leg] + XCH, lane, Cft, cft);
+      leg_apply_contacts<K_SHANK, K_FOOT>(Csh, csh, Cft, cft, tau, dt, st, lb, Ab, g6);
+    }
+    float rb[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rb[i] = -g6[i];
+    eliminate_leg(lb, Ab, rb);
+    lds_put_sym(lds.xch[leg], lane, Ab, rb);
+    T1_PROF_MARK(4);
+    Sym6<float> Ac;
+    float r[6];
+    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r[i] = -r[i];
+    T1_PROF_MARK(6);
+    __syncthreads();  // S3
+    T1_PROF_MARK(12);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+#pragma unroll
+      for (int i = 0; i < 21; ++i) Ac.a[i] += lds.xch[l][i][lane];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) r[i] += lds.xch[l][21 + i][lane];
+    }
+    solve_base(Ac, r);
+    float dq[NLEG];
+    backsub_leg(lb, r, dq);
+    integrate_base(sb, r, dt);
+    integrate_leg(M, leg, q, qd, dq, dt);
+    T1_PROF_MARK(9);
+    if (sub == L.s_dof) {
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { CAP[k][lane] = q[k]; CAP[NLEG + k][lane] = qd[k]; }
+    }
+    if (leg == 0 && sub == L.s_imu) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) CAP[2 * NLEG + i][lane] = sb.quat[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) CAP[2 * NLEG + 4 + i][lane] = sb.w[i];
+    }
+  }
+  T1_PROF_MARK(7);
+  if (active) {
+    if (L.s_dof < C.decimation) {  // the sensor-lag samples captured in the loop
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { L.dof_dst[j0 + k] = CAP[k][lane]; L.dof_dst[12 + j0 + k] = CAP[NLEG + k][lane]; }
+    }
+    if (leg == 0 && L.s_imu < C.decimation) {
+      const float quat[4] = {CAP[2 * NLEG][lane], CAP[2 * NLEG + 1][lane], CAP[2 * NLEG + 2][lane], CAP[2 * NLEG + 3][lane]};
+      const float w[3] = {CAP[2 * NLEG + 4][lane], CAP[2 * NLEG + 5][lane], CAP[2 * NLEG + 6][lane]};
+      capture_imu(quat, w, L.imu_dst);
+    }
+    leg_report(M, T, B, PB, sb, q, qd, tau, n, leg, j0);
+  }
+  T1_PROF_MARK(11);
+  if constexpr (FUSED) {
+    __syncthreads();  // all four waves: both legs' outputs are in memory
+    T1_PROF_MARK(12);
+    if (leg == 0) fused_epilogue(M, C, B, A, S, FA, dyn_blocks, lane);
+  }
+  T1_PROF_END();
+}
+
+int t1_dyn_waves_default() { return 4; }
 
 int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
                        const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
-                       int shift_blocks, const FusedArgs* fused, hipStream_t s) {
+                       const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s) {
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
-  const dim3 grid(dyn_blocks + shift_blocks), block(DYN_BLOCK);
+  // history-shift workgroups: the workgroup slots the dynamics leave free (a wave of either kernel holds a
+  // whole SIMD's registers: 2 workgroups/CU for k_dynamics, 1 for k_dyn4), at least MIN_SHIFT_BLOCKS
+  constexpr int MIN_SHIFT_BLOCKS = 64;
+  const int per_cu = cfg.waves == 4 ? 1 : 2;
+  int shift_blocks = cfg.shift_blocks > 0 ? cfg.shift_blocks : per_cu * cfg.cus - dyn_blocks;
+  if (shift_blocks < MIN_SHIFT_BLOCKS) shift_blocks = MIN_SHIFT_BLOCKS;
   const FusedArgs FA = fused ? *fused : FusedArgs{};
-  if (fused) {
-    if (T.type == 0)
-      hipLaunchKernelGGL((k_dynamics<false, true>), grid, block, 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA);
-    else
-      hipLaunchKernelGGL((k_dynamics<true, true>), grid, block, 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA);
-  } else if (T.type == 0) {
-    hipLaunchKernelGGL((k_dynamics<false, false>), grid, block, 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA);
+  const dim3 grid(dyn_blocks + shift_blocks);
+#define T1_LAUNCH(KERNEL, BS, HF, FU) \
+  hipLaunchKernelGGL((KERNEL<HF, FU>), grid, dim3(BS), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA)
+  const bool hf = T.type != 0;
+  if (cfg.waves == 4) {
+    if (fused) { if (hf) T1_LAUNCH(k_dyn4, D4_BLOCK, true, true); else T1_LAUNCH(k_dyn4, D4_BLOCK, false, true); }
+    else { if (hf) T1_LAUNCH(k_dyn4, D4_BLOCK, true, false); else T1_LAUNCH(k_dyn4, D4_BLOCK, false, false); }
   } else {
-    hipLaunchKernelGGL((k_dynamics<true, false>), grid, block, 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA);
+    if (fused) { if (hf) T1_LAUNCH(k_dynamics, DYN_BLOCK, true, true); else T1_LAUNCH(k_dynamics, DYN_BLOCK, false, true); }
+    else { if (hf) T1_LAUNCH(k_dynamics, DYN_BLOCK, true, false); else T1_LAUNCH(k_dynamics, DYN_BLOCK, false, false); }
   }
+#undef T1_LAUNCH
   return (int)hipGetLastError();
 }
 
 #ifdef T1_PHASE_PROF
-// profiling build only: summed clock deltas per [wave = leg][bucket] since the last reset
+// profiling build only: summed clock deltas per [wave][bucket] since the last reset
 extern "C" int t1env_debug_phase_cycles(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_prof), sizeof(g_t1_prof));
   if (e == hipSuccess && reset) {
-    static const unsigned long long zero[2][T1_NPROF] = {};
+    static const unsigned long long zero[T1_PROF_WAVES][T1_NPROF] = {};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_t1_prof), zero, sizeof(zero));
   }
   return (int)e;

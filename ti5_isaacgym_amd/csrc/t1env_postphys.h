@@ -515,7 +515,7 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
 #pragma unroll
   for (int i = 0; i < 96; ++i) B.dof_hist[(size_t)n * 96 + i] = 0.0f;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) B.imu_hist[(size_t)n * 12 + i] = 0.0f;
+  for (int i = 0; i < 16; ++i) B.imu_hist[(size_t)n * 16 + i] = 0.0f;
   B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_ACTION);
   B.dof_lag_timestep[n] = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_DOF);
   B.imu_lag_timestep[n] = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_IMU);
@@ -605,10 +605,11 @@ __device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config
   if (any_reset && resample_commands_r(C, A, X.el, X.gt, X.cmd, genv, ctr)) strow(B.commands + n * 4, X.cmd);
   // lagged sensor samples (need the lag lengths loaded above)
   const float* ldp = B.dof_hist + ((size_t)n * 4 + ((A.counter - (uint32_t)(X.dl / 10)) & 3u)) * 24;
-  const float* lip = B.imu_hist + ((size_t)n * 2 + ((A.counter - (uint32_t)(X.il / 10)) & 1u)) * 6;
-  float ld[24], li[6];
+  const float* lip = B.imu_hist + ((size_t)n * 2 + ((A.counter - (uint32_t)(X.il / 10)) & 1u)) * 8;
+  float ld[24], lraw[8], li[6];
   ldrow(ld, ldp);
-  ldrow(li, lip);
+  ldrow(lraw, lip);
+  imu_sample(lraw, li);
   // ---- compute_observations
   const float* cmd = X.cmd;
   const float* dof = X.dof;

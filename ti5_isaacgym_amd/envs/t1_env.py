@@ -202,7 +202,7 @@ class T1DHStandEnv(VecEnv):
         self.episode_sums = {k: self._episode_sums[i] for i, k in enumerate(REWARD_NAMES) if k in self.reward_scales}
         self.env_frictions, self.restitution_coeffs, self.body_mass = z(N, 1), z(N, 1), z(N, 1)
         self.lag_timestep, self.dof_lag_timestep, self.imu_lag_timestep = z(N, dtype=i32), z(N, dtype=i32), z(N, dtype=i32)
-        self._act_hist, self._dof_hist, self._imu_hist = z(N, 4, 12), z(N, 4, 24), z(N, 2, 6)
+        self._act_hist, self._dof_hist, self._imu_hist = z(N, 4, 12), z(N, 4, 24), z(N, 2, 8)
         self.terrain_levels, self.terrain_types = z(N, dtype=i32), z(N, dtype=i32)
         self.terrain_origins = z(1, 1, 3)
         self._extras_ring = torch.full((EXTRAS_RING, 32), float("nan"), device=d)

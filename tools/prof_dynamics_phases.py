@@ -19,7 +19,14 @@ BUCKETS = ["pd_torque+base_frame", "leg forward pass", "leg backward (no contact
            "leg elimination", "base-box contacts", "LDS write + base block", "substep tail / loop",
            "barrier wait", "base solve + backsub + integrate", "prologue loads", "report (outputs)",
            "epilogue barrier", "post_a (fused)", "post_b (fused)", "handoff + zeroing + finalize"]
+# k_dyn4 (4 waves): the same mark ids, with these meanings
+BUCKETS4 = ["pd torques", "forward pass (+ pose publish)", "backward pass (no contact)", "shank + foot contacts",
+            "contact fold-in + elimination", "base-box contacts",
+            "base block", "substep loop / captures", "S1 wait (poses)", "base solve + backsub + integrate",
+            "prologue loads", "S2 wait / report", "S3 wait / epilogue barrier", "post_a (fused)", "post_b (fused)",
+            "handoff + zeroing + finalize"]
 NB = len(BUCKETS)
+NW = 4
 
 
 def main():
@@ -41,7 +48,7 @@ def main():
     env = make_t1_env(num_envs=a.num_envs, mesh_type=a.mesh, seed=5, device="cuda:0")
     env.set_fused(not a.split)
     lib = ctypes.CDLL(PROF_LIB)
-    buf = (ctypes.c_ulonglong * (2 * NB))()
+    buf = (ctypes.c_ulonglong * (NW * NB))()
     env.reset()
     g = torch.Generator(device="cuda:0").manual_seed(0)
     acts = [torch.randn(a.num_envs, 12, device="cuda:0", generator=g) for _ in range(8)]
@@ -60,11 +67,14 @@ def main():
     waves = (a.num_envs + 63) // 64
     print(f"k_dynamics {kern_us:.1f} us/launch (events), {a.mesh}, {a.num_envs} envs, {a.steps} steps, "
           f"{'split' if a.split else 'fused'}")
-    for w in range(2):
+    four = os.environ.get("T1ENV_DYN_WAVES", "4") != "2"
+    names = BUCKETS4 if four else BUCKETS
+    roles = ["left leg", "right leg", "left contact helper", "right contact helper"]
+    for w in range(4 if four else 2):
         cyc = [buf[w * NB + i] / (waves * a.steps) for i in range(NB)]
         tot = sum(cyc)
-        print(f"wave {w} ({'left' if w == 0 else 'right'} leg): {tot:.0f} cycles/launch")
-        for name, c in sorted(zip(BUCKETS, cyc), key=lambda x: -x[1]):
+        print(f"wave {w} ({roles[w]}): {tot:.0f} cycles/launch")
+        for name, c in sorted(zip(names, cyc), key=lambda x: -x[1]):
             if c > 0:
                 print(f"   {name:34s} {c:10.0f} cyc  {100 * c / tot:5.1f}%  ~{kern_us * c / tot:6.1f} us")
 
