@@ -141,6 +141,10 @@ __device__ __forceinline__ void shift_workgroup(const ShiftArgs& S, const FusedA
   }
 }
 
+__device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const t1env_buffers& B,
+                                                    const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
+                                                    int dyn_blocks, int lane, bool do_reset, bool active, int n);
+
 // The fused step's post-physics for one dynamics workgroup's 64 envs, run by one whole wave after the
 // dynamics outputs of the workgroup are in memory (t1env_postphys.h: the same code as k_post_a / k_post_b),
 // then the reset-row handoff and the extras finalisation.
@@ -155,6 +159,14 @@ __device__ __forceinline__ void fused_epilogue(const DynModel& M, const t1env_co
   T1_PROF_MARK(13);
   if (active) post_b_env(M, C, B, A, n, do_reset, do_reset);
   T1_PROF_MARK(14);
+  fused_epilogue_tail(C, B, A, S, FA, dyn_blocks, lane, do_reset, active, n);
+}
+
+// after post-physics: the terrain-level sum, the reset-row handoff and the extras finalisation
+__device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const t1env_buffers& B,
+                                                    const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
+                                                    int dyn_blocks, int lane, bool do_reset, bool active, int n) {
+  const int N = C.num_envs;
   if (C.terrain_curriculum) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
   // ---- reset rows: hand off each of the workgroup's shift units with its 8-bit reset mask
   const unsigned long long m = __ballot(do_reset && active);
@@ -351,7 +363,21 @@ __global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restri
 // ---------------------------------------------------------------------------------------------------
 constexpr int POSE_F = 18, POSE_B = 18, POSE_N = POSE_F + 2 * POSE_B;
 constexpr int CT_N = 2 * XCH;
-constexpr int CAP_N = 2 * NLEG + 8;  // dof capture (q, qd of the leg), IMU capture (raw, leg 0)
+constexpr int CAP_N = 2 * NLEG + 8 + NLEG;  // dof capture (q, qd of the leg), IMU capture (raw, leg 0), actions
+constexpr int CAP_ACT = 2 * NLEG + 8;
+// fused epilogue staging (post-physics inputs of the workgroup's 64 envs in LDS):
+//   epi (EPI_N rows): the state post-physics reads that the step has not changed, prefetched with coalesced
+//        row loads by the helper waves while the leg waves run the last substep
+//   fresh (FR_N rows, in the ct region once the loop is over): this step's dynamics outputs, from registers
+enum : int {
+  E_LA = 0, E_LLA = 12, E_LRV = 24, E_LDV = 30, E_REF = 42, E_CMD = 54, E_AT = 58, E_FH = 60, E_LFZ = 62,
+  E_EF = 64, E_ET = 67, E_GT = 70, E_EL = 73, E_PL = 75, E_GS = 77, E_LC = 78, E_FRIC = 80, E_MASS = 81,
+  E_DL = 82, E_IL = 83, E_ESUM = 84, EPI_N = 84 + T1_NREW
+};
+enum : int {
+  F_ROOT = 0, F_DOF = 13, F_TQ = 37, F_F0 = 49, F_F1 = 62, F_K0 = 75, F_K1 = 77, F_CFB = 79, F_C0 = 82, F_C1 = 85,
+  FR_N = 88
+};
 constexpr int K_SHANK = 3, K_FOOT = 5;
 static_assert(T1_LEG_CONTACT_MASK == ((1 << K_SHANK) | (1 << K_FOOT)), "k_dyn4 assumes shank + foot contact bodies");
 
@@ -361,7 +387,9 @@ struct Dyn4Lds {
   float xch[4][XCH][DYN_ENVS];
   PdStage<DYN_ENVS> pd[2];
   float cap[2][CAP_N][DYN_ENVS];
+  float epi[EPI_N][DYN_ENVS];
 };
+static_assert(FR_N <= 2 * CT_N, "the fresh outputs fit the contact-term region");
 
 __device__ __forceinline__ void lds_put_m3(float (*dst)[DYN_ENVS], int lane, const M3<float>& R) {
 #pragma unroll
@@ -403,6 +431,271 @@ __device__ __forceinline__ void body_terms(const DynModel& M, const Terrain& T, 
   lds_put_sym(dst, lane, Cc, cc);
 }
 
+// ---- fused-epilogue staging by the two helper waves (STAGE_NT threads).  Rows [nb, nb + nv) of the workgroup;
+// a row-major source is read as one contiguous run (consecutive threads, consecutive words: coalesced) and
+// transposed into [value][env].  All loads of a thread are issued before the first LDS write (stage_ld for
+// every source, then stage_st), so the staging costs one memory latency.
+constexpr int STAGE_NT = 2 * DYN_ENVS;
+template <int L> constexpr int stage_n() { return (DYN_ENVS * L + STAGE_NT - 1) / STAGE_NT; }
+template <typename T> __device__ __forceinline__ float stage_bits(T v) {
+  if constexpr (sizeof(T) == 4) return __builtin_bit_cast(float, v);
+  else return __int_as_float((int)v);
+}
+template <int L, typename T>
+__device__ __forceinline__ void stage_ld(const T* __restrict__ src, int nb, int nv, int t, float (&v)[stage_n<L>()]) {
+  const T* base = src + (size_t)nb * L;
+#pragma unroll
+  for (int i = 0; i < stage_n<L>(); ++i) {
+    const int e = t + STAGE_NT * i;
+    v[i] = e < nv * L ? stage_bits(base[e]) : 0.0f;
+  }
+}
+template <int L>
+__device__ __forceinline__ void stage_st(float (*dst)[DYN_ENVS], int nv, int t, const float (&v)[stage_n<L>()]) {
+#pragma unroll
+  for (int i = 0; i < stage_n<L>(); ++i) {
+    const int e = t + STAGE_NT * i;
+    if (e < nv * L) dst[e % L][e / L] = v[i];
+  }
+}
+__device__ __forceinline__ void stage_epilogue_inputs(const t1env_buffers& B, int N, int nb, int t,
+                                                      float (*E)[DYN_ENVS]) {
+  const int nv = N - nb < DYN_ENVS ? N - nb : DYN_ENVS;
+  float la[stage_n<12>()], lla[stage_n<12>()], lrv[stage_n<6>()], ldv[stage_n<12>()], ref[stage_n<12>()];
+  float cmd[stage_n<4>()], at[stage_n<2>()], fh[stage_n<2>()], lfz[stage_n<2>()], ef[stage_n<3>()];
+  float et[stage_n<3>()], gt[stage_n<3>()], el[stage_n<2>()], pl[stage_n<2>()], gs[stage_n<1>()], lc[stage_n<2>()];
+  float fr[stage_n<1>()], ms[stage_n<1>()], dl[stage_n<1>()], il[stage_n<1>()];
+  constexpr int NES = (T1_NREW * DYN_ENVS + STAGE_NT - 1) / STAGE_NT;
+  float es[NES];
+  stage_ld<12>(B.last_actions, nb, nv, t, la);
+  stage_ld<12>(B.last_last_actions, nb, nv, t, lla);
+  stage_ld<6>(B.last_root_vel, nb, nv, t, lrv);
+  stage_ld<12>(B.last_dof_vel, nb, nv, t, ldv);
+  stage_ld<12>(B.ref_dof_pos, nb, nv, t, ref);
+  stage_ld<4>(B.commands, nb, nv, t, cmd);
+  stage_ld<2>(B.feet_air_time, nb, nv, t, at);
+  stage_ld<2>(B.feet_height, nb, nv, t, fh);
+  stage_ld<2>(B.last_feet_z, nb, nv, t, lfz);
+  stage_ld<3>(B.ext_forces, nb, nv, t, ef);
+  stage_ld<3>(B.ext_torques, nb, nv, t, et);
+  stage_ld<3>(B.gait_time, nb, nv, t, gt);
+  stage_ld<2>(reinterpret_cast<const uint32_t*>(B.episode_length_buf), nb, nv, t, el);
+  stage_ld<2>(reinterpret_cast<const uint32_t*>(B.phase_length_buf), nb, nv, t, pl);
+  stage_ld<1>(B.gait_start, nb, nv, t, gs);
+  stage_ld<2>(B.last_contacts, nb, nv, t, lc);
+  stage_ld<1>(B.friction, nb, nv, t, fr);
+  stage_ld<1>(B.body_mass, nb, nv, t, ms);
+  stage_ld<1>(B.dof_lag_timestep, nb, nv, t, dl);
+  stage_ld<1>(B.imu_lag_timestep, nb, nv, t, il);
+#pragma unroll
+  for (int i = 0; i < NES; ++i) {  // episode_sums is [reward][env]: already row-contiguous
+    const int e = t + STAGE_NT * i;
+    es[i] = e < T1_NREW * nv ? B.episode_sums[(size_t)(e / nv) * N + nb + e % nv] : 0.0f;
+  }
+  stage_st<12>(E + E_LA, nv, t, la);
+  stage_st<12>(E + E_LLA, nv, t, lla);
+  stage_st<6>(E + E_LRV, nv, t, lrv);
+  stage_st<12>(E + E_LDV, nv, t, ldv);
+  stage_st<12>(E + E_REF, nv, t, ref);
+  stage_st<4>(E + E_CMD, nv, t, cmd);
+  stage_st<2>(E + E_AT, nv, t, at);
+  stage_st<2>(E + E_FH, nv, t, fh);
+  stage_st<2>(E + E_LFZ, nv, t, lfz);
+  stage_st<3>(E + E_EF, nv, t, ef);
+  stage_st<3>(E + E_ET, nv, t, et);
+  stage_st<3>(E + E_GT, nv, t, gt);
+  stage_st<2>(E + E_EL, nv, t, el);
+  stage_st<2>(E + E_PL, nv, t, pl);
+  stage_st<1>(E + E_GS, nv, t, gs);
+  stage_st<2>(E + E_LC, nv, t, lc);
+  stage_st<1>(E + E_FRIC, nv, t, fr);
+  stage_st<1>(E + E_MASS, nv, t, ms);
+  stage_st<1>(E + E_DL, nv, t, dl);
+  stage_st<1>(E + E_IL, nv, t, il);
+#pragma unroll
+  for (int i = 0; i < NES; ++i) {
+    const int e = t + STAGE_NT * i;
+    if (e < T1_NREW * nv) E[E_ESUM + e / nv][e % nv] = es[i];
+  }
+}
+
+// The fused step's post-physics for one k_dyn4 workgroup, run by wave 0: every input from LDS (fresh outputs,
+// staged state, the actions in the capture rows), post_a's results handed to post_b in registers.
+__device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                                      const t1env_step_args& A, const ShiftArgs& S,
+                                                      const FusedArgs& FA, int dyn_blocks, int lane,
+                                                      const float (*E)[DYN_ENVS], const float (*FR)[DYN_ENVS],
+                                                      const float (*cap0)[DYN_ENVS], const float (*cap1)[DYN_ENVS]) {
+  const int N = C.num_envs;
+  const int n0 = blockIdx.x * DYN_ENVS + lane;
+  const bool active = n0 < N;
+  const int n = active ? n0 : N - 1;
+  PostAIn X;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) X.root[i] = FR[F_ROOT + i][lane];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) X.dof[i] = FR[F_DOF + i][lane];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) { X.f0[i] = FR[F_F0 + i][lane]; X.f1[i] = FR[F_F1 + i][lane]; }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { X.k0[i] = FR[F_K0 + i][lane]; X.k1[i] = FR[F_K1 + i][lane]; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { X.cfb[i] = FR[F_CFB + i][lane]; X.c0[i] = FR[F_C0 + i][lane]; X.c1[i] = FR[F_C1 + i][lane]; }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) X.tq[i] = FR[F_TQ + i][lane];
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) { X.a[k] = cap0[CAP_ACT + k][lane]; X.a[NLEG + k] = cap1[CAP_ACT + k][lane]; }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    X.la[i] = E[E_LA + i][lane]; X.lla[i] = E[E_LLA + i][lane];
+    X.ldv[i] = E[E_LDV + i][lane]; X.ref[i] = E[E_REF + i][lane];
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) X.lrv[i] = E[E_LRV + i][lane];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) X.cmd[i] = E[E_CMD + i][lane];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    X.at[i] = E[E_AT + i][lane]; X.fh[i] = E[E_FH + i][lane]; X.lfz[i] = E[E_LFZ + i][lane];
+    X.lc[i] = (uint8_t)__float_as_int(E[E_LC + i][lane]);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    X.ef[i] = E[E_EF + i][lane]; X.et[i] = E[E_ET + i][lane];
+    X.gt[i] = __float_as_int(E[E_GT + i][lane]);
+  }
+#pragma unroll
+  for (int k = 0; k < T1_NREW; ++k) X.esum[k] = E[E_ESUM + k][lane];
+  X.el = (int64_t)(((uint64_t)(uint32_t)__float_as_int(E[E_EL + 1][lane]) << 32) |
+                   (uint32_t)__float_as_int(E[E_EL][lane]));
+  X.pl = (int64_t)(((uint64_t)(uint32_t)__float_as_int(E[E_PL + 1][lane]) << 32) |
+                   (uint32_t)__float_as_int(E[E_PL][lane]));
+  X.gstart = E[E_GS][lane];
+  BaseQ bq;
+  const bool do_reset = post_a_core(M, C, B, A, n0, X, bq);
+  T1_PROF_MARK(13);
+  if (active) {
+    ObsIn O;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) O.cmd[i] = X.cmd[i];
+#pragma unroll
+    for (int i = 0; i < 24; ++i) O.dof[i] = X.dof[i];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) { O.act[i] = X.a[i]; O.la[i] = X.la[i]; }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) O.rv[i] = X.root[7 + i];
+    O.bq = bq;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) O.gt[i] = X.gt[i];
+    O.el = X.el;
+    O.pl = X.pl;
+    O.gstart = X.gstart;
+    O.dl = __float_as_int(E[E_DL][lane]);
+    O.il = __float_as_int(E[E_IL][lane]);
+    ObsExtra Ex;
+    Ex.ef[0] = X.ef[0]; Ex.ef[1] = X.ef[1];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Ex.et[i] = X.et[i];
+    Ex.cfz[0] = X.c0[2]; Ex.cfz[1] = X.c1[2];
+    Ex.fric = E[E_FRIC][lane];
+    Ex.mass = E[E_MASS][lane];
+    post_b_core(M, C, B, A, n, do_reset, do_reset, O, Ex);
+  }
+  T1_PROF_MARK(14);
+  fused_epilogue_tail(C, B, A, S, FA, dyn_blocks, lane, do_reset, active, n);
+}
+
+// k_dyn4's report, split between the waves: the leg wave writes its bodies' rigid states (and the root for
+// leg 0), zeros the contact rows of its bodies without contact points, and publishes the end-of-step base frame
+// and contact-body poses; after a barrier the helper evaluates the contact forces of the shank, foot (and the
+// base box, leg 0) -- the height queries and point forces that dominate the report.
+// FR (fused step): this step's outputs post-physics reads are also written to LDS rows (every lane)
+__device__ __forceinline__ void leg_report_rigid(const DynModel& M, const t1env_buffers& B, const BaseParams<float>& PB,
+                                                 const BaseState<float>& sb, const BaseFrame<float>& F,
+                                                 const float q[NLEG], const float qd[NLEG], int n, int leg, bool active,
+                                                 float (*P)[DYN_ENVS], int lane, float (*FR)[DYN_ENVS]) {
+  float* rig = B.rigid_state + (size_t)n * 169;
+  float* cf = B.contact_forces + (size_t)n * 39;
+  if (leg == 0) {
+    const V3<float> c0 = base_com(M, PB, F.R0);
+    const V3<float> vcom = v3<float>(sb.vo[0], sb.vo[1], sb.vo[2]) + cross(v3<float>(sb.w[0], sb.w[1], sb.w[2]), c0);
+    const float body[13] = {sb.pos[0], sb.pos[1], sb.pos[2], sb.quat[0], sb.quat[1], sb.quat[2], sb.quat[3],
+                            vcom.x, vcom.y, vcom.z, sb.w[0], sb.w[1], sb.w[2]};
+    if (active)
+#pragma unroll
+      for (int i = 0; i < 13; ++i) { B.root_states[(size_t)n * 13 + i] = body[i]; rig[i] = body[i]; }
+    if (FR)
+#pragma unroll
+      for (int i = 0; i < 13; ++i) FR[F_ROOT + i][lane] = body[i];
+  }
+  BodyState<float> Bk[NLEG];
+  leg_fk(M, leg, F.R0, q, Bk);
+  float V[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) V[i] = F.V0[i];
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    const int b = 1 + 6 * leg + k;
+    float S6[6];
+    motion_subspace(M, b, Bk[k], S6);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) V[i] += S6[i] * qd[k];
+    if (k == K_SHANK || k == K_FOOT) {
+      float (*D)[DYN_ENVS] = P + POSE_F + (k == K_FOOT ? POSE_B : 0);
+      lds_put_m3(D, lane, Bk[k].Rot);
+      D[9][lane] = Bk[k].p.x; D[10][lane] = Bk[k].p.y; D[11][lane] = Bk[k].p.z;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) D[12 + i][lane] = V[i];
+    }
+    const V3<float> c = Bk[k].p + mul(Bk[k].Rot, v3<float>(M.com[b][0], M.com[b][1], M.com[b][2]));
+    const V3<float> om{V[0], V[1], V[2]};
+    const V3<float> vc = v3<float>(V[3], V[4], V[5]) + cross(om, c);
+    float qb[4];
+    mat_to_quat(Bk[k].Rot, qb);
+    const float out[13] = {Bk[k].p.x + F.abs.x, Bk[k].p.y + F.abs.y, Bk[k].p.z + F.abs.z, qb[0], qb[1], qb[2], qb[3],
+                           vc.x, vc.y, vc.z, om.x, om.y, om.z};
+    if (FR) {
+      if (k == K_FOOT)
+#pragma unroll
+        for (int i = 0; i < 13; ++i) FR[(leg == 0 ? F_F0 : F_F1) + i][lane] = out[i];
+      if (k == K_SHANK) { FR[(leg == 0 ? F_K0 : F_K1)][lane] = out[0]; FR[(leg == 0 ? F_K0 : F_K1) + 1][lane] = out[1]; }
+    }
+    if (!active) continue;
+#pragma unroll
+    for (int i = 0; i < 13; ++i) rig[b * 13 + i] = out[i];
+    if (k != K_SHANK && k != K_FOOT) { cf[b * 3 + 0] = 0.0f; cf[b * 3 + 1] = 0.0f; cf[b * 3 + 2] = 0.0f; }
+  }
+}
+__device__ __forceinline__ void helper_report_contacts(const DynModel& M, const Terrain& T, const t1env_buffers& B,
+                                                       const float (*P)[DYN_ENVS], int n, int leg, float mu, int lane,
+                                                       bool active, float (*FR)[DYN_ENVS]) {
+  float* cf = B.contact_forces + (size_t)n * 39;
+  const V3<float> abs = v3<float>(P[9][lane], P[10][lane], P[11][lane]);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const float (*D)[DYN_ENVS] = P + POSE_F + s * POSE_B;
+    const int b = 1 + 6 * leg + (s == 0 ? K_SHANK : K_FOOT);
+    float Vb[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) Vb[i] = D[12 + i][lane];
+    const V3<float> f = body_contact_force(M, T, b, lds_get_m3(D, lane), v3<float>(D[9][lane], D[10][lane], D[11][lane]),
+                                           abs, Vb, mu);
+    if (active) { cf[b * 3 + 0] = f.x; cf[b * 3 + 1] = f.y; cf[b * 3 + 2] = f.z; }
+    if (FR && s == 1) {
+      const int r = leg == 0 ? F_C0 : F_C1;
+      FR[r][lane] = f.x; FR[r + 1][lane] = f.y; FR[r + 2][lane] = f.z;
+    }
+  }
+  if (leg == 0) {
+    float V0[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) V0[i] = P[12 + i][lane];
+    const V3<float> f = body_contact_force(M, T, 0, lds_get_m3(P, lane), v3<float>(0, 0, 0), abs, V0, mu);
+    if (active) { cf[0] = f.x; cf[1] = f.y; cf[2] = f.z; }
+    if (FR) { FR[F_CFB][lane] = f.x; FR[F_CFB + 1][lane] = f.y; FR[F_CFB + 2][lane] = f.z; }
+  }
+}
+
 template <bool HF, bool FUSED>
 __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
                                                    t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
@@ -434,6 +727,9 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
     const float (*P)[DYN_ENVS] = lds.pose[leg];
     T1_PROF_MARK(10);
     for (int sub = 0; sub < C.decimation; ++sub) {
+      if constexpr (FUSED)  // the leg waves run the last substep: stage the epilogue's inputs meanwhile
+        if (sub == C.decimation - 1)
+          stage_epilogue_inputs(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, lds.epi);
       T1_PROF_MARK(7);
       __syncthreads();  // S1: poses of this substep published
       T1_PROF_MARK(8);
@@ -463,6 +759,12 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
       __syncthreads();  // S3: base system complete
       T1_PROF_MARK(12);
     }
+    T1_PROF_MARK(7);
+    __syncthreads();  // R1: end-of-step poses published
+    T1_PROF_MARK(8);
+    float (*FR)[DYN_ENVS] = FUSED ? reinterpret_cast<float (*)[DYN_ENVS]>(&lds.ct[0][0][0]) : nullptr;
+    helper_report_contacts(M, T, B, P, n, leg, mu, lane, active, FR);
+    T1_PROF_MARK(11);
     if constexpr (FUSED) __syncthreads();  // the epilogue barrier
     T1_PROF_END();
     return;
@@ -481,6 +783,10 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
   pd_stage(B, n, j0, lane, PD);  // this step's action slot was written by leg_setup (same lane)
   float (*P)[DYN_ENVS] = lds.pose[leg];
   float (*CAP)[DYN_ENVS] = lds.cap[leg];
+  if constexpr (FUSED)  // the clipped actions, for the epilogue
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k)
+      CAP[CAP_ACT + k][lane] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
   T1_PROF_MARK(10);
   for (int sub = 0; sub < C.decimation; ++sub) {
     T1_PROF_MARK(7);
@@ -569,13 +875,37 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
       const float w[3] = {CAP[2 * NLEG + 4][lane], CAP[2 * NLEG + 5][lane], CAP[2 * NLEG + 6][lane]};
       capture_imu(quat, w, L.imu_dst);
     }
-    leg_report(M, T, B, PB, sb, q, qd, tau, n, leg, j0);
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
+      B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
+      B.torques[n * 12 + j0 + k] = tau[k];
+    }
+  }
+  float (*FR)[DYN_ENVS] = FUSED ? reinterpret_cast<float (*)[DYN_ENVS]>(&lds.ct[0][0][0]) : nullptr;
+  if constexpr (FUSED) {
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      FR[F_DOF + 2 * (j0 + k)][lane] = q[k];
+      FR[F_DOF + 2 * (j0 + k) + 1][lane] = qd[k];
+      FR[F_TQ + j0 + k][lane] = tau[k];
+    }
+  }
+  {
+    BaseFrame<float> F;
+    base_frame(sb, F);
+    lds_put_m3(P, lane, F.R0);
+    P[9][lane] = F.abs.x; P[10][lane] = F.abs.y; P[11][lane] = F.abs.z;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) P[12 + i][lane] = F.V0[i];
+    leg_report_rigid(M, B, PB, sb, F, q, qd, n, leg, active, P, lane, FR);
   }
   T1_PROF_MARK(11);
+  __syncthreads();  // R1: end-of-step poses published (the helpers write the contact forces)
   if constexpr (FUSED) {
-    __syncthreads();  // all four waves: both legs' outputs are in memory
+    __syncthreads();  // all four waves: every output of the workgroup is in memory
     T1_PROF_MARK(12);
-    if (leg == 0) fused_epilogue(M, C, B, A, S, FA, dyn_blocks, lane);
+    if (leg == 0) fused_epilogue_staged(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, FR, lds.cap[0], lds.cap[1]);
   }
   T1_PROF_END();
 }

@@ -156,52 +156,92 @@ __device__ __forceinline__ void finalize_extras(const t1env_buffers& B, const t1
 // compiler knows) cost one memory round trip per access, and the pass is latency-bound (one lane per env).
 // Called by a whole wave (the extras sums are wave reductions); lane = env n0 (lanes past num_envs shadow the
 // last env).  Returns this env's reset decision.
-__device__ __forceinline__ bool post_a_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
-                                           const t1env_step_args& A, int n0) {
+// the inputs of post_a for one env (loaded by load_post_a_in in the split kernels, staged through LDS in the
+// fused k_dyn4 epilogue); el / pl as stored, before this step's increment
+struct PostAIn {
+  float root[13], dof[24], f0[13], f1[13], k0[2], k1[2], cfb[3], c0[3], c1[3];
+  float a[12], la[12], lla[12], lrv[6], ldv[12], tq[12], ref[12], cmd[4], esum[T1_NREW];
+  float at[2], fh[2], lfz[2], ef[3], et[3];
+  uint8_t lc[2];
+  int32_t gt[3];
+  int64_t el, pl;
+  float gstart;
+};
+__device__ __forceinline__ void load_post_a_in(const t1env_buffers& B, size_t N, int n, PostAIn& X) {
+  const float* rig = B.rigid_state + (size_t)n * 169;
+  const float* cf = B.contact_forces + (size_t)n * 39;
+  ldrow(X.root, B.root_states + n * 13);
+  ldrow(X.dof, B.dof_state + (size_t)n * 24);
+  ldrow(X.f0, rig + 6 * 13);
+  ldrow(X.f1, rig + 12 * 13);
+  ldrow(X.k0, rig + 4 * 13);
+  ldrow(X.k1, rig + 10 * 13);
+  ldrow(X.cfb, cf);
+  ldrow(X.c0, cf + 6 * 3);
+  ldrow(X.c1, cf + 12 * 3);
+  ldrow(X.a, B.actions + n * 12);
+  ldrow(X.la, B.last_actions + n * 12);
+  ldrow(X.lla, B.last_last_actions + n * 12);
+  ldrow(X.lrv, B.last_root_vel + n * 6);
+  ldrow(X.ldv, B.last_dof_vel + n * 12);
+  ldrow(X.tq, B.torques + n * 12);
+  ldrow(X.ref, B.ref_dof_pos + n * 12);
+  ldrow(X.cmd, B.commands + n * 4);
+  ldrow(X.at, B.feet_air_time + n * 2);
+  ldrow(X.fh, B.feet_height + n * 2);
+  ldrow(X.lfz, B.last_feet_z + n * 2);
+  ldrow(X.ef, B.ext_forces + n * 3);
+  ldrow(X.et, B.ext_torques + n * 3);
+  ldrow(X.lc, B.last_contacts + n * 2);
+  ldrow(X.gt, B.gait_time + n * 3);
+#pragma unroll
+  for (int k = 0; k < T1_NREW; ++k) X.esum[k] = B.episode_sums[k * N + n];
+  X.el = B.episode_length_buf[n];
+  X.pl = B.phase_length_buf[n];
+  X.gstart = B.gait_start[n];
+}
+
+// Called by a whole wave (the extras sums are wave reductions); lane = env n0 (lanes past num_envs shadow the
+// last env).  Returns this env's reset decision; on return X holds the post-callback state (root after a push,
+// resampled commands, incremented episode / phase counters, external force and torque) and bq the base
+// quantities, which the fused epilogue hands to post_b without a reload.
+__device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                            const t1env_step_args& A, int n0, PostAIn& X, BaseQ& bq) {
   const bool live = n0 < C.num_envs;
   const int n = live ? n0 : C.num_envs - 1;
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   const uint32_t ctr = A.counter + 1u;  // common_step_counter += 1 happened before the callback
   const size_t N = (size_t)C.num_envs;
-  // ---- inputs
-  float root[13], dof[24], f0[13], f1[13], k0[2], k1[2], cfb[3], c0[3], c1[3];
-  float a[12], la[12], lla[12], lrv[6], ldv[12], tq[12], ref[12], cmd[4], esum[T1_NREW];
-  float at[2], fh[2], lfz[2], ef[3];
-  uint8_t lc[2];
-  int32_t gt[3];
-  const float* rig = B.rigid_state + (size_t)n * 169;
-  const float* cf = B.contact_forces + (size_t)n * 39;
-  ldrow(root, B.root_states + n * 13);
-  ldrow(dof, B.dof_state + (size_t)n * 24);
-  ldrow(f0, rig + 6 * 13);
-  ldrow(f1, rig + 12 * 13);
-  ldrow(k0, rig + 4 * 13);
-  ldrow(k1, rig + 10 * 13);
-  ldrow(cfb, cf);
-  ldrow(c0, cf + 6 * 3);
-  ldrow(c1, cf + 12 * 3);
-  ldrow(a, B.actions + n * 12);
-  ldrow(la, B.last_actions + n * 12);
-  ldrow(lla, B.last_last_actions + n * 12);
-  ldrow(lrv, B.last_root_vel + n * 6);
-  ldrow(ldv, B.last_dof_vel + n * 12);
-  ldrow(tq, B.torques + n * 12);
-  ldrow(ref, B.ref_dof_pos + n * 12);
-  ldrow(cmd, B.commands + n * 4);
-  ldrow(at, B.feet_air_time + n * 2);
-  ldrow(fh, B.feet_height + n * 2);
-  ldrow(lfz, B.last_feet_z + n * 2);
-  ldrow(ef, B.ext_forces + n * 3);
-  ldrow(lc, B.last_contacts + n * 2);
-  ldrow(gt, B.gait_time + n * 3);
-#pragma unroll
-  for (int k = 0; k < T1_NREW; ++k) esum[k] = B.episode_sums[k * N + n];
-  const int64_t el = B.episode_length_buf[n] + 1;
-  int64_t pl = B.phase_length_buf[n] + 1;
-  const float gstart = B.gait_start[n];
+  float (&root)[13] = X.root;
+  const float (&dof)[24] = X.dof;
+  const float (&f0)[13] = X.f0;
+  const float (&f1)[13] = X.f1;
+  const float (&k0)[2] = X.k0;
+  const float (&k1)[2] = X.k1;
+  const float (&cfb)[3] = X.cfb;
+  const float (&c0)[3] = X.c0;
+  const float (&c1)[3] = X.c1;
+  const float (&a)[12] = X.a;
+  const float (&la)[12] = X.la;
+  const float (&lla)[12] = X.lla;
+  const float (&lrv)[6] = X.lrv;
+  const float (&ldv)[12] = X.ldv;
+  const float (&tq)[12] = X.tq;
+  const float (&ref)[12] = X.ref;
+  float (&cmd)[4] = X.cmd;
+  float (&esum)[T1_NREW] = X.esum;
+  float (&at)[2] = X.at;
+  float (&fh)[2] = X.fh;
+  float (&lfz)[2] = X.lfz;
+  float (&ef)[3] = X.ef;
+  float (&et)[3] = X.et;
+  uint8_t (&lc)[2] = X.lc;
+  const int32_t (&gt)[3] = X.gt;
+  const int64_t el = X.el + 1;
+  int64_t pl = X.pl + 1;
+  const float gstart = X.gstart;
   // (lanes past num_envs shadow the last env: they compute but neither store nor contribute)
   // ---- base quantities (legged_robot.py:469-477) of the post-physics root state, feet euler angles
-  BaseQ bq;
   base_quantities_r(root, bq);
   const float* blv = bq.lin;
   const float* bav = bq.ang;
@@ -222,7 +262,7 @@ __device__ __forceinline__ bool post_a_env(const DynModel& M, const t1env_config
     root[11] = rand_float(-C.push_ang, C.push_ang, C.seed, genv, ctr, SLOT_PUSH_ANG + 1);
     root[12] = rand_float(-C.push_ang, C.push_ang, C.seed, genv, ctr, SLOT_PUSH_ANG + 2);
   }
-  float af[3] = {0.0f, 0.0f, 0.0f}, et[3];
+  float af[3] = {0.0f, 0.0f, 0.0f};
   bool ext_store = true;
   if (A.ext_force_call) {  // _add_ext_force (t1:233-247)
     if (A.ext_force_first) {
@@ -454,7 +494,18 @@ __device__ __forceinline__ bool post_a_env(const DynModel& M, const t1env_config
   for (int k = 0; k < T1_NREW; ++k) part[k] = contrib[k];
   part[T1_NREW] = do_reset ? 1.0f : 0.0f;
   wave_atomic_add_n(B.ep_accum, part);  // ep_accum[0..23] episode sums, [24] reset count
+  X.el = el;
+  X.pl = pl;
   return do_reset;
+}
+
+__device__ __forceinline__ bool post_a_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                           const t1env_step_args& A, int n0) {
+  const int n = n0 < C.num_envs ? n0 : C.num_envs - 1;
+  PostAIn X;
+  load_post_a_in(B, (size_t)C.num_envs, n, X);
+  BaseQ bq;
+  return post_a_core(M, C, B, A, n0, X, bq);
 }
 
 // =====================================================================================================
@@ -586,18 +637,37 @@ __device__ __forceinline__ void load_obs_in(const t1env_buffers& B, int n, ObsIn
 
 // Load-first like k_post_a: the inputs are read before any store; an env that resets this step rewrites its
 // state in memory (reset_env) and reloads them.
+// the rest of post_b's per-env inputs (reset_idx leaves them unchanged)
+struct ObsExtra {
+  float ef[2], et[3], cfz[2], fric, mass;
+};
+__device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                            const t1env_step_args& A, int n, bool do_reset, bool any_reset, ObsIn& X,
+                                            const ObsExtra& E);
 __device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                            const t1env_step_args& A, int n, bool do_reset, bool any_reset) {
-  const uint32_t genv = (uint32_t)(C.env_offset + n);
-  const uint32_t ctr = A.counter + 1u;
   ObsIn X;
   load_obs_in(B, n, X);
-  float ef[2], et[3], cfz[2];
-  ldrow(ef, B.ext_forces + n * 3);
-  ldrow(et, B.ext_torques + n * 3);
-  cfz[0] = B.contact_forces[(size_t)n * 39 + 6 * 3 + 2];
-  cfz[1] = B.contact_forces[(size_t)n * 39 + 12 * 3 + 2];
-  const float fric = B.friction[n], mass = B.body_mass[n];
+  ObsExtra E;
+  ldrow(E.ef, B.ext_forces + n * 3);
+  ldrow(E.et, B.ext_torques + n * 3);
+  E.cfz[0] = B.contact_forces[(size_t)n * 39 + 6 * 3 + 2];
+  E.cfz[1] = B.contact_forces[(size_t)n * 39 + 12 * 3 + 2];
+  E.fric = B.friction[n];
+  E.mass = B.body_mass[n];
+  post_b_core(M, C, B, A, n, do_reset, any_reset, X, E);
+}
+
+// X: the inputs as they stand after post_a (reloaded here after a reset)
+__device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                            const t1env_step_args& A, int n, bool do_reset, bool any_reset, ObsIn& X,
+                                            const ObsExtra& E) {
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  const uint32_t ctr = A.counter + 1u;
+  const float (&ef)[2] = E.ef;
+  const float (&et)[3] = E.et;
+  const float (&cfz)[2] = E.cfz;
+  const float fric = E.fric, mass = E.mass;
   if (do_reset) {
     reset_env(M, C, B, A, n, genv, ctr, true);
     load_obs_in(B, n, X);
