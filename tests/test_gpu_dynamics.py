@@ -1,4 +1,5 @@
-"""k_dynamics (the HIP articulated-body solver + PD loop) against an independent host replica in fp64.
+"""The HIP dynamics kernels (articulated-body solver + PD loop: k_dyn4, the default, and the 2-wave
+k_dynamics) against an independent host replica in fp64.
 
 PhysX itself cannot run anywhere here, so the simulator step is checked against the same algorithm run in
 double precision on the host (oracle/cpu_env.py: numpy oracle PD/post-physics + oracle/dyn_cpu.cpp fp64),
@@ -40,8 +41,14 @@ def _state(root, dof):
             "q": dof[..., 0], "qd": dof[..., 1]}
 
 
+@pytest.fixture(params=["4", "2"], ids=["dyn4", "dyn2"])
+def dyn_waves(request, monkeypatch):
+    monkeypatch.setenv("T1ENV_DYN_WAVES", request.param)  # read by t1env_create
+    return request.param
+
+
 @pytest.mark.parametrize("mesh", ["plane", "trimesh"])
-def test_dynamics_one_step_matches_fp64_host(mesh):
+def test_dynamics_one_step_matches_fp64_host(mesh, dyn_waves):
     from ti5_isaacgym_amd import make_t1_env
     env = make_t1_env(num_envs=N, mesh_type=mesh, seed=5, device="cuda:0",
                       cfg_hook=_terrain_hook if mesh != "plane" else None)

@@ -726,10 +726,10 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
     base_contact_range(M, leg, cb, ce);
     const float (*P)[DYN_ENVS] = lds.pose[leg];
     T1_PROF_MARK(10);
+    // the epilogue's inputs the step does not change, staged while the leg waves set up and run the first
+    // forward pass (nothing writes them before the epilogue)
+    if constexpr (FUSED) stage_epilogue_inputs(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, lds.epi);
     for (int sub = 0; sub < C.decimation; ++sub) {
-      if constexpr (FUSED)  // the leg waves run the last substep: stage the epilogue's inputs meanwhile
-        if (sub == C.decimation - 1)
-          stage_epilogue_inputs(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, lds.epi);
       T1_PROF_MARK(7);
       __syncthreads();  // S1: poses of this substep published
       T1_PROF_MARK(8);
