@@ -33,9 +33,12 @@ sys.path.insert(0, REPO)
 
 B_ALG = 30678          # algorithmic bytes per env-step (fp32, default t1 config)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# timer slots of include/t1env.h: slot "k_dynamics" brackets the dynamics launch, which on a normal step is the
+# whole fused step (k_dyn4: dynamics + post-physics epilogue + history-shift workgroups, t1env_dynamics.hip);
+# k_post_a / k_post_b only launch on the split (command-curriculum, 1 in 2400) steps
 KERNELS = ["k_dynamics", "k_post_a", "k_post_b"]
-# per-kernel algorithmic bytes per env (reads + writes it must do)
-# the k_dynamics launch also runs the history shift in its tail workgroups (t1env_dynamics.hip)
+FUSED_KERNEL = "k_dynamics" if os.environ.get("T1ENV_DYN_WAVES") == "2" else "k_dyn4"
+# per-kernel algorithmic bytes per env (reads + writes it must do) for the split sequence
 SHIFT_BYTES = 2 * 4 * ((3102 - 47) + (219 - 73))
 KERNEL_BYTES = {
     "k_dynamics": 4 * (13 + 24 + 12 + 48 + 12 * 6 + 13 + 3 + 3) + 4 * (13 + 24 + 169 + 39 + 12 + 12 + 12 + 24 + 6)
@@ -58,7 +61,7 @@ def parse():
                         "0 = never, 1 = every step)")
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01k.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
     return p.parse_args()
 
@@ -140,17 +143,24 @@ def main():
     steps = args.steps
     value = N * world * steps / elapsed
     # live per-kernel HIP-event timing on the sampled steps
+    fused = kt["k_post_a"]["launches"] == 0  # no split step inside the timed region: every launch is the whole step
     per_kernel = {}
     for k in KERNELS:
         ms = kt[k]["ms"] / max(1, kt[k]["launches"])
-        per_kernel[k] = {"avg_ms": round(ms, 5), "timed_launches": kt[k]["launches"],
-                         "alg_bytes_per_launch": KERNEL_BYTES[k] * N,
-                         "alg_GBs": round(KERNEL_BYTES[k] * N / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
-    dom = max(KERNELS, key=lambda k: kt[k]["ms"])
+        alg = (B_ALG if (fused and k == "k_dynamics") else KERNEL_BYTES[k]) * N
+        name = FUSED_KERNEL if (fused and k == "k_dynamics") else k
+        per_kernel[name] = {"avg_ms": round(ms, 5), "timed_launches": kt[k]["launches"], "alg_bytes_per_launch": alg,
+                            "alg_GBs": round(alg / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
+    dom = max(per_kernel, key=lambda k: per_kernel[k]["avg_ms"] * per_kernel[k]["timed_launches"])
     step_span_ms = kt["step"]["ms"] / kt["step"]["launches"] if kt["step"]["launches"] else None
-    # roofline.achieved = env_steps_per_s x B_alg (the env step is the unit of work; on one GPU
-    # the rank's steps/s)
-    achieved = value / world * B_ALG / 1e9
+    # roofline of the dominant kernel: its algorithmic bytes per launch (SURVEY.md §8(d) B_alg x envs when the launch
+    # is the whole fused step) / its live HIP-event launch duration.  Without sampled events (--time-every 0) fall
+    # back to the wall clock of the timed steps (env_steps_per_s x B_alg).
+    dk = per_kernel[dom]
+    if dk["alg_GBs"] is not None:
+        achieved, basis = dk["alg_GBs"], f"{dom} alg bytes / live HIP-event launch duration"
+    else:
+        achieved, basis = value / world * B_ALG / 1e9, "wall clock: env-steps/s x B_alg"
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -167,12 +177,13 @@ def main():
         "config": {"workload": f"t1_dh_stand {N} envs/GPU, {args.mesh} curriculum terrain + full DR, "
                                "random N(0,1) actions (policy excluded), 10 substeps/step",
                    "num_envs_per_gpu": N, "global_envs": N * world, "mesh": args.mesh, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": "t1env_step (k_dynamics + history-shift workgroups, k_post_a, k_post_b)",
+        "roofline": {"bound": "hbm", "kernel": dom, "basis": basis,
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_step": B_ALG * N, "alg_bytes_per_env_step": B_ALG,
+                     "wall_clock_GBs": round(value / world * B_ALG / 1e9, 1),
                      "step_span_ms_timed": round(step_span_ms, 4) if step_span_ms else None,
-                     "dominant_kernel": dom, "kernels": per_kernel},
+                     "kernels": per_kernel},
         "finite": ok,
     }
     if world == 1 and not args.no_cpu_baseline:

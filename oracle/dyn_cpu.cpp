@@ -49,7 +49,7 @@ template <typename R>
 int substep_batch(const t1env_model* model, int N, float* root, float* dof, const float* tau, const float* body_mass,
                   const float* link_scale, const float* com_disp, const float* armature, const float* friction,
                   const float* ext_force, float dt, int nsub, const int16_t* hf, int rows, int cols, float hs, float vs,
-                  float border, int mesh, float* rigid, float* contact) {
+                  float border, int mesh, float* rigid, float* contact, bool split) {
   DynModel M;
   if (make_dyn_model(model, &M)) return -1;
   Terrain T = make_terrain(hf, rows, cols, mesh, hs, vs, border);
@@ -62,7 +62,7 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
     for (int j = 0; j < ND; ++j) t[j] = tau[(size_t)n * 12 + j];
     for (int k = 0; k < nsub; ++k) {
       V3<R> ef = (ext_force && k == 0) ? v3<R>(ext_force[n * 3], ext_force[n * 3 + 1], ext_force[n * 3 + 2]) : v3<R>(0, 0, 0);
-      substep(M, T, P, s, t, ef, R(dt));
+      substep(M, T, P, s, t, ef, R(dt), split);
     }
     Writer<R> W{root + (size_t)n * 13, rigid ? rigid + (size_t)n * 169 : nullptr, contact ? contact + (size_t)n * 39 : nullptr};
     report(M, T, P, s, W);
@@ -74,14 +74,18 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
 
 extern "C" {
 // Advance N envs by nsub substeps with constant joint torques (root: Gym layout, COM velocity).
-int t1dyn_substeps(const t1env_model* model, int N, int fp64, float* root, float* dof, const float* tau,
+// flags: bit 0 = fp64, bit 1 = the k_dyn4 split composition (compute_delta_split) instead of compute_delta.
+int t1dyn_substeps(const t1env_model* model, int N, int flags, float* root, float* dof, const float* tau,
                    const float* body_mass, const float* link_scale, const float* com_disp, const float* armature,
                    const float* friction, const float* ext_force, float dt, int nsub, const int16_t* hf, int rows,
                    int cols, float hs, float vs, float border, int mesh, float* rigid, float* contact) {
-  return fp64 ? substep_batch<double>(model, N, root, dof, tau, body_mass, link_scale, com_disp, armature, friction,
-                                      ext_force, dt, nsub, hf, rows, cols, hs, vs, border, mesh, rigid, contact)
-              : substep_batch<float>(model, N, root, dof, tau, body_mass, link_scale, com_disp, armature, friction,
-                                     ext_force, dt, nsub, hf, rows, cols, hs, vs, border, mesh, rigid, contact);
+  const bool split = (flags & 2) != 0;
+  return (flags & 1) ? substep_batch<double>(model, N, root, dof, tau, body_mass, link_scale, com_disp, armature,
+                                             friction, ext_force, dt, nsub, hf, rows, cols, hs, vs, border, mesh, rigid,
+                                             contact, split)
+                     : substep_batch<float>(model, N, root, dof, tau, body_mass, link_scale, com_disp, armature,
+                                            friction, ext_force, dt, nsub, hf, rows, cols, hs, vs, border, mesh, rigid,
+                                            contact, split);
 }
 
 // Solver accelerations in fp64 for one env with internal state (pos, quat, w, v_O, q, qd): returns

@@ -190,3 +190,54 @@ def test_joint_limit_holds_against_torque(dyn, model):
     for _ in range(300):
         s.step(tau, nsub=1)
     assert s.dof[0, 6] > -0.02, s.dof[0, 6]
+
+
+def _run_flags(dyn, m, flags, root, dof, tau, hf, mesh, nsub):
+    """t1dyn_substeps on copies of (root, dof); returns (root, dof, rigid, contact)."""
+    fp = C.POINTER(C.c_float)
+    n = root.shape[0]
+    root, dof = root.copy(), dof.copy()
+    bm = np.full(n, m.mass[0], np.float32)
+    rng = np.random.default_rng(7)
+    ls = rng.uniform(0.9, 1.1, (n, 12)).astype(np.float32)
+    cd = rng.uniform(-0.05, 0.05, (n, 3)).astype(np.float32)
+    arm = rng.uniform(0.05, 0.5, (n, 12)).astype(np.float32)
+    fr = rng.uniform(0.2, 1.3, n).astype(np.float32)
+    rigid = np.zeros((n, 13, 13), np.float32)
+    contact = np.zeros((n, 13, 3), np.float32)
+    tau = np.ascontiguousarray(tau, np.float32)
+    hf = np.ascontiguousarray(hf)
+    rc = dyn.t1dyn_substeps(C.byref(m), n, flags, root.ctypes.data_as(fp), dof.ctypes.data_as(fp),
+                            tau.ctypes.data_as(fp), bm.ctypes.data_as(fp), ls.ctypes.data_as(fp), cd.ctypes.data_as(fp),
+                            arm.ctypes.data_as(fp), fr.ctypes.data_as(fp), None, C.c_float(0.001), nsub,
+                            hf.ctypes.data_as(C.POINTER(C.c_int16)), hf.shape[0], hf.shape[1], C.c_float(0.1),
+                            C.c_float(0.005), C.c_float(1.0), mesh, rigid.ctypes.data_as(fp), contact.ctypes.data_as(fp))
+    assert rc == 0
+    return root, dof, rigid, contact
+
+
+@pytest.mark.parametrize("mesh", [0, 2])
+def test_split_composition_matches_assembled(dyn, model, mesh):
+    """k_dyn4's split composition (contact-free passes + contact fold-in, compute_delta_split) is the same
+    linear system as the assembled one (compute_delta): in fp64 the two agree to rounding, with the feet and
+    shanks in contact on a plane and on a rough height field."""
+    m, _ = model
+    n = 48
+    rng = np.random.default_rng(3)
+    root = np.zeros((n, 13), np.float32)
+    root[:, 0:2] = rng.uniform(1.5, 2.5, (n, 2))
+    root[:, 2] = rng.uniform(0.90, 0.96, n)
+    yaw = rng.uniform(-np.pi, np.pi, n)
+    root[:, 5], root[:, 6] = np.sin(yaw / 2), np.cos(yaw / 2)
+    root[:, 7:13] = rng.normal(0, 0.3, (n, 6))
+    dof = np.zeros((n, 24), np.float32)
+    dof[:, 0::2] = np.array([0, 0, -0.3, 0.6, -0.3, 0] * 2) + rng.uniform(-0.3, 0.3, (n, 12))
+    dof[:, 1::2] = rng.normal(0, 2.0, (n, 12))
+    tau = rng.normal(0, 30.0, (n, 12)).astype(np.float32)
+    hf = (rng.integers(-20, 20, (40, 40)) if mesh else np.zeros((2, 2))).astype(np.int16)
+    a = _run_flags(dyn, m, 1, root, dof, tau, hf, mesh, 20)
+    b = _run_flags(dyn, m, 3, root, dof, tau, hf, mesh, 20)
+    assert np.abs(a[3]).sum() > 0, "no contact exercised"
+    for x, y, name in zip(a, b, ["root", "dof", "rigid", "contact"]):
+        scale = np.abs(x).max() + 1.0
+        np.testing.assert_allclose(y, x, rtol=1e-6, atol=1e-6 * scale, err_msg=name)

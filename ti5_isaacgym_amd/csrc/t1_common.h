@@ -44,6 +44,29 @@ T1_HD int32_t rand_int(int32_t lo, int32_t hi, uint32_t seed, uint32_t env, uint
   uint64_t h = hash4(seed, env, ctr, slot) >> 8;
   return lo + (int32_t)((h * (uint64_t)(hi - lo)) >> 24);
 }
+// The first three mixes of hash4 depend only on (seed, env, ctr): a draw site that makes many draws for one env
+// and step takes the key once and pays one mix per draw (same values as hash4 by construction).
+struct RngKey { uint32_t h; };
+T1_HD RngKey rng_key(uint32_t seed, uint32_t env, uint32_t ctr) {
+  uint32_t h = mix32(seed ^ 0x9E3779B9u);
+  h = mix32(h ^ env);
+  return RngKey{mix32(h + ctr * 0x9E3779B1u)};
+}
+T1_HD uint32_t hash_k(RngKey k, uint32_t slot) { return mix32(k.h ^ (slot * 0x85EBCA77u)); }
+T1_HD float uniform01(RngKey k, uint32_t slot) { return (float)(hash_k(k, slot) >> 8) * (1.0f / 16777216.0f); }
+T1_HD float rand_float(float lo, float hi, RngKey k, uint32_t slot) {
+  float u = uniform01(k, slot);
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __fadd_rn(__fmul_rn(hi - lo, u), lo);
+#else
+  volatile float p = (hi - lo) * u;
+  return p + lo;
+#endif
+}
+T1_HD int32_t rand_int(int32_t lo, int32_t hi, RngKey k, uint32_t slot) {
+  uint64_t h = hash_k(k, slot) >> 8;
+  return lo + (int32_t)((h * (uint64_t)(hi - lo)) >> 24);
+}
 
 // slot table (mirror of oracle/rng.py)
 enum : uint32_t {

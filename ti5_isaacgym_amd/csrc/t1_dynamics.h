@@ -1039,11 +1039,83 @@ T1_HD void compute_delta(const DynModel& M, const Terrain& T, const EnvParams<R>
   for (int leg = 0; leg < 2; ++leg) backsub_leg(lb[leg], rb, delta + 6 + 6 * leg);
 }
 
+// The same substep composed the way k_dyn4 runs it (t1env_dynamics.hip): per leg the contact-free passes
+// (leg_forward_nc / leg_backward_nc), the shank / foot contact terms from the forward pass's poses, the fold-in
+// (leg_apply_contacts), the elimination, and the base-box contact share of the leg; summed base block, solve,
+// back-substitution.  Host builds run it to check the split algebra against compute_delta (tests/test_dynamics.py).
+template <typename R>
+T1_HD void compute_delta_split(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s,
+                               const R tau[ND], V3<R> ext_f, R dt, R delta[6 + ND]) {
+  constexpr int KS = 3, KF = 5;
+  static_assert(T1_LEG_CONTACT_MASK == ((1 << KS) | (1 << KF)), "split composition assumes shank + foot contacts");
+  BaseFrame<R> F;
+  base_frame(s, F);
+  Sym6<R> Ac;
+  R gc[6];
+  base_block(M, P.base, F, ext_f, dt, Ac, gc);
+  R rb[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) rb[i] = -gc[i];
+  LegBlock<R> lb[2];
+  const R mu = P.base.friction;
+  for (int leg = 0; leg < 2; ++leg) {
+    const R* q = s.q + 6 * leg;
+    const R* qd = s.qd + 6 * leg;
+    LegPass<R> st;
+    M3<R> Rc[2];
+    V3<R> pc[2];
+    R Vc[2][6];
+    leg_forward_nc<T1_LEG_CONTACT_MASK>(M, P.leg[leg], F, q, qd, leg, dt, st,
+                                        [&](auto kc, const M3<R>& Rk, V3<R> pk, const R* V) {
+                                          constexpr int i = decltype(kc)::value == KF ? 1 : 0;
+                                          Rc[i] = Rk;
+                                          pc[i] = pk;
+                                          for (int j = 0; j < 6; ++j) Vc[i][j] = V[j];
+                                        });
+    Sym6<R> Ab;
+    R g6[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+    sym_zero(Ab);
+    leg_backward_nc(M, P.leg[leg], q, qd, leg, dt, st, lb[leg], Ab, g6);
+    Sym6<R> Cc[2];
+    R cc[2][6];
+    for (int i = 0; i < 2; ++i) {
+      const int b = 1 + 6 * leg + (i ? KF : KS);
+      sym_zero(Cc[i]);
+      for (int j = 0; j < 6; ++j) cc[i][j] = R(0);
+      const int32_t bound = terrain_bound_raw_any(T, pc[i].x + F.abs.x, pc[i].y + F.abs.y);
+      body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pc[i].z + F.abs.z - R(M.contact_radius[b]), bound,
+                                             M.contact_start[b], Rc[i], pc[i], F.abs, Vc[i], mu, dt, Cc[i], cc[i]);
+    }
+    leg_apply_contacts<KS, KF>(Cc[0], cc[0], Cc[1], cc[1], tau + 6 * leg, dt, st, lb[leg], Ab, g6);
+    R r[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r[i] = -g6[i];
+    eliminate_leg(lb[leg], Ab, r);
+    // base-box contact share of this leg
+    int cb, ce;
+    base_contact_range(M, leg, cb, ce);
+    Sym6<R> Cb;
+    R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+    sym_zero(Cb);
+    const int32_t bound = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
+    body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - R(M.contact_radius[0]), bound, cb, F.R0,
+                                               v3<R>(0, 0, 0), F.abs, F.V0, mu, dt, Cb, gw);
+    sym_add(Ac, Ab);
+    sym_add(Ac, Cb);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rb[i] += r[i] - gw[i];
+  }
+  solve_base(Ac, rb);
+  for (int i = 0; i < 6; ++i) delta[i] = rb[i];
+  for (int leg = 0; leg < 2; ++leg) backsub_leg(lb[leg], rb, delta + 6 + 6 * leg);
+}
+
 template <typename R>
 T1_HD void substep(const DynModel& M, const Terrain& T, const EnvParams<R>& P, EnvState<R>& s, const R tau[ND],
-                   V3<R> ext_f, R dt) {
+                   V3<R> ext_f, R dt, bool split = false) {
   R delta[6 + ND];
-  compute_delta(M, T, P, s, tau, ext_f, dt, delta);
+  if (split) compute_delta_split(M, T, P, s, tau, ext_f, dt, delta);
+  else compute_delta(M, T, P, s, tau, ext_f, dt, delta);
   integrate_base(s, delta, dt);
   for (int leg = 0; leg < 2; ++leg) integrate_leg(M, leg, s.q + 6 * leg, s.qd + 6 * leg, delta + 6 + 6 * leg, dt);
 }

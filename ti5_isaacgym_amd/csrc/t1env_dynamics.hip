@@ -8,7 +8,7 @@
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py): lane 0 of every dynamics wave accumulates shader-clock
 // deltas between T1_PROF_MARK points into per-phase buckets; never part of the product build.
 #ifdef T1_PHASE_PROF
-constexpr int T1_NPROF = 16, T1_PROF_WAVES = 4;
+constexpr int T1_NPROF = 24, T1_PROF_WAVES = 4;
 __device__ unsigned long long g_t1_prof[T1_PROF_WAVES][T1_NPROF];
 __shared__ unsigned long long t1_prof_acc[T1_PROF_WAVES][T1_NPROF + 1];  // [wave][bucket], last = previous mark
 __device__ __forceinline__ void t1_prof_mark(int i) {
@@ -163,11 +163,9 @@ __device__ __forceinline__ void fused_epilogue(const DynModel& M, const t1env_co
 }
 
 // after post-physics: the terrain-level sum, the reset-row handoff and the extras finalisation
-__device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const t1env_buffers& B,
-                                                    const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
-                                                    int dyn_blocks, int lane, bool do_reset, bool active, int n) {
+__device__ __forceinline__ void epilogue_handoff(const t1env_config& C, const ShiftArgs& S, const FusedArgs& FA, int lane,
+                                                 bool do_reset, bool active) {
   const int N = C.num_envs;
-  if (C.terrain_curriculum) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
   // ---- reset rows: hand off each of the workgroup's shift units with its 8-bit reset mask
   const unsigned long long m = __ballot(do_reset && active);
   const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
@@ -181,11 +179,14 @@ __device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const
     todo &= todo - 1;
     zero_unit_resets(S, blockIdx.x * (DYN_ENVS / SHIFT_UNIT) + l, __shfl(w, l, 64), lane, DYN_ENVS);
   }
-  // ---- the last dynamics workgroup to finish finalises the step's extras.  Only atomics cross workgroups
-  // here (the ep_accum sums and this counter; agent-scope atomics are performed past the L2s), so waiting for
-  // this wave's atomics to complete orders them before the increment; the finaliser reads ep_accum through
-  // atomics as well.
-  __builtin_amdgcn_s_waitcnt(0);
+}
+// The last dynamics workgroup to finish finalises the step's extras.  Only atomics cross workgroups here (the
+// ep_accum sums and this counter; agent-scope atomics are performed past the L2s), so once every atomic of the
+// workgroup has completed (the caller's s_waitcnt, and a barrier when two waves contributed) the increment is
+// ordered after them; the finaliser reads ep_accum through atomics as well.
+__device__ __forceinline__ void epilogue_finalize(const t1env_config& C, const t1env_buffers& B,
+                                                  const t1env_step_args& A, const FusedArgs& FA, int dyn_blocks,
+                                                  int lane) {
   unsigned prev = 0;
   if (lane == 0) prev = __hip_atomic_fetch_add(FA.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   prev = __shfl(prev, 0, 64);
@@ -193,6 +194,14 @@ __device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const
     finalize_extras(B, C, (int)((A.counter + 1u) % T1ENV_EXTRAS_RING));
     if (lane == 0) __hip_atomic_store(FA.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+__device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const t1env_buffers& B,
+                                                    const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
+                                                    int dyn_blocks, int lane, bool do_reset, bool active, int n) {
+  if (C.terrain_curriculum) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
+  epilogue_handoff(C, S, FA, lane, do_reset, active);
+  __builtin_amdgcn_s_waitcnt(0);
+  epilogue_finalize(C, B, A, FA, dyn_blocks, lane);
   T1_PROF_MARK(15);
 }
 
@@ -519,8 +528,12 @@ __device__ __forceinline__ void stage_epilogue_inputs(const t1env_buffers& B, in
   }
 }
 
-// The fused step's post-physics for one k_dyn4 workgroup, run by wave 0: every input from LDS (fresh outputs,
-// staged state, the actions in the capture rows), post_a's results handed to post_b in registers.
+// The fused step's post-physics for one k_dyn4 workgroup, run by the two leg waves: every input from LDS (fresh
+// outputs, staged state, the actions in the capture rows).  Both waves run post_a's callback + termination
+// prefix; wave 0 (PART = POST_A_REWARDS) then the 24 rewards, their stores and extras sums and the reset-row
+// handoff, wave 1 (POST_A_STATE) the state stores, post_b (reset_idx, observations, newest history frame) and
+// the terrain-level sum.  After one barrier wave 0 signals completion (the extras finaliser).
+template <int PART>
 __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                                       const t1env_step_args& A, const ShiftArgs& S,
                                                       const FusedArgs& FA, int dyn_blocks, int lane,
@@ -572,8 +585,16 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
                    (uint32_t)__float_as_int(E[E_PL][lane]));
   X.gstart = E[E_GS][lane];
   BaseQ bq;
-  const bool do_reset = post_a_core(M, C, B, A, n0, X, bq);
+  const bool do_reset = post_a_core<PART>(M, C, B, A, n0, X, bq);
   T1_PROF_MARK(13);
+  if constexpr (PART == POST_A_REWARDS) {
+    epilogue_handoff(C, S, FA, lane, do_reset, active);
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's atomics (extras sums) complete
+    __syncthreads();                // E2: wave 1's terrain-level sum complete
+    epilogue_finalize(C, B, A, FA, dyn_blocks, lane);
+    T1_PROF_MARK(15);
+    return;
+  }
   if (active) {
     ObsIn O;
 #pragma unroll
@@ -599,10 +620,14 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
     Ex.cfz[0] = X.c0[2]; Ex.cfz[1] = X.c1[2];
     Ex.fric = E[E_FRIC][lane];
     Ex.mass = E[E_MASS][lane];
-    post_b_core(M, C, B, A, n, do_reset, do_reset, O, Ex);
+    post_b_core(M, C, B, A, n, do_reset, do_reset, O, Ex, /*zero_reward_state=*/false);
   }
   T1_PROF_MARK(14);
-  fused_epilogue_tail(C, B, A, S, FA, dyn_blocks, lane, do_reset, active, n);
+  // the terrain-level sum reads the levels reset_idx may just have changed
+  if (C.terrain_curriculum) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();  // E2
+  T1_PROF_MARK(15);
 }
 
 // k_dyn4's report, split between the waves: the leg wave writes its bodies' rigid states (and the root for
@@ -905,7 +930,10 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
   if constexpr (FUSED) {
     __syncthreads();  // all four waves: every output of the workgroup is in memory
     T1_PROF_MARK(12);
-    if (leg == 0) fused_epilogue_staged(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, FR, lds.cap[0], lds.cap[1]);
+    if (leg == 0)
+      fused_epilogue_staged<POST_A_REWARDS>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, FR, lds.cap[0], lds.cap[1]);
+    else
+      fused_epilogue_staged<POST_A_STATE>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, FR, lds.cap[0], lds.cap[1]);
   }
   T1_PROF_END();
 }

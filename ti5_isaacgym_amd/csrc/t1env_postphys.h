@@ -57,9 +57,10 @@ __device__ __forceinline__ bool resample_commands_r(const t1env_config& C, const
     if (el != (int64_t)gt[i]) continue;
     dirty = true;
     const int kind = C.gait_kind[i];
-    const float x = rand_float(A.cmd_ranges[0][0], A.cmd_ranges[0][1], C.seed, genv, ctr, SLOT_CMD_X);
-    const float y = rand_float(A.cmd_ranges[1][0], A.cmd_ranges[1][1], C.seed, genv, ctr, SLOT_CMD_Y);
-    const float z = rand_float(A.cmd_ranges[2][0], A.cmd_ranges[2][1], C.seed, genv, ctr, SLOT_CMD_YAW);
+    const RngKey K = rng_key(C.seed, genv, ctr);
+    const float x = rand_float(A.cmd_ranges[0][0], A.cmd_ranges[0][1], K, SLOT_CMD_X);
+    const float y = rand_float(A.cmd_ranges[1][0], A.cmd_ranges[1][1], K, SLOT_CMD_Y);
+    const float z = rand_float(A.cmd_ranges[2][0], A.cmd_ranges[2][1], K, SLOT_CMD_YAW);
     if (kind == 0) { cmd[0] = x; cmd[1] = y; cmd[2] = z; }              // walk_omnidirectional
     else if (kind == 1) { cmd[0] = 0.0f; cmd[1] = 0.0f; cmd[2] = 0.0f; }  // stand
     else if (kind == 2) { cmd[0] = x; cmd[1] = 0.0f; cmd[2] = 0.0f; }     // walk_sagittal
@@ -205,12 +206,20 @@ __device__ __forceinline__ void load_post_a_in(const t1env_buffers& B, size_t N,
 // last env).  Returns this env's reset decision; on return X holds the post-callback state (root after a push,
 // resampled commands, incremented episode / phase counters, external force and torque) and bq the base
 // quantities, which the fused epilogue hands to post_b without a reload.
+// PART (fused k_dyn4 epilogue, two waves): POST_A_ALL runs everything (split kernels, one wave); POST_A_REWARDS
+// runs the callback + termination prefix, the rewards and the reward-owned stores (rew, episode sums, feet
+// state, extras sums) and zeroes the reward state of resetting envs itself; POST_A_STATE runs the same prefix
+// and the state-owned stores (counters, base quantities, commands, push, external force, reset / time-out
+// flags) for the wave that continues with post_b.  The prefix is deterministic, so both waves agree.
+enum : int { POST_A_ALL = 0, POST_A_REWARDS = 1, POST_A_STATE = 2 };
+template <int PART = POST_A_ALL>
 __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                             const t1env_step_args& A, int n0, PostAIn& X, BaseQ& bq) {
   const bool live = n0 < C.num_envs;
   const int n = live ? n0 : C.num_envs - 1;
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   const uint32_t ctr = A.counter + 1u;  // common_step_counter += 1 happened before the callback
+  const RngKey K = rng_key(C.seed, genv, ctr);
   const size_t N = (size_t)C.num_envs;
   float (&root)[13] = X.root;
   const float (&dof)[24] = X.dof;
@@ -248,30 +257,31 @@ __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_confi
   const float* pg = bq.grav;
   const float* be = bq.euler;
   float fe[6];
-  {
+  if constexpr (PART != POST_A_STATE) {
     const float q0[4] = {f0[3], f0[4], f0[5], f0[6]}, q1[4] = {f1[3], f1[4], f1[5], f1[6]};
     euler_xyz(q0, fe);
     euler_xyz(q1, fe + 3);
   }
+  T1_PROF_MARK(16);
   // ---- _post_physics_step_callback (t1_dh_stand_env.py:179-215)
   const bool cmd_dirty = resample_commands_r(C, A, el, gt, cmd, genv, ctr);
   if (A.push_call) {  // _push_robots (t1:217-231): drawn every call (is_first_push reset is commented out)
-    root[7] = rand_float(-C.push_vel_xy, C.push_vel_xy, C.seed, genv, ctr, SLOT_PUSH_VEL + 0);
-    root[8] = rand_float(-C.push_vel_xy, C.push_vel_xy, C.seed, genv, ctr, SLOT_PUSH_VEL + 1);
-    root[10] = rand_float(-C.push_ang, C.push_ang, C.seed, genv, ctr, SLOT_PUSH_ANG + 0);
-    root[11] = rand_float(-C.push_ang, C.push_ang, C.seed, genv, ctr, SLOT_PUSH_ANG + 1);
-    root[12] = rand_float(-C.push_ang, C.push_ang, C.seed, genv, ctr, SLOT_PUSH_ANG + 2);
+    root[7] = rand_float(-C.push_vel_xy, C.push_vel_xy, K, SLOT_PUSH_VEL + 0);
+    root[8] = rand_float(-C.push_vel_xy, C.push_vel_xy, K, SLOT_PUSH_VEL + 1);
+    root[10] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 0);
+    root[11] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 1);
+    root[12] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 2);
   }
   float af[3] = {0.0f, 0.0f, 0.0f};
   bool ext_store = true;
   if (A.ext_force_call) {  // _add_ext_force (t1:233-247)
     if (A.ext_force_first) {
-      ef[0] = rand_float(-C.ext_force_max[0] / 2, C.ext_force_max[0], C.seed, genv, ctr, SLOT_EXT_FORCE + 0);
-      ef[1] = rand_float(-C.ext_force_max[1], C.ext_force_max[1], C.seed, genv, ctr, SLOT_EXT_FORCE + 1);
-      ef[2] = rand_float(-C.ext_force_max[2], C.ext_force_max[2], C.seed, genv, ctr, SLOT_EXT_FORCE + 2);
+      ef[0] = rand_float(-C.ext_force_max[0] / 2, C.ext_force_max[0], K, SLOT_EXT_FORCE + 0);
+      ef[1] = rand_float(-C.ext_force_max[1], C.ext_force_max[1], K, SLOT_EXT_FORCE + 1);
+      ef[2] = rand_float(-C.ext_force_max[2], C.ext_force_max[2], K, SLOT_EXT_FORCE + 2);
 #pragma unroll
       for (int k = 0; k < 3; ++k)
-        et[k] = rand_float(-C.ext_torque_max, C.ext_torque_max, C.seed, genv, ctr, SLOT_EXT_TORQUE + k);
+        et[k] = rand_float(-C.ext_torque_max, C.ext_torque_max, K, SLOT_EXT_TORQUE + k);
     } else {
       const float st = is_stand(C, cmd) ? 1.0f : 0.0f;
       af[0] = ef[0] * st; af[1] = ef[1] * st; af[2] = ef[2] * st;
@@ -281,6 +291,7 @@ __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_confi
     ef[0] = ef[1] = ef[2] = 0.0f;
     et[0] = et[1] = et[2] = 0.0f;
   }
+  T1_PROF_MARK(17);
   // ---- check_termination (legged_robot.py:509-517)
   const bool term = norm3(cfb[0], cfb[1], cfb[2]) > 1.0f;
   const bool tout = (float)el > C.max_episode_length;
@@ -292,208 +303,227 @@ __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_confi
   const float dtf = (float)(C.sim_dt * C.decimation);
   const bool contact0 = c0[2] > 5.0f, contact1 = c1[2] > 5.0f;
   float r[T1_NREW];
-  {  // 0 action_smoothness
-    float t1s = 0.0f, t2s = 0.0f, t3s = 0.0f;
+  if constexpr (PART != POST_A_STATE) {
+    {  // 0 action_smoothness
+      float t1s = 0.0f, t2s = 0.0f, t3s = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      const float d1 = (la[j] - a[j]) * 1.0f;
-      const float d2 = ((a[j] + lla[j]) - 2.0f * la[j]) * 1.0f;
-      t1s += d1 * d1;
-      t2s += d2 * d2;
-      t3s += fabsf(a[j] * 1.0f);
+      for (int j = 0; j < 12; ++j) {
+        const float d1 = (la[j] - a[j]) * 1.0f;
+        const float d2 = ((a[j] + lla[j]) - 2.0f * la[j]) * 1.0f;
+        t1s += d1 * d1;
+        t2s += d2 * d2;
+        t3s += fabsf(a[j] * 1.0f);
+      }
+      r[0] = (t1s + t2s) + 0.05f * t3s;
     }
-    r[0] = (t1s + t2s) + 0.05f * t3s;
-  }
-  {  // 1 base_acc (root velocity after a push, like the reference's root_states)
-    float s = 0.0f;
+    {  // 1 base_acc (root velocity after a push, like the reference's root_states)
+      float s = 0.0f;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) { const float d = lrv[i] - root[7 + i]; s += d * d; }
-    r[1] = expf(-sqrtf(s) * 3.0f);
-  }
-  {  // 2 base_height
-    const float mh = (f0[2] * ph.stance[0] + f1[2] * ph.stance[1]) / (ph.stance[0] + ph.stance[1]);
-    const float bh = root[2] - (mh - 0.05f);
-    r[2] = expf(-fabsf(bh - C.base_height_target) * 100.0f);
-  }
-  r[3] = norm3(cfb[0], cfb[1], cfb[2]) > 0.1f ? 1.0f : 0.0f;  // 3 collision (penalised_contact_indices = base)
-  {  // 4 default_joint_pos
-    float jd[12], s = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) { jd[j] = dof[2 * j] - M.default_dof_pos[j]; s += jd[j] * jd[j]; }
-    float yr = norm3(jd[0], jd[1], jd[5]) + norm3(jd[6], jd[7], jd[11]);
-    yr = clampf(yr - 0.1f, 0.0f, 50.0f);
-    r[4] = expf(-yr * 100.0f) - 0.01f * sqrtf(s);
-  }
-  {  // 5 dof_acc, 6 dof_vel
-    float s5 = 0.0f, s6 = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      const float d = (ldv[j] - dof[2 * j + 1]) / dtf;
-      s5 += d * d;
-      s6 += dof[2 * j + 1] * dof[2 * j + 1];
+      for (int i = 0; i < 6; ++i) { const float d = lrv[i] - root[7 + i]; s += d * d; }
+      r[1] = expf(-sqrtf(s) * 3.0f);
     }
-    r[5] = s5;
-    r[6] = s6;
-  }
-  {  // 7 feet_air_time (mutates feet_air_time, last_contacts)
-    float sm0 = ph.stance[0], sm1 = ph.stance[1];
-    if (norm3(cmd[0], cmd[1], cmd[2]) < 0.05f) { sm0 = 1.0f; sm1 = 1.0f; }
-    const bool filt0 = contact0 || sm0 > 0.0f || lc[0];
-    const bool filt1 = contact1 || sm1 > 0.0f || lc[1];
-    lc[0] = contact0; lc[1] = contact1;
-    const bool first0 = at[0] > 0.0f && filt0, first1 = at[1] > 0.0f && filt1;
-    const float a0 = at[0] + dtf, a1 = at[1] + dtf;
-    const float air0 = clampf(a0, 0.0f, 0.5f) * (first0 ? 1.0f : 0.0f);
-    const float air1 = clampf(a1, 0.0f, 0.5f) * (first1 ? 1.0f : 0.0f);
-    at[0] = a0 * (filt0 ? 0.0f : 1.0f);
-    at[1] = a1 * (filt1 ? 0.0f : 1.0f);
-    r[7] = air0 + air1;
-  }
-  {  // 8 feet_clearance (mutates feet_height, last_feet_z)
-    const float z0 = f0[2], z1 = f1[2];
-    const float h0 = fh[0] + (z0 - lfz[0]), h1 = fh[1] + (z1 - lfz[1]);
-    lfz[0] = z0; lfz[1] = z1;
-    const float sw0 = 1.0f - ph.stance[0], sw1 = 1.0f - ph.stance[1];
-    const float rp0 = (h0 > C.target_feet_height && h0 < C.target_feet_height_max) ? 1.0f : 0.0f;
-    const float rp1 = (h1 > C.target_feet_height && h1 < C.target_feet_height_max) ? 1.0f : 0.0f;
-    r[8] = rp0 * sw0 + rp1 * sw1;
-    fh[0] = h0 * (contact0 ? 0.0f : 1.0f);
-    fh[1] = h1 * (contact1 ? 0.0f : 1.0f);
-  }
-  // 9 feet_contact_forces
-  r[9] = clampf(norm3(c0[0], c0[1], c0[2]) - C.max_contact_force, 0.0f, 400.0f) +
-         clampf(norm3(c1[0], c1[1], c1[2]) - C.max_contact_force, 0.0f, 400.0f);
-  {  // 10 feet_contact_number
-    float sm0 = ph.stance[0], sm1 = ph.stance[1];
-    if (stand) { sm0 = 1.0f; sm1 = 1.0f; }
-    const float q0 = ((contact0 ? 1.0f : 0.0f) == sm0) ? 1.0f : -0.3f;
-    const float q1 = ((contact1 ? 1.0f : 0.0f) == sm1) ? 1.0f : -0.3f;
-    r[10] = (q0 + q1) / 2.0f;
-  }
-  {  // 11 feet_distance, 15 knee_distance
-    const float fd = norm2(f0[0] - f1[0], f0[1] - f1[1]);
-    const float kd = norm2(k0[0] - k1[0], k0[1] - k1[1]);
-    const float fmn = clampf(fd - C.foot_min_dist, -0.5f, 0.0f), fmx = clampf(fd - C.foot_max_dist, 0.0f, 0.5f);
-    const float kmn = clampf(kd - C.knee_min_dist, -0.5f, 0.0f), kmx = clampf(kd - C.knee_max_dist, 0.0f, 0.5f);
-    r[11] = (expf(-fabsf(fmn) * 100.0f) + expf(-fabsf(fmx) * 100.0f)) / 2.0f;
-    r[15] = (expf(-fabsf(kmn) * 100.0f) + expf(-fabsf(kmx) * 100.0f)) / 2.0f;
-  }
-  {  // 12 feet_rotation
-    const float rot = fe[1] * fe[1] + fe[4] * fe[4];
-    const float x = rot / 1.0f;
-    r[12] = 1.0f * expf(-(x * x));
-  }
-  {  // 13 foot_slip (rigid_state[..., 10:12] as in the reference)
-    const float s0 = sqrtf(norm2(f0[10], f0[11])), s1 = sqrtf(norm2(f1[10], f1[11]));
-    r[13] = s0 * (contact0 ? 1.0f : 0.0f) + s1 * (contact1 ? 1.0f : 0.0f);
-  }
-  {  // 14 joint_pos (ref_dof_pos from the previous compute_observations)
-    float s = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      const float tgt = stand ? M.default_dof_pos[j] : ref[j];
-      const float d = dof[2 * j] - tgt;
-      s += d * d;
+    {  // 2 base_height
+      const float mh = (f0[2] * ph.stance[0] + f1[2] * ph.stance[1]) / (ph.stance[0] + ph.stance[1]);
+      const float bh = root[2] - (mh - 0.05f);
+      r[2] = expf(-fabsf(bh - C.base_height_target) * 100.0f);
     }
-    const float nr = sqrtf(s);
-    r[14] = stand ? 1.0f : expf(-2.0f * nr) - 0.2f * clampf(nr, 0.0f, 0.5f);
-  }
-  {  // 16 low_speed
-    const float sp = fabsf(blv[0]), cm = fabsf(cmd[0]);
-    const bool low = sp < 0.5f * cm, high = sp > 1.2f * cm, ok = !(low || high);
-    const bool mis = signf(blv[0]) != signf(cmd[0]);
-    float v = 0.0f;
-    if (low) v = -1.0f;
-    if (high) v = 0.0f;
-    if (ok) v = 1.2f;
-    if (mis) v = -2.0f;
-    r[16] = v * (fabsf(cmd[0]) > 0.05f ? 1.0f : 0.0f);
-  }
-  {  // 17 orientation
-    const float qm = expf(-(fabsf(be[0]) + fabsf(be[1])) * 10.0f);
-    const float o = expf(-norm2(pg[0], pg[1]) * 20.0f);
-    r[17] = (qm + o) / 2.0f;
-  }
-  {  // 18 stand_still
-    const int idx[8] = {0, 1, 2, 3, 5, 6, 7, 8};
-    const float w[10] = {2.0f, 2.0f, 1.0f, 1.0f, 1.0f, 2.0f, 2.0f, 1.0f, 1.0f, 1.0f};
-    float s = 0.0f;
+    r[3] = norm3(cfb[0], cfb[1], cfb[2]) > 0.1f ? 1.0f : 0.0f;  // 3 collision (penalised_contact_indices = base)
+    {  // 4 default_joint_pos
+      float jd[12], s = 0.0f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float e = (dof[2 * idx[k]] - M.default_dof_pos[idx[k]]) * w[k];
-      s += e * e;
+      for (int j = 0; j < 12; ++j) { jd[j] = dof[2 * j] - M.default_dof_pos[j]; s += jd[j] * jd[j]; }
+      float yr = norm3(jd[0], jd[1], jd[5]) + norm3(jd[6], jd[7], jd[11]);
+      yr = clampf(yr - 0.1f, 0.0f, 50.0f);
+      r[4] = expf(-yr * 100.0f) - 0.01f * sqrtf(s);
     }
-    const float e8 = fe[1] * w[8], e9 = fe[4] * w[9];
-    s += e8 * e8;
-    s += e9 * e9;
-    r[18] = stand ? expf(-s) : 0.0f;
-  }
-  {  // 19 torques
-    float s = 0.0f;
+    {  // 5 dof_acc, 6 dof_vel
+      float s5 = 0.0f, s6 = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 12; ++j) s += tq[j] * tq[j];
-    r[19] = s;
+      for (int j = 0; j < 12; ++j) {
+        const float d = (ldv[j] - dof[2 * j + 1]) / dtf;
+        s5 += d * d;
+        s6 += dof[2 * j + 1] * dof[2 * j + 1];
+      }
+      r[5] = s5;
+      r[6] = s6;
+    }
+    {  // 7 feet_air_time (mutates feet_air_time, last_contacts)
+      float sm0 = ph.stance[0], sm1 = ph.stance[1];
+      if (norm3(cmd[0], cmd[1], cmd[2]) < 0.05f) { sm0 = 1.0f; sm1 = 1.0f; }
+      const bool filt0 = contact0 || sm0 > 0.0f || lc[0];
+      const bool filt1 = contact1 || sm1 > 0.0f || lc[1];
+      lc[0] = contact0; lc[1] = contact1;
+      const bool first0 = at[0] > 0.0f && filt0, first1 = at[1] > 0.0f && filt1;
+      const float a0 = at[0] + dtf, a1 = at[1] + dtf;
+      const float air0 = clampf(a0, 0.0f, 0.5f) * (first0 ? 1.0f : 0.0f);
+      const float air1 = clampf(a1, 0.0f, 0.5f) * (first1 ? 1.0f : 0.0f);
+      at[0] = a0 * (filt0 ? 0.0f : 1.0f);
+      at[1] = a1 * (filt1 ? 0.0f : 1.0f);
+      r[7] = air0 + air1;
+    }
+    {  // 8 feet_clearance (mutates feet_height, last_feet_z)
+      const float z0 = f0[2], z1 = f1[2];
+      const float h0 = fh[0] + (z0 - lfz[0]), h1 = fh[1] + (z1 - lfz[1]);
+      lfz[0] = z0; lfz[1] = z1;
+      const float sw0 = 1.0f - ph.stance[0], sw1 = 1.0f - ph.stance[1];
+      const float rp0 = (h0 > C.target_feet_height && h0 < C.target_feet_height_max) ? 1.0f : 0.0f;
+      const float rp1 = (h1 > C.target_feet_height && h1 < C.target_feet_height_max) ? 1.0f : 0.0f;
+      r[8] = rp0 * sw0 + rp1 * sw1;
+      fh[0] = h0 * (contact0 ? 0.0f : 1.0f);
+      fh[1] = h1 * (contact1 ? 0.0f : 1.0f);
+    }
+    // 9 feet_contact_forces
+    r[9] = clampf(norm3(c0[0], c0[1], c0[2]) - C.max_contact_force, 0.0f, 400.0f) +
+           clampf(norm3(c1[0], c1[1], c1[2]) - C.max_contact_force, 0.0f, 400.0f);
+    {  // 10 feet_contact_number
+      float sm0 = ph.stance[0], sm1 = ph.stance[1];
+      if (stand) { sm0 = 1.0f; sm1 = 1.0f; }
+      const float q0 = ((contact0 ? 1.0f : 0.0f) == sm0) ? 1.0f : -0.3f;
+      const float q1 = ((contact1 ? 1.0f : 0.0f) == sm1) ? 1.0f : -0.3f;
+      r[10] = (q0 + q1) / 2.0f;
+    }
+    {  // 11 feet_distance, 15 knee_distance
+      const float fd = norm2(f0[0] - f1[0], f0[1] - f1[1]);
+      const float kd = norm2(k0[0] - k1[0], k0[1] - k1[1]);
+      const float fmn = clampf(fd - C.foot_min_dist, -0.5f, 0.0f), fmx = clampf(fd - C.foot_max_dist, 0.0f, 0.5f);
+      const float kmn = clampf(kd - C.knee_min_dist, -0.5f, 0.0f), kmx = clampf(kd - C.knee_max_dist, 0.0f, 0.5f);
+      r[11] = (expf(-fabsf(fmn) * 100.0f) + expf(-fabsf(fmx) * 100.0f)) / 2.0f;
+      r[15] = (expf(-fabsf(kmn) * 100.0f) + expf(-fabsf(kmx) * 100.0f)) / 2.0f;
+    }
+    {  // 12 feet_rotation
+      const float rot = fe[1] * fe[1] + fe[4] * fe[4];
+      const float x = rot / 1.0f;
+      r[12] = 1.0f * expf(-(x * x));
+    }
+    {  // 13 foot_slip (rigid_state[..., 10:12] as in the reference)
+      const float s0 = sqrtf(norm2(f0[10], f0[11])), s1 = sqrtf(norm2(f1[10], f1[11]));
+      r[13] = s0 * (contact0 ? 1.0f : 0.0f) + s1 * (contact1 ? 1.0f : 0.0f);
+    }
+    {  // 14 joint_pos (ref_dof_pos from the previous compute_observations)
+      float s = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        const float tgt = stand ? M.default_dof_pos[j] : ref[j];
+        const float d = dof[2 * j] - tgt;
+        s += d * d;
+      }
+      const float nr = sqrtf(s);
+      r[14] = stand ? 1.0f : expf(-2.0f * nr) - 0.2f * clampf(nr, 0.0f, 0.5f);
+    }
+    {  // 16 low_speed
+      const float sp = fabsf(blv[0]), cm = fabsf(cmd[0]);
+      const bool low = sp < 0.5f * cm, high = sp > 1.2f * cm, ok = !(low || high);
+      const bool mis = signf(blv[0]) != signf(cmd[0]);
+      float v = 0.0f;
+      if (low) v = -1.0f;
+      if (high) v = 0.0f;
+      if (ok) v = 1.2f;
+      if (mis) v = -2.0f;
+      r[16] = v * (fabsf(cmd[0]) > 0.05f ? 1.0f : 0.0f);
+    }
+    {  // 17 orientation
+      const float qm = expf(-(fabsf(be[0]) + fabsf(be[1])) * 10.0f);
+      const float o = expf(-norm2(pg[0], pg[1]) * 20.0f);
+      r[17] = (qm + o) / 2.0f;
+    }
+    {  // 18 stand_still
+      const int idx[8] = {0, 1, 2, 3, 5, 6, 7, 8};
+      const float w[10] = {2.0f, 2.0f, 1.0f, 1.0f, 1.0f, 2.0f, 2.0f, 1.0f, 1.0f, 1.0f};
+      float s = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float e = (dof[2 * idx[k]] - M.default_dof_pos[idx[k]]) * w[k];
+        s += e * e;
+      }
+      const float e8 = fe[1] * w[8], e9 = fe[4] * w[9];
+      s += e8 * e8;
+      s += e9 * e9;
+      r[18] = stand ? expf(-s) : 0.0f;
+    }
+    {  // 19 torques
+      float s = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 12; ++j) s += tq[j] * tq[j];
+      r[19] = s;
+    }
+    {  // 20 track_vel_hard
+      const float le = norm2(cmd[0] - blv[0], cmd[1] - blv[1]);
+      const float ae = fabsf(cmd[2] - bav[2]);
+      r[20] = (expf(-le * 10.0f) + expf(-ae * 10.0f)) / 2.0f - 0.2f * (le + ae);
+    }
+    {  // 21 tracking_ang_vel
+      const float d = cmd[2] - bav[2];
+      r[21] = stand ? expf(-fabsf(d) * (C.tracking_sigma * 2.0f)) : expf(-(d * d) * C.tracking_sigma);
+    }
+    {  // 22 tracking_lin_vel
+      const float dx = cmd[0] - blv[0], dy = cmd[1] - blv[1];
+      r[22] = stand ? expf(-(fabsf(dx) + fabsf(dy)) * (C.tracking_sigma * 2.0f))
+                    : expf(-(dx * dx + dy * dy) * C.tracking_sigma);
+    }
+    {  // 23 vel_mismatch_exp
+      const float lm = expf(-(blv[2] * blv[2]) * 10.0f);
+      const float am = expf(-norm2(bav[0], bav[1]) * 5.0f);
+      r[23] = (lm + am) / 2.0f;
+    }
   }
-  {  // 20 track_vel_hard
-    const float le = norm2(cmd[0] - blv[0], cmd[1] - blv[1]);
-    const float ae = fabsf(cmd[2] - bav[2]);
-    r[20] = (expf(-le * 10.0f) + expf(-ae * 10.0f)) / 2.0f - 0.2f * (le + ae);
-  }
-  {  // 21 tracking_ang_vel
-    const float d = cmd[2] - bav[2];
-    r[21] = stand ? expf(-fabsf(d) * (C.tracking_sigma * 2.0f)) : expf(-(d * d) * C.tracking_sigma);
-  }
-  {  // 22 tracking_lin_vel
-    const float dx = cmd[0] - blv[0], dy = cmd[1] - blv[1];
-    r[22] = stand ? expf(-(fabsf(dx) + fabsf(dy)) * (C.tracking_sigma * 2.0f))
-                  : expf(-(dx * dx + dy * dy) * C.tracking_sigma);
-  }
-  {  // 23 vel_mismatch_exp
-    const float lm = expf(-(blv[2] * blv[2]) * 10.0f);
-    const float am = expf(-norm2(bav[0], bav[1]) * 5.0f);
-    r[23] = (lm + am) / 2.0f;
-  }
+  T1_PROF_MARK(18);
   float rew = 0.0f, contrib[T1_NREW];
+  if constexpr (PART != POST_A_STATE) {
 #pragma unroll
-  for (int k = 0; k < T1_NREW; ++k) {
-    const float v = r[k] * C.reward_scales[k];
-    rew = rew + v;
-    esum[k] = esum[k] + v;
-    contrib[k] = do_reset ? esum[k] : 0.0f;
+    for (int k = 0; k < T1_NREW; ++k) {
+      const float v = r[k] * C.reward_scales[k];
+      rew = rew + v;
+      esum[k] = esum[k] + v;
+      contrib[k] = do_reset ? esum[k] : 0.0f;
+    }
+    if (C.only_positive_rewards) rew = fmaxf(rew, 0.0f);
   }
-  if (C.only_positive_rewards) rew = fmaxf(rew, 0.0f);
+  T1_PROF_MARK(19);
   // ---- outputs
   if (live) {
-    B.episode_length_buf[n] = el;
-    B.phase_length_buf[n] = pl;
-    store_base_quantities(B, n, bq);
-    strow(B.feet_euler_xyz + n * 6, fe);
-    if (cmd_dirty) strow(B.commands + n * 4, cmd);
-    if (A.push_call) {
-      float* rs = B.root_states + n * 13;
-      rs[7] = root[7]; rs[8] = root[8]; rs[10] = root[10]; rs[11] = root[11]; rs[12] = root[12];
+    if constexpr (PART != POST_A_REWARDS) {
+      B.episode_length_buf[n] = el;
+      B.phase_length_buf[n] = pl;
+      store_base_quantities(B, n, bq);
+      if (cmd_dirty) strow(B.commands + n * 4, cmd);
+      if (A.push_call) {
+        float* rs = B.root_states + n * 13;
+        rs[7] = root[7]; rs[8] = root[8]; rs[10] = root[10]; rs[11] = root[11]; rs[12] = root[12];
+      }
+      strow(B.applied_force + n * 3, af);
+      if (ext_store) {
+        strow(B.ext_forces + n * 3, ef);
+        strow(B.ext_torques + n * 3, et);
+      }
+      B.reset_buf[n] = do_reset ? 1 : 0;
+      B.time_out_buf[n] = tout ? 1 : 0;
     }
-    strow(B.applied_force + n * 3, af);
-    if (ext_store) {
-      strow(B.ext_forces + n * 3, ef);
-      strow(B.ext_torques + n * 3, et);
-    }
-    B.reset_buf[n] = do_reset ? 1 : 0;
-    B.time_out_buf[n] = tout ? 1 : 0;
-    strow(B.last_contacts + n * 2, lc);
-    strow(B.feet_air_time + n * 2, at);
-    strow(B.feet_height + n * 2, fh);
-    strow(B.last_feet_z + n * 2, lfz);
+    if constexpr (PART != POST_A_STATE) {
+      strow(B.feet_euler_xyz + n * 6, fe);
+      strow(B.last_contacts + n * 2, lc);
+      strow(B.feet_height + n * 2, fh);
+      strow(B.last_feet_z + n * 2, lfz);
+      if constexpr (PART == POST_A_REWARDS) {  // reset_idx's zeroing of the reward state, done here (fused)
+        const float keep = do_reset ? 0.0f : 1.0f;
+        at[0] *= keep; at[1] *= keep;
 #pragma unroll
-    for (int k = 0; k < T1_NREW; ++k) B.episode_sums[k * N + n] = esum[k];
-    B.rew_buf[n] = rew;
+        for (int k = 0; k < T1_NREW; ++k) B.episode_sums[k * N + n] = do_reset ? 0.0f : esum[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < T1_NREW; ++k) B.episode_sums[k * N + n] = esum[k];
+      }
+      strow(B.feet_air_time + n * 2, at);
+      B.rew_buf[n] = rew;
+    }
   }
-  // extras["episode"] means over reset envs: partial sums (finalised by k_post_b's last block)
-  float part[T1_NREW + 1];
+  if constexpr (PART != POST_A_STATE) {
+    // extras["episode"] means over reset envs: partial sums (finalised by k_post_b's last block)
+    float part[T1_NREW + 1];
 #pragma unroll
-  for (int k = 0; k < T1_NREW; ++k) part[k] = contrib[k];
-  part[T1_NREW] = do_reset ? 1.0f : 0.0f;
-  wave_atomic_add_n(B.ep_accum, part);  // ep_accum[0..23] episode sums, [24] reset count
+    for (int k = 0; k < T1_NREW; ++k) part[k] = contrib[k];
+    part[T1_NREW] = do_reset ? 1.0f : 0.0f;
+    wave_atomic_add_n(B.ep_accum, part);  // ep_accum[0..23] episode sums, [24] reset count
+  }
   X.el = el;
   X.pl = pl;
   return do_reset;
@@ -511,9 +541,11 @@ __device__ __forceinline__ bool post_a_env(const DynModel& M, const t1env_config
 // =====================================================================================================
 // reset_idx for one env (t1_dh_stand_env.py:483-559 + legged_robot.py:604-651, 732-783, 1076-1120, 1138-1158)
 // =====================================================================================================
+// zero_reward_state = false: the caller's reward pass zeroes feet_air_time and the episode sums itself (the fused
+// epilogue, where that pass runs on another wave concurrently: post_a_core<POST_A_REWARDS>)
 __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B, const t1env_step_args& A,
-                          int n, uint32_t genv, uint32_t ctr, bool do_terrain) {
-  const uint32_t seed = C.seed;
+                          int n, uint32_t genv, uint32_t ctr, bool do_terrain, bool zero_reward_state = true) {
+  const RngKey K = rng_key(C.seed, genv, ctr);
   if (do_terrain && C.terrain_curriculum) {  // _update_terrain_curriculum
     const float* r = B.root_states + n * 13;
     const float* o = B.env_origins + n * 3;
@@ -522,7 +554,7 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
     const float* cmd = B.commands + n * 4;
     const bool down = (dist < norm2(cmd[0], cmd[1]) * (C.episode_length_s * 0.5f)) && !up;
     int lv = B.terrain_levels[n] + (up ? 1 : 0) - (down ? 1 : 0);
-    const int rnd = rand_int(0, C.num_terrain_rows, seed, genv, ctr, SLOT_TERRAIN_LEVEL_RAND);
+    const int rnd = rand_int(0, C.num_terrain_rows, K, SLOT_TERRAIN_LEVEL_RAND);
     lv = lv >= C.num_terrain_rows ? rnd : (lv < 0 ? 0 : lv);
     B.terrain_levels[n] = lv;
     const float* to = B.terrain_origins + ((size_t)lv * C.num_terrain_cols + B.terrain_types[n]) * 3;
@@ -534,7 +566,7 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
     B.dof_state[n * 24 + 2 * j] =
-        M.default_dof_pos[j] + rand_float(-C.reset_dof_range, C.reset_dof_range, seed, genv, ctr, SLOT_RESET_DOF + j);
+        M.default_dof_pos[j] + rand_float(-C.reset_dof_range, C.reset_dof_range, K, SLOT_RESET_DOF + j);
     B.dof_state[n * 24 + 2 * j + 1] = 0.0f;
   }
   // _reset_root_states
@@ -545,20 +577,20 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   for (int i = 0; i < 3; ++i) r[i] += B.env_origins[n * 3 + i];
   if (C.custom_origins) {
     const float p3 = C.reset_xy_range;
-    r[0] += rand_float(-p3, p3, seed, genv, ctr, SLOT_RESET_ROOT_XY + 0);
-    r[1] += rand_float(-p3, p3, seed, genv, ctr, SLOT_RESET_ROOT_XY + 1);
+    r[0] += rand_float(-p3, p3, K, SLOT_RESET_ROOT_XY + 0);
+    r[1] += rand_float(-p3, p3, K, SLOT_RESET_ROOT_XY + 1);
   }
   // randomize_dof_props (torque_multi is redrawn every substep anyway; its reset draw has no effect)
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
     B.motor_offsets[n * 12 + j] =
-        rand_float(C.motor_offset_range[0], C.motor_offset_range[1], seed, genv, ctr, SLOT_DR_OFFSET + j);
-    B.kp[n * 12 + j] = rand_float(C.kp_mult_range[0], C.kp_mult_range[1], seed, genv, ctr, SLOT_DR_KP + j) * M.p_gains[j];
-    B.kd[n * 12 + j] = rand_float(C.kd_mult_range[0], C.kd_mult_range[1], seed, genv, ctr, SLOT_DR_KD + j) * M.d_gains[j];
-    B.coulomb[n * 12 + j] = rand_float(C.coulomb_range[0], C.coulomb_range[1], seed, genv, ctr, SLOT_DR_COULOMB + j);
-    B.viscous[n * 12 + j] = rand_float(C.viscous_range[0], C.viscous_range[1], seed, genv, ctr, SLOT_DR_VISCOUS + j);
+        rand_float(C.motor_offset_range[0], C.motor_offset_range[1], K, SLOT_DR_OFFSET + j);
+    B.kp[n * 12 + j] = rand_float(C.kp_mult_range[0], C.kp_mult_range[1], K, SLOT_DR_KP + j) * M.p_gains[j];
+    B.kd[n * 12 + j] = rand_float(C.kd_mult_range[0], C.kd_mult_range[1], K, SLOT_DR_KD + j) * M.d_gains[j];
+    B.coulomb[n * 12 + j] = rand_float(C.coulomb_range[0], C.coulomb_range[1], K, SLOT_DR_COULOMB + j);
+    B.viscous[n * 12 + j] = rand_float(C.viscous_range[0], C.viscous_range[1], K, SLOT_DR_VISCOUS + j);
     B.armature[n * 12 + j] =
-        rand_float(C.armature_range[j][0], C.armature_range[j][1], seed, genv, ctr, SLOT_DR_ARMATURE + j);
+        rand_float(C.armature_range[j][0], C.armature_range[j][1], K, SLOT_DR_ARMATURE + j);
   }
   // randomize_lag_props: zero the lag rings, redraw lag lengths
 #pragma unroll
@@ -567,9 +599,9 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   for (int i = 0; i < 96; ++i) B.dof_hist[(size_t)n * 96 + i] = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) B.imu_hist[(size_t)n * 16 + i] = 0.0f;
-  B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_ACTION);
-  B.dof_lag_timestep[n] = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_DOF);
-  B.imu_lag_timestep[n] = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, seed, genv, ctr, SLOT_LAG_IMU);
+  B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, K, SLOT_LAG_ACTION);
+  B.dof_lag_timestep[n] = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, K, SLOT_LAG_DOF);
+  B.imu_lag_timestep[n] = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, K, SLOT_LAG_IMU);
   // buffers
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
@@ -580,17 +612,19 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   }
 #pragma unroll
   for (int i = 0; i < 6; ++i) B.last_root_vel[n * 6 + i] = 0.0f;
-  B.feet_air_time[n * 2 + 0] = 0.0f;
-  B.feet_air_time[n * 2 + 1] = 0.0f;
+  if (zero_reward_state) {
+    B.feet_air_time[n * 2 + 0] = 0.0f;
+    B.feet_air_time[n * 2 + 1] = 0.0f;
+  }
   B.episode_length_buf[n] = 0;
   B.phase_length_buf[n] = 0;
   B.reset_buf[n] = 1;
-  B.gait_start[n] = (float)rand_int(0, 2, seed, genv, ctr, SLOT_GAIT_START) * 0.5f;
+  B.gait_start[n] = (float)rand_int(0, 2, K, SLOT_GAIT_START) * 0.5f;
   // generate_gait_time (t1:109-124)
   float g[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
-    g[i] = rand_float(C.gait_time_range[i][0], C.gait_time_range[i][1], seed, genv, ctr, SLOT_GAIT_TIME + i);
+    g[i] = rand_float(C.gait_time_range[i][0], C.gait_time_range[i][1], K, SLOT_GAIT_TIME + i);
   const float s = (g[0] + g[1]) + g[2];
   const float f = C.max_episode_length / s;
   const float s0 = g[0] * f, s1 = g[1] * f;
@@ -598,8 +632,9 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   B.gait_time[n * 3 + 1] = (int32_t)(0.0f + s0);
   B.gait_time[n * 3 + 2] = (int32_t)((0.0f + s0) + s1);
   // episode sums are zeroed after the extras reduction; obs/critic history rows zeroed in the stack pass
+  if (zero_reward_state)
 #pragma unroll
-  for (int k = 0; k < T1_NREW; ++k) B.episode_sums[(size_t)k * C.num_envs + n] = 0.0f;
+    for (int k = 0; k < T1_NREW; ++k) B.episode_sums[(size_t)k * C.num_envs + n] = 0.0f;
   // base quantities of the reset env from the freshly written root state (t1:548-552)
   base_quantities(B, n);
 }
@@ -643,7 +678,7 @@ struct ObsExtra {
 };
 __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                             const t1env_step_args& A, int n, bool do_reset, bool any_reset, ObsIn& X,
-                                            const ObsExtra& E);
+                                            const ObsExtra& E, bool zero_reward_state = true);
 __device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                            const t1env_step_args& A, int n, bool do_reset, bool any_reset) {
   ObsIn X;
@@ -661,17 +696,19 @@ __device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config
 // X: the inputs as they stand after post_a (reloaded here after a reset)
 __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                             const t1env_step_args& A, int n, bool do_reset, bool any_reset, ObsIn& X,
-                                            const ObsExtra& E) {
+                                            const ObsExtra& E, bool zero_reward_state) {
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   const uint32_t ctr = A.counter + 1u;
+  const RngKey K = rng_key(C.seed, genv, ctr);
   const float (&ef)[2] = E.ef;
   const float (&et)[3] = E.et;
   const float (&cfz)[2] = E.cfz;
   const float fric = E.fric, mass = E.mass;
   if (do_reset) {
-    reset_env(M, C, B, A, n, genv, ctr, true);
+    reset_env(M, C, B, A, n, genv, ctr, true, zero_reward_state);
     load_obs_in(B, n, X);
   }
+  T1_PROF_MARK(20);
   if (any_reset && resample_commands_r(C, A, X.el, X.gt, X.cmd, genv, ctr)) strow(B.commands + n * 4, X.cmd);
   // lagged sensor samples (need the lag lengths loaded above)
   const float* ldp = B.dof_hist + ((size_t)n * 4 + ((A.counter - (uint32_t)(X.dl / 10)) & 3u)) * 24;
@@ -709,6 +746,7 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
     for (int j = 0; j < 12; ++j) ref[j] = ref[j] + M.default_dof_pos[j];
   }
   const Phase ph = gait_phase(phase);
+  T1_PROF_MARK(21);
   float* priv = B.priv_buf[A.obs_slot] + (size_t)n * (T1_NPRIV * T1_CHIST) + T1_NPRIV * (T1_CHIST - 1);
   float* obs = B.obs_buf[A.obs_slot] + (size_t)n * (T1_NOBS * T1_HIST) + T1_NOBS * (T1_HIST - 1);
   const float clipo = C.clip_obs;
@@ -745,6 +783,7 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
 #pragma unroll
     for (int i = 0; i < T1_NPRIV; ++i) priv[i] = clampf(v[i], -clipo, clipo);
   }
+  T1_PROF_MARK(22);
   {  // actor frame (47) from the lagged sensor rings + noise
     float v[T1_NOBS];
     int k = 0;
@@ -762,11 +801,12 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
     for (int i = 0; i < 3; ++i) v[k++] = li[3 + i] * C.quat_obs_scale;
 #pragma unroll
     for (int i = 0; i < T1_NOBS; ++i) {
-      const float u = uniform01(C.seed, genv, ctr, SLOT_OBS_NOISE + i);
+      const float u = uniform01(K, SLOT_OBS_NOISE + i);
       const float nz = ((2.0f * u - 1.0f) * C.noise_vec[i]) * C.noise_level;
       obs[i] = clampf(v[i] + nz, -clipo, clipo);
     }
   }
+  T1_PROF_MARK(23);
   strow(B.ref_dof_pos + n * 12, ref);
   // last_* (legged_robot.py:496-502)
   strow(B.last_last_actions + n * 12, X.la);

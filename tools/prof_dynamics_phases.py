@@ -25,6 +25,13 @@ BUCKETS4 = ["pd torques", "forward pass (+ pose publish)", "backward pass (no co
             "base block", "substep loop / captures", "S1 wait (poses)", "base solve + backsub + integrate",
             "prologue loads", "S2 wait / report", "S3 wait / epilogue barrier", "post_a (fused)", "post_b (fused)",
             "handoff + zeroing + finalize"]
+# finer marks inside the post-physics epilogue (t1env_postphys.h)
+SUB = ["post_a: base quantities + feet euler", "post_a: callback (commands, push, ext force)",
+       "post_a: termination + 24 rewards", "post_a: reward sum + episode sums",
+       "post_b: reset_env (resetting lanes) + reload", "post_b: lag reads, phase, ref state",
+       "post_b: privileged frame", "post_b: actor frame + noise"]
+BUCKETS += SUB
+BUCKETS4 += SUB
 NB = len(BUCKETS)
 NW = 4
 
