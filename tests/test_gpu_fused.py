@@ -17,9 +17,13 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-EXACT = ["reset_buf", "time_out_buf", "episode_length_buf", "last_contacts", "gait_time"]
+EXACT = ["reset_buf", "time_out_buf", "episode_length_buf", "phase_length_buf", "last_contacts", "gait_time",
+         "terrain_levels"]
+# the fused epilogue splits post-physics over two waves (rewards | state + observations): the reward-owned
+# buffers (episode sums, feet state) and the state-owned ones are both compared
 CLOSE = ["obs_buf", "privileged_obs_buf", "rew_buf", "root_states", "dof_state", "rigid_state", "contact_forces",
-         "commands", "last_actions", "feet_air_time", "base_lin_vel", "ref_dof_pos"]
+         "commands", "last_actions", "feet_air_time", "feet_height", "last_feet_z", "feet_euler_xyz",
+         "_episode_sums", "base_lin_vel", "ref_dof_pos", "env_origins"]
 
 
 def _sync(dst, src):

@@ -122,9 +122,10 @@ __device__ __forceinline__ void pd_stage(const t1env_buffers& B, int n, int j0, 
     for (int k = 0; k < NLEG; ++k) P.act[s][k][lane] = B.act_hist[((size_t)n * 4 + s) * 12 + j0 + k];
 }
 // pd_torques<NLEG> with the constants from a PdStage (same arithmetic, same order)
+// K = rng_key(C.seed, genv, ctr), taken once per env step by the caller (one mix per torque multiplier draw)
 template <int LANES>
 __device__ __forceinline__ void pd_torques_staged(const DynModel& M, const t1env_config& C, const PdStage<LANES>& P,
-                                                  int lane, uint32_t genv, uint32_t ctr, int sub, int lag, int j0,
+                                                  int lane, RngKey K, uint32_t ctr, int sub, int lag, int j0,
                                                   const float q[NLEG], const float qd[NLEG], float tau[NLEG]) {
   const int d = lag > sub ? (lag - sub + 9) / 10 : 0;
   const int slot = (int)((ctr - (uint32_t)d) & 3u);
@@ -136,8 +137,7 @@ __device__ __forceinline__ void pd_torques_staged(const DynModel& M, const t1env
     t = t - kd * qd[k];
     t = t - P.visc[k][lane] * qd[k];
     t = t - P.coul[k][lane] * signf(qd[k]);
-    const float tm = rand_float(C.torque_mult_range[0], C.torque_mult_range[1], C.seed, genv, ctr,
-                                SLOT_TORQUE_MULT + sub * 12 + j);
+    const float tm = rand_float(C.torque_mult_range[0], C.torque_mult_range[1], K, SLOT_TORQUE_MULT + sub * 12 + j);
     t = t * tm;
     const float lim = M.torque_limit[j];
     tau[k] = fminf(fmaxf(t, -lim), lim);

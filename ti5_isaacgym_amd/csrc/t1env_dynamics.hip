@@ -11,10 +11,19 @@
 constexpr int T1_NPROF = 24, T1_PROF_WAVES = 4;
 __device__ unsigned long long g_t1_prof[T1_PROF_WAVES][T1_NPROF];
 __shared__ unsigned long long t1_prof_acc[T1_PROF_WAVES][T1_NPROF + 1];  // [wave][bucket], last = previous mark
+// a stamp is one asm statement (s_memtime + its lgkmcnt wait) fenced by scheduling barriers, so the compiler
+// cannot move work across it (cdna_hip_programming.md, In-kernel stamps); profiling build only
+__device__ __forceinline__ unsigned long long t1_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 __device__ __forceinline__ void t1_prof_mark(int i) {
   const int w = threadIdx.x / 64;
+  const unsigned long long now = t1_stamp();
   if ((threadIdx.x & 63) == 0) {
-    const unsigned long long now = clock64();
     t1_prof_acc[w][i] += now - t1_prof_acc[w][T1_NPROF];
     t1_prof_acc[w][T1_NPROF] = now;
   }
@@ -23,7 +32,7 @@ __device__ __forceinline__ void t1_prof_begin() {
   const int w = threadIdx.x / 64;
   if ((threadIdx.x & 63) == 0) {
     for (int i = 0; i < T1_NPROF; ++i) t1_prof_acc[w][i] = 0;
-    t1_prof_acc[w][T1_NPROF] = clock64();
+    t1_prof_acc[w][T1_NPROF] = t1_stamp();
   }
 }
 __device__ __forceinline__ void t1_prof_end() {
@@ -423,9 +432,12 @@ __device__ __forceinline__ void lds_get_sym(const float (*src)[DYN_ENVS], int la
   for (int i = 0; i < 6; ++i) g[i] = src[21 + i][lane];
 }
 
-// contact terms (Sym6 + wrench) of a leg contact body from its published pose
+// contact terms (Sym6 + wrench) of a leg contact body from its published pose; `bound` = its terrain height
+// bound sample (terrain_bound_raw_any, loaded by the caller ahead of time) or T1_NO_BOUND
+constexpr int32_t T1_NO_BOUND = 0x7fffffff;  // bound_height() = +inf: the body is always evaluated
 __device__ __forceinline__ void body_terms(const DynModel& M, const Terrain& T, const float (*P)[DYN_ENVS], int lane,
-                                           int b, V3<float> abs, float mu, float dt, float (*dst)[DYN_ENVS]) {
+                                           int b, V3<float> abs, float mu, float dt, float (*dst)[DYN_ENVS],
+                                           int32_t bound) {
   Sym6<float> Cc;
   float cc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   sym_zero(Cc);
@@ -434,7 +446,6 @@ __device__ __forceinline__ void body_terms(const DynModel& M, const Terrain& T, 
   float Vb[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) Vb[i] = P[12 + i][lane];
-  const int32_t bound = terrain_bound_raw_any(T, pb.x + abs.x, pb.y + abs.y);
   body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pb.z + abs.z - M.contact_radius[b], bound, M.contact_start[b], Rb, pb,
                                          abs, Vb, mu, dt, Cc, cc);
   lds_put_sym(dst, lane, Cc, cc);
@@ -759,8 +770,14 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
       __syncthreads();  // S1: poses of this substep published
       T1_PROF_MARK(8);
       const V3<float> abs = v3<float>(P[9][lane], P[10][lane], P[11][lane]);
-      body_terms(M, T, P + POSE_F, lane, 1 + 6 * leg + K_SHANK, abs, mu, dt, lds.ct[leg]);
-      body_terms(M, T, P + POSE_F + POSE_B, lane, 1 + 6 * leg + K_FOOT, abs, mu, dt, lds.ct[leg] + XCH);
+      // the height bounds of the shank and of the base box are loaded first, so their latency hides under the
+      // foot's contact terms; the foot goes without a bound test (some foot among a wave's 64 envs is always
+      // near the ground, so the test would never skip it and would only add a dependent memory round trip)
+      const float (*Psh)[DYN_ENVS] = P + POSE_F;
+      const int32_t bound_sh = terrain_bound_raw_any(T, Psh[9][lane] + abs.x, Psh[10][lane] + abs.y);
+      const int32_t bound_base = terrain_bound_raw_any(T, abs.x, abs.y);
+      body_terms(M, T, P + POSE_F + POSE_B, lane, 1 + 6 * leg + K_FOOT, abs, mu, dt, lds.ct[leg] + XCH, T1_NO_BOUND);
+      body_terms(M, T, Psh, lane, 1 + 6 * leg + K_SHANK, abs, mu, dt, lds.ct[leg], bound_sh);
       T1_PROF_MARK(3);
       __syncthreads();  // S2: contact terms published
       T1_PROF_MARK(11);
@@ -773,8 +790,7 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
         Sym6<float> Cb;
         float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         sym_zero(Cb);
-        const int32_t bound = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
-        body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - M.contact_radius[0], bound, cb, F.R0,
+        body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - M.contact_radius[0], bound_base, cb, F.R0,
                                                    v3<float>(0, 0, 0), F.abs, F.V0, mu, dt, Cb, gw);
 #pragma unroll
         for (int i = 0; i < 6; ++i) gw[i] = -gw[i];
@@ -798,6 +814,7 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
   const int j0 = 6 * leg;
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   const uint32_t ctr = A.counter;
+  const RngKey K = rng_key(C.seed, genv, ctr);
   BaseParams<float> PB;
   LegParams<float> PL;
   BaseState<float> sb;
@@ -834,7 +851,7 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
     T1_PROF_MARK(1);
     __syncthreads();  // S1
     T1_PROF_MARK(8);
-    pd_torques_staged(M, C, PD, lane, genv, ctr, sub, L.lag, j0, q, qd, tau);
+    pd_torques_staged(M, C, PD, lane, K, ctr, sub, L.lag, j0, q, qd, tau);
     T1_PROF_MARK(0);
     LegBlock<float> lb;
     Sym6<float> Ab;

@@ -32,6 +32,9 @@ SUB = ["post_a: base quantities + feet euler", "post_a: callback (commands, push
        "post_b: privileged frame", "post_b: actor frame + noise"]
 BUCKETS += SUB
 BUCKETS4 += SUB
+# the helper waves reuse ids 16-18 inside body_contact_np (they never run the epilogue)
+HELPER_SUB = {16: "contacts: transforms + height queries (issue)", 17: "contacts: height-load latency",
+              18: "contacts: contact math (points in contact)"}
 NB = len(BUCKETS)
 NW = 4
 
@@ -81,7 +84,8 @@ def main():
         cyc = [buf[w * NB + i] / (waves * a.steps) for i in range(NB)]
         tot = sum(cyc)
         print(f"wave {w} ({roles[w]}): {tot:.0f} cycles/launch")
-        for name, c in sorted(zip(names, cyc), key=lambda x: -x[1]):
+        wn = [HELPER_SUB.get(i, nm) if (four and w >= 2) else nm for i, nm in enumerate(names)]
+        for name, c in sorted(zip(wn, cyc), key=lambda x: -x[1]):
             if c > 0:
                 print(f"   {name:34s} {c:10.0f} cyc  {100 * c / tot:5.1f}%  ~{kern_us * c / tot:6.1f} us")
 
