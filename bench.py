@@ -144,10 +144,17 @@ def main():
     value = N * world * steps / elapsed
     # live per-kernel HIP-event timing on the sampled steps
     fused = kt["k_post_a"]["launches"] == 0  # no split step inside the timed region: every launch is the whole step
+    # at large N the history shift runs as its own launch ahead of the fused kernel (t1_shift_prelaunch)
+    pre_shift = kt["k_shift"]["launches"] > 0
     per_kernel = {}
-    for k in KERNELS:
+    for k in KERNELS + (["k_shift"] if pre_shift else []):
         ms = kt[k]["ms"] / max(1, kt[k]["launches"])
-        alg = (B_ALG if (fused and k == "k_dynamics") else KERNEL_BYTES[k]) * N
+        if k == "k_shift":
+            alg = SHIFT_BYTES * N
+        elif fused and k == "k_dynamics":
+            alg = (B_ALG - (SHIFT_BYTES if pre_shift else 0)) * N
+        else:
+            alg = KERNEL_BYTES[k] * N
         name = FUSED_KERNEL if (fused and k == "k_dynamics") else k
         per_kernel[name] = {"avg_ms": round(ms, 5), "timed_launches": kt[k]["launches"], "alg_bytes_per_launch": alg,
                             "alg_GBs": round(alg / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}

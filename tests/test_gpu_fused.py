@@ -49,7 +49,10 @@ def dyn_waves(request, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("n,mesh", [(8192, "trimesh"), (777, "plane")], ids=["8192_trimesh", "ragged777_plane"])
+# 16384 envs: k_dyn4 fills every CU, so the history shift runs as its own launch ahead of the fused kernel and
+# the epilogue zeroes the reset rows directly (t1_shift_prelaunch)
+@pytest.mark.parametrize("n,mesh", [(8192, "trimesh"), (777, "plane"), (16384, "plane")],
+                         ids=["8192_trimesh", "ragged777_plane", "16384_plane_prelaunched_shift"])
 def test_fused_step_equals_split_sequence(n, mesh, dyn_waves):
     fused, split = _env(n, mesh, True), _env(n, mesh, False)
     g = torch.Generator(device="cuda:0").manual_seed(1)

@@ -1,17 +1,15 @@
-// t1env.hip -- MI355X (gfx950) kernels + C ABI for the T1 humanoid LeggedRobot.step() hot path.
+// t1env.hip -- MI355X (gfx950) C ABI for the T1 humanoid LeggedRobot.step() hot path, plus the small kernels
+// around the step (creation-time DR, reset_all, the split post-physics kernels, the stand-alone history shift).
 //
-// Per env step (t1env_step), four launches on the caller's stream, no host sync:
-//   k_physics  : actions -> 10 x (PD torque with actuator lag + DR, dynamics substep, sensor-lag capture);
-//                writes root/dof/rigid/contact/torques.  One env per lane, state in registers.
+// Per env step (t1env_step), normally ONE launch on the caller's stream and no host sync: k_dyn4 in
+// t1env_dynamics.hip runs the 10 substeps, the post-physics epilogue and, in extra workgroups on the CUs the
+// dynamics leave idle, the 65/2-frame history shift.  Split sequence (command-curriculum steps, golden parity):
+//   k_dyn4<FUSED=false> (+ shift workgroups) -> k_post_a -> k_post_b
 //   k_post_a   : base kinematics, command/ext-force callback, termination, 24 rewards (alphabetical),
 //                episode sums, per-step extras reduction (legged_robot.py:458-489, 509-517, 654-680)
-//   k_post_b   : masked reset_idx, compute_observations -> newest obs/priv frame, last_* bookkeeping
-//                (legged_robot.py:490-502, t1_dh_stand_env.py:368-559)
-//   shift      : 65 older frames of the 66-frame (and 3-frame critic) history shifted into the ping-pong
-//                output buffer, lane per 4 floats, fully coalesced (the HBM-dominant part: ~26 KB per env
-//                per step).  It does not depend on this step's physics, so it runs as extra workgroups of the
-//                k_dynamics launch on the CUs the dynamics leaves idle (t1env_dynamics.hip); k_post_b, next
-//                on the stream, writes the newest frame and zeroes the history rows of reset envs.
+//   k_post_b   : masked reset_idx, compute_observations -> newest obs/priv frame, last_* bookkeeping, reset-row
+//                zeroing, extras finalisation (legged_robot.py:490-502, t1_dh_stand_env.py:368-559)
+// At large N (no idle CUs) the shift runs as its own launch (k_shift) ahead of the dynamics.
 // See include/t1env.h for the ABI and DESIGN.md for layouts and rooflines.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -23,7 +21,6 @@
 #include "t1_model_conv.h"
 #include "t1env_device.h"
 #include "t1env_internal.h"
-#include "t1env_postphys.h"
 #include "t1env_postphys.h"
 
 using namespace t1;
@@ -422,13 +419,17 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
   if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
   const int N = e->cfg.num_envs;
   e->step_timer = t_begin(e, 5, s);
+  // large N: the shift as its own launch ahead of the dynamics (k_post_b zeroes the reset rows)
+  const bool pre = !inj && t1_shift_prelaunch(N, e->dyn);
+  if (pre)
+    if (int rc = launch_shift(e, a, s)) return rc;
   int t = t_begin(e, 0, s);
   if (inj)
     hipLaunchKernelGGL(k_physics_injected, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
                        actions, *a, *inj);
   else
     HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, N,
-                                           shift_args(e, a), e->dyn, nullptr, s));
+                                           shift_args(e, a), e->dyn, nullptr, s, pre));
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
   if (inj) {
@@ -478,10 +479,15 @@ int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* strea
 static int launch_fused(t1env* e, const float* actions, const t1env_step_args* a, hipStream_t s) {
   if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
   e->step_timer = t_begin(e, 5, s);
+  // large N: no idle CUs for shift workgroups -- the shift runs as its own launch first, the epilogue then
+  // zeroes the reset rows without the handoff
+  const bool pre = t1_shift_prelaunch(e->cfg.num_envs, e->dyn);
+  if (pre)
+    if (int rc = launch_shift(e, a, s)) return rc;
   const int t = t_begin(e, 0, s);
-  const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch};
+  const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch, pre ? 1 : 0};
   HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, e->cfg.num_envs,
-                                         shift_args(e, a), e->dyn, &FA, s));
+                                         shift_args(e, a), e->dyn, &FA, s, pre));
   t_end(e, t, s);
   t_end(e, e->step_timer, s);
   e->step_timer = -1;

@@ -175,8 +175,17 @@ __device__ __forceinline__ void fused_epilogue(const DynModel& M, const t1env_co
 __device__ __forceinline__ void epilogue_handoff(const t1env_config& C, const ShiftArgs& S, const FusedArgs& FA, int lane,
                                                  bool do_reset, bool active) {
   const int N = C.num_envs;
-  // ---- reset rows: hand off each of the workgroup's shift units with its 8-bit reset mask
   const unsigned long long m = __ballot(do_reset && active);
+  if (FA.shift_done) {  // the shift completed before this launch (stream order): zero the reset rows now
+    unsigned long long todo = m;
+    while (todo) {
+      const int l = __ffsll(todo) - 1;
+      todo &= todo - 1;
+      zero_history_row(S, (int64_t)blockIdx.x * DYN_ENVS + l, lane, DYN_ENVS);
+    }
+    return;
+  }
+  // ---- reset rows: hand off each of the workgroup's shift units with its 8-bit reset mask
   const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
   const int u = blockIdx.x * (DYN_ENVS / SHIFT_UNIT) + lane;
   uint32_t w = 0;
@@ -957,16 +966,25 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
 
 int t1_dyn_waves_default() { return 4; }
 
+constexpr int MIN_SHIFT_BLOCKS = 64;
+bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg) {
+  if (cfg.shift_blocks > 0) return false;  // explicit shift-workgroup count (tuning)
+  const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
+  const int per_cu = cfg.waves == 4 ? 1 : 2;
+  return per_cu * cfg.cus - dyn_blocks < MIN_SHIFT_BLOCKS;
+}
+
 int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
                        const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
-                       const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s) {
+                       const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s, bool shift_prelaunched) {
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
   // history-shift workgroups: the workgroup slots the dynamics leave free (a wave of either kernel holds a
-  // whole SIMD's registers: 2 workgroups/CU for k_dynamics, 1 for k_dyn4), at least MIN_SHIFT_BLOCKS
-  constexpr int MIN_SHIFT_BLOCKS = 64;
+  // whole SIMD's registers: 2 workgroups/CU for k_dynamics, 1 for k_dyn4), at least MIN_SHIFT_BLOCKS; none
+  // when the caller ran the shift as its own launch (t1_shift_prelaunch)
   const int per_cu = cfg.waves == 4 ? 1 : 2;
   int shift_blocks = cfg.shift_blocks > 0 ? cfg.shift_blocks : per_cu * cfg.cus - dyn_blocks;
   if (shift_blocks < MIN_SHIFT_BLOCKS) shift_blocks = MIN_SHIFT_BLOCKS;
+  if (shift_prelaunched) shift_blocks = 0;
   const FusedArgs FA = fused ? *fused : FusedArgs{};
   const dim3 grid(dyn_blocks + shift_blocks);
 #define T1_LAUNCH(KERNEL, BS, HF, FU) \

@@ -12,6 +12,8 @@ struct FusedArgs {
   unsigned* done;                  // dynamics-workgroup completion counter (the last one finalises the extras)
   uint32_t* unit_state;            // per shift unit: epoch-tagged handoff word (reset mask inside)
   uint32_t epoch;                  // launch number (unique per fused step)
+  int32_t shift_done;              // 1: the history shift ran as its own launch before this one (large N):
+                                   //    the epilogue zeroes its reset rows directly, no handoff
 };
 
 // launch shape of the dynamics kernel
@@ -23,7 +25,13 @@ struct DynLaunch {
 int t1_dyn_waves_default();
 
 // dynamics launch (t1env_dynamics.hip) plus history-shift workgroups running the shift S; fused != nullptr:
-// the whole step (post-physics in the epilogue).  Returns a hipError_t.
+// the whole step (post-physics in the epilogue).  shift_prelaunched: the caller already enqueued the shift as
+// its own launch (no shift workgroups).  Returns a hipError_t.
 int t1_launch_dynamics(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B,
                        const t1::Terrain& T, const float* actions, const t1env_step_args& A, int num_envs,
-                       const t1::ShiftArgs& S, const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s);
+                       const t1::ShiftArgs& S, const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s,
+                       bool shift_prelaunched = false);
+// Whether the history shift should run as its own launch ahead of the dynamics: the dynamics workgroups (one
+// per CU for k_dyn4: 148 KB of LDS) leave fewer than MIN_SHIFT_BLOCKS CUs idle, and shift workgroups of the
+// dynamics launch would each hold a whole CU's LDS for a small slice of the 26 KB/env stream.
+bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg);
