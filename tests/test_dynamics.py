@@ -241,3 +241,26 @@ def test_split_composition_matches_assembled(dyn, model, mesh):
     for x, y, name in zip(a, b, ["root", "dof", "rigid", "contact"]):
         scale = np.abs(x).max() + 1.0
         np.testing.assert_allclose(y, x, rtol=1e-6, atol=1e-6 * scale, err_msg=name)
+
+
+def test_host_dynamics_under_sanitizers(model, tmp_path):
+    """The dynamics header's host build (assembled and split compositions, fp32 and fp64, contact on a rough
+    height field) runs clean under AddressSanitizer + UndefinedBehaviorSanitizer (sanitizers
+    on host code)."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    m, _ = model
+    blob = tmp_path / "model.bin"
+    blob.write_bytes(bytes(m))
+    exe = tmp_path / "asan_dyn"
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fopenmp", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-o", str(exe),
+                    os.path.join(here, "asan_main.cpp")], check=True)
+    # verify_asan_link_order=0: the process environment may preload other libraries ahead of the ASan runtime
+    env = dict(os.environ, OMP_NUM_THREADS="2", ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0")
+    r = subprocess.run([str(exe), str(blob)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
