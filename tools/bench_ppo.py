@@ -31,5 +31,31 @@ r.learn(a.iters)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 steps = a.iters * cfg["runner"]["num_steps_per_env"] * a.num_envs
+
+# phase breakdown: rollout (policy inference + env.step + storage) vs the PPO update
+alg, T = r.alg, r.num_steps_per_env
+obs, cobs = env.get_observations(), env.get_privileged_observations()
+t_roll = t_env = t_upd = 0.0
+for _ in range(a.iters):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.inference_mode():
+        for i in range(T):
+            act = alg.act(obs, cobs)
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            obs, cobs, rew, dones, infos = env.step(act)
+            torch.cuda.synchronize()
+            t_env += time.perf_counter() - te
+            alg.process_env_step(rew, dones, infos)
+        alg.compute_returns(cobs)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    alg.update()
+    torch.cuda.synchronize()
+    t_upd += time.perf_counter() - t1
+    t_roll += t1 - t0
 print(json.dumps({"num_envs": a.num_envs, "iters": a.iters, "env_steps_per_s_incl_update": round(steps / dt, 1),
-                  "s_per_iter": round(dt / a.iters, 4)}))
+                  "s_per_iter": round(dt / a.iters, 4),
+                  "phases_s_per_iter": {"rollout": round(t_roll / a.iters, 4), "env_step_in_rollout": round(t_env / a.iters, 4),
+                                        "update": round(t_upd / a.iters, 4)}}))
