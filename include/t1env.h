@@ -213,6 +213,19 @@ int t1env_step_physics_and_rewards(t1env* env, const float* actions, const t1env
 int t1env_step_reset_and_observe(t1env* env, const t1env_step_args* args, void* stream);
 int t1env_step_injected(t1env* env, const float* actions, const t1env_step_args* args, const t1env_injected* inj,
                         void* stream);
+/* Height scan (terrain.measure_heights = True; inactive in DHT1StandCfg).  With it on, a step
+ * runs the split sequence with the scan between the phases, as the reference orders it:
+ *   t1env_step_physics_and_rewards -> t1env_measure_heights -> t1env_step_reset_and_observe -> t1env_critic_heights
+ * t1env_measure_heights replaces LeggedRobot._get_heights (legged_robot.py:1551-1587, called from the callback,
+ *   t1_dh_stand_env.py:190-191): measured (N, npts) from the post-physics, pre-reset base pose in root_states and
+ *   points (npts, 2) = the base-frame (x, y) of _init_height_points (legged_robot.py:1535-1549); zeros on a plane.
+ * t1env_critic_heights replaces the critic-history concatenation (t1_dh_stand_env.py:466-468, 548-558):
+ *   out (N, 3, 73 + npts), frame f = [priv_buf[obs_slot] frame f | heights frame f]; heights frames 0-1 = prev
+ *   frames 1-2 (zero for envs reset this step), frame 2 = clip(root_z - 0.5 - measured, -1, 1) * scale, all
+ *   clipped to +-clip_obs.  prev = the previous step's out (zeroed by the caller at reset_all). */
+int t1env_measure_heights(t1env* env, const float* points, int32_t npts, float* measured, void* stream);
+int t1env_critic_heights(t1env* env, int32_t obs_slot, int32_t npts, float scale, const float* measured,
+                         const float* prev, float* out, void* stream);
 /* t1env_step runs the whole step as ONE launch by default (fused): the history shift and post-physics ride in
  * the dynamics kernel (post-physics in its epilogue).  enable = 0 makes t1env_step run the split sequence
  * (physics_and_rewards + reset_and_observe) instead; both give the same buffers.  The split entry points are

@@ -17,6 +17,9 @@ Follows, function by function (file:line in /root/reference):
                                         1076-1120, 1138-1169)
   T1.compute_observations               t1_dh_stand_env.py:368-481 (+ _get_phase 80-92, compute_ref_state
                                         250-274, _get_gait_phase 95-107, generate_gait_time 109-124)
+  height scan (measure_heights=True;    legged_robot.py:1535-1587 (_init_height_points, _get_heights),
+    inactive in DHT1StandCfg)           utils/math.py:8-12 (quat_apply_yaw), t1_dh_stand_env.py:190-191,
+                                        466-468 (callback, critic-obs concatenation)
 Physics (Isaac Gym ``simulate``) is not part of the oracle: it is injected through ``physics(g, torques,
 state)`` so the same oracle serves the injected-state parity tests and the CPU baseline (with the CPU
 build of the dynamics plugged in).  Random draws come from oracle/rng.py (see its docstring).
@@ -73,6 +76,10 @@ REWARD_SCALES = dict(joint_pos=4, feet_clearance=1, feet_contact_number=1.2, fee
                      stand_still=2.5)    # :383-410
 REWARD_NAMES = sorted(REWARD_SCALES)    # class_to_dict iterates dir() -> alphabetical (helpers.py:18)
 BASE_MASS = 23.644        # base_link 9.999 + collapsed upper body 13.645 (t1.urdf)
+HEIGHT_X = [round(-0.8 + 0.1 * i, 1) for i in range(17)]   # legged_robot_config.py:29
+HEIGHT_Y = [round(-0.5 + 0.1 * i, 1) for i in range(11)]   # legged_robot_config.py:30
+NUM_HEIGHT = len(HEIGHT_X) * len(HEIGHT_Y)                  # 187 (legged_robot_config.py:36)
+HEIGHT_OBS_SCALE = 5.0    # obs_scales.height_measurements (t1_dh_stand_config.py:424)
 
 
 def euler_xyz(q):
@@ -101,6 +108,38 @@ def quat_rotate_inverse(q, v):
     return (a - b + c).astype(f32)
 
 
+def height_points():
+    """_init_height_points (legged_robot.py:1535-1549): torch.meshgrid(x, y) ('ij') flattened -> (187, 2) base-frame
+    (x, y), point k = ix * 11 + iy."""
+    gx, gy = np.meshgrid(np.array(HEIGHT_X, f32), np.array(HEIGHT_Y, f32), indexing="ij")
+    return np.stack([gx.ravel(), gy.ravel()], 1).astype(f32)
+
+
+def get_heights(base_pos, base_quat, pts, height_samples, horizontal_scale, vertical_scale, border_size):
+    """_get_heights (legged_robot.py:1551-1587) for all envs on a height field: the points rotated by the base yaw
+    (quat_apply_yaw, utils/math.py:8-12: roll/pitch components zeroed, normalised, quat_apply), offset by the base
+    position and the border, truncated (`.long()`) to samples, clipped to [0, rows-2] x [0, cols-2], min of the
+    sample and its +x and +y neighbours, times vertical_scale.  fp32 as the reference computes it."""
+    q = base_quat.astype(f32).copy()
+    q[:, :2] = 0
+    q = (q / np.maximum(_norm(q)[:, None], f32(1e-9))).astype(f32)            # torch_utils.normalize
+    n, m = q.shape[0], pts.shape[0]
+    v = np.zeros((n, m, 3), f32)
+    v[:, :, :2] = pts[None]
+    xyz = np.broadcast_to(q[:, None, :3], v.shape)
+    t = (np.cross(xyz, v) * f32(2)).astype(f32)                                 # torch_utils.quat_apply
+    p = (v + q[:, None, 3:4] * t + np.cross(xyz, t)).astype(f32)
+    p = (p + base_pos[:, None, :3].astype(f32)).astype(f32)
+    p = (p + f32(border_size)).astype(f32)
+    p = np.trunc(p / f32(horizontal_scale)).astype(np.int64)
+    rows, cols = height_samples.shape
+    px = np.clip(p[..., 0], 0, rows - 2)
+    py = np.clip(p[..., 1], 0, cols - 2)
+    hs = height_samples
+    h = np.minimum(np.minimum(hs[px, py], hs[px + 1, py]), hs[px, py + 1])
+    return (h.astype(f32) * f32(vertical_scale)).astype(f32)
+
+
 def _norm(x, axis=-1):
     return np.sqrt(np.sum(x * x, axis=axis)).astype(f32)
 
@@ -109,9 +148,11 @@ class T1Oracle:
     """Numpy mirror of T1DHStandEnv's state and step.  ``physics(g, torques, st)`` must return
     (root (N,13), dof (N,12,2), rigid (N,13,13), contact (N,13,3)) after global substep g."""
 
-    def __init__(self, num_envs, seed=5, mesh_type="plane", terrain=None, env_offset=0, reduce_fn=None):
+    def __init__(self, num_envs, seed=5, mesh_type="plane", terrain=None, env_offset=0, reduce_fn=None,
+                 measure_heights=False):
         """reduce_fn: sharded runs only -- (sum, count) -> (sum, count) over all ranks, so the command
-        curriculum sees the same mean as an unsharded run."""
+        curriculum sees the same mean as an unsharded run.  measure_heights: the height scan
+        (inactive in DHT1StandCfg): 187 heights appended to every critic frame (260 per frame)."""
         N = num_envs
         self.N, self.seed, self.env_offset = N, int(seed), int(env_offset)
         self.reduce_fn = reduce_fn
@@ -173,9 +214,14 @@ class T1Oracle:
         # buffers (legged_robot.py:116-349, base_task.py:55-74, t1_dh_stand_env.py:72-77, 562-569)
         z = lambda *s: np.zeros(s, f32)  # noqa: E731
         self.obs_buf = z(N, FRAME_STACK * NUM_SINGLE_OBS)
-        self.priv_buf = z(N, C_FRAME_STACK * SINGLE_PRIV)
+        self.measure_heights = bool(measure_heights)
+        self.priv_width = SINGLE_PRIV + (NUM_HEIGHT if self.measure_heights else 0)
+        self.terrain = terrain
+        self.height_points = height_points()
+        self.measured_heights = z(N, NUM_HEIGHT)
+        self.priv_buf = z(N, C_FRAME_STACK * self.priv_width)
         self.obs_hist = z(N, FRAME_STACK, NUM_SINGLE_OBS)
-        self.priv_hist = z(N, C_FRAME_STACK, SINGLE_PRIV)
+        self.priv_hist = z(N, C_FRAME_STACK, self.priv_width)
         self.rew_buf = z(N)
         self.reset_buf = np.ones(N, bool)
         self.time_out_buf = np.zeros(N, bool)
@@ -311,9 +357,19 @@ class T1Oracle:
                 self.commands[ids, 1] = self._rf(cr["lin_vel_y"][0], cr["lin_vel_y"][1], ids, R.SLOT_CMD_Y)
                 self.commands[ids, 2] = self._rf(cr["ang_vel_yaw"][0], cr["ang_vel_yaw"][1], ids, R.SLOT_CMD_YAW)
 
+    def _get_heights(self):
+        """legged_robot.py:1551-1587 on the post-physics (pre-reset) base pose; zeros on a plane (:1564-1565)."""
+        if self.mesh_type == "plane":
+            return np.zeros((self.N, NUM_HEIGHT), f32)
+        t = self.terrain
+        return get_heights(self.root[:, :3], self.root[:, 3:7], self.height_points, t["height_samples"],
+                           t["horizontal_scale"], t["vertical_scale"], t["border_size"])
+
     def _callback(self):
         self.phase_length_buf += 1
         self._resample_commands()
+        if self.measure_heights:                                 # t1_dh_stand_env.py:190-191
+            self.measured_heights = self._get_heights()
         i = int(self.common_step_counter / ADD_UPDATE_STEP)
         i = min(i, len(ADD_DURATION) - 1)
         duration = ADD_DURATION[i] / DT
@@ -661,6 +717,9 @@ class T1Oracle:
                                self.base_lin_vel * f32(2), self.base_ang_vel * f32(1),
                                self.base_euler_xyz * f32(1), pf, pt, self.friction[:, None],
                                (self.body_mass / f32(30.0))[:, None], stance, cmask], 1).astype(f32)
+        if self.measure_heights:                                 # t1_dh_stand_env.py:466-468
+            hts = np.clip(self.root[:, 2:3] - f32(0.5) - self.measured_heights, -1, 1) * f32(HEIGHT_OBS_SCALE)
+            priv = np.concatenate([priv, hts.astype(f32)], 1)
         ar = np.arange(self.N)
         lq = self.dof_lag_buffer[ar, :12, self.dof_lag_timestep]
         ldq = self.dof_lag_buffer[ar, 12:, self.dof_lag_timestep]

@@ -61,6 +61,8 @@ def snapshot(env):
     lfz = env.last_feet_z
     s["last_feet_z"] = _np(lfz) if isinstance(lfz, torch.Tensor) else np.full((env.num_envs, 2), lfz, np.float32)
     s["episode_sums"] = np.stack([_np(env.episode_sums[n]) for n in REWARD_NAMES])
+    if env.cfg.terrain.measure_heights:
+        s["measured_heights"] = _np(env.measured_heights)
     return s
 
 
@@ -84,6 +86,9 @@ def run(name, num_envs=16, mesh_type="plane", n_steps=10, cfg_hook=None, after_r
         init["terrain_types"] = _np(env.terrain_types)
         init["terrain_origins"] = _np(env.terrain_origins)
         init["height_samples"] = _np(env.height_samples).astype(np.int16)
+        if cfg.terrain.measure_heights:
+            tc = cfg.terrain
+            init["terrain_scales"] = np.array([tc.horizontal_scale, tc.vertical_scale, tc.border_size], np.float64)
     for k, v in init.items():
         out["init_" + k] = v
     # --- reset(): reset_idx(all) + step(zeros) --------------------------------------------------
@@ -170,8 +175,22 @@ def trimesh_overrides(env):
     return {"episode_length_buf": el.clone()}
 
 
+def heights_hook(cfg):
+    # the inactive height scan (legged_robot.py:1535-1587, t1_dh_stand_env.py:190-191,466-468) switched on
+    # on rough / sloped sub-terrains (the default proportions give only flat and rough-flat columns at 4 cols)
+    trimesh_hook(cfg)
+    cfg.terrain.measure_heights = True
+    cfg.terrain.terrain_proportions = [0.0, 0.25, 0.25, 0.25, 0.25, 0.0, 0.0, 0.0, 0.0, 0.0]
+
+
+SCENARIOS = {
+    "plane16": lambda: run("plane16", 16, "plane", 10, after_reset=plane16_overrides),
+    "events16": lambda: run("events16", 16, "plane", 14, after_reset=events16_overrides),
+    "config1_64": lambda: run("config1_64", 64, "plane", 2),
+    "trimesh16": lambda: run("trimesh16", 16, "trimesh", 6, cfg_hook=trimesh_hook, after_reset=trimesh_overrides),
+    "heights16": lambda: run("heights16", 16, "trimesh", 6, cfg_hook=heights_hook, after_reset=trimesh_overrides),
+}
+
 if __name__ == "__main__":
-    run("plane16", 16, "plane", 10, after_reset=plane16_overrides)
-    run("events16", 16, "plane", 14, after_reset=events16_overrides)
-    run("config1_64", 64, "plane", 2)
-    run("trimesh16", 16, "trimesh", 6, cfg_hook=trimesh_hook, after_reset=trimesh_overrides)
+    for name in sys.argv[1:] or list(SCENARIOS):
+        SCENARIOS[name]()

@@ -6,7 +6,7 @@ import numpy as np
 import synth
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16"]
+SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16", "heights16"]
 
 
 def load(name):
@@ -16,8 +16,16 @@ def load(name):
 
 def terrain_of(fx):
     if str(fx["mesh_type"]) in ("trimesh", "heightfield"):
-        return {"terrain_origins": fx["init_terrain_origins"], "height_samples": fx["init_height_samples"]}
+        t = {"terrain_origins": fx["init_terrain_origins"], "height_samples": fx["init_height_samples"]}
+        if "init_terrain_scales" in fx:   # the height-scan scenario: the scan needs the field's geometry
+            hs, vs, border = (float(x) for x in fx["init_terrain_scales"])
+            t.update(horizontal_scale=hs, vertical_scale=vs, border_size=border)
+        return t
     return None
+
+
+def measures_heights(fx):
+    return "step_measured_heights" in fx
 
 
 def synth_physics(fx):

@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 import synth
-from golden_util import assert_close, load
+from golden_util import assert_close, load, measures_heights
 
 REWARD_NAMES = sorted(["joint_pos", "feet_clearance", "feet_contact_number", "feet_air_time", "foot_slip",
                        "feet_distance", "knee_distance", "feet_rotation", "feet_contact_forces",
@@ -23,11 +23,30 @@ def make_env_for(fx, device="cuda:0"):
     from ti5_isaacgym_amd import make_t1_env
 
     name_hook = None
+    heights = measures_heights(fx)
     if str(fx["mesh_type"]) == "trimesh":
         def name_hook(cfg):
             cfg.terrain.num_rows, cfg.terrain.num_cols, cfg.terrain.border_size = 6, 4, 5
-    return make_t1_env(num_envs=int(fx["num_envs"]), mesh_type=str(fx["mesh_type"]), seed=int(fx["seed"]),
-                       device=device, cfg_hook=name_hook)
+            if heights:   # gen_golden.heights_hook
+                cfg.terrain.measure_heights = True
+                cfg.terrain.terrain_proportions = [0.0, 0.25, 0.25, 0.25, 0.25, 0.0, 0.0, 0.0, 0.0, 0.0]
+    env = make_t1_env(num_envs=int(fx["num_envs"]), mesh_type=str(fx["mesh_type"]), seed=int(fx["seed"]),
+                      device=device, cfg_hook=name_hook)
+    if heights:
+        # the scan samples the field: run it on the reference's own height samples (the terrain generator's
+        # numpy draws are not the reference's, and the injected-physics scenarios never touch the field)
+        from ti5_isaacgym_amd import _lib
+        hf = torch.from_numpy(fx["init_height_samples"]).to(env.device)
+        assert hf.shape == env.height_samples.shape
+        env.height_samples.copy_(hf)
+        # and its origins (rough / sloped sub-terrains: the origin z follows the random samples)
+        env.terrain_origins.copy_(torch.from_numpy(fx["init_terrain_origins"]).to(env.device))
+        env.env_origins.copy_(torch.from_numpy(fx["init_env_origins"]).to(env.device))
+        tc = env.cfg.terrain
+        _lib.check(env._lib.t1env_set_terrain(env._handle, env.height_samples.data_ptr(), hf.shape[0], hf.shape[1],
+                                              tc.horizontal_scale, tc.vertical_scale, float(tc.border_size), 2),
+                   "t1env_set_terrain")
+    return env
 
 
 class Injector:
@@ -78,7 +97,8 @@ def snapshot(env):
         full_obs=env.obs_buf.cpu().numpy(), gait_start=env.gait_start.cpu().numpy(),
         dof_lag=env.dof_lag_timestep.cpu().numpy(), imu_lag=env.imu_lag_timestep.cpu().numpy(),
         lag=env.lag_timestep.cpu().numpy(), kp=env.randomized_p_gains.cpu().numpy(),
-        armature=env.joint_armatures.cpu().numpy())
+        armature=env.joint_armatures.cpu().numpy(),
+        measured_heights=env.measured_heights.cpu().numpy() if env.measure_heights else None)
 
 
 def run_parity(name, max_steps=None, device="cuda:0", check=True):
@@ -129,6 +149,9 @@ def compare(name, fx, outs):
         assert_close("obs", s["obs"], fx["step_obs"][t], ctx=ctx)
         assert_close("priv", s["priv"], fx["step_priv"][t], ctx=ctx)
         assert_close("rew", s["rew"], fx["step_rew"][t], ctx=ctx)
+        if measures_heights(fx):   # int16 samples x vertical_scale: exact (a wrong cell is off by >= 0.005)
+            np.testing.assert_array_equal(s["measured_heights"], fx["step_measured_heights"][t],
+                                          err_msg="measured_heights" + ctx)
         if t > 0:
             assert_close("extras_episode", s["extras_episode"], fx["step_extras_episode"][t], ctx=ctx)
             assert abs(s["max_command_x"] - float(fx["step_extras_max_command_x"][t])) < 1e-6, ctx

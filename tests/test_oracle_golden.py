@@ -6,7 +6,7 @@ bool / integer state.  Obs/priv are compared after clipping, as returned by step
 import numpy as np
 import pytest
 
-from golden_util import SCENARIOS, assert_close, load, synth_physics, terrain_of
+from golden_util import SCENARIOS, assert_close, load, measures_heights, synth_physics, terrain_of
 from oracle import rng as R
 from oracle.t1_oracle import REWARD_NAMES, T1Oracle
 
@@ -14,7 +14,8 @@ from oracle.t1_oracle import REWARD_NAMES, T1Oracle
 def run_oracle(fx):
     n = int(fx["num_envs"])
     terrain = terrain_of(fx)
-    o = T1Oracle(n, seed=int(fx["seed"]), mesh_type=str(fx["mesh_type"]), terrain=terrain)
+    o = T1Oracle(n, seed=int(fx["seed"]), mesh_type=str(fx["mesh_type"]), terrain=terrain,
+                 measure_heights=measures_heights(fx))
     phys = synth_physics(fx)
     outs = []
     o.reset(phys)
@@ -41,7 +42,7 @@ def snapshot(o):
                 episode_sums=np.stack([o.episode_sums[k] for k in REWARD_NAMES]),
                 extras_episode=np.array([o.extras["episode"]["rew_" + k] for k in REWARD_NAMES], np.float32),
                 max_command_x=o.extras["episode"]["max_command_x"], applied_force=o.applied_force.copy(),
-                full_obs=o.obs_buf.copy())
+                full_obs=o.obs_buf.copy(), measured_heights=o.measured_heights.copy())
 
 
 @pytest.mark.parametrize("name", SCENARIOS)
@@ -66,6 +67,9 @@ def test_oracle_matches_reference(name):
         assert_close("obs", s["obs"], fx["step_obs"][t], ctx=ctx)
         assert_close("priv", s["priv"], fx["step_priv"][t], ctx=ctx)
         assert_close("rew", s["rew"], fx["step_rew"][t], ctx=ctx)
+        if measures_heights(fx):   # sample heights are int16 x vertical_scale: a wrong cell is off by >= 0.005
+            np.testing.assert_array_equal(s["measured_heights"], fx["step_measured_heights"][t],
+                                          err_msg="measured_heights" + ctx)
         if t > 0:
             ref_ep = fx["step_extras_episode"][t]
             assert_close("extras_episode", s["extras_episode"], ref_ep, ctx=ctx)

@@ -188,6 +188,69 @@ __global__ __launch_bounds__(256) void k_terrain_level_sum(t1env_buffers B, cons
   wave_atomic_add(B.ep_accum + 25, v);
 }
 
+// -----------------------------------------------------------------------------------------------------
+// Height scan (terrain.measure_heights; inactive in DHT1StandCfg).  k_measure_heights restates _get_heights
+// (legged_robot.py:1551-1587) with quat_apply_yaw (utils/math.py:8-12) for every (env, point): the base-frame
+// point rotated by the base yaw, offset by the base position and the border, truncated to a sample (`.long()`),
+// clipped to [0, rows-2] x [0, cols-2], min of the sample and its +x / +y neighbours, times vertical_scale.  The
+// sample index is discontinuous in the coordinates, so the chain is computed with the reference's fp32
+// roundings (no FMA contraction, true division).  One thread per (env, point); reads root_states, which
+// t1env_step_physics_and_rewards left at the post-physics, pre-reset pose the reference's callback samples.
+// k_critic_heights assembles the critic history with heights (t1_dh_stand_env.py:466-468, 548-558): one
+// thread per (env, column) of (N, 3, 73 + npts).
+// -----------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_measure_heights(const float* __restrict__ root, const float* __restrict__ pts,
+                                                         int npts, int N, Terrain T, float* __restrict__ measured) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * npts) return;
+  const int n = (int)(i / npts), p = (int)(i - (int64_t)n * npts);
+  if (T.type == 0) {  // plane (legged_robot.py:1564-1565)
+    measured[i] = 0.0f;
+    return;
+  }
+  const float* r = root + (size_t)n * 13;
+  // normalize((0, 0, qz, qw)) with the norm clamped at 1e-9 (torch_utils.normalize)
+  float qz = r[5], qw = r[6];
+  const float nrm = fmaxf(__fsqrt_rn(__fadd_rn(__fmul_rn(qz, qz), __fmul_rn(qw, qw))), 1e-9f);
+  qz = __fdiv_rn(qz, nrm);
+  qw = __fdiv_rn(qw, nrm);
+  // quat_apply(q, v), v = (px, py, 0): t = 2 (q_xyz x v); v + w t + q_xyz x t
+  const float px = pts[2 * p], py = pts[2 * p + 1];
+  const float tx = __fmul_rn(-__fmul_rn(qz, py), 2.0f), ty = __fmul_rn(__fmul_rn(qz, px), 2.0f);
+  float x = __fadd_rn(__fadd_rn(px, __fmul_rn(qw, tx)), -__fmul_rn(qz, ty));
+  float y = __fadd_rn(__fadd_rn(py, __fmul_rn(qw, ty)), __fmul_rn(qz, tx));
+  x = __fadd_rn(__fadd_rn(x, r[0]), T.border);
+  y = __fadd_rn(__fadd_rn(y, r[1]), T.border);
+  int ix = (int)truncf(__fdiv_rn(x, T.hscale)), iy = (int)truncf(__fdiv_rn(y, T.hscale));
+  ix = min(max(ix, 0), T.rows - 2);
+  iy = min(max(iy, 0), T.cols - 2);
+  const int16_t* h = T.h + (size_t)ix * T.cols + iy;
+  const int hm = min(min((int)h[0], (int)h[T.cols]), (int)h[1]);
+  measured[i] = __fmul_rn((float)hm, T.vscale);
+}
+
+__global__ __launch_bounds__(256) void k_critic_heights(const float* __restrict__ priv, const float* __restrict__ root,
+                                                        const uint8_t* __restrict__ reset,
+                                                        const float* __restrict__ measured,
+                                                        const float* __restrict__ prev, float* __restrict__ out,
+                                                        int npts, int N, float scale, float clip_obs) {
+  const int W = T1_NPRIV + npts, RW = T1_CHIST * W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * RW) return;
+  const int n = (int)(i / RW), c = (int)(i - (int64_t)n * RW);
+  const int f = c / W, k = c - f * W;
+  float v;
+  if (k < T1_NPRIV) {
+    v = priv[(size_t)n * (T1_NPRIV * T1_CHIST) + f * T1_NPRIV + k];
+  } else if (f < T1_CHIST - 1) {  // older frames: shifted by one, cleared for envs reset this step
+    v = reset[n] ? 0.0f : prev[(size_t)n * RW + (f + 1) * W + k];
+  } else {
+    const float d = __fadd_rn(__fadd_rn(root[(size_t)n * 13 + 2], -0.5f), -measured[(size_t)n * npts + (k - T1_NPRIV)]);
+    v = fminf(fmaxf(__fmul_rn(fminf(fmaxf(d, -1.0f), 1.0f), scale), -clip_obs), clip_obs);
+  }
+  out[i] = v;
+}
+
 // creation-time state (see t1env_init in include/t1env.h)
 __global__ __launch_bounds__(BLOCK) void k_init(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
                                                 t1env_buffers B) {
@@ -498,6 +561,30 @@ static int launch_fused(t1env* e, const float* actions, const t1env_step_args* a
 int t1env_set_fused(t1env* e, int32_t enable) {
   if (!e) return fail(T1ENV_E_ARG, "t1env_set_fused: null env");
   e->fused = enable ? 1 : 0;
+  return 0;
+}
+
+int t1env_measure_heights(t1env* e, const float* points, int32_t npts, float* measured, void* stream) {
+  if (!e || !points || !measured || npts <= 0) return fail(T1ENV_E_ARG, "t1env_measure_heights: bad argument");
+  const int N = e->cfg.num_envs;
+  if (e->terrain.type != 0 && !e->terrain.h) return fail(T1ENV_E_STATE, "t1env_measure_heights: no terrain set");
+  const int64_t total = (int64_t)N * npts;
+  hipLaunchKernelGGL(k_measure_heights, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     e->buf.root_states, points, npts, N, e->terrain, measured);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int t1env_critic_heights(t1env* e, int32_t obs_slot, int32_t npts, float scale, const float* measured,
+                         const float* prev, float* out, void* stream) {
+  if (!e || !measured || !prev || !out || npts <= 0 || (obs_slot & ~1))
+    return fail(T1ENV_E_ARG, "t1env_critic_heights: bad argument");
+  const int N = e->cfg.num_envs;
+  const int64_t total = (int64_t)N * T1_CHIST * (T1_NPRIV + npts);
+  hipLaunchKernelGGL(k_critic_heights, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     e->buf.priv_buf[obs_slot], e->buf.root_states, e->buf.reset_buf, measured, prev, out, npts, N,
+                     scale, e->cfg.clip_obs);
+  HIP_TRY(hipGetLastError());
   return 0;
 }
 

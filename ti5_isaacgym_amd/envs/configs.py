@@ -266,8 +266,12 @@ class DHT1StandCfgPPO(LeggedRobotCfgPPO):
 
     class algorithm(LeggedRobotCfgPPO.algorithm):
         entropy_coef, learning_rate, num_learning_epochs, gamma, lam, num_mini_batches = 0.001, 1e-5, 2, 0.994, 0.9, 4
-        lin_vel_idx = DHT1StandCfg.env.single_num_privileged_obs * (DHT1StandCfg.env.c_frame_stack - 1) \
-            + DHT1StandCfg.env.single_linvel_index
+        if DHT1StandCfg.terrain.measure_heights:   # t1_dh_stand_config.py:460-466
+            lin_vel_idx = (DHT1StandCfg.env.single_num_privileged_obs + DHT1StandCfg.terrain.num_height) \
+                * (DHT1StandCfg.env.c_frame_stack - 1) + DHT1StandCfg.env.single_linvel_index
+        else:
+            lin_vel_idx = DHT1StandCfg.env.single_num_privileged_obs * (DHT1StandCfg.env.c_frame_stack - 1) \
+                + DHT1StandCfg.env.single_linvel_index
 
     class runner:
         policy_class_name, algorithm_class_name, num_steps_per_env, max_iterations = "ActorCriticDH", "DHPPO", 24, 30000

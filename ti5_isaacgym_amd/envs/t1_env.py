@@ -122,8 +122,9 @@ class T1DHStandEnv(VecEnv):
         if (self.num_single_obs, e.single_num_privileged_obs, e.frame_stack, e.c_frame_stack, self.num_actions) != \
                 (_lib.NOBS, _lib.NPRIV, _lib.HIST, _lib.CHIST, _lib.ND):
             raise ValueError("the HIP kernels are specialised for the t1_dh_stand layout (47 x 66 obs, 73 x 3 priv)")
-        if cfg.terrain.measure_heights:
-            raise NotImplementedError("measure_heights=True (187 height samples) is not on the t1_dh_stand path")
+        # height scan (inactive in DHT1StandCfg): 187 heights per critic frame, t1env_measure_heights /
+        # t1env_critic_heights between and after the split step phases
+        self.measure_heights = bool(cfg.terrain.measure_heights)
         self.env_offset = int(env_offset)
         self.num_envs_total = int(num_envs_total) if num_envs_total is not None else N
         self.dt = cfg.control.decimation * self.sim_params.dt
@@ -212,6 +213,19 @@ class T1DHStandEnv(VecEnv):
         self.dof_vel = self.dof_state.view(N, 12, 2)[..., 1]
         self.base_quat = self.root_states[:, 3:7]
         self.torque_multi = torch.ones(N, 12, device=d)
+        self.measured_heights = 0      # legged_robot.py:210
+        if self.measure_heights:
+            t = self.cfg.terrain
+            gx, gy = np.meshgrid(np.array(t.measured_points_x, np.float32), np.array(t.measured_points_y, np.float32),
+                                 indexing="ij")                      # _init_height_points (legged_robot.py:1535-1549)
+            pts = np.stack([gx.ravel(), gy.ravel()], 1)
+            self.num_height_points = pts.shape[0]
+            self._height_pts = torch.tensor(pts, device=d).contiguous()
+            self.height_points = torch.zeros(N, self.num_height_points, 3, device=d)
+            self.height_points[:, :, :2] = self._height_pts
+            self.measured_heights = z(N, self.num_height_points)
+            w = self.cfg.env.c_frame_stack * (self.cfg.env.single_num_privileged_obs + self.num_height_points)
+            self._priv_ext = [z(N, w), z(N, w)]
 
     def _build_model(self, urdf_path):
         cfg = self.cfg
@@ -402,6 +416,8 @@ class T1DHStandEnv(VecEnv):
 
     @property
     def privileged_obs_buf(self):
+        if self.measure_heights:   # (N, 3 * (73 + 187)): the critic history with heights
+            return self._priv_ext[self._slot ^ 1]
         return self._priv[self._slot ^ 1]
 
     def get_observations(self):
@@ -474,7 +490,7 @@ class T1DHStandEnv(VecEnv):
         a = self._args(self.common_step_counter, ext_call, ext_first, push_call)
         ctr_post = self.common_step_counter + 1
         needs_curriculum = self.cfg.commands.curriculum and ctr_post % self.max_episode_length == 0
-        if _injected is None and not needs_curriculum:
+        if _injected is None and not needs_curriculum and not self.measure_heights:
             _lib.check(lib.t1env_step(h, _ptr(actions), _lib.C.byref(a), s), "t1env_step")
         else:
             if _injected is None:
@@ -482,12 +498,20 @@ class T1DHStandEnv(VecEnv):
             else:
                 _lib.check(lib.t1env_step_injected(h, _ptr(actions), _lib.C.byref(a), _lib.C.byref(_injected), s),
                            "t1env_step_injected")
+            if self.measure_heights:   # the callback's _get_heights, before reset_idx (t1_dh_stand_env.py:190)
+                _lib.check(lib.t1env_measure_heights(h, _ptr(self._height_pts), self.num_height_points,
+                                                     _ptr(self.measured_heights), s), "t1env_measure_heights")
             if needs_curriculum:
                 idx = REWARD_NAMES.index("tracking_lin_vel")
                 acc = self._ep_accum.cpu()
                 self._command_curriculum(float(acc[idx]), float(acc[24]))
                 a = self._args(self.common_step_counter, ext_call, ext_first, push_call)
             _lib.check(lib.t1env_step_reset_and_observe(h, _lib.C.byref(a), s), "t1env_step_reset_and_observe")
+            if self.measure_heights:
+                _lib.check(lib.t1env_critic_heights(h, self._slot, self.num_height_points,
+                                                    float(self.obs_scales.height_measurements),
+                                                    _ptr(self.measured_heights), _ptr(self._priv_ext[self._slot ^ 1]),
+                                                    _ptr(self._priv_ext[self._slot]), s), "t1env_critic_heights")
         self.common_step_counter += 1
         self._slot ^= 1
         self._fill_extras(self.common_step_counter % EXTRAS_RING)
@@ -518,6 +542,9 @@ class T1DHStandEnv(VecEnv):
             self._command_curriculum(float(self.episode_sums["tracking_lin_vel"].sum()), float(self.num_envs))
         a = self._args(self.common_step_counter)
         _lib.check(self._lib.t1env_reset_all(self._handle, _lib.C.byref(a), self._stream()), "t1env_reset_all")
+        if self.measure_heights:   # reset_idx clears the critic history deque (t1_dh_stand_env.py:548-558)
+            for t in self._priv_ext:
+                t.zero_()
         self._fill_extras(self.common_step_counter % EXTRAS_RING)
 
     def reset(self):
