@@ -51,8 +51,12 @@ def dyn_waves(request, monkeypatch):
 
 # 16384 envs: k_dyn4 fills every CU, so the history shift runs as its own launch ahead of the fused kernel and
 # the epilogue zeroes the reset rows directly (t1_shift_prelaunch)
-@pytest.mark.parametrize("n,mesh", [(8192, "trimesh"), (777, "plane"), (16384, "plane")],
-                         ids=["8192_trimesh", "ragged777_plane", "16384_plane_prelaunched_shift"])
+# 1 env: one workgroup with 63 shadow lanes; 65 envs: a second workgroup holding one live env; 13001: the
+# prelaunched shift with a ragged last workgroup
+@pytest.mark.parametrize("n,mesh", [(8192, "trimesh"), (777, "plane"), (16384, "plane"), (1, "plane"),
+                                    (65, "trimesh"), (13001, "plane")],
+                         ids=["8192_trimesh", "ragged777_plane", "16384_plane_prelaunched_shift", "single_env",
+                              "65_trimesh", "ragged13001_prelaunched_shift"])
 def test_fused_step_equals_split_sequence(n, mesh, dyn_waves):
     fused, split = _env(n, mesh, True), _env(n, mesh, False)
     g = torch.Generator(device="cuda:0").manual_seed(1)
