@@ -16,7 +16,7 @@ roofline: SURVEY.md §8(d): achieved = env_steps_per_s x B_alg (30,678 algorithm
 the 8 TB/s HBM3E peak; `traffic` = PMC-measured HBM bytes per step (profiles/traffic_*.json, tools/
 pmc_traffic.py).  Per-kernel durations are measured live with HIP events around each launch on every
 --time-every'th timed step (event records cost host time, so not on every step), with each kernel's own
-algorithmic bytes; the dominant kernel is k_dynamics (VALU-bound).
+algorithmic bytes; the dominant kernel is k_dyn4, the whole fused step (latency-bound at one wave per SIMD).
 cpu_baseline: the build's CPU restatement (numpy oracle post-physics + OpenMP dynamics), rank 0, N = 1 only.
 """
 import argparse
