@@ -26,3 +26,44 @@ def test_runner_over_hip_env(tmp_path):
     with torch.no_grad():
         a = pol(env.get_observations())
     assert a.shape == (256, 12) and torch.isfinite(a).all()
+    # the rollout's act() ran as replayed HIP graphs, one per env observation buffer pair
+    assert runner.alg.graph_act and 1 <= len(runner.alg._act_graphs) <= 2
+
+
+def test_graphed_act_matches_eager():
+    """The graphed act() (DHPPO._graphed_act) against the eager ActorCriticDH calls on the same buffers:
+    mean, std, value exactly (same kernels), the log-prob of the sampled actions exactly, samples distinct
+    across replays, and the graph follows in-place weight updates."""
+    from ti5_isaacgym_amd import task_registry
+    from ti5_isaacgym_amd.algo.dh_policy import ActorCriticDH
+    from ti5_isaacgym_amd.algo.dh_update import DHPPO
+    from torch.distributions import Normal
+    env_cfg, train_cfg = task_registry.get_cfgs("t1_dh_stand")
+    pc = train_cfg.policy
+    torch.manual_seed(0)
+    ac = ActorCriticDH(235, 47, 219, 12, actor_hidden_dims=pc.actor_hidden_dims, critic_hidden_dims=pc.critic_hidden_dims,
+                       state_estimator_hidden_dims=pc.state_estimator_hidden_dims, in_channels=66, kernel_size=pc.kernel_size,
+                       filter_size=pc.filter_size, stride_size=pc.stride_size, lh_output_dim=pc.lh_output_dim,
+                       init_noise_std=pc.init_noise_std)
+    alg = DHPPO(ac, device="cuda:0")
+    n = 1024
+    obs = torch.randn(n, 66 * 47, device="cuda:0")
+    cobs = torch.randn(n, 219, device="cuda:0")
+    tol = dict(rtol=1e-6, atol=1e-6)  # the same kernels; a library may still pick another GEMM solution
+    with torch.inference_mode():
+        a1, v1, lp1, m1, s1 = [t.clone() for t in alg._graphed_act(obs, cobs)]
+        a2 = alg._graphed_act(obs, cobs)[0].clone()
+        mean = ac.actor(ac.actor_input(obs))
+        torch.testing.assert_close(m1, mean, **tol)
+        torch.testing.assert_close(s1, (mean * 0.0 + ac.std).expand_as(s1), **tol)
+        torch.testing.assert_close(v1, ac.critic(cobs), **tol)
+        lp = Normal(m1, s1, validate_args=False).log_prob(a1).sum(-1)
+        torch.testing.assert_close(lp1, lp, **tol)
+        assert not torch.equal(a1, a2)
+    with torch.no_grad():
+        for p in ac.parameters():   # in-place update (what the optimizer step does)
+            p.add_(0.01)
+    with torch.inference_mode():
+        m3 = alg._graphed_act(obs, cobs)[3]
+        torch.testing.assert_close(m3, ac.actor(ac.actor_input(obs)), **tol)
+    assert len(alg._act_graphs) == 1

@@ -7,10 +7,16 @@ Same constructor arguments, API (``init_storage``, ``act``, ``process_env_step``
 Additions for data-parallel training over RCCL (distributed.py): one bucketed gradient all-reduce between
 backward() and clip_grad_norm_, the KL mean all-reduced before the adaptive learning-rate decision, and
 rank-0 weights broadcast at start.  Losses are accumulated on the device and read once per update.
+On a HIP device the rollout's act() (policy sample, value, log-prob) replays a captured HIP graph, one per
+pair of observation buffers the env hands out (its ping-pong buffers): the same kernels as the eager call,
+without the per-kernel launch cost that dominates at one call per env step.
 """
+import warnings
+
 import torch
 import torch.nn as nn
 import torch.optim as optim
+from torch.distributions import Normal
 
 from . import distributed as dist_util
 from .dh_policy import ActorCriticDH
@@ -40,6 +46,9 @@ class DHPPO:
         self.lin_vel_idx = lin_vel_idx
         self.grads = dist_util.GradientBucket(self.actor_critic.parameters())
         self.grads.broadcast_params_()
+        # graphed rollout act(): {(obs ptr, critic obs ptr, shapes): (graph, static outputs)}; None = eager
+        self.graph_act = torch.device(device).type == "cuda"
+        self._act_graphs = {}
 
     def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
@@ -51,8 +60,49 @@ class DHPPO:
     def train_mode(self):
         self.actor_critic.train()
 
+    def _act_body(self, obs, critic_obs):
+        """act() as one fixed kernel sequence (ActorCriticDH.act / evaluate / get_actions_log_prob).  Two host
+        checks cannot run inside a graph: the distribution's argument validation (built without it) and
+        torch.normal's std >= 0 test (the sample is drawn as mean + std * N(0, 1), the same distribution)."""
+        ac = self.actor_critic
+        mean = ac.actor(ac.actor_input(obs))
+        std = mean * 0.0 + ac.std
+        dist = Normal(mean, std, validate_args=False)
+        actions = mean + std * torch.randn_like(mean)
+        return actions, ac.critic(critic_obs), dist.log_prob(actions).sum(dim=-1), mean, std
+
+    def _graphed_act(self, obs, critic_obs):
+        key = (obs.data_ptr(), critic_obs.data_ptr(), tuple(obs.shape), tuple(critic_obs.shape))
+        entry = self._act_graphs.get(key)
+        if entry is None:
+            if len(self._act_graphs) >= 4:  # not the env's fixed buffers: stay eager
+                return None
+            side = torch.cuda.Stream(device=obs.device)
+            side.wait_stream(torch.cuda.current_stream(obs.device))
+            with torch.cuda.stream(side):  # warm-up outside the capture (allocator, library handles)
+                for _ in range(2):
+                    self._act_body(obs, critic_obs)
+            torch.cuda.current_stream(obs.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph):
+                    outs = self._act_body(obs, critic_obs)
+            except RuntimeError as e:  # a library call that cannot be captured: the eager act() from now on
+                warnings.warn(f"DHPPO: act() graph capture failed, running eager: {e}")
+                self.graph_act = False
+                return None
+            entry = self._act_graphs[key] = (graph, outs)
+        entry[0].replay()
+        return entry[1]
+
     def act(self, obs, critic_obs):
         ac, t = self.actor_critic, self.transition
+        outs = self._graphed_act(obs, critic_obs) if self.graph_act and obs.is_cuda else None
+        if outs is not None:
+            t.actions, t.values, t.actions_log_prob, t.action_mean, t.action_sigma = outs
+            t.observations = obs
+            t.critic_observations = critic_obs
+            return t.actions
         t.actions = ac.act(obs).detach()
         t.values = ac.evaluate(critic_obs).detach()
         t.actions_log_prob = ac.get_actions_log_prob(t.actions).detach()

@@ -18,12 +18,14 @@ from ti5_isaacgym_amd.utils.helpers import class_to_dict  # noqa: E402
 p = argparse.ArgumentParser()
 p.add_argument("--num-envs", type=int, default=8192)
 p.add_argument("--iters", type=int, default=3)
+p.add_argument("--no-graph", action="store_true", help="eager act() in the rollout (DHPPO.graph_act off)")
 a = p.parse_args()
 env = make_t1_env(num_envs=a.num_envs, mesh_type="trimesh", seed=5, device="cuda:0")
 _, tc = task_registry.get_cfgs("t1_dh_stand")
 cfg = class_to_dict(tc)
 torch.manual_seed(0)
 r = DHOnPolicyRunner(env, cfg, None, device="cuda:0")
+r.alg.graph_act = not a.no_graph
 r.learn(1)  # warm-up (allocations, kernels)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
@@ -55,7 +57,7 @@ for _ in range(a.iters):
     torch.cuda.synchronize()
     t_upd += time.perf_counter() - t1
     t_roll += t1 - t0
-print(json.dumps({"num_envs": a.num_envs, "iters": a.iters, "env_steps_per_s_incl_update": round(steps / dt, 1),
+print(json.dumps({"num_envs": a.num_envs, "iters": a.iters, "graph_act": r.alg.graph_act, "env_steps_per_s_incl_update": round(steps / dt, 1),
                   "s_per_iter": round(dt / a.iters, 4),
                   "phases_s_per_iter": {"rollout": round(t_roll / a.iters, 4), "env_step_in_rollout": round(t_env / a.iters, 4),
                                         "update": round(t_upd / a.iters, 4)}}))
