@@ -19,7 +19,9 @@ p = argparse.ArgumentParser()
 p.add_argument("--num-envs", type=int, default=8192)
 p.add_argument("--iters", type=int, default=3)
 p.add_argument("--no-graph", action="store_true", help="eager act() in the rollout (DHPPO.graph_act off)")
+p.add_argument("--conv-search", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find) for the conv")
 a = p.parse_args()
+torch.backends.cudnn.benchmark = a.conv_search
 env = make_t1_env(num_envs=a.num_envs, mesh_type="trimesh", seed=5, device="cuda:0")
 _, tc = task_registry.get_cfgs("t1_dh_stand")
 cfg = class_to_dict(tc)
