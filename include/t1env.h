@@ -200,6 +200,12 @@ int t1env_set_terrain(t1env* env, const int16_t* heights_dev, int32_t rows, int3
                       float vertical_scale, float border_size, int32_t mesh_type /* 0 plane, 1 hf, 2 trimesh */);
 /* reset_idx(arange(N)); counter = common_step_counter (RNG key). */
 int t1env_reset_all(t1env* env, const t1env_step_args* args, void* stream);
+/* reset_idx(env_ids) between steps (t1_dh_stand_env.py:483-559): mask (N,) uint8 device, nonzero = reset.  The same
+ * per-env reset as a step's, keyed by args->counter = common_step_counter; extras slot counter % RING gets the
+ * means over the masked envs; every frame of the masked envs' obs / critic history rows is zeroed in ping-pong
+ * buffer args->obs_slot (the one holding the current observations, which the next step shifts from).  The
+ * command curriculum (legged_robot.py:1160-1169) is the caller's, as for t1env_reset_all. */
+int t1env_reset_idx(t1env* env, const uint8_t* mask, const t1env_step_args* args, void* stream);
 /* Phase A of post-physics ends with the per-env reset decision; curriculum steps (counter+1) % 2400 == 0
  * need the host to read ep_accum between the phases, so the step is exposed in two halves:
  *   t1env_step_physics_and_rewards  -> physics, post_a (callback, termination, rewards, extras reduction)

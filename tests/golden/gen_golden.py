@@ -66,7 +66,9 @@ def snapshot(env):
     return s
 
 
-def run(name, num_envs=16, mesh_type="plane", n_steps=10, cfg_hook=None, after_reset=None, act_scale=0.5):
+def run(name, num_envs=16, mesh_type="plane", n_steps=10, cfg_hook=None, after_reset=None, act_scale=0.5,
+        mid_reset=None):
+    """mid_reset = (t, env_ids): the reference's reset_idx(env_ids) called between step t and step t + 1."""
     env, cfg, gym = refenv.make_env(num_envs, mesh_type, cfg_hook)
     assert list(env.reward_names) == REWARD_NAMES, env.reward_names
     gym.provider = make_provider(env, num_envs, SYNTH_SEED)
@@ -108,6 +110,9 @@ def run(name, num_envs=16, mesh_type="plane", n_steps=10, cfg_hook=None, after_r
     actions[:, 0, :] = 0.0     # one env with exact-zero actions
     actions[min(2, n_steps - 1), 1, 3] = 150.0   # exercises clip_actions = 100
     out["actions"] = actions
+    if mid_reset is not None:
+        out["mid_reset_step"] = np.int64(mid_reset[0])
+        out["mid_reset_ids"] = np.asarray(mid_reset[1], np.int64)
     for t in range(n_steps):
         n_torque, n_force = len(gym.torque_log), len(gym.force_log)
         env.step(torch.from_numpy(actions[t]).clone())
@@ -124,6 +129,8 @@ def run(name, num_envs=16, mesh_type="plane", n_steps=10, cfg_hook=None, after_r
                  extras_max_command_x=np.float32(ep.get("max_command_x", np.nan)),
                  extras_terrain_level=np.float32(ep.get("terrain_level", np.nan)))
         rec.append(r)
+        if mid_reset is not None and t == mid_reset[0]:
+            env.reset_idx(torch.tensor(mid_reset[1], dtype=torch.long))
     keys = sorted(set().union(*[r.keys() for r in rec[1:]]))
     for k in keys:
         vals = [r.get(k) for r in rec]
@@ -188,6 +195,7 @@ SCENARIOS = {
     "events16": lambda: run("events16", 16, "plane", 14, after_reset=events16_overrides),
     "config1_64": lambda: run("config1_64", 64, "plane", 2),
     "trimesh16": lambda: run("trimesh16", 16, "trimesh", 6, cfg_hook=trimesh_hook, after_reset=trimesh_overrides),
+    "resetidx16": lambda: run("resetidx16", 16, "trimesh", 6, cfg_hook=trimesh_hook, mid_reset=(2, [1, 4, 9, 15])),
     "heights16": lambda: run("heights16", 16, "trimesh", 6, cfg_hook=heights_hook, after_reset=trimesh_overrides),
 }
 

@@ -6,7 +6,7 @@ import numpy as np
 import synth
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16", "heights16"]
+SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16", "heights16", "resetidx16"]
 
 
 def load(name):
@@ -21,6 +21,13 @@ def terrain_of(fx):
             hs, vs, border = (float(x) for x in fx["init_terrain_scales"])
             t.update(horizontal_scale=hs, vertical_scale=vs, border_size=border)
         return t
+    return None
+
+
+def mid_reset(fx, t):
+    """env ids the reference's reset_idx was called on between step t and t + 1 (scenario resetidx16), or None"""
+    if "mid_reset_step" in fx and int(fx["mid_reset_step"]) == t:
+        return fx["mid_reset_ids"]
     return None
 
 

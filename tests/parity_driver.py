@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 import synth
-from golden_util import assert_close, load, measures_heights
+from golden_util import assert_close, load, measures_heights, mid_reset
 
 REWARD_NAMES = sorted(["joint_pos", "feet_clearance", "feet_contact_number", "feet_air_time", "foot_slip",
                        "feet_distance", "knee_distance", "feet_rotation", "feet_contact_forces",
@@ -125,6 +125,9 @@ def run_parity(name, max_steps=None, device="cuda:0", check=True):
     for t in range(steps):
         env.step(torch.from_numpy(fx["actions"][t]).to(env.device), _injected=inj.next())
         outs.append(dict(snapshot(env), torques=inj.torque_log.cpu().numpy()))
+        ids = mid_reset(fx, t)
+        if ids is not None:   # the reference's reset_idx(env_ids) between two steps
+            env.reset_idx(torch.from_numpy(ids))
     if check:
         compare(name, fx, outs)
     return env, outs

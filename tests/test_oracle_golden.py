@@ -6,7 +6,7 @@ bool / integer state.  Obs/priv are compared after clipping, as returned by step
 import numpy as np
 import pytest
 
-from golden_util import SCENARIOS, assert_close, load, measures_heights, synth_physics, terrain_of
+from golden_util import SCENARIOS, assert_close, load, measures_heights, mid_reset, synth_physics, terrain_of
 from oracle import rng as R
 from oracle.t1_oracle import REWARD_NAMES, T1Oracle
 
@@ -29,6 +29,9 @@ def run_oracle(fx):
     for t in range(fx["actions"].shape[0]):
         o.step(fx["actions"][t], phys)
         outs.append(snapshot(o))
+        ids = mid_reset(fx, t)
+        if ids is not None:
+            o.reset_idx(np.asarray(ids))
     return o, outs
 
 

@@ -86,7 +86,7 @@ class Injected(C.Structure):
 EXPORTS = ["t1env_create", "t1env_destroy", "t1env_init", "t1env_set_terrain", "t1env_reset_all", "t1env_step",
            "t1env_step_physics_and_rewards", "t1env_step_reset_and_observe", "t1env_step_injected",
            "t1env_set_fused", "t1env_set_timing", "t1env_get_timing", "t1env_last_error", "t1env_version",
-           "t1env_measure_heights", "t1env_critic_heights"]
+           "t1env_measure_heights", "t1env_critic_heights", "t1env_reset_idx"]
 
 _lib = None
 
@@ -117,6 +117,7 @@ def load():
         "t1env_last_error": ([], C.c_char_p),
         "t1env_version": ([], C.c_char_p),
         "t1env_measure_heights": ([vp, vp, i32, vp, vp], C.c_int),
+        "t1env_reset_idx": ([vp, vp, P(StepArgs), vp], C.c_int),
         "t1env_critic_heights": ([vp, i32, i32, f32, vp, vp, vp, vp], C.c_int),
     }
     for name, (args, res) in sig.items():

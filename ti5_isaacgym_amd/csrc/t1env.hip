@@ -303,11 +303,13 @@ __global__ __launch_bounds__(BLOCK) void k_init(const DynModel* __restrict__ Mp,
 }
 
 // reset_idx(arange(N)) -- LeggedRobot.reset() (legged_robot.py:450-455)
+// reset_idx of every env (mask == nullptr: t1env_reset_all) or of the masked envs (t1env_reset_idx)
 __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
-                                                     t1env_buffers B, t1env_step_args A) {
+                                                     t1env_buffers B, t1env_step_args A,
+                                                     const uint8_t* __restrict__ mask) {
   const int n0 = blockIdx.x * BLOCK + threadIdx.x;
   const t1env_config& C = *Cp;
-  const bool live = n0 < C.num_envs;
+  const bool live = n0 < C.num_envs && (mask == nullptr || mask[n0] != 0);
   const int n = live ? n0 : C.num_envs - 1;
   float contrib[T1_NREW];
   for (int k = 0; k < T1_NREW; ++k) contrib[k] = live ? B.episode_sums[(size_t)k * C.num_envs + n] : 0.0f;
@@ -317,6 +319,18 @@ __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict_
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   reset_env(*Mp, C, B, A, n, genv, A.counter, true);
   resample_commands(C, B, A, n, genv, A.counter);
+}
+
+// reset_idx's obs / critic history clearing (t1_dh_stand_env.py:553-558) for the masked envs: every frame of
+// their rows in the buffer the next step shifts from; one workgroup per env
+__global__ __launch_bounds__(256) void k_zero_masked_rows(float* __restrict__ obs, float* __restrict__ priv,
+                                                          const uint8_t* __restrict__ mask, int N) {
+  const int n = blockIdx.x;
+  if (n >= N || mask[n] == 0) return;
+  float* o = obs + (size_t)n * (T1_NOBS * T1_HIST);
+  for (int c = threadIdx.x; c < T1_NOBS * T1_HIST; c += blockDim.x) o[c] = 0.0f;
+  float* p = priv + (size_t)n * (T1_NPRIV * T1_CHIST);
+  for (int c = threadIdx.x; c < T1_NPRIV * T1_CHIST; c += blockDim.x) p[c] = 0.0f;
 }
 
 // coarse height bound: out[ci][cj] = max height sample of rows [(ci-K)c, (ci+K+1)c] x cols [(cj-K)c, (cj+K+1)c]
@@ -620,7 +634,8 @@ int t1env_reset_all(t1env* e, const t1env_step_args* a, void* stream) {
   if (!e || !a) return fail(T1ENV_E_ARG, "t1env_reset_all: null argument");
   hipStream_t s = (hipStream_t)stream;
   const int N = e->cfg.num_envs;
-  hipLaunchKernelGGL(k_reset_all, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a);
+  hipLaunchKernelGGL(k_reset_all, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,
+                     (const uint8_t*)nullptr);
   HIP_TRY(hipGetLastError());
   if (e->cfg.terrain_curriculum) {
     hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
@@ -633,6 +648,25 @@ int t1env_reset_all(t1env* e, const t1env_step_args* a, void* stream) {
     HIP_TRY(hipMemsetAsync(e->buf.obs_buf[k], 0, sizeof(float) * (size_t)N * T1_NOBS * T1_HIST, s));
     HIP_TRY(hipMemsetAsync(e->buf.priv_buf[k], 0, sizeof(float) * (size_t)N * T1_NPRIV * T1_CHIST, s));
   }
+  return 0;
+}
+
+int t1env_reset_idx(t1env* e, const uint8_t* mask, const t1env_step_args* a, void* stream) {
+  if (!e || !mask || !a) return fail(T1ENV_E_ARG, "t1env_reset_idx: null argument");
+  if (a->obs_slot & ~1) return fail(T1ENV_E_ARG, "t1env_reset_idx: obs_slot must be 0 or 1");
+  hipStream_t s = (hipStream_t)stream;
+  const int N = e->cfg.num_envs;
+  hipLaunchKernelGGL(k_reset_all, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a, mask);
+  HIP_TRY(hipGetLastError());
+  if (e->cfg.terrain_curriculum) {
+    hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg, (int)(a->counter % T1ENV_EXTRAS_RING));
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_zero_masked_rows, dim3(N), dim3(256), 0, s, e->buf.obs_buf[a->obs_slot],
+                     e->buf.priv_buf[a->obs_slot], mask, N);
+  HIP_TRY(hipGetLastError());
   return 0;
 }
 

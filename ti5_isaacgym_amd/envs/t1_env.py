@@ -547,6 +547,27 @@ class T1DHStandEnv(VecEnv):
                 t.zero_()
         self._fill_extras(self.common_step_counter % EXTRAS_RING)
 
+    def reset_idx(self, env_ids):
+        """reset_idx(env_ids) between steps (t1_dh_stand_env.py:483-559): the same per-env reset as a step's, keyed by
+        common_step_counter; extras["episode"] = means over env_ids.  The cleared history rows are zeroed in the
+        buffer the next step shifts from, i.e. in place in the current obs_buf / privileged_obs_buf (the
+        reference's stacked obs_buf keeps the old rows until the next step)."""
+        ids = torch.as_tensor(env_ids, device=self.device, dtype=torch.long).flatten()
+        if ids.numel() == 0:
+            return
+        if self.cfg.commands.curriculum and self.common_step_counter % self.max_episode_length == 0 and \
+                "tracking_lin_vel" in self.episode_sums:
+            self._command_curriculum(float(self.episode_sums["tracking_lin_vel"][ids].sum()), float(ids.numel()))
+        mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        mask[ids] = 1
+        a = self._args(self.common_step_counter)
+        a.obs_slot = self._slot ^ 1   # the buffer holding the current observations
+        _lib.check(self._lib.t1env_reset_idx(self._handle, _ptr(mask), _lib.C.byref(a), self._stream()),
+                   "t1env_reset_idx")
+        if self.measure_heights:
+            self._priv_ext[self._slot ^ 1][ids] = 0.0
+        self._fill_extras(self.common_step_counter % EXTRAS_RING)
+
     def reset(self):
         """LeggedRobot.reset (legged_robot.py:450-455)."""
         self.reset_idx_all()
