@@ -1,0 +1,44 @@
+"""env.reset_idx(env_ids) between steps on the real-physics path (t1env_reset_idx), 8192 envs on trimesh: the
+masked envs restart (episode length 0, reset flag, zeroed history in the buffer the next step shifts from, DR
+redrawn), the others are untouched, and after the next step the masked envs' 65 older obs frames / 2 older
+critic frames are zero while the other envs' history is the shifted previous one.  The golden scenario
+resetidx16 (test_gpu_parity.py) pins the values against the reference's own reset_idx."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_reset_idx_between_steps():
+    from ti5_isaacgym_amd import make_t1_env
+    n = 8192
+    env = make_t1_env(num_envs=n, mesh_type="trimesh", seed=9, device="cuda:0")
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    for _ in range(5):
+        env.step(0.3 * torch.randn(n, 12, device="cuda:0", generator=g))
+    ids = torch.arange(3, n, 97, device="cuda:0")
+    mask = torch.zeros(n, dtype=torch.bool, device="cuda:0")
+    mask[ids] = True
+    kp_before = env.randomized_p_gains.clone()
+    el_before = env.episode_length_buf.clone()
+    obs_prev = env.obs_buf.clone()
+    env.reset_idx(ids)
+    torch.cuda.synchronize()
+    assert (env.episode_length_buf[mask] == 0).all()
+    assert torch.equal(env.episode_length_buf[~mask], el_before[~mask])
+    assert env.reset_buf[mask].all()
+    assert not env.obs_buf[mask].any() and not env.privileged_obs_buf[mask].any()
+    assert torch.equal(env.obs_buf[~mask], obs_prev[~mask])
+    assert not torch.equal(env.randomized_p_gains[mask], kp_before[mask])
+    assert torch.equal(env.randomized_p_gains[~mask], kp_before[~mask])
+    ep = env.extras["episode"]
+    assert all(torch.isfinite(torch.as_tensor(v)).all() for v in ep.values())
+    prev = env.obs_buf.clone()
+    env.step(0.3 * torch.randn(n, 12, device="cuda:0", generator=g))
+    r = env.reset_buf.bool() | mask
+    assert not env.obs_buf[mask, :-47].any() and not env.privileged_obs_buf[mask, :-73].any()
+    keep = ~r
+    torch.testing.assert_close(env.obs_buf[keep, :-47], prev[keep, 47:], rtol=0, atol=0)
+    assert (env.episode_length_buf[mask & ~env.reset_buf.bool()] == 1).all()
+    assert torch.isfinite(env.obs_buf).all() and torch.isfinite(env.root_states).all()
