@@ -61,7 +61,7 @@ def parse():
                         "0 = never, 1 = every step)")
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01m.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02a.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
     return p.parse_args()
 
