@@ -188,6 +188,24 @@ typedef struct t1env_injected {
   float* torque_log;       /* (decimation, N, 12) out: torques sent per substep, or NULL */
 } t1env_injected;
 
+/* Substep log of the product step (tests): what the dynamics kernel handed to each substep's post-simulate code,
+ * in the Gym layouts the reference's Python sees after refresh_*_tensor (legged_robot.py:405-434).  With a log set,
+ * t1env_step's fused launch (k_dyn4, the product kernel) also writes, for every substep s:
+ *   root[s]   (decimation, N, 13) root state after substep s (pos, quat xyzw, COM lin vel, ang vel; world),
+ *             before post-physics (pushes, resets) -- root[decimation-1] is what post-physics starts from
+ *   dof[s]    (decimation, N, 12, 2) dof state after substep s
+ *   torque[s] (decimation, N, 12) the torques _compute_torques produced for substep s
+ * rigid_state / contact_forces are the end-of-step values already (post-physics never writes them).  Replaying
+ * these states through the oracle's injected-physics step re-derives the PD torques, lag captures, observations
+ * and rewards of the product kernel (tests/test_gpu_product_parity.py).  log = NULL switches it off.  Only the
+ * fused step logs: while a log is set, t1env_step on a split step and t1env_step_physics_and_rewards fail
+ * (T1ENV_E_STATE) rather than leave substeps unlogged. */
+typedef struct t1env_substep_log {
+  float* root;
+  float* dof;
+  float* torque;
+} t1env_substep_log;
+
 typedef struct t1env t1env;
 
 int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_buffers* bufs, t1env** out);
@@ -237,6 +255,7 @@ int t1env_critic_heights(t1env* env, int32_t obs_slot, int32_t npts, float scale
  * (physics_and_rewards + reset_and_observe) instead; both give the same buffers.  The split entry points are
  * unaffected (they are what command-curriculum steps use). */
 int t1env_set_fused(t1env* env, int32_t enable);
+int t1env_set_substep_log(t1env* env, const t1env_substep_log* log);
 /* Per-kernel timing with HIP events recorded around every launch (bench.py's live roofline).  Ids:
  * 0 k_dynamics incl. its history-shift workgroups (or the injected-physics kernel), 1 k_post_a, 2 k_post_b (its
  * last block also finalises the extras), 3 stand-alone k_shift (injected physics or phase B without phase A),

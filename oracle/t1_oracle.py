@@ -66,6 +66,11 @@ EXT_TORQUE_MAX = 0.0                  # :200
 EXT_INTERVAL = float(np.ceil(4 / DT))     # legged_robot.py:113 -> 400
 ADD_UPDATE_STEP = 4000 * 24               # :202
 ADD_DURATION = (0.0, 0.05, 0.1, 0.15)     # :203
+PUSH_INTERVAL_S = 6                       # :190 (push_robots = False by default, :188)
+PUSH_UPDATE_STEP = 2500 * 24              # :191
+PUSH_DURATION = (0, 0.05, 0.1, 0.15, 0.2, 0.25, 0.3)  # :192
+MAX_PUSH_VEL_XY = 0.2                     # :193
+MAX_PUSH_ANG_VEL = 0.2                    # :194
 ARMATURE_RANGE = [(0.15 * 0.8, 0.15 * 1.2), (0.15 * 0.8, 0.15 * 1.2), (3.6 * 0.5, 3.6 * 1.0),
                   (3.6 * 0.5, 3.6 * 1.0), (0.1 * 0.5, 0.1 * 1.1), (0.028 * 0.5, 0.028 * 1.5)] * 2  # :273-285
 REWARD_SCALES = dict(joint_pos=4, feet_clearance=1, feet_contact_number=1.2, feet_air_time=1, foot_slip=-0.5,
@@ -149,10 +154,11 @@ class T1Oracle:
     (root (N,13), dof (N,12,2), rigid (N,13,13), contact (N,13,3)) after global substep g."""
 
     def __init__(self, num_envs, seed=5, mesh_type="plane", terrain=None, env_offset=0, reduce_fn=None,
-                 measure_heights=False):
+                 measure_heights=False, push_robots=False, push_interval_s=PUSH_INTERVAL_S):
         """reduce_fn: sharded runs only -- (sum, count) -> (sum, count) over all ranks, so the command
         curriculum sees the same mean as an unsharded run.  measure_heights: the height scan
-        (inactive in DHT1StandCfg): 187 heights appended to every critic frame (260 per frame)."""
+        (inactive in DHT1StandCfg): 187 heights appended to every critic frame (260 per frame).  push_robots /
+        push_interval_s: domain_rand.push_robots (off in DHT1StandCfg, on in BASELINE config 5)."""
         N = num_envs
         self.N, self.seed, self.env_offset = N, int(seed), int(env_offset)
         self.reduce_fn = reduce_fn
@@ -169,6 +175,8 @@ class T1Oracle:
         self.noise_vec[44:47] = f32(0.1 * OBS_SCALES["quat"])
         self.common_step_counter = 0
         self.substep_counter = 0
+        self.push_robots = bool(push_robots)
+        self.push_interval = float(np.ceil(push_interval_s / DT))          # legged_robot.py:112
         # creation-time DR (legged_robot.py:692-730, 786-824, 852-885)
         self.payload = R.rand_float(-2.5, 2.5, seed, self.ids, 0, R.SLOT_PAYLOAD)
         self.body_mass = (f32(BASE_MASS) + self.payload).astype(f32)
@@ -370,6 +378,13 @@ class T1Oracle:
         self._resample_commands()
         if self.measure_heights:                                 # t1_dh_stand_env.py:190-191
             self.measured_heights = self._get_heights()
+        if self.push_robots:                                     # t1_dh_stand_env.py:193-202
+            i = min(int(self.common_step_counter / PUSH_UPDATE_STEP), len(PUSH_DURATION) - 1)
+            if self.common_step_counter % self.push_interval <= PUSH_DURATION[i] / DT:
+                self._push_robots()
+            else:
+                self.rand_push_force[:] = 0
+                self.rand_push_torque[:] = 0
         i = int(self.common_step_counter / ADD_UPDATE_STEP)
         i = min(i, len(ADD_DURATION) - 1)
         duration = ADD_DURATION[i] / DT
@@ -379,6 +394,19 @@ class T1Oracle:
             self.ext_forces[:] = 0
             self.ext_torques[:] = 0
             self.is_first_add_force = True
+
+    def _push_robots(self):
+        """t1_dh_stand_env.py:217-231: root linear velocity xy U(+-0.2) and angular velocity U(+-0.2) of EVERY env,
+        redrawn on every call (`is_first_push = False` is commented out, :227), written into the root state the
+        next simulate() starts from (set_actor_root_state_tensor, :230).  The base quantities of this step were
+        taken before the callback, so only the root state (base_acc, last_root_vel, the next step) sees it."""
+        allids = np.arange(self.N)
+        self.rand_push_force[:, :2] = np.stack([self._rf(-MAX_PUSH_VEL_XY, MAX_PUSH_VEL_XY, allids, R.SLOT_PUSH_VEL + k)
+                                                for k in range(2)], 1)
+        self.rand_push_torque = np.stack([self._rf(-MAX_PUSH_ANG_VEL, MAX_PUSH_ANG_VEL, allids, R.SLOT_PUSH_ANG + k)
+                                          for k in range(3)], 1)
+        self.root[:, 7:9] = self.rand_push_force[:, :2]
+        self.root[:, 10:13] = self.rand_push_torque
 
     def _add_ext_force(self):
         """t1_dh_stand_env.py:233-247: forces drawn on the first call, applied (base, standing envs only)

@@ -67,13 +67,16 @@ def snapshot(env):
 
 
 def run(name, num_envs=16, mesh_type="plane", n_steps=10, cfg_hook=None, after_reset=None, act_scale=0.5,
-        mid_reset=None):
-    """mid_reset = (t, env_ids): the reference's reset_idx(env_ids) called between step t and step t + 1."""
+        mid_reset=None, cfg_keys=None):
+    """mid_reset = (t, env_ids): the reference's reset_idx(env_ids) called between step t and step t + 1.
+    cfg_keys: config values the scenario's cfg_hook changed, stored as cfg_<key> so the replays set the same."""
     env, cfg, gym = refenv.make_env(num_envs, mesh_type, cfg_hook)
     assert list(env.reward_names) == REWARD_NAMES, env.reward_names
     gym.provider = make_provider(env, num_envs, SYNTH_SEED)
     out = {"num_envs": np.int64(num_envs), "synth_seed": np.int64(SYNTH_SEED), "seed": np.int64(cfg.seed),
            "mesh_type": np.array(mesh_type)}
+    for k, v in (cfg_keys or {}).items():
+        out["cfg_" + k] = np.asarray(v)
     init = {
         "env_frictions": _np(env.env_frictions), "body_mass": _np(env.body_mass),
         "payload_masses": _np(env.payload_masses), "link_masses": _np(env.link_masses),
@@ -190,6 +193,15 @@ def heights_hook(cfg):
     cfg.terrain.terrain_proportions = [0.0, 0.25, 0.25, 0.25, 0.25, 0.0, 0.0, 0.0, 0.0, 0.0]
 
 
+PUSH_INTERVAL_S = 0.03   # push_interval = 3 steps: pushes at counters 3, 6, 9 (duration index 0 -> counter % 3 == 0)
+
+
+def push_hook(cfg):
+    # BASELINE config 5's push perturbation (t1_dh_stand_env.py:193-202, 217-231), off in DHT1StandCfg (:188)
+    cfg.domain_rand.push_robots = True
+    cfg.domain_rand.push_interval_s = PUSH_INTERVAL_S
+
+
 SCENARIOS = {
     "plane16": lambda: run("plane16", 16, "plane", 10, after_reset=plane16_overrides),
     "events16": lambda: run("events16", 16, "plane", 14, after_reset=events16_overrides),
@@ -197,6 +209,8 @@ SCENARIOS = {
     "trimesh16": lambda: run("trimesh16", 16, "trimesh", 6, cfg_hook=trimesh_hook, after_reset=trimesh_overrides),
     "resetidx16": lambda: run("resetidx16", 16, "trimesh", 6, cfg_hook=trimesh_hook, mid_reset=(2, [1, 4, 9, 15])),
     "heights16": lambda: run("heights16", 16, "trimesh", 6, cfg_hook=heights_hook, after_reset=trimesh_overrides),
+    "push16": lambda: run("push16", 16, "plane", 10, cfg_hook=push_hook, after_reset=plane16_overrides,
+                          cfg_keys={"push_interval_s": PUSH_INTERVAL_S}),
 }
 
 if __name__ == "__main__":

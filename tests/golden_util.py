@@ -6,7 +6,7 @@ import numpy as np
 import synth
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16", "heights16", "resetidx16"]
+SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16", "heights16", "resetidx16", "push16"]
 
 
 def load(name):
@@ -29,6 +29,11 @@ def mid_reset(fx, t):
     if "mid_reset_step" in fx and int(fx["mid_reset_step"]) == t:
         return fx["mid_reset_ids"]
     return None
+
+
+def push_interval_s(fx):
+    """push_robots scenario (push16): the scenario's push_interval_s, else None (push_robots off, the default)"""
+    return float(fx["cfg_push_interval_s"]) if "cfg_push_interval_s" in fx else None
 
 
 def measures_heights(fx):

@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 import synth
-from golden_util import assert_close, load, measures_heights, mid_reset
+from golden_util import assert_close, load, measures_heights, mid_reset, push_interval_s
 
 REWARD_NAMES = sorted(["joint_pos", "feet_clearance", "feet_contact_number", "feet_air_time", "foot_slip",
                        "feet_distance", "knee_distance", "feet_rotation", "feet_contact_forces",
@@ -24,12 +24,17 @@ def make_env_for(fx, device="cuda:0"):
 
     name_hook = None
     heights = measures_heights(fx)
+    push = push_interval_s(fx)
     if str(fx["mesh_type"]) == "trimesh":
         def name_hook(cfg):
             cfg.terrain.num_rows, cfg.terrain.num_cols, cfg.terrain.border_size = 6, 4, 5
             if heights:   # gen_golden.heights_hook
                 cfg.terrain.measure_heights = True
                 cfg.terrain.terrain_proportions = [0.0, 0.25, 0.25, 0.25, 0.25, 0.0, 0.0, 0.0, 0.0, 0.0]
+    if push is not None:   # gen_golden.push_hook
+        def name_hook(cfg):
+            cfg.domain_rand.push_robots = True
+            cfg.domain_rand.push_interval_s = push
     env = make_t1_env(num_envs=int(fx["num_envs"]), mesh_type=str(fx["mesh_type"]), seed=int(fx["seed"]),
                       device=device, cfg_hook=name_hook)
     if heights:

@@ -6,7 +6,8 @@ bool / integer state.  Obs/priv are compared after clipping, as returned by step
 import numpy as np
 import pytest
 
-from golden_util import SCENARIOS, assert_close, load, measures_heights, mid_reset, synth_physics, terrain_of
+from golden_util import (SCENARIOS, assert_close, load, measures_heights, mid_reset, push_interval_s, synth_physics,
+                         terrain_of)
 from oracle import rng as R
 from oracle.t1_oracle import REWARD_NAMES, T1Oracle
 
@@ -14,8 +15,10 @@ from oracle.t1_oracle import REWARD_NAMES, T1Oracle
 def run_oracle(fx):
     n = int(fx["num_envs"])
     terrain = terrain_of(fx)
+    push = push_interval_s(fx)
     o = T1Oracle(n, seed=int(fx["seed"]), mesh_type=str(fx["mesh_type"]), terrain=terrain,
-                 measure_heights=measures_heights(fx))
+                 measure_heights=measures_heights(fx), push_robots=push is not None,
+                 **({"push_interval_s": push} if push is not None else {}))
     phys = synth_physics(fx)
     outs = []
     o.reset(phys)

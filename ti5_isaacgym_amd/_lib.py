@@ -83,10 +83,14 @@ class Injected(C.Structure):
     _fields_ = [("root", fp), ("dof", fp), ("rigid", fp), ("contact", fp), ("torque_log", fp)]
 
 
+class SubstepLog(C.Structure):
+    _fields_ = [("root", fp), ("dof", fp), ("torque", fp)]
+
+
 EXPORTS = ["t1env_create", "t1env_destroy", "t1env_init", "t1env_set_terrain", "t1env_reset_all", "t1env_step",
            "t1env_step_physics_and_rewards", "t1env_step_reset_and_observe", "t1env_step_injected",
            "t1env_set_fused", "t1env_set_timing", "t1env_get_timing", "t1env_last_error", "t1env_version",
-           "t1env_measure_heights", "t1env_critic_heights", "t1env_reset_idx"]
+           "t1env_measure_heights", "t1env_critic_heights", "t1env_reset_idx", "t1env_set_substep_log"]
 
 _lib = None
 
@@ -112,6 +116,7 @@ def load():
         "t1env_step_reset_and_observe": ([vp, P(StepArgs), vp], C.c_int),
         "t1env_step_injected": ([vp, vp, P(StepArgs), P(Injected), vp], C.c_int),
         "t1env_set_fused": ([vp, i32], C.c_int),
+        "t1env_set_substep_log": ([vp, P(SubstepLog)], C.c_int),
         "t1env_set_timing": ([vp, i32], C.c_int),
         "t1env_get_timing": ([vp, C.POINTER(C.c_double), i32p], C.c_int),
         "t1env_last_error": ([], C.c_char_p),

@@ -69,6 +69,8 @@ struct t1env {
   unsigned* d_done;       // k_post_b block-completion counter (its last block finalises the extras)
   int16_t* d_hmax;        // coarse terrain height bound (Terrain::hmax), built by t1env_set_terrain
   float max_contact_radius;
+  SubLog log;             // t1env_set_substep_log (tests): fused steps write it
+  int log_on;
 };
 
 // k_physics_injected: the same decimation loop with the physics states supplied by the caller (golden
@@ -494,6 +496,7 @@ static int launch_shift(t1env* e, const t1env_step_args* a, hipStream_t s) {
 static int launch_physics(t1env* e, const float* actions, const t1env_step_args* a, const t1env_injected* inj,
                           hipStream_t s) {
   if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
+  if (e->log_on && !inj) return fail(T1ENV_E_STATE, "substep log set: only the fused step logs (t1env_set_substep_log)");
   const int N = e->cfg.num_envs;
   e->step_timer = t_begin(e, 5, s);
   // large N: the shift as its own launch ahead of the dynamics (k_post_b zeroes the reset rows)
@@ -564,7 +567,7 @@ static int launch_fused(t1env* e, const float* actions, const t1env_step_args* a
   const int t = t_begin(e, 0, s);
   const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch, pre ? 1 : 0};
   HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, e->cfg.num_envs,
-                                         shift_args(e, a), e->dyn, &FA, s, pre));
+                                         shift_args(e, a), e->dyn, &FA, s, pre, e->log_on ? &e->log : nullptr));
   t_end(e, t, s);
   t_end(e, e->step_timer, s);
   e->step_timer = -1;
@@ -575,6 +578,20 @@ static int launch_fused(t1env* e, const float* actions, const t1env_step_args* a
 int t1env_set_fused(t1env* e, int32_t enable) {
   if (!e) return fail(T1ENV_E_ARG, "t1env_set_fused: null env");
   e->fused = enable ? 1 : 0;
+  return 0;
+}
+
+int t1env_set_substep_log(t1env* e, const t1env_substep_log* log) {
+  if (!e) return fail(T1ENV_E_ARG, "t1env_set_substep_log: null env");
+  if (!log) {
+    e->log_on = 0;
+    e->log = SubLog{};
+    return 0;
+  }
+  if (!log->root || !log->dof || !log->torque) return fail(T1ENV_E_ARG, "t1env_set_substep_log: null buffer");
+  if (e->dyn.waves != 4) return fail(T1ENV_E_STATE, "t1env_set_substep_log: the log is written by k_dyn4 only");
+  e->log = SubLog{log->root, log->dof, log->torque};
+  e->log_on = 1;
   return 0;
 }
 

@@ -285,7 +285,7 @@ __global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restri
                                                         const t1env_config* __restrict__ Cp, t1env_buffers B,
                                                         Terrain Tin, const float* __restrict__ actions,
                                                         t1env_step_args A, ShiftArgs S, int dyn_blocks,
-                                                        FusedArgs FA) {
+                                                        FusedArgs FA, SubLog) {
   __shared__ float xch[2][2][XCH][DYN_ENVS];  // [substep parity][leg][value][env]
   if ((int)blockIdx.x >= dyn_blocks) {
     shift_workgroup<FUSED, DYN_BLOCK>(S, FA, Cp->num_envs, blockIdx.x - dyn_blocks, gridDim.x - dyn_blocks,
@@ -650,6 +650,18 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
   T1_PROF_MARK(15);
 }
 
+// the Gym root-state row (pos, quat xyzw, COM linear velocity, angular velocity; world) of the internal base state
+// (base-origin velocity): the report's root and the substep log's root rows
+__device__ __forceinline__ void root_row(const DynModel& M, const BaseParams<float>& PB, const BaseState<float>& sb,
+                                         const BaseFrame<float>& F, float body[13]) {
+  const V3<float> c0 = base_com(M, PB, F.R0);
+  const V3<float> vcom = v3<float>(sb.vo[0], sb.vo[1], sb.vo[2]) + cross(v3<float>(sb.w[0], sb.w[1], sb.w[2]), c0);
+  const float r[13] = {sb.pos[0], sb.pos[1], sb.pos[2], sb.quat[0], sb.quat[1], sb.quat[2], sb.quat[3],
+                       vcom.x, vcom.y, vcom.z, sb.w[0], sb.w[1], sb.w[2]};
+#pragma unroll
+  for (int i = 0; i < 13; ++i) body[i] = r[i];
+}
+
 // k_dyn4's report, split between the waves: the leg wave writes its bodies' rigid states (and the root for
 // leg 0), zeros the contact rows of its bodies without contact points, and publishes the end-of-step base frame
 // and contact-body poses; after a barrier the helper evaluates the contact forces of the shank, foot (and the
@@ -662,10 +674,8 @@ __device__ __forceinline__ void leg_report_rigid(const DynModel& M, const t1env_
   float* rig = B.rigid_state + (size_t)n * 169;
   float* cf = B.contact_forces + (size_t)n * 39;
   if (leg == 0) {
-    const V3<float> c0 = base_com(M, PB, F.R0);
-    const V3<float> vcom = v3<float>(sb.vo[0], sb.vo[1], sb.vo[2]) + cross(v3<float>(sb.w[0], sb.w[1], sb.w[2]), c0);
-    const float body[13] = {sb.pos[0], sb.pos[1], sb.pos[2], sb.quat[0], sb.quat[1], sb.quat[2], sb.quat[3],
-                            vcom.x, vcom.y, vcom.z, sb.w[0], sb.w[1], sb.w[2]};
+    float body[13];
+    root_row(M, PB, sb, F, body);
     if (active)
 #pragma unroll
       for (int i = 0; i < 13; ++i) { B.root_states[(size_t)n * 13 + i] = body[i]; rig[i] = body[i]; }
@@ -741,10 +751,14 @@ __device__ __forceinline__ void helper_report_contacts(const DynModel& M, const 
   }
 }
 
-template <bool HF, bool FUSED>
+// LOG (tests only, fused step): the substep log (t1env_substep_log) -- each leg wave writes its joints' torques and
+// post-substep (q, qd), leg wave 0 the post-substep root row; a separate instantiation, so the product kernel is
+// unchanged by it.
+template <bool HF, bool FUSED, bool LOG = false>
 __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
                                                    t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
-                                                   t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA) {
+                                                   t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA,
+                                                   SubLog LG) {
   __shared__ Dyn4Lds lds;
   if ((int)blockIdx.x >= dyn_blocks) {
     shift_workgroup<FUSED, D4_BLOCK>(S, FA, Cp->num_envs, blockIdx.x - dyn_blocks, gridDim.x - dyn_blocks,
@@ -904,6 +918,25 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
     integrate_base(sb, r, dt);
     integrate_leg(M, leg, q, qd, dq, dt);
     T1_PROF_MARK(9);
+    if constexpr (LOG) {
+      if (active) {
+        const size_t row = (size_t)sub * N + n;
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) {
+          LG.torque[row * 12 + j0 + k] = tau[k];
+          LG.dof[row * 24 + 2 * (j0 + k)] = q[k];
+          LG.dof[row * 24 + 2 * (j0 + k) + 1] = qd[k];
+        }
+        if (leg == 0) {
+          BaseFrame<float> FL;
+          base_frame(sb, FL);
+          float body[13];
+          root_row(M, PB, sb, FL, body);
+#pragma unroll
+          for (int i = 0; i < 13; ++i) LG.root[row * 13 + i] = body[i];
+        }
+      }
+    }
     if (sub == L.s_dof) {
 #pragma unroll
       for (int k = 0; k < NLEG; ++k) { CAP[k][lane] = q[k]; CAP[NLEG + k][lane] = qd[k]; }
@@ -976,7 +1009,8 @@ bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg) {
 
 int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
                        const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
-                       const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s, bool shift_prelaunched) {
+                       const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s, bool shift_prelaunched,
+                       const SubLog* log) {
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
   // history-shift workgroups: the workgroup slots the dynamics leave free (a wave of either kernel holds a
   // whole SIMD's registers: 2 workgroups/CU for k_dynamics, 1 for k_dyn4), at least MIN_SHIFT_BLOCKS; none
@@ -986,10 +1020,21 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
   if (shift_blocks < MIN_SHIFT_BLOCKS) shift_blocks = MIN_SHIFT_BLOCKS;
   if (shift_prelaunched) shift_blocks = 0;
   const FusedArgs FA = fused ? *fused : FusedArgs{};
+  const SubLog LG = log ? *log : SubLog{};
   const dim3 grid(dyn_blocks + shift_blocks);
-#define T1_LAUNCH(KERNEL, BS, HF, FU) \
-  hipLaunchKernelGGL((KERNEL<HF, FU>), grid, dim3(BS), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA)
   const bool hf = T.type != 0;
+  if (log) {  // the substep log: fused k_dyn4 only (the caller checks)
+    if (cfg.waves != 4 || !fused) return (int)hipErrorInvalidValue;
+    if (hf)
+      hipLaunchKernelGGL((k_dyn4<true, true, true>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S,
+                         dyn_blocks, FA, LG);
+    else
+      hipLaunchKernelGGL((k_dyn4<false, true, true>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S,
+                         dyn_blocks, FA, LG);
+    return (int)hipGetLastError();
+  }
+#define T1_LAUNCH(KERNEL, BS, HF, FU) \
+  hipLaunchKernelGGL((KERNEL<HF, FU>), grid, dim3(BS), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA, LG)
   if (cfg.waves == 4) {
     if (fused) { if (hf) T1_LAUNCH(k_dyn4, D4_BLOCK, true, true); else T1_LAUNCH(k_dyn4, D4_BLOCK, false, true); }
     else { if (hf) T1_LAUNCH(k_dyn4, D4_BLOCK, true, false); else T1_LAUNCH(k_dyn4, D4_BLOCK, false, false); }

@@ -16,6 +16,13 @@ struct FusedArgs {
                                    //    the epilogue zeroes its reset rows directly, no handoff
 };
 
+// substep log of the fused k_dyn4 (t1env_substep_log; all null = off)
+struct SubLog {
+  float* root;
+  float* dof;
+  float* torque;
+};
+
 // launch shape of the dynamics kernel
 struct DynLaunch {
   int waves;         // 4: k_dyn4 (leg waves + contact helper waves, default), 2: k_dynamics
@@ -26,11 +33,11 @@ int t1_dyn_waves_default();
 
 // dynamics launch (t1env_dynamics.hip) plus history-shift workgroups running the shift S; fused != nullptr:
 // the whole step (post-physics in the epilogue).  shift_prelaunched: the caller already enqueued the shift as
-// its own launch (no shift workgroups).  Returns a hipError_t.
+// its own launch (no shift workgroups).  log: the substep log (fused k_dyn4 only).  Returns a hipError_t.
 int t1_launch_dynamics(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B,
                        const t1::Terrain& T, const float* actions, const t1env_step_args& A, int num_envs,
                        const t1::ShiftArgs& S, const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s,
-                       bool shift_prelaunched = false);
+                       bool shift_prelaunched = false, const SubLog* log = nullptr);
 // Whether the history shift should run as its own launch ahead of the dynamics: the dynamics workgroups (one
 // per CU for k_dyn4: 148 KB of LDS) leave fewer than MIN_SHIFT_BLOCKS CUs idle, and shift workgroups of the
 // dynamics launch would each hold a whole CU's LDS for a small slice of the 26 KB/env stream.

@@ -578,6 +578,23 @@ class T1DHStandEnv(VecEnv):
         """t1env_step as one fused launch (default) or the split kernel sequence (same results; tests)."""
         _lib.check(self._lib.t1env_set_fused(self._handle, int(bool(enable))), "t1env_set_fused")
 
+    def set_substep_log(self, enable=True):
+        """Test hook (t1env_set_substep_log): every following fused step also writes its per-substep root / dof
+        states and torques to ``self.substep_log`` = dict(root (dec, N, 13), dof (dec, N, 12, 2), torque (dec, N, 12)),
+        the states the reference's post-simulate code would see.  Split steps (command curriculum, height scan)
+        raise while it is on."""
+        if not enable:
+            _lib.check(self._lib.t1env_set_substep_log(self._handle, None), "t1env_set_substep_log")
+            self.substep_log = None
+            return
+        dec, N, d = self.cfg.control.decimation, self.num_envs, self.device
+        self.substep_log = dict(root=torch.zeros(dec, N, 13, device=d), dof=torch.zeros(dec, N, 12, 2, device=d),
+                                torque=torch.zeros(dec, N, 12, device=d))
+        lg = _lib.SubstepLog()
+        for k, t in self.substep_log.items():
+            setattr(lg, k, _lib.C.cast(t.data_ptr(), _lib.fp))
+        _lib.check(self._lib.t1env_set_substep_log(self._handle, _lib.C.byref(lg)), "t1env_set_substep_log")
+
     def set_timing(self, enable=True, reset=True):
         """Record HIP events around every kernel launch (bench.py's live per-kernel timing).  reset=False keeps
         the events recorded so far (bench.py samples every k-th step)."""
