@@ -2,7 +2,8 @@
 
 TEST INFRASTRUCTURE (oracle/): only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
 may import this package.  The product kernels carry their own copy of the same function in
-``ti5_isaacgym_amd/csrc/t1_rng.h``; ``tests/test_rng.py`` pins the two against each other.
+``ti5_isaacgym_amd/csrc/t1_common.h``; ``tests/test_rng.py`` compiles that header for the host and pins the two
+against each other.
 
 Why a counter RNG: the reference draws from torch's global generator in call order
 (``torch_rand_float`` / ``torch.rand_like`` / ``torch.randint``; e.g. legged_robot.py:1071,
@@ -24,6 +25,11 @@ Definition (all arithmetic mod 2**32):
 import numpy as np
 
 M32 = np.uint64(0xFFFFFFFF)
+# reset_idx(env_ids) called BETWEEN steps keys its draws on (common_step_counter | BETWEEN_STEP_SALT): the in-step
+# resets of the step that produced that counter already used the plain counter, and an env reset in that step and
+# reset again before the next one must draw fresh DR / lags / gait / start / commands as the reference's generator
+# does (its stream simply advances).  The step counter stays below 2**31 (2400 steps/episode).
+BETWEEN_STEP_SALT = 0x80000000
 
 
 def _u32(x):

@@ -154,18 +154,20 @@ class T1Oracle:
     (root (N,13), dof (N,12,2), rigid (N,13,13), contact (N,13,3)) after global substep g."""
 
     def __init__(self, num_envs, seed=5, mesh_type="plane", terrain=None, env_offset=0, reduce_fn=None,
-                 measure_heights=False, push_robots=False, push_interval_s=PUSH_INTERVAL_S):
+                 measure_heights=False, push_robots=False, push_interval_s=PUSH_INTERVAL_S, terrain_curriculum=True):
         """reduce_fn: sharded runs only -- (sum, count) -> (sum, count) over all ranks, so the command
         curriculum sees the same mean as an unsharded run.  measure_heights: the height scan
         (inactive in DHT1StandCfg): 187 heights appended to every critic frame (260 per frame).  push_robots /
-        push_interval_s: domain_rand.push_robots (off in DHT1StandCfg, on in BASELINE config 5)."""
+        push_interval_s: domain_rand.push_robots (off in DHT1StandCfg, on in BASELINE config 5).  terrain_curriculum:
+        cfg.terrain.curriculum (on in DHT1StandCfg; off: levels drawn over every row, no level updates, start xy
+        within terrain_length / 2, legged_robot.py:1103-1108, 1487)."""
         N = num_envs
         self.N, self.seed, self.env_offset = N, int(seed), int(env_offset)
         self.reduce_fn = reduce_fn
         self.ids = np.arange(N, dtype=np.int64) + env_offset
         self.mesh_type = mesh_type
-        self.curriculum = mesh_type in ("heightfield", "trimesh")   # legged_robot.py:104-105
-        self.custom_origins = self.curriculum
+        self.custom_origins = mesh_type in ("heightfield", "trimesh")   # legged_robot.py:1481-1482
+        self.curriculum = self.custom_origins and bool(terrain_curriculum)  # legged_robot.py:104-105
         self.command_ranges = dict(lin_vel_x=[-0.5, 0.5], lin_vel_y=[-0.5, 0.5], ang_vel_yaw=[-0.5, 0.5])
         self.reward_scales = {k: v * DT for k, v in REWARD_SCALES.items()}   # legged_robot.py:357-364
         self.noise_vec = np.zeros(NUM_SINGLE_OBS, f32)                       # t1_dh_stand_env.py:326-357
@@ -174,6 +176,7 @@ class T1Oracle:
         self.noise_vec[41:44] = f32(0.2 * OBS_SCALES["ang_vel"])
         self.noise_vec[44:47] = f32(0.1 * OBS_SCALES["quat"])
         self.common_step_counter = 0
+        self._key_salt = 0         # R.BETWEEN_STEP_SALT while reset_idx runs between steps
         self.substep_counter = 0
         self.push_robots = bool(push_robots)
         self.push_interval = float(np.ceil(push_interval_s / DT))          # legged_robot.py:112
@@ -196,7 +199,7 @@ class T1Oracle:
             self.terrain_origins = t["terrain_origins"].astype(f32)
             self.env_length = float(t.get("env_length", 8.0))
             self.platform = float(t.get("platform", 3.0))
-            max_init = int(t.get("max_init_terrain_level", 5))
+            max_init = int(t.get("max_init_terrain_level", 5)) if self.curriculum else self.num_rows - 1  # :1486-1487
             self.terrain_levels = R.randint(0, max_init + 1, seed, self.ids, 0, R.SLOT_TERRAIN_LEVEL_INIT)
             n_total = int(t.get("num_envs_total", N))
             self.terrain_types = np.floor(self.ids / (n_total / self.num_cols)).astype(np.int64)
@@ -274,12 +277,14 @@ class T1Oracle:
         self.force_pending = False
 
     # ---------------------------------------------------------------- random helpers
+    def _key_ctr(self):
+        return self.common_step_counter | self._key_salt
+
     def _rf(self, lo, hi, ids, slot, ctr=None):
-        return R.rand_float(lo, hi, self.seed, ids + self.env_offset, self.common_step_counter if ctr is None else ctr,
-                            slot)
+        return R.rand_float(lo, hi, self.seed, ids + self.env_offset, self._key_ctr() if ctr is None else ctr, slot)
 
     def _ri(self, lo, hi, ids, slot):
-        return R.randint(lo, hi, self.seed, ids + self.env_offset, self.common_step_counter, slot)
+        return R.randint(lo, hi, self.seed, ids + self.env_offset, self._key_ctr(), slot)
 
     # ---------------------------------------------------------------- step
     def step(self, actions, physics):
@@ -630,7 +635,15 @@ class T1Oracle:
         cr[0] = float(np.clip(cr[0] - 0.25, -1.5 / 2, 0.0))
         cr[1] = float(np.clip(cr[1] + 0.5, 0.0, 1.5))
 
-    def reset_idx(self, env_ids):
+    def reset_idx(self, env_ids, between_steps=False):
+        """t1_dh_stand_env.py:483-559.  between_steps: called by the user between two steps (not by
+        post_physics_step / reset()): the draws take the between-step key domain (oracle/rng.py BETWEEN_STEP_SALT)."""
+        if between_steps:
+            self._key_salt = R.BETWEEN_STEP_SALT
+            try:
+                return self.reset_idx(env_ids)
+            finally:
+                self._key_salt = 0
         curriculum_step = self.common_step_counter % MAX_EPISODE_LEN == 0
         if self.reduce_fn is not None and curriculum_step:
             # sharded: every rank takes part, also with no local resets (the mean is over all ranks' resets)
@@ -656,7 +669,7 @@ class T1Oracle:
         self.root[env_ids] = init
         self.root[env_ids, :3] += self.env_origins[env_ids]
         if self.custom_origins:
-            p3 = self.platform / 3
+            p3 = self.platform / 3 if self.curriculum else self.env_length / 2
             self.root[env_ids, 0] += self._rf(-p3, p3, env_ids, R.SLOT_RESET_ROOT_XY + 0)
             self.root[env_ids, 1] += self._rf(-p3, p3, env_ids, R.SLOT_RESET_ROOT_XY + 1)
         # randomize_dof_props (legged_robot.py:732-783)

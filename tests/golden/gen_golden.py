@@ -133,7 +133,12 @@ def run(name, num_envs=16, mesh_type="plane", n_steps=10, cfg_hook=None, after_r
                  extras_terrain_level=np.float32(ep.get("terrain_level", np.nan)))
         rec.append(r)
         if mid_reset is not None and t == mid_reset[0]:
-            env.reset_idx(torch.tensor(mid_reset[1], dtype=torch.long))
+            import draws   # the between-step key domain (oracle/rng.py BETWEEN_STEP_SALT)
+            draws.CTR_SALT = draws.R.BETWEEN_STEP_SALT
+            try:
+                env.reset_idx(torch.tensor(mid_reset[1], dtype=torch.long))
+            finally:
+                draws.CTR_SALT = 0
     keys = sorted(set().union(*[r.keys() for r in rec[1:]]))
     for k in keys:
         vals = [r.get(k) for r in rec]
@@ -178,6 +183,13 @@ def trimesh_hook(cfg):
     cfg.terrain.border_size = 5
 
 
+def trimesh_nocurr_hook(cfg):
+    # trimesh with the terrain curriculum off: levels over every row, no level updates, start xy over the whole
+    # sub-terrain, and extras["episode"]["terrain_level"] still reported (t1_dh_stand_env.py:535-536)
+    trimesh_hook(cfg)
+    cfg.terrain.curriculum = False
+
+
 def trimesh_overrides(env):
     el = env.episode_length_buf
     el[0:8] = 2399                 # time out at step 2 -> terrain curriculum on reset
@@ -209,6 +221,8 @@ SCENARIOS = {
     "trimesh16": lambda: run("trimesh16", 16, "trimesh", 6, cfg_hook=trimesh_hook, after_reset=trimesh_overrides),
     "resetidx16": lambda: run("resetidx16", 16, "trimesh", 6, cfg_hook=trimesh_hook, mid_reset=(2, [1, 4, 9, 15])),
     "heights16": lambda: run("heights16", 16, "trimesh", 6, cfg_hook=heights_hook, after_reset=trimesh_overrides),
+    "trimesh_nocurr16": lambda: run("trimesh_nocurr16", 16, "trimesh", 6, cfg_hook=trimesh_nocurr_hook,
+                                    after_reset=trimesh_overrides, cfg_keys={"terrain_curriculum": 0}),
     "push16": lambda: run("push16", 16, "plane", 10, cfg_hook=push_hook, after_reset=plane16_overrides,
                           cfg_keys={"push_interval_s": PUSH_INTERVAL_S}),
 }

@@ -13,6 +13,7 @@ import torch
 from oracle import rng as R
 
 SEED = 5
+CTR_SALT = 0      # R.BETWEEN_STEP_SALT while the driver calls reset_idx between steps (gen_golden.run mid_reset)
 LOG = []          # (func, line, shape) of every draw, for debugging / site discovery
 DISCOVER = False  # when True, unknown sites fall back to torch.rand and are only logged
 
@@ -84,7 +85,7 @@ def _ids_and_ctr(frame, n_rows):
     if ids is None or len(ids) != n_rows:
         ids = np.arange(n_rows, dtype=np.int64)
     ctr = int(getattr(self, "common_step_counter", 0)) if self is not None else 0
-    return ids, ctr, loc
+    return ids, ctr | CTR_SALT, loc
 
 
 def _site(frame):

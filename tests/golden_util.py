@@ -6,7 +6,7 @@ import numpy as np
 import synth
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16", "heights16", "resetidx16", "push16"]
+SCENARIOS = ["plane16", "events16", "config1_64", "trimesh16", "heights16", "resetidx16", "push16", "trimesh_nocurr16"]
 
 
 def load(name):
@@ -34,6 +34,11 @@ def mid_reset(fx, t):
 def push_interval_s(fx):
     """push_robots scenario (push16): the scenario's push_interval_s, else None (push_robots off, the default)"""
     return float(fx["cfg_push_interval_s"]) if "cfg_push_interval_s" in fx else None
+
+
+def terrain_curriculum(fx):
+    """cfg.terrain.curriculum of the scenario (on unless the fixture says otherwise: trimesh_nocurr16)"""
+    return bool(int(fx["cfg_terrain_curriculum"])) if "cfg_terrain_curriculum" in fx else True
 
 
 def measures_heights(fx):

@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 import synth
-from golden_util import assert_close, load, measures_heights, mid_reset, push_interval_s
+from golden_util import assert_close, load, measures_heights, mid_reset, push_interval_s, terrain_curriculum
 
 REWARD_NAMES = sorted(["joint_pos", "feet_clearance", "feet_contact_number", "feet_air_time", "foot_slip",
                        "feet_distance", "knee_distance", "feet_rotation", "feet_contact_forces",
@@ -28,6 +28,7 @@ def make_env_for(fx, device="cuda:0"):
     if str(fx["mesh_type"]) == "trimesh":
         def name_hook(cfg):
             cfg.terrain.num_rows, cfg.terrain.num_cols, cfg.terrain.border_size = 6, 4, 5
+            cfg.terrain.curriculum = terrain_curriculum(fx)   # gen_golden.trimesh_nocurr_hook
             if heights:   # gen_golden.heights_hook
                 cfg.terrain.measure_heights = True
                 cfg.terrain.terrain_proportions = [0.0, 0.25, 0.25, 0.25, 0.25, 0.0, 0.0, 0.0, 0.0, 0.0]
@@ -38,8 +39,8 @@ def make_env_for(fx, device="cuda:0"):
     env = make_t1_env(num_envs=int(fx["num_envs"]), mesh_type=str(fx["mesh_type"]), seed=int(fx["seed"]),
                       device=device, cfg_hook=name_hook)
     if heights:
-        # the scan samples the field: run it on the reference's own height samples (the terrain generator's
-        # numpy draws are not the reference's, and the injected-physics scenarios never touch the field)
+        # the scan samples the field: run it on the reference's own height samples, so this scenario does not
+        # depend on the terrain generator (tests/test_terrain.py pins that one against the same fixture)
         from ti5_isaacgym_amd import _lib
         hf = torch.from_numpy(fx["init_height_samples"]).to(env.device)
         assert hf.shape == env.height_samples.shape
@@ -98,7 +99,9 @@ def snapshot(env):
         root_states=env.root_states.cpu().numpy(), dof_state=env.dof_state.view(n, 12, 2).cpu().numpy(),
         episode_sums=np.stack([env.episode_sums[k].cpu().numpy() for k in REWARD_NAMES]),
         extras_episode=np.array([float(ex["rew_" + k]) for k in REWARD_NAMES], np.float32) if ex else None,
-        max_command_x=ex.get("max_command_x") if ex else None, applied_force=env.applied_force.cpu().numpy(),
+        max_command_x=ex.get("max_command_x") if ex else None,
+        terrain_level=float(ex["terrain_level"]) if ex and "terrain_level" in ex else None,
+        applied_force=env.applied_force.cpu().numpy(),
         full_obs=env.obs_buf.cpu().numpy(), gait_start=env.gait_start.cpu().numpy(),
         dof_lag=env.dof_lag_timestep.cpu().numpy(), imu_lag=env.imu_lag_timestep.cpu().numpy(),
         lag=env.lag_timestep.cpu().numpy(), kp=env.randomized_p_gains.cpu().numpy(),
@@ -111,6 +114,11 @@ def run_parity(name, max_steps=None, device="cuda:0", check=True):
     env = make_env_for(fx, device)
     assert_close("env_frictions", env.env_frictions.cpu().numpy(), fx["init_env_frictions"])
     assert_close("body_mass", env.body_mass.cpu().numpy(), fx["init_body_mass"])
+    # creation-time DR of k_init vs the reference's randomize_rigid_body_props / _process_rigid_shape_props
+    # (legged_robot.py:692-730, 786-824)
+    assert_close("link_masses", env.link_mass_scale.cpu().numpy(), fx["init_link_masses"].reshape(-1, 12))
+    assert_close("com_displacements", env.com_displacements.cpu().numpy(), fx["init_com_displacements"])
+    assert_close("restitution", env.restitution_coeffs.cpu().numpy(), fx["init_restitution"].reshape(-1, 1))
     if "init_terrain_levels" in fx:
         np.testing.assert_array_equal(env.terrain_levels.cpu().numpy(), fx["init_terrain_levels"])
         np.testing.assert_array_equal(env.terrain_types.cpu().numpy(), fx["init_terrain_types"])
@@ -163,6 +171,8 @@ def compare(name, fx, outs):
         if t > 0:
             assert_close("extras_episode", s["extras_episode"], fx["step_extras_episode"][t], ctx=ctx)
             assert abs(s["max_command_x"] - float(fx["step_extras_max_command_x"][t])) < 1e-6, ctx
+            if str(fx["mesh_type"]) == "trimesh":   # reported whatever the curriculum setting (t1:535-536)
+                assert abs(s["terrain_level"] - float(fx["step_extras_terrain_level"][t])) < 1e-5, ctx
             if fx["step_force_applied"][t]:
                 assert_close("applied_force", s["applied_force"], fx["step_applied_force"][t][:, 0, :], ctx=ctx)
     if len(outs) == len(fx["step_rew"]):

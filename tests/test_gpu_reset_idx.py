@@ -42,3 +42,24 @@ def test_reset_idx_between_steps():
     torch.testing.assert_close(env.obs_buf[keep, :-47], prev[keep, 47:], rtol=0, atol=0)
     assert (env.episode_length_buf[mask & ~env.reset_buf.bool()] == 1).all()
     assert torch.isfinite(env.obs_buf).all() and torch.isfinite(env.root_states).all()
+
+
+def test_reset_idx_after_in_step_reset_draws_fresh_values():
+    """An env that terminated inside step c and is passed to reset_idx before step c + 1 must redraw its DR (the
+    reference's generator advances): the between-step reset keys on counter | BETWEEN_STEP_SALT, the in-step reset
+    of step c on the plain counter."""
+    from ti5_isaacgym_amd import make_t1_env
+    n = 256
+    env = make_t1_env(num_envs=n, mesh_type="plane", seed=9, device="cuda:0")
+    env.reset()
+    env.episode_length_buf[::5] = int(env.max_episode_length)   # these envs time out in the next step
+    env.step(torch.zeros(n, 12, device="cuda:0"))
+    r = env.reset_buf.bool()
+    assert r[::5].all()
+    kp, lag, gs = env.randomized_p_gains.clone(), env.lag_timestep.clone(), env.gait_time.clone()
+    ids = torch.nonzero(r).flatten()
+    env.reset_idx(ids)
+    torch.cuda.synchronize()
+    assert (env.randomized_p_gains[r] != kp[r]).all(dim=1).all(), "reset_idx reused the in-step reset's draws"
+    assert not torch.equal(env.lag_timestep[r], lag[r]) or not torch.equal(env.gait_time[r], gs[r])
+    assert torch.equal(env.randomized_p_gains[~r], kp[~r])

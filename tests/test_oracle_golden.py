@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from golden_util import (SCENARIOS, assert_close, load, measures_heights, mid_reset, push_interval_s, synth_physics,
-                         terrain_of)
+                         terrain_curriculum, terrain_of)
 from oracle import rng as R
 from oracle.t1_oracle import REWARD_NAMES, T1Oracle
 
@@ -18,6 +18,7 @@ def run_oracle(fx):
     push = push_interval_s(fx)
     o = T1Oracle(n, seed=int(fx["seed"]), mesh_type=str(fx["mesh_type"]), terrain=terrain,
                  measure_heights=measures_heights(fx), push_robots=push is not None,
+                 terrain_curriculum=terrain_curriculum(fx),
                  **({"push_interval_s": push} if push is not None else {}))
     phys = synth_physics(fx)
     outs = []
@@ -34,7 +35,7 @@ def run_oracle(fx):
         outs.append(snapshot(o))
         ids = mid_reset(fx, t)
         if ids is not None:
-            o.reset_idx(np.asarray(ids))
+            o.reset_idx(np.asarray(ids), between_steps=True)
     return o, outs
 
 
@@ -47,7 +48,8 @@ def snapshot(o):
                 env_origins=o.env_origins.copy(), dof_state=o.dof.copy(), root_states=o.root.copy(),
                 episode_sums=np.stack([o.episode_sums[k] for k in REWARD_NAMES]),
                 extras_episode=np.array([o.extras["episode"]["rew_" + k] for k in REWARD_NAMES], np.float32),
-                max_command_x=o.extras["episode"]["max_command_x"], applied_force=o.applied_force.copy(),
+                max_command_x=o.extras["episode"]["max_command_x"],
+                terrain_level=o.extras["episode"].get("terrain_level"), applied_force=o.applied_force.copy(),
                 full_obs=o.obs_buf.copy(), measured_heights=o.measured_heights.copy())
 
 
@@ -80,6 +82,8 @@ def test_oracle_matches_reference(name):
             ref_ep = fx["step_extras_episode"][t]
             assert_close("extras_episode", s["extras_episode"], ref_ep, ctx=ctx)
             assert s["max_command_x"] == pytest.approx(float(fx["step_extras_max_command_x"][t])), ctx
+            if str(fx["mesh_type"]) == "trimesh":
+                assert s["terrain_level"] == pytest.approx(float(fx["step_extras_terrain_level"][t])), ctx
             if fx["step_force_applied"][t]:
                 assert_close("applied_force", s["applied_force"], fx["step_applied_force"][t], ctx=ctx)
     assert_close("obs_full_last", outs[-1]["full_obs"], fx["obs_full_last"])

@@ -12,7 +12,7 @@
 namespace t1 {
 
 // ---------------------------------------------------------------------------------------------------
-// Counter RNG: identical definition to oracle/rng.py (pinned by tests/test_rng.py).
+// Counter RNG: identical definition to oracle/rng.py (the two are compared by tests/test_rng.py).
 // Every reference draw site maps to (seed, global env id, step counter, slot) -> uniform; see
 // oracle/rng.py for the slot table and the reference file:line of each site.
 // ---------------------------------------------------------------------------------------------------
@@ -67,6 +67,10 @@ T1_HD int32_t rand_int(int32_t lo, int32_t hi, RngKey k, uint32_t slot) {
   uint64_t h = hash_k(k, slot) >> 8;
   return lo + (int32_t)((h * (uint64_t)(hi - lo)) >> 24);
 }
+
+// reset_idx(env_ids) between steps keys its draws on (counter | T1_BETWEEN_STEP_SALT) (oracle/rng.py
+// BETWEEN_STEP_SALT): the in-step resets of the step that produced `counter` used the plain counter
+constexpr uint32_t T1_BETWEEN_STEP_SALT = 0x80000000u;
 
 // slot table (mirror of oracle/rng.py)
 enum : uint32_t {

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ M
   const bool any_reset = B.ep_accum[24] > 0.0f;
   if (live) post_b_env(*Mp, C, B, A, n, do_reset, any_reset);
   // extras["episode"]["terrain_level"] = mean level over all envs after this step's resets (legged_robot.py:1158)
-  if (C.terrain_curriculum && any_reset) wave_atomic_add(B.ep_accum + 25, live ? (float)B.terrain_levels[n] : 0.0f);
+  if (C.custom_origins && any_reset) wave_atomic_add(B.ep_accum + 25, live ? (float)B.terrain_levels[n] : 0.0f);
   // reset_idx zeroes the obs / critic history of the reset envs (t1:548-558): k_shift wrote the 65 (2) older
   // frames of every row, so the wave zeroes those of its reset envs here, one row at a time, coalesced
   uint64_t m = __ballot(do_reset);
@@ -186,7 +186,7 @@ __global__ void k_finalize(t1env_buffers B, const t1env_config* __restrict__ Cp,
 __global__ __launch_bounds__(256) void k_terrain_level_sum(t1env_buffers B, const t1env_config* __restrict__ Cp) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const t1env_config& C = *Cp;
-  const float v = (n < C.num_envs && C.terrain_curriculum && B.ep_accum[24] > 0.0f) ? (float)B.terrain_levels[n] : 0.0f;
+  const float v = (n < C.num_envs && C.custom_origins && B.ep_accum[24] > 0.0f) ? (float)B.terrain_levels[n] : 0.0f;
   wave_atomic_add(B.ep_accum + 25, v);
 }
 
@@ -319,8 +319,11 @@ __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict_
   wave_atomic_add(B.ep_accum + 24, live ? 1.0f : 0.0f);
   if (!live) return;
   const uint32_t genv = (uint32_t)(C.env_offset + n);
-  reset_env(*Mp, C, B, A, n, genv, A.counter, true);
-  resample_commands(C, B, A, n, genv, A.counter);
+  // t1env_reset_idx (mask): the between-step key domain, so an env reset in the step that produced A.counter draws
+  // fresh values here (t1_common.h T1_BETWEEN_STEP_SALT)
+  const uint32_t key_ctr = mask ? (A.counter | T1_BETWEEN_STEP_SALT) : A.counter;
+  reset_env(*Mp, C, B, A, n, genv, key_ctr, true);
+  resample_commands(C, B, A, n, genv, key_ctr);
 }
 
 // reset_idx's obs / critic history clearing (t1_dh_stand_env.py:553-558) for the masked envs: every frame of
@@ -654,7 +657,7 @@ int t1env_reset_all(t1env* e, const t1env_step_args* a, void* stream) {
   hipLaunchKernelGGL(k_reset_all, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a,
                      (const uint8_t*)nullptr);
   HIP_TRY(hipGetLastError());
-  if (e->cfg.terrain_curriculum) {
+  if (e->cfg.custom_origins) {
     hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
     HIP_TRY(hipGetLastError());
   }
@@ -675,7 +678,7 @@ int t1env_reset_idx(t1env* e, const uint8_t* mask, const t1env_step_args* a, voi
   const int N = e->cfg.num_envs;
   hipLaunchKernelGGL(k_reset_all, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf, *a, mask);
   HIP_TRY(hipGetLastError());
-  if (e->cfg.terrain_curriculum) {
+  if (e->cfg.custom_origins) {
     hipLaunchKernelGGL(k_terrain_level_sum, dim3(grid(N, 256)), dim3(256), 0, s, e->buf, e->d_cfg);
     HIP_TRY(hipGetLastError());
   }

@@ -216,7 +216,7 @@ __device__ __forceinline__ void epilogue_finalize(const t1env_config& C, const t
 __device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const t1env_buffers& B,
                                                     const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
                                                     int dyn_blocks, int lane, bool do_reset, bool active, int n) {
-  if (C.terrain_curriculum) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
+  if (C.custom_origins) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
   epilogue_handoff(C, S, FA, lane, do_reset, active);
   __builtin_amdgcn_s_waitcnt(0);
   epilogue_finalize(C, B, A, FA, dyn_blocks, lane);
@@ -246,6 +246,9 @@ __device__ __forceinline__ LegSetup leg_setup(const DynModel& M, const t1env_con
   LegSetup L;
   L.lag = B.lag_timestep[n];
   L.s_dof = 9 - B.dof_lag_timestep[n] % 10;
+#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
+  L.s_dof = L.s_dof > 0 ? L.s_dof - 1 : 0;
+#endif
   L.s_imu = 9 - B.imu_lag_timestep[n] % 10;
   L.dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
   L.imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
@@ -644,7 +647,7 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
   }
   T1_PROF_MARK(14);
   // the terrain-level sum reads the levels reset_idx may just have changed
-  if (C.terrain_curriculum) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
+  if (C.custom_origins) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();  // E2
   T1_PROF_MARK(15);
