@@ -44,6 +44,7 @@ class DHPPO:
         self.use_clipped_value_loss = use_clipped_value_loss
         self.num_short_obs = self.actor_critic.num_short_obs
         self.lin_vel_idx = lin_vel_idx
+        # .grad of every parameter is a view into one flat bucket: the DP gradient all-reduce is one collective
         self.grads = dist_util.GradientBucket(self.actor_critic.parameters())
         self.grads.broadcast_params_()
         # graphed rollout act(): {(obs ptr, critic obs ptr, shapes): (graph, static outputs)}; None = eager
@@ -168,7 +169,7 @@ class DHPPO:
                 value_loss = (returns_b - value_b).pow(2).mean()
             se_loss = mse(est_lin_vel, ref_lin_vel)
             loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean() + se_loss
-            self.optimizer.zero_grad()
+            self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
             loss.backward()
             self.grads.all_reduce_()
             nn.utils.clip_grad_norm_(ac.parameters(), self.max_grad_norm)

@@ -53,33 +53,56 @@ def global_mean_std(x):
 
 
 class GradientBucket:
-    """All-reduce every parameter gradient as one contiguous fp32 bucket (mean over ranks)."""
+    """Every parameter's .grad is a view into one contiguous fp32 bucket, so the gradient all-reduce (mean over
+    ranks) is one collective on the bucket itself: backward() accumulates straight into it and no copy in or out
+    is needed.  The owner must zero the gradients in place (optimizer.zero_grad(set_to_none=False)) so that
+    autograd keeps accumulating into the views; bind_() re-attaches them if something replaced a .grad."""
 
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.views = []
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.views.append(self.flat[off:off + k].view_as(p))
+            off += k
+        self.bind_()
+
+    def bind_(self):
+        """Point every .grad at its bucket view (copying a gradient some other code put there)."""
+        for p, v in zip(self.params, self.views):
+            g = p.grad
+            if g is None or g.data_ptr() != v.data_ptr():
+                if g is not None:
+                    v.copy_(g)
+                else:
+                    v.zero_()
+                p.grad = v
 
     def all_reduce_(self):
         if not active():
             return
-        off = 0
-        for p in self.params:
-            k = p.numel()
-            if p.grad is None:
-                self.flat[off:off + k].zero_()
-            else:
-                self.flat[off:off + k].copy_(p.grad.reshape(-1))
-            off += k
+        self.bind_()   # no-op unless a .grad was replaced
+        timed = self.timing is not None and self.flat.is_cuda
+        if timed:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         all_reduce_mean_(self.flat)
-        off = 0
-        for p in self.params:
-            k = p.numel()
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            p.grad.copy_(self.flat[off:off + k].view_as(p))
-            off += k
+        if timed:
+            ev[1].record()
+            self.timing.append(ev)
+
+    timing = None   # a list: every all_reduce_ appends its (start, stop) CUDA events (tools/bench_ppo.py)
+
+    def all_reduce_ms(self):
+        """Mean milliseconds of the timed all-reduces (synchronises)."""
+        if not self.timing:
+            return None
+        torch.cuda.synchronize(self.flat.device)
+        return sum(a.elapsed_time(b) for a, b in self.timing) / len(self.timing)
 
     def broadcast_params_(self, src=0):
         """Start every rank from rank src's weights."""

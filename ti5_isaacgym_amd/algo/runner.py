@@ -6,8 +6,9 @@ and checkpoint layout as the reference.  Differences, all outside the arithmetic
     once per iteration instead of a nonzero() host sync every env step; the buffers receive the same values
     in the same order;
   * data-parallel runs (one process per GPU, torchrun): every rank rolls out its own env shard, DHPPO
-    all-reduces gradients / KL / advantage statistics, rank 0 logs and saves; logged means are averaged
-    over ranks;
+    all-reduces gradients / KL / advantage statistics (so losses, learning rate and weights are the same on every
+    rank), rank 0 logs and saves.  The episode statistics rank 0 logs (mean reward / length, extras["episode"])
+    are those of its own env shard, not reduced over ranks; fps and total timesteps count all ranks;
   * TensorBoard is optional (not in this image): scalars then go to ``<log_dir>/scalars.jsonl``.
 """
 import json

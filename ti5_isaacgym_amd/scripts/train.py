@@ -30,10 +30,10 @@ def train(args):
     n = args.num_envs or env_cfg.env.num_envs
     env, env_cfg = task_registry.make_env(name=args.task, args=args, env_offset=rank * n, num_envs_total=world * n)
     torch.manual_seed((args.seed if args.seed is not None else train_cfg.seed) + rank)  # per-rank action sampling
+    # resume (--resume / train_cfg.runner.resume, --load_run, --checkpoint) is make_alg_runner's, as in the
+    # reference (task_registry.py:136-143): every rank loads the same checkpoint, rank 0 alone logs
     runner, train_cfg, log_dir = task_registry.make_alg_runner(env=env, name=args.task, args=args,
-                                                                log_root="default" if rank == 0 else None)
-    if args.resume and args.load_run:
-        runner.load(args.load_run)
+                                                                log_to_dir=rank == 0)
     runner.learn(num_learning_iterations=train_cfg.runner.max_iterations, init_at_random_ep_len=False)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -45,6 +45,25 @@ def set_seed(seed):
     return seed
 
 
+def get_load_path(root, load_run=-1, checkpoint=-1):
+    """Checkpoint path of a run (reference humanoid/utils/helpers.py:94-125): the last run under root (sorted names,
+    "exported" skipped) unless load_run names one, and in it model_<checkpoint>.pt or the last model file."""
+    try:
+        runs = sorted(os.listdir(root))
+        if "exported" in runs:
+            runs.remove("exported")
+        last_run = os.path.join(root, runs[-1])
+    except Exception:
+        raise ValueError("No runs in this directory: " + str(root))
+    load_run = last_run if load_run == -1 else os.path.join(root, load_run)
+    if checkpoint == -1:
+        models = sorted((f for f in os.listdir(load_run) if "model" in f), key=lambda m: "{0:0>15}".format(m))
+        model = models[-1]
+    else:
+        model = "model_{}.pt".format(checkpoint)
+    return os.path.join(load_run, model)
+
+
 def update_cfg_from_args(env_cfg, cfg_train, args):
     if env_cfg is not None and getattr(args, "num_envs", None) is not None:
         env_cfg.env.num_envs = args.num_envs

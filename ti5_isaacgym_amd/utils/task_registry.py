@@ -8,7 +8,7 @@ import copy
 import os
 from datetime import datetime
 
-from .helpers import class_to_dict, get_args, set_seed, update_cfg_from_args
+from .helpers import class_to_dict, get_args, get_load_path, set_seed, update_cfg_from_args
 
 
 class TaskRegistry:
@@ -49,7 +49,7 @@ class TaskRegistry:
         self.env_cfg_for_wandb = env_cfg
         return env, env_cfg
 
-    def make_alg_runner(self, env, name=None, args=None, train_cfg=None, log_root="default"):
+    def make_alg_runner(self, env, name=None, args=None, train_cfg=None, log_root="default", log_to_dir=True):
         if args is None:
             args = get_args()
         if train_cfg is None:
@@ -61,12 +61,19 @@ class TaskRegistry:
         if log_root == "default":
             log_root = os.path.join("logs", train_cfg.runner.experiment_name, "exported_data")
         log_dir = None if log_root is None else os.path.join(log_root, stamp + train_cfg.runner.run_name)
+        if not log_to_dir:   # data-parallel ranks other than 0 resolve the resume path but write nothing
+            log_dir = None
         all_cfg = {**class_to_dict(train_cfg), **class_to_dict(self.env_cfg_for_wandb)}
         cls = self.runner_classes.get(train_cfg.runner_class_name)
         if cls is None:
             raise ValueError(f"runner class {train_cfg.runner_class_name!r} not registered "
                              "(task_registry.register_runner(name, cls))")
         runner = cls(env, all_cfg, log_dir, device=getattr(args, "rl_device", "cuda:0"))
+        if train_cfg.runner.resume:   # task_registry.py:136-143: weights only, the optimizer starts fresh
+            resume_path = get_load_path(log_root, load_run=train_cfg.runner.load_run,
+                                        checkpoint=train_cfg.runner.checkpoint)
+            print(f"Loading model from: {resume_path}")
+            runner.load(resume_path, load_optimizer=False)
         return runner, train_cfg, log_dir
 
 
