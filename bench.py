@@ -48,6 +48,14 @@ KERNEL_BYTES = {
 }
 
 
+def alg_bytes(state_dtype):
+    """(B_alg, history-shift bytes) per env-step: SURVEY.md §8(d)'s 30,678 B with fp32 histories; with fp16 histories
+    (config 5) the four history terms (obs write 12,408 + read 12,220, priv write 876 + read 584) halve -> 17,634."""
+    if state_dtype == "fp16":
+        return B_ALG - (12408 + 12220 + 876 + 584) // 2, SHIFT_BYTES // 2
+    return B_ALG, SHIFT_BYTES
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -55,6 +63,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--num-envs", type=int, default=8192)
     p.add_argument("--mesh", default="trimesh", choices=["plane", "heightfield", "trimesh"])
+    p.add_argument("--state-dtype", default="fp32", choices=["fp32", "fp16"],
+                   help="storage dtype of the obs / critic histories (fp16: BASELINE config 5's fp16 state)")
+    p.add_argument("--push", action="store_true", help="domain_rand.push_robots on (BASELINE config 5), every 6 s")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--time-every", type=int, default=8,
                    help="record per-kernel HIP events on every k-th timed step (event records cost host time; "
@@ -105,8 +116,12 @@ def main():
     dev = torch.device(f"cuda:{local}")
     from ti5_isaacgym_amd import make_t1_env
     N = args.num_envs
+    def hook(cfg):
+        cfg.env.state_dtype = args.state_dtype
+        cfg.domain_rand.push_robots = bool(args.push)
     env = make_t1_env(num_envs=N, mesh_type=args.mesh, seed=5, device=str(dev), env_offset=rank * N,
-                      num_envs_total=N * world)
+                      num_envs_total=N * world, cfg_hook=hook)
+    b_alg, shift_bytes = alg_bytes(args.state_dtype)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
     pool = [torch.randn(N, 12, device=dev, generator=gen) for _ in range(8)]
@@ -150,9 +165,9 @@ def main():
     for k in KERNELS + (["k_shift"] if pre_shift else []):
         ms = kt[k]["ms"] / max(1, kt[k]["launches"])
         if k == "k_shift":
-            alg = SHIFT_BYTES * N
+            alg = shift_bytes * N
         elif fused and k == "k_dynamics":
-            alg = (B_ALG - (SHIFT_BYTES if pre_shift else 0)) * N
+            alg = (b_alg - (shift_bytes if pre_shift else 0)) * N
         else:
             alg = KERNEL_BYTES[k] * N
         name = FUSED_KERNEL if (fused and k == "k_dynamics") else k
@@ -167,12 +182,13 @@ def main():
     if dk["alg_GBs"] is not None:
         achieved, basis = dk["alg_GBs"], f"{dom} alg bytes / live HIP-event launch duration"
     else:
-        achieved, basis = value / world * B_ALG / 1e9, "wall clock: env-steps/s x B_alg"
+        achieved, basis = value / world * b_alg / 1e9, "wall clock: env-steps/s x B_alg"
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("num_envs") == N and tj.get("mesh") == args.mesh:
+            if tj.get("num_envs") == N and tj.get("mesh") == args.mesh and \
+                    tj.get("state_dtype", "fp32") == args.state_dtype:
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
@@ -180,15 +196,18 @@ def main():
         "metric": "env-steps/sec at 8192 envs, t1_dh_stand, 1/2/4/8 MI355X; obs/reward parity",
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"t1_dh_stand {N} envs/GPU, {args.mesh} curriculum terrain + full DR, "
-                               "random N(0,1) actions (policy excluded), 10 substeps/step",
+        "vs_baseline": None, "dtype": "f32" if args.state_dtype == "fp32" else "f32 compute, f16 obs/critic histories",
+        "data": "synthetic",
+        "config": {"workload": f"t1_dh_stand {N} envs/GPU, {args.mesh} curriculum terrain + full DR"
+                               + (", pushes" if args.push else "") + ", random N(0,1) actions (policy excluded), "
+                               f"10 substeps/step, {args.state_dtype} obs/critic histories",
+                   "state_dtype": args.state_dtype,
                    "num_envs_per_gpu": N, "global_envs": N * world, "mesh": args.mesh, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "basis": basis,
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes_per_step": B_ALG * N, "alg_bytes_per_env_step": B_ALG,
-                     "wall_clock_GBs": round(value / world * B_ALG / 1e9, 1),
+                     "alg_bytes_per_step": b_alg * N, "alg_bytes_per_env_step": b_alg,
+                     "wall_clock_GBs": round(value / world * b_alg / 1e9, 1),
                      "step_span_ms_timed": round(step_span_ms, 4) if step_span_ms else None,
                      "kernels": per_kernel},
         "finite": ok,

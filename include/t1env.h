@@ -103,6 +103,10 @@ typedef struct t1env_config {
   int32_t custom_origins;       /* terrain origins (heightfield/trimesh) instead of a grid */
   int32_t max_init_terrain_level;
   float reset_xy_range;         /* custom origins: +- platform/3 (curriculum) or terrain_length/2 */
+  /* 1: obs_buf / priv_buf hold fp16 (BASELINE config 5's fp16 state storage: the 66/3-frame histories, ~85% of
+   * the step's bytes, are stored, shifted and returned as fp16; every value is computed in fp32 and rounded once,
+   * round-to-nearest-even).  0: fp32 (DHT1StandCfg). */
+  int32_t obs_half;
 } t1env_config;
 
 /* Device buffers (caller-owned).  Shapes follow the reference's tensors. */
@@ -111,8 +115,8 @@ typedef struct t1env_buffers {
   float* dof_state;         /* (N,12,2) pos, vel */
   float* rigid_state;       /* (N,13,13) */
   float* contact_forces;    /* (N,13,3) net contact force, world */
-  float* obs_buf[2];        /* ping-pong (N,3102); step k writes obs_buf[k & 1] */
-  float* priv_buf[2];       /* ping-pong (N,219) */
+  float* obs_buf[2];        /* ping-pong (N,3102); step k writes obs_buf[k & 1]; fp16 data when cfg.obs_half */
+  float* priv_buf[2];       /* ping-pong (N,219); fp16 data when cfg.obs_half */
   float* rew_buf;           /* (N,) */
   uint8_t* reset_buf;       /* (N,) bool */
   uint8_t* time_out_buf;    /* (N,) bool */

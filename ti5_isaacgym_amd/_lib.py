@@ -50,7 +50,7 @@ class Config(C.Structure):
         ("dr_base_mass", i32), ("dr_link_mass", i32), ("dr_com", i32), ("dr_friction", i32),
         ("added_mass_range", f32 * 2), ("link_mass_range", f32 * 2), ("com_range", (f32 * 2) * 3),
         ("friction_range", f32 * 2), ("restitution_range", f32 * 2), ("custom_origins", i32),
-        ("max_init_terrain_level", i32), ("reset_xy_range", f32),
+        ("max_init_terrain_level", i32), ("reset_xy_range", f32), ("obs_half", i32),
     ]
 
 

@@ -66,6 +66,7 @@ class DHPPO:
         checks cannot run inside a graph: the distribution's argument validation (built without it) and
         torch.normal's std >= 0 test (the sample is drawn as mean + std * N(0, 1), the same distribution)."""
         ac = self.actor_critic
+        obs, critic_obs = obs.float(), critic_obs.float()   # fp16 env histories (state_dtype="fp16"): no-op for fp32
         mean = ac.actor(ac.actor_input(obs))
         std = mean * 0.0 + ac.std
         dist = Normal(mean, std, validate_args=False)
@@ -104,8 +105,8 @@ class DHPPO:
             t.observations = obs
             t.critic_observations = critic_obs
             return t.actions
-        t.actions = ac.act(obs).detach()
-        t.values = ac.evaluate(critic_obs).detach()
+        t.actions = ac.act(obs.float()).detach()
+        t.values = ac.evaluate(critic_obs.float()).detach()
         t.actions_log_prob = ac.get_actions_log_prob(t.actions).detach()
         t.action_mean = ac.action_mean.detach()
         t.action_sigma = ac.action_std.detach()

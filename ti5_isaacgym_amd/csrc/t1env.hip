@@ -154,10 +154,9 @@ __global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ M
     const int l = __ffsll((unsigned long long)m) - 1;
     m &= m - 1;
     const size_t row = (size_t)blockIdx.x * BLOCK + l;
-    float* o = B.obs_buf[A.obs_slot] + row * (T1_NOBS * T1_HIST);
-    for (int c = threadIdx.x; c < T1_NOBS * (T1_HIST - 1); c += BLOCK) o[c] = 0.0f;
-    float* p = B.priv_buf[A.obs_slot] + row * (T1_NPRIV * T1_CHIST);
-    for (int c = threadIdx.x; c < T1_NPRIV * (T1_CHIST - 1); c += BLOCK) p[c] = 0.0f;
+    zero_hist(B.obs_buf[A.obs_slot], C.obs_half, row, T1_NOBS * T1_HIST, T1_NOBS * (T1_HIST - 1), threadIdx.x, BLOCK);
+    zero_hist(B.priv_buf[A.obs_slot], C.obs_half, row, T1_NPRIV * T1_CHIST, T1_NPRIV * (T1_CHIST - 1), threadIdx.x,
+              BLOCK);
   }
   // the last block to finish finalises the step's extras (no separate launch)
   __threadfence();
@@ -329,13 +328,11 @@ __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict_
 // reset_idx's obs / critic history clearing (t1_dh_stand_env.py:553-558) for the masked envs: every frame of
 // their rows in the buffer the next step shifts from; one workgroup per env
 __global__ __launch_bounds__(256) void k_zero_masked_rows(float* __restrict__ obs, float* __restrict__ priv,
-                                                          const uint8_t* __restrict__ mask, int N) {
+                                                          const uint8_t* __restrict__ mask, int N, int half) {
   const int n = blockIdx.x;
   if (n >= N || mask[n] == 0) return;
-  float* o = obs + (size_t)n * (T1_NOBS * T1_HIST);
-  for (int c = threadIdx.x; c < T1_NOBS * T1_HIST; c += blockDim.x) o[c] = 0.0f;
-  float* p = priv + (size_t)n * (T1_NPRIV * T1_CHIST);
-  for (int c = threadIdx.x; c < T1_NPRIV * T1_CHIST; c += blockDim.x) p[c] = 0.0f;
+  zero_hist(obs, half, n, T1_NOBS * T1_HIST, T1_NOBS * T1_HIST, threadIdx.x, blockDim.x);
+  zero_hist(priv, half, n, T1_NPRIV * T1_CHIST, T1_NPRIV * T1_CHIST, threadIdx.x, blockDim.x);
 }
 
 // coarse height bound: out[ci][cj] = max height sample of rows [(ci-K)c, (ci+K+1)c] x cols [(cj-K)c, (cj+K+1)c]
@@ -390,6 +387,7 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
         cfg->dof_lag_range[0] < 0 || cfg->imu_lag_range[0] < 0)
       return fail(T1ENV_E_ARG, "t1env_create: lag ranges must lie in [0,30] (dof/action) and [0,10] (imu)");
   }
+  if (cfg->obs_half != 0 && cfg->obs_half != 1) return fail(T1ENV_E_ARG, "t1env_create: obs_half must be 0 or 1");
   if (cfg->decimation != 10 && (cfg->lag_range[1] > 0 || cfg->dof_lag_range[1] > 0 || cfg->imu_lag_range[1] > 0))
     return fail(T1ENV_E_ARG, "t1env_create: sensor/actuator lag rings assume decimation == 10");
   DynModel dm;
@@ -484,7 +482,7 @@ static ShiftArgs shift_args(const t1env* e, const t1env_step_args* a) {
   const int64_t N = e->cfg.num_envs;
   const int in = a->obs_slot ^ 1, out = a->obs_slot;
   return ShiftArgs{e->buf.obs_buf[in], e->buf.obs_buf[out], e->buf.priv_buf[in], e->buf.priv_buf[out],
-                   N * T1_NOBS * T1_HIST, N * T1_NPRIV * T1_CHIST};
+                   N * T1_NOBS * T1_HIST, N * T1_NPRIV * T1_CHIST, e->cfg.obs_half ? 1 : 0};
 }
 
 // the history shift as its own launch, in stream order (paths without k_dynamics)
@@ -613,6 +611,7 @@ int t1env_critic_heights(t1env* e, int32_t obs_slot, int32_t npts, float scale, 
                          const float* prev, float* out, void* stream) {
   if (!e || !measured || !prev || !out || npts <= 0 || (obs_slot & ~1))
     return fail(T1ENV_E_ARG, "t1env_critic_heights: bad argument");
+  if (e->cfg.obs_half) return fail(T1ENV_E_STATE, "t1env_critic_heights: fp16 histories (obs_half) are not supported");
   const int N = e->cfg.num_envs;
   const int64_t total = (int64_t)N * T1_CHIST * (T1_NPRIV + npts);
   hipLaunchKernelGGL(k_critic_heights, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
@@ -665,8 +664,9 @@ int t1env_reset_all(t1env* e, const t1env_step_args* a, void* stream) {
   HIP_TRY(hipGetLastError());
   // every history row restarts from zeros: clear both ping-pong buffers (the next step shifts from either)
   for (int k = 0; k < 2; ++k) {
-    HIP_TRY(hipMemsetAsync(e->buf.obs_buf[k], 0, sizeof(float) * (size_t)N * T1_NOBS * T1_HIST, s));
-    HIP_TRY(hipMemsetAsync(e->buf.priv_buf[k], 0, sizeof(float) * (size_t)N * T1_NPRIV * T1_CHIST, s));
+    const size_t es = e->cfg.obs_half ? 2 : 4;
+    HIP_TRY(hipMemsetAsync(e->buf.obs_buf[k], 0, es * (size_t)N * T1_NOBS * T1_HIST, s));
+    HIP_TRY(hipMemsetAsync(e->buf.priv_buf[k], 0, es * (size_t)N * T1_NPRIV * T1_CHIST, s));
   }
   return 0;
 }
@@ -685,7 +685,7 @@ int t1env_reset_idx(t1env* e, const uint8_t* mask, const t1env_step_args* a, voi
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, e->buf, e->d_cfg, (int)(a->counter % T1ENV_EXTRAS_RING));
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_zero_masked_rows, dim3(N), dim3(256), 0, s, e->buf.obs_buf[a->obs_slot],
-                     e->buf.priv_buf[a->obs_slot], mask, N);
+                     e->buf.priv_buf[a->obs_slot], mask, N, e->cfg.obs_half ? 1 : 0);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -172,7 +172,8 @@ struct ShiftArgs {
   float* obs_out;
   const float* priv_in;
   float* priv_out;
-  int64_t total_obs, total_priv;  // floats
+  int64_t total_obs, total_priv;  // elements
+  int32_t half;                   // 1: the histories hold fp16 (t1env_config.obs_half; the pointers are fp16 data)
 };
 constexpr int SHIFT_UNROLL = 4;
 
@@ -246,17 +247,105 @@ __device__ __forceinline__ void shift_range(const float* __restrict__ in, float*
   }
 }
 
+// ---- fp16 histories (BASELINE config 5's fp16 state, t1env_config.obs_half): the same flat shift by F elements
+// over 16-B chunks of 8 halves.  The source offset inside the two aligned loads, F % 8, is a compile-time
+// constant (every chunk starts on a multiple of 8), so the output chunk is four funnel shifts of 32-bit words
+// (v_alignbyte) for odd F, or plain word moves for even F.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool SC1> __device__ __forceinline__ void store16B(uint16_t* p, u32x4 v) {
+  if constexpr (SC1) asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+  else *reinterpret_cast<u32x4*>(p) = v;
+}
+template <bool SC1> __device__ __forceinline__ void store2B(uint16_t* p, uint16_t v) {
+  if constexpr (SC1) {
+    const uint32_t w = v;
+    asm volatile("global_store_short %0, %1, off sc1" : : "v"(p), "v"(w) : "memory");
+  } else {
+    *p = v;
+  }
+}
+template <int F, int H, bool SC1 = false>
+__device__ __forceinline__ void shift_range_h(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                              int64_t total, int64_t lo8, int64_t hi8, int64_t t0, int64_t stride) {
+  constexpr int ROW = F * H, REM = F % 8, M = REM / 2;
+  for (int64_t base = lo8 + t0; base < hi8; base += SHIFT_UNROLL * stride) {
+    u32x4 a[SHIFT_UNROLL], b[SHIFT_UNROLL];
+#pragma unroll
+    for (int u = 0; u < SHIFT_UNROLL; ++u) {
+      const int64_t sa = ((base + u * stride) * 8 + F) & ~(int64_t)7;
+      const int64_t sc = sa + 16 <= total ? sa : (total - 16) & ~(int64_t)7;  // tail: aligned in-bounds dummy
+      a[u] = *reinterpret_cast<const u32x4*>(in + sc);
+      b[u] = *reinterpret_cast<const u32x4*>(in + sc + 8);
+    }
+#pragma unroll
+    for (int u = 0; u < SHIFT_UNROLL; ++u) {
+      const int64_t c8 = base + u * stride;
+      if (c8 >= hi8) break;
+      const int64_t i = c8 * 8, sa = (i + F) & ~(int64_t)7;
+      uint32_t w[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
+      if (sa + 16 > total) {  // the last chunks of the buffer: element loads, zero past the end
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t lo = sa + 2 * k < total ? in[sa + 2 * k] : 0u;
+          const uint32_t hi = sa + 2 * k + 1 < total ? in[sa + 2 * k + 1] : 0u;
+          w[k] = lo | (hi << 16);
+        }
+      }
+      u32x4 o;
+      if constexpr (REM % 2 == 0) {
+        o = u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
+      } else {  // halves REM .. REM + 7 = the upper half of word M, ..., the lower half of word M + 4
+        o = u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], 2), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], 2),
+                  __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], 2), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], 2)};
+      }
+      const int64_t row0 = i / ROW;
+      const int col0 = (int)(i - row0 * ROW);
+      if (col0 + 7 < ROW - F && i + 7 < total) {
+        store16B<SC1>(out + i, o);
+        continue;
+      }
+      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int64_t e = i + k;
+        if (e >= total) break;
+        const int64_t row = e / ROW;
+        if ((int)(e - row * ROW) < ROW - F) store2B<SC1>(out + e, (uint16_t)(ow[k / 2] >> (16 * (k & 1))));
+      }
+    }
+  }
+}
+
 // lane `t0` of `stride` lanes: the obs history, then the critic history
 __device__ __forceinline__ void shift_history(const ShiftArgs& S, int64_t t0, int64_t stride) {
+  if (S.half) {
+    shift_range_h<T1_NOBS, T1_HIST>(reinterpret_cast<const uint16_t*>(S.obs_in), reinterpret_cast<uint16_t*>(S.obs_out),
+                                    S.total_obs, 0, (S.total_obs + 7) / 8, t0, stride);
+    shift_range_h<T1_NPRIV, T1_CHIST>(reinterpret_cast<const uint16_t*>(S.priv_in),
+                                      reinterpret_cast<uint16_t*>(S.priv_out), S.total_priv, 0, (S.total_priv + 7) / 8,
+                                      t0, stride);
+    return;
+  }
   shift_range<T1_NOBS, T1_HIST>(S.obs_in, S.obs_out, S.total_obs, 0, (S.total_obs + 3) / 4, t0, stride);
   shift_range<T1_NPRIV, T1_CHIST>(S.priv_in, S.priv_out, S.total_priv, 0, (S.total_priv + 3) / 4, t0, stride);
 }
 
-// the rows [r0, r1) of both histories (r0 a multiple of 4, so both row ranges start on a 16-B chunk), with
-// agent-coherent (sc1) stores
+// the rows [r0, r1) of both histories (r0 a multiple of 8, so both row ranges start on a 16-B chunk of either
+// element size), with agent-coherent (sc1) stores
 __device__ __forceinline__ void shift_rows_range_sc1(const ShiftArgs& S, int64_t r0, int64_t r1, int64_t t0,
                                                  int64_t stride) {
   constexpr int64_t RO = T1_NOBS * T1_HIST, RP = T1_NPRIV * T1_CHIST;
+  if (S.half) {
+    const int64_t n8o = (S.total_obs + 7) / 8, n8p = (S.total_priv + 7) / 8;
+    const int64_t ho = (r1 * RO + 7) / 8, hp = (r1 * RP + 7) / 8;
+    shift_range_h<T1_NOBS, T1_HIST, true>(reinterpret_cast<const uint16_t*>(S.obs_in),
+                                          reinterpret_cast<uint16_t*>(S.obs_out), S.total_obs, r0 * RO / 8,
+                                          ho < n8o ? ho : n8o, t0, stride);
+    shift_range_h<T1_NPRIV, T1_CHIST, true>(reinterpret_cast<const uint16_t*>(S.priv_in),
+                                            reinterpret_cast<uint16_t*>(S.priv_out), S.total_priv, r0 * RP / 8,
+                                            hp < n8p ? hp : n8p, t0, stride);
+    return;
+  }
   const int64_t n4o = (S.total_obs + 3) / 4, n4p = (S.total_priv + 3) / 4;
   const int64_t ho = (r1 * RO + 3) / 4, hp = (r1 * RP + 3) / 4;
   shift_range<T1_NOBS, T1_HIST, true>(S.obs_in, S.obs_out, S.total_obs, r0 * RO / 4, ho < n4o ? ho : n4o, t0,
@@ -265,13 +354,22 @@ __device__ __forceinline__ void shift_rows_range_sc1(const ShiftArgs& S, int64_t
                                         stride);
 }
 
+// zero `count` elements of row `row` (row width `width`) of a history buffer, fp32 or fp16
+__device__ __forceinline__ void zero_hist(float* buf, bool half, int64_t row, int width, int count, int t0, int stride) {
+  if (half) {
+    uint16_t* o = reinterpret_cast<uint16_t*>(buf) + row * width;
+    for (int c = t0; c < count; c += stride) o[c] = 0;
+  } else {
+    float* o = buf + row * width;
+    for (int c = t0; c < count; c += stride) o[c] = 0.0f;
+  }
+}
+
 // reset_idx clears the obs / critic history deques of a reset env (t1_dh_stand_env.py:548-558): the 65 (2)
 // older frames of `row` in the freshly shifted output, lane t0 of `stride` lanes
 __device__ __forceinline__ void zero_history_row(const ShiftArgs& S, int64_t row, int t0, int stride) {
-  float* o = S.obs_out + row * (T1_NOBS * T1_HIST);
-  for (int c = t0; c < T1_NOBS * (T1_HIST - 1); c += stride) o[c] = 0.0f;
-  float* p = S.priv_out + row * (T1_NPRIV * T1_CHIST);
-  for (int c = t0; c < T1_NPRIV * (T1_CHIST - 1); c += stride) p[c] = 0.0f;
+  zero_hist(S.obs_out, S.half, row, T1_NOBS * T1_HIST, T1_NOBS * (T1_HIST - 1), t0, stride);
+  zero_hist(S.priv_out, S.half, row, T1_NPRIV * T1_CHIST, T1_NPRIV * (T1_CHIST - 1), t0, stride);
 }
 
 }  // namespace t1

@@ -747,8 +747,13 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
   }
   const Phase ph = gait_phase(phase);
   T1_PROF_MARK(21);
-  float* priv = B.priv_buf[A.obs_slot] + (size_t)n * (T1_NPRIV * T1_CHIST) + T1_NPRIV * (T1_CHIST - 1);
-  float* obs = B.obs_buf[A.obs_slot] + (size_t)n * (T1_NOBS * T1_HIST) + T1_NOBS * (T1_HIST - 1);
+  // newest frames: fp32, or rounded once to fp16 (round to nearest even, as torch's .half()) with obs_half
+  const size_t priv_at = (size_t)n * (T1_NPRIV * T1_CHIST) + T1_NPRIV * (T1_CHIST - 1);
+  const size_t obs_at = (size_t)n * (T1_NOBS * T1_HIST) + T1_NOBS * (T1_HIST - 1);
+  float* priv = B.priv_buf[A.obs_slot] + priv_at;
+  float* obs = B.obs_buf[A.obs_slot] + obs_at;
+  _Float16* priv_h = reinterpret_cast<_Float16*>(B.priv_buf[A.obs_slot]) + priv_at;
+  _Float16* obs_h = reinterpret_cast<_Float16*>(B.obs_buf[A.obs_slot]) + obs_at;
   const float clipo = C.clip_obs;
   float cin[5] = {sp, cp, cmd[0] * C.lin_vel_obs_scale, cmd[1] * C.lin_vel_obs_scale, cmd[2] * C.ang_vel_obs_scale};
   {  // privileged frame (73)
@@ -780,8 +785,13 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
     v[k++] = ph.stance[1];
     v[k++] = cfz[0] > 5.0f ? 1.0f : 0.0f;
     v[k++] = cfz[1] > 5.0f ? 1.0f : 0.0f;
+    if (C.obs_half) {
 #pragma unroll
-    for (int i = 0; i < T1_NPRIV; ++i) priv[i] = clampf(v[i], -clipo, clipo);
+      for (int i = 0; i < T1_NPRIV; ++i) priv_h[i] = (_Float16)clampf(v[i], -clipo, clipo);
+    } else {
+#pragma unroll
+      for (int i = 0; i < T1_NPRIV; ++i) priv[i] = clampf(v[i], -clipo, clipo);
+    }
   }
   T1_PROF_MARK(22);
   {  // actor frame (47) from the lagged sensor rings + noise
@@ -803,7 +813,14 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
     for (int i = 0; i < T1_NOBS; ++i) {
       const float u = uniform01(K, SLOT_OBS_NOISE + i);
       const float nz = ((2.0f * u - 1.0f) * C.noise_vec[i]) * C.noise_level;
-      obs[i] = clampf(v[i] + nz, -clipo, clipo);
+      v[i] = clampf(v[i] + nz, -clipo, clipo);
+    }
+    if (C.obs_half) {
+#pragma unroll
+      for (int i = 0; i < T1_NOBS; ++i) obs_h[i] = (_Float16)v[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < T1_NOBS; ++i) obs[i] = v[i];
     }
   }
   T1_PROF_MARK(23);

@@ -32,6 +32,9 @@ class LeggedRobotCfg(BaseConfig):
         num_envs, num_observations, num_privileged_obs, num_actions = 4096, 235, None, 12
         short_frame_stack, env_spacing, send_timeouts, episode_length_s, num_commands = 4, 3, True, 20, 5
         add_stand_bool, add_target_dof_scale = False, False
+        # build extension (not in the reference): storage dtype of the obs / critic histories the env returns;
+        # "fp16" = BASELINE config 5's fp16 state (values computed in fp32 and rounded once)
+        state_dtype = "fp32"
 
     class terrain:
         mesh_type, horizontal_scale, vertical_scale, border_size, curriculum = "trimesh", 0.1, 0.005, 25, True

@@ -125,6 +125,12 @@ class T1DHStandEnv(VecEnv):
         # height scan (inactive in DHT1StandCfg): 187 heights per critic frame, t1env_measure_heights /
         # t1env_critic_heights between and after the split step phases
         self.measure_heights = bool(cfg.terrain.measure_heights)
+        sd = getattr(cfg.env, "state_dtype", "fp32")
+        if sd not in ("fp32", "fp16"):
+            raise ValueError(f"cfg.env.state_dtype must be 'fp32' or 'fp16', got {sd!r}")
+        self.obs_dtype = torch.float16 if sd == "fp16" else torch.float32
+        if self.obs_dtype == torch.float16 and self.measure_heights:
+            raise NotImplementedError("fp16 histories (state_dtype='fp16') with measure_heights=True")
         self.env_offset = int(env_offset)
         self.num_envs_total = int(num_envs_total) if num_envs_total is not None else N
         self.dt = cfg.control.decimation * self.sim_params.dt
@@ -178,8 +184,11 @@ class T1DHStandEnv(VecEnv):
         self.dof_state = z(N * 12, 2)
         self.rigid_state = z(N, 13, 13)
         self.contact_forces = z(N, 13, 3)
-        self._obs = [z(N, self.num_obs), z(N, self.num_obs)]
-        self._priv = [z(N, self.num_privileged_obs), z(N, self.num_privileged_obs)]
+        # obs / critic histories: fp32 (the reference's), or fp16 storage with cfg.env.state_dtype = "fp16"
+        # (BASELINE config 5; computed in fp32, rounded once; the runner's RolloutStorage converts on copy)
+        h = self.obs_dtype
+        self._obs = [z(N, self.num_obs, dtype=h), z(N, self.num_obs, dtype=h)]
+        self._priv = [z(N, self.num_privileged_obs, dtype=h), z(N, self.num_privileged_obs, dtype=h)]
         self.rew_buf = z(N)
         self.reset_buf = torch.ones(N, dtype=b, device=d)
         self.time_out_buf = z(N, dtype=b)
@@ -362,6 +371,7 @@ class T1DHStandEnv(VecEnv):
                                        else cfg.terrain.num_rows - 1)
         c.reset_xy_range = (c.platform / 3 if cfg.terrain.curriculum else cfg.terrain.terrain_length / 2) \
             if self.custom_origins else 0.0
+        c.obs_half = int(self.obs_dtype == torch.float16)
         self.max_terrain_level = cfg.terrain.num_rows
         return c
 
