@@ -19,14 +19,120 @@ import torch.nn as nn
 from torch.distributions import Normal
 
 
+SPLITK_ROWS = 2048      # rows of the batch (K of the weight-gradient GEMM) per split-K slice
+
+
+def wgrad_splitk(gy, x):
+    """dW = gy^T x for a batch of K rows (gy: K x M, x: K x N) as a batched GEMM over K-slices of SPLITK_ROWS rows plus
+    a sum: the PPO update's weight gradients have K = 49,152 (688,128 for the first conv) and M x N of a few hundred
+    squared, so a single GEMM has only a handful of output tiles -- a few workgroups on 256 CUs.  Slicing K gives
+    every slice its own tiles (hipBLASLt strided-batched GEMM), then one reduction."""
+    K, M = gy.shape
+    S = K // SPLITK_ROWS
+    if S < 2:
+        return gy.t().mm(x)
+    c = S * SPLITK_ROWS
+    gw = torch.bmm(gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1)).sum(0)
+    if c < K:
+        gw = gw.addmm(gy[c:].t(), x[c:])
+    return gw
+
+
+class _LinearSplitK(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gy.mm(w) if ctx.needs_input_grad[0] else None
+        gw = wgrad_splitk(gy, x) if ctx.needs_input_grad[1] else None
+        gb = gy.sum(0) if ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+def linear(x, layer):
+    """layer(x) for an nn.Linear on 2-D x; on the MI355X with split-K weight gradients (same math, fp32 summation
+    order aside), on the host exactly nn.Linear (the reference's CPU path)."""
+    if x.is_cuda and x.dim() == 2 and torch.is_grad_enabled():
+        return _LinearSplitK.apply(x.contiguous(), layer.weight, layer.bias)
+    return nn.functional.linear(x, layer.weight, layer.bias)
+
+
+class Linear(nn.Linear):
+    """nn.Linear (same parameters and state-dict keys) with the split-K weight gradient on the device."""
+
+    def forward(self, x):
+        return linear(x, self)
+
+
+def plain_copy(module):
+    """A copy of a policy sub-network built from plain torch layers only (nn.Linear for Linear, nn.Sequential for
+    HistoryEncoder), same parameters: what TorchScript export scripts (scripts/export_policy.py)."""
+    import copy
+    if isinstance(module, Linear):
+        m = nn.Linear(module.in_features, module.out_features)
+        m.load_state_dict(module.state_dict())
+        return m
+    if isinstance(module, nn.Sequential):
+        return nn.Sequential(*[plain_copy(m) for m in module])
+    return copy.deepcopy(module)
+
+
 def _mlp(sizes, act):
     """Linear layers between consecutive sizes, `act` after every hidden layer (not after the output)."""
     layers = []
     for i, (a, b) in enumerate(zip(sizes[:-1], sizes[1:])):
-        layers.append(nn.Linear(a, b))
+        layers.append(Linear(a, b))
         if i < len(sizes) - 2:
             layers.append(act)
     return nn.Sequential(*layers)
+
+
+def conv1d_as_gemm(x, conv, channels_last=False):
+    """nn.Conv1d (no padding / dilation / groups) as one GEMM over unfolded windows.  x: (B, C, L), or (B, L, C) with
+    channels_last; returns (B, Lout, O) (channels last).  The windows x[b, :, s*l : s*l + k] become rows of a
+    (B*Lout, C*k) matrix (c-major, then tap: the layout of conv.weight.view(O, C*k)), so the product is one
+    hipBLASLt GEMM + bias, and autograd's unfold backward (a strided scatter-add) gives the input gradient."""
+    k, st = conv.kernel_size[0], conv.stride[0]
+    if channels_last:
+        win = x.unfold(1, k, st)                      # (B, Lout, C, k)
+    else:
+        win = x.unfold(2, k, st).permute(0, 2, 1, 3)  # (B, C, Lout, k) -> (B, Lout, C, k)
+    B, Lout, C, _ = win.shape
+    rows = win.reshape(B * Lout, C * k)
+    w = conv.weight.reshape(conv.out_channels, C * k)
+    if torch.is_grad_enabled():   # split-K weight gradient (K = B * Lout rows)
+        y = _LinearSplitK.apply(rows, w, conv.bias)
+    else:
+        y = torch.addmm(conv.bias, rows, w.t())
+    return y.view(B, Lout, conv.out_channels)
+
+
+class HistoryEncoder(nn.Sequential):
+    """The reference's long-history CNN (actor_critic_dh.py:75-96): the same nn.Sequential layers and parameter
+    names (so checkpoints load either way).  On the host the layers run as written (nn.Conv1d, bit-identical to the
+    reference's CPU path); on the MI355X the two Conv1d run as unfold + GEMM (conv1d_as_gemm) with the activations
+    kept channels-last: MIOpen's Conv1d kernels for this shape (66-channel, length-47 input, batch 49,152 in the PPO
+    update) were the update's dominant cost.  Same arithmetic up to fp32 summation order."""
+
+    def forward(self, x):
+        if not x.is_cuda:
+            return super().forward(x)
+        last = False   # x is (B, C, L) until the first conv; channels-last after it
+        for m in self:
+            if isinstance(m, nn.Conv1d):
+                x = conv1d_as_gemm(x, m, channels_last=last)
+                last = True
+            elif isinstance(m, nn.Flatten) and last:
+                x = x.transpose(1, 2).reshape(x.shape[0], -1)   # (B, O, Lout) order, as nn.Flatten of NCL
+                last = False
+            else:
+                x = m(x)
+        return x
 
 
 def _history_encoder(frames, features, filters, kernels, strides, code_dim):
@@ -35,8 +141,8 @@ def _history_encoder(frames, features, filters, kernels, strides, code_dim):
         layers += [nn.Conv1d(ch, out_ch, kernel_size=k, stride=s), nn.ReLU()]
         length = (length - k + s) // s  # the reference's length bookkeeping (equals floor((L - k) / s) + 1)
         ch = out_ch
-    layers += [nn.Flatten(), nn.Linear(length * ch, 128), nn.ELU(), nn.Linear(128, code_dim)]
-    return nn.Sequential(*layers)
+    layers += [nn.Flatten(), Linear(length * ch, 128), nn.ELU(), Linear(128, code_dim)]
+    return HistoryEncoder(*layers)
 
 
 class ActorCriticDH(nn.Module):

@@ -6,7 +6,6 @@ The exported module maps the 66-frame observation history (N, 3102) to (action m
 linear velocity (N, 3)) -- the deployment interface of the reference's policy_dh.jit.  Checkpoints are read
 with weights_only=True.
 """
-import copy
 import os
 import sys
 
@@ -16,6 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, REPO)
 
 from ti5_isaacgym_amd.algo import ActorCriticDH  # noqa: E402
+from ti5_isaacgym_amd.algo.dh_policy import plain_copy  # noqa: E402
 from ti5_isaacgym_amd.envs.configs import DHT1StandCfgPPO  # noqa: E402
 from ti5_isaacgym_amd.utils.helpers import class_to_dict  # noqa: E402
 
@@ -23,9 +23,10 @@ from ti5_isaacgym_amd.utils.helpers import class_to_dict  # noqa: E402
 class ExportedDH(torch.nn.Module):
     def __init__(self, ac: ActorCriticDH):
         super().__init__()
-        self.actor = copy.deepcopy(ac.actor).cpu()
-        self.long_history = copy.deepcopy(ac.long_history).cpu()
-        self.state_estimator = copy.deepcopy(ac.state_estimator).cpu()
+        # plain torch layers (the device-path Linear / HistoryEncoder subclasses are not scriptable)
+        self.actor = plain_copy(ac.actor).cpu()
+        self.long_history = plain_copy(ac.long_history).cpu()
+        self.state_estimator = plain_copy(ac.state_estimator).cpu()
         self.num_short_obs = ac.num_short_obs
         self.in_channels = ac.in_channels
         self.num_proprio_obs = ac.num_proprio_obs
