@@ -1,6 +1,6 @@
 """Build libt1env_hip.so for gfx950 in-tree (the .so travels to the GPU box with the repo snapshot).
 
-    python -m ti5_isaacgym_amd.build [--debug]
+    python -m ti5_isaacgym_amd.build [--out=PATH] [--dyn-opt=-O3] [extra hipcc flags]
 """
 import os
 import subprocess
@@ -8,17 +8,21 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-# translation unit -> optimisation level.  k_dynamics is built at -O1: at -O2/-O3 the optimiser produced wrong
-# dynamics for it (caught by tests/test_gpu_dynamics.py) and -O1 is also the fastest build of it.
+# translation unit -> optimisation level.  The dynamics unit is built at -O1, its fastest level (-O2/-O3 are correct
+# and 6-7 % slower).  Round 1's -O2/-O3 wrong dynamics bisected to the load/store vectorizer over the __restrict__
+# model-pointer loads; the -O3 guard build (OUT_O3) keeps every level under the fp64 check.
 UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1")]
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
+# guard build: the dynamics unit at -O3 (tests/test_gpu_opt_levels.py keeps it under the fp64 dynamics check)
+OUT_O3 = os.path.join(HERE, "_lib", "var", "libt1env_hip_dyn_o3.so")
 DEPS = [os.path.join(CSRC, f) for f in ("t1env.hip", "t1env_dynamics.hip", "t1_dynamics.h", "t1_common.h", "t1env_post.h",
                                        "t1_model_conv.h", "t1env_device.h", "t1env_internal.h")] + \
     [os.path.join(os.path.dirname(HERE), "include", "t1env.h")]
 ARCH = os.environ.get("T1ENV_ARCH", "gfx950")
 
 
-def build(force=False, extra=(), out=None):
+def build(force=False, extra=(), out=None, dyn_opt=None):
+    """dyn_opt: optimisation level of the dynamics unit for A/B and guard variants (default -O1)."""
     out = out or OUT
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in DEPS):
         return out
@@ -27,15 +31,24 @@ def build(force=False, extra=(), out=None):
     # -fno-slp-vectorize: the SLP pass packs scalar pairs of the dynamics into v_pk_* ops, which forces aligned
     # register pairs and piles up v_mov shuffles; in k_dynamics that alone turned ~40 scratch ops into ~470.
     common = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result", "-fno-slp-vectorize", *extra]
-    objs = []
-    for src, opt in UNITS:
+    objs, procs = [], []
+    for src, opt in UNITS:  # the units compile concurrently
+        if dyn_opt and src == "t1env_dynamics.hip":
+            opt = dyn_opt
         obj = os.path.join(os.path.dirname(out), os.path.splitext(src)[0] + ".o")
-        subprocess.run([hipcc, opt, *common, "-c", "-o", obj, os.path.join(CSRC, src)], check=True)
+        procs.append(subprocess.Popen([hipcc, opt, *common, "-c", "-o", obj, os.path.join(CSRC, src)]))
         objs.append(obj)
+    for pr in procs:
+        if pr.wait() != 0:
+            raise subprocess.CalledProcessError(pr.returncode, pr.args)
     subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs], check=True)
     os.replace(out + ".tmp", out)
     return out
 
 
 if __name__ == "__main__":
-    print(build(force=True, extra=[a for a in sys.argv[1:] if a.startswith("-")]))
+    args = sys.argv[1:]
+    out = next((a.split("=", 1)[1] for a in args if a.startswith("--out=")), None)
+    dyn_opt = next((a.split("=", 1)[1] for a in args if a.startswith("--dyn-opt=")), None)
+    print(build(force=True, out=out, dyn_opt=dyn_opt,
+                extra=[a for a in args if a.startswith("-") and not a.startswith(("--out=", "--dyn-opt="))]))
