@@ -275,6 +275,11 @@ template <typename R> T1_HD void motion_subspace(const DynModel& M, int b, const
 }
 
 // world inertia about COM (xx yy zz xy xz yz) of body b
+// timing-only what-if builds (never the product): the body-frame inertia used as if the body were unrotated
+template <typename R> T1_HD void world_inertia_unrotated(const DynModel& M, int b, R scale, R out[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) out[i] = scale * R(M.inertia[b][i]);
+}
 template <typename R>
 T1_HD void world_inertia(const DynModel& M, int b, const M3<R>& Rb, R scale, R out[6]) {
   const float* I = M.inertia[b];
@@ -933,7 +938,11 @@ T1_HD void leg_forward_nc(const DynModel& M, const LegParams<R>& P, const BaseFr
     for (int i = 0; i < 6; ++i) A[i] += cr[i];
     if constexpr ((CM >> k) & 1) pub(kc, Rk, pk, V);
     R Icw[6];
+#ifdef T1_WHATIF_FWD_NOROT
+    world_inertia_unrotated(M, b, P.inertia_scale[k], Icw);
+#else
     world_inertia(M, b, Rk, P.inertia_scale[k], Icw);
+#endif
     const V3<R> c = pk + mul(Rk, v3<R>(M.com[b][0], M.com[b][1], M.com[b][2]));
     rnea_bias_com(P.mass[k], c, Icw, V, A, dt, st.g[k]);
   };
@@ -970,7 +979,11 @@ T1_HD void leg_backward_nc(const DynModel& M, const LegParams<R>& P, const R q[N
     joint_subspace<T1_LEG_AXIS[k]>(M, b, Rk, pk, Sk);
     {
       R Icw[6];
+#ifdef T1_WHATIF_BWD_NOROT
+      world_inertia_unrotated(M, b, P.inertia_scale[k], Icw);
+#else
       world_inertia(M, b, Rk, P.inertia_scale[k], Icw);
+#endif
       const V3<R> c = pk + mul(Rk, v3<R>(M.com[b][0], M.com[b][1], M.com[b][2]));
       composite_add(Ac, P.mass[k], c, Icw);
     }

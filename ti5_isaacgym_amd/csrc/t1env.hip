@@ -422,8 +422,8 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
     if (const char* w = getenv("T1ENV_DYN_WAVES"))
       if (atoi(w) == 2 || atoi(w) == 4) e->dyn.waves = atoi(w);
     e->dyn.shift_blocks = 0;
-    if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))
-      if (atoi(sb) > 0) e->dyn.shift_blocks = atoi(sb);
+    if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))  // > 0: shift workgroups in the launch; -1: stand-alone shift
+      if (atoi(sb) > 0 || atoi(sb) == -1) e->dyn.shift_blocks = atoi(sb);
   }
   for (int b = 0; b < NB; ++b) e->max_contact_radius = fmaxf(e->max_contact_radius, dm.contact_radius[b]);
   *out = e;

@@ -217,20 +217,20 @@ __device__ __forceinline__ void shift_store(float* __restrict__ out, int64_t tot
 }
 
 // chunks [lo4, hi4) of one history buffer, lane t0 of `stride` lanes
-template <int F, int H, bool SC1 = false>
+template <int F, int H, bool SC1 = false, int U = SHIFT_UNROLL>
 __device__ __forceinline__ void shift_range(const float* __restrict__ in, float* __restrict__ out, int64_t total,
                                             int64_t lo4, int64_t hi4, int64_t t0, int64_t stride) {
-  for (int64_t base = lo4 + t0; base < hi4; base += SHIFT_UNROLL * stride) {
-    float4 a[SHIFT_UNROLL], b[SHIFT_UNROLL];
+  for (int64_t base = lo4 + t0; base < hi4; base += U * stride) {
+    float4 a[U], b[U];
 #pragma unroll
-    for (int u = 0; u < SHIFT_UNROLL; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int64_t sa = ((base + u * stride) * 4 + F) & ~(int64_t)3;
       const int64_t sc = sa + 8 <= total ? sa : (total - 8) & ~(int64_t)3;  // tail: aligned in-bounds dummy
       a[u] = *reinterpret_cast<const float4*>(in + sc);
       b[u] = *reinterpret_cast<const float4*>(in + sc + 4);
     }
 #pragma unroll
-    for (int u = 0; u < SHIFT_UNROLL; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int64_t i4 = base + u * stride;
       if (i4 >= hi4) break;
       const int64_t i = i4 * 4, s = i + F, sa = s & ~(int64_t)3;
@@ -243,6 +243,58 @@ __device__ __forceinline__ void shift_range(const float* __restrict__ in, float*
         y = make_float4(t[4], t[5], t[6], t[7]);
       }
       shift_store<F, H, SC1>(out, total, i, x, y, (int)(s - sa));
+    }
+  }
+}
+
+// The in-launch shift's form of shift_range over whole rows [r0, r1): indices relative to the first row fit 32 bits,
+// so the per-chunk row / column split is a 32-bit division by the constant row width instead of a 64-bit one (the
+// fused step's shift workgroups run one wave per SIMD, where that integer work, not HBM, set their rate).
+template <int F, int H, bool SC1, int U>
+__device__ __forceinline__ void shift_rows_f32(const float* __restrict__ in, float* __restrict__ out, int64_t total,
+                                               int64_t r0, int64_t r1, int t0, int stride) {
+  constexpr uint32_t ROW = F * H;
+  const float* __restrict__ in0 = in + r0 * ROW;
+  float* __restrict__ out0 = out + r0 * ROW;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);  // elements from in0 to the buffer end
+  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
+  const uint32_t nel = span < lim ? span : lim;
+  const uint32_t n4 = (nel + 3) / 4;
+  for (uint32_t base = t0; base < n4; base += U * stride) {
+    float4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sa = ((base + u * stride) * 4 + F) & ~3u;
+      const uint32_t sc = sa + 8 <= lim ? sa : (lim - 8) & ~3u;  // tail: aligned in-bounds dummy
+      a[u] = *reinterpret_cast<const float4*>(in0 + sc);
+      b[u] = *reinterpret_cast<const float4*>(in0 + sc + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = base + u * stride;
+      if (c >= n4) break;
+      const uint32_t i = c * 4, sidx = i + F, sa = sidx & ~3u;
+      float4 x = a[u], y = b[u];
+      if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
+        float t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
+        x = make_float4(t[0], t[1], t[2], t[3]);
+        y = make_float4(t[4], t[5], t[6], t[7]);
+      }
+      const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+      const int rem = (int)(sidx - sa);
+      const uint32_t col0 = i - (i / ROW) * ROW;
+      if (col0 + 3 < ROW - F && i + 3 < lim) {  // 4 older-frame columns of one row
+        store4<SC1>(out0 + i, make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]));
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t e = i + k;
+        if (e >= lim) break;
+        if (e - (e / ROW) * ROW < ROW - F) store1<SC1>(out0 + e, src[rem + k]);
+      }
     }
   }
 }
@@ -264,21 +316,21 @@ template <bool SC1> __device__ __forceinline__ void store2B(uint16_t* p, uint16_
     *p = v;
   }
 }
-template <int F, int H, bool SC1 = false>
+template <int F, int H, bool SC1 = false, int U = SHIFT_UNROLL>
 __device__ __forceinline__ void shift_range_h(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                               int64_t total, int64_t lo8, int64_t hi8, int64_t t0, int64_t stride) {
   constexpr int ROW = F * H, REM = F % 8, M = REM / 2;
-  for (int64_t base = lo8 + t0; base < hi8; base += SHIFT_UNROLL * stride) {
-    u32x4 a[SHIFT_UNROLL], b[SHIFT_UNROLL];
+  for (int64_t base = lo8 + t0; base < hi8; base += U * stride) {
+    u32x4 a[U], b[U];
 #pragma unroll
-    for (int u = 0; u < SHIFT_UNROLL; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int64_t sa = ((base + u * stride) * 8 + F) & ~(int64_t)7;
       const int64_t sc = sa + 16 <= total ? sa : (total - 16) & ~(int64_t)7;  // tail: aligned in-bounds dummy
       a[u] = *reinterpret_cast<const u32x4*>(in + sc);
       b[u] = *reinterpret_cast<const u32x4*>(in + sc + 8);
     }
 #pragma unroll
-    for (int u = 0; u < SHIFT_UNROLL; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int64_t c8 = base + u * stride;
       if (c8 >= hi8) break;
       const int64_t i = c8 * 8, sa = (i + F) & ~(int64_t)7;
@@ -316,6 +368,63 @@ __device__ __forceinline__ void shift_range_h(const uint16_t* __restrict__ in, u
   }
 }
 
+// shift_range_h's in-launch form over whole rows [r0, r1) with 32-bit local indices (see shift_rows_f32)
+template <int F, int H, bool SC1, int U>
+__device__ __forceinline__ void shift_rows_f16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                               int64_t total, int64_t r0, int64_t r1, int t0, int stride) {
+  constexpr uint32_t ROW = F * H, REM = F % 8, M = REM / 2;
+  const uint16_t* __restrict__ in0 = in + r0 * ROW;
+  uint16_t* __restrict__ out0 = out + r0 * ROW;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
+  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
+  const uint32_t nel = span < lim ? span : lim;
+  const uint32_t n8 = (nel + 7) / 8;
+  for (uint32_t base = t0; base < n8; base += U * stride) {
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sa = ((base + u * stride) * 8 + F) & ~7u;
+      const uint32_t sc = sa + 16 <= lim ? sa : (lim - 16) & ~7u;
+      a[u] = *reinterpret_cast<const u32x4*>(in0 + sc);
+      b[u] = *reinterpret_cast<const u32x4*>(in0 + sc + 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c8 = base + u * stride;
+      if (c8 >= n8) break;
+      const uint32_t i = c8 * 8, sa = (i + F) & ~7u;
+      uint32_t w[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
+      if (sa + 16 > lim) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t lo = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
+          const uint32_t hi = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
+          w[k] = lo | (hi << 16);
+        }
+      }
+      u32x4 o;
+      if constexpr (REM % 2 == 0) {
+        o = u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
+      } else {
+        o = u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], 2), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], 2),
+                  __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], 2), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], 2)};
+      }
+      const uint32_t col0 = i - (i / ROW) * ROW;
+      if (col0 + 7 < ROW - F && i + 7 < lim) {
+        store16B<SC1>(out0 + i, o);
+        continue;
+      }
+      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t e = i + k;
+        if (e >= lim) break;
+        if (e - (e / ROW) * ROW < ROW - F) store2B<SC1>(out0 + e, (uint16_t)(ow[k / 2] >> (16 * (k & 1))));
+      }
+    }
+  }
+}
+
 // lane `t0` of `stride` lanes: the obs history, then the critic history
 __device__ __forceinline__ void shift_history(const ShiftArgs& S, int64_t t0, int64_t stride) {
   if (S.half) {
@@ -332,26 +441,20 @@ __device__ __forceinline__ void shift_history(const ShiftArgs& S, int64_t t0, in
 
 // the rows [r0, r1) of both histories (r0 a multiple of 8, so both row ranges start on a 16-B chunk of either
 // element size), with agent-coherent (sc1) stores
+template <int U = SHIFT_UNROLL>
 __device__ __forceinline__ void shift_rows_range_sc1(const ShiftArgs& S, int64_t r0, int64_t r1, int64_t t0,
                                                  int64_t stride) {
-  constexpr int64_t RO = T1_NOBS * T1_HIST, RP = T1_NPRIV * T1_CHIST;
   if (S.half) {
-    const int64_t n8o = (S.total_obs + 7) / 8, n8p = (S.total_priv + 7) / 8;
-    const int64_t ho = (r1 * RO + 7) / 8, hp = (r1 * RP + 7) / 8;
-    shift_range_h<T1_NOBS, T1_HIST, true>(reinterpret_cast<const uint16_t*>(S.obs_in),
-                                          reinterpret_cast<uint16_t*>(S.obs_out), S.total_obs, r0 * RO / 8,
-                                          ho < n8o ? ho : n8o, t0, stride);
-    shift_range_h<T1_NPRIV, T1_CHIST, true>(reinterpret_cast<const uint16_t*>(S.priv_in),
-                                            reinterpret_cast<uint16_t*>(S.priv_out), S.total_priv, r0 * RP / 8,
-                                            hp < n8p ? hp : n8p, t0, stride);
+    shift_rows_f16<T1_NOBS, T1_HIST, true, U>(reinterpret_cast<const uint16_t*>(S.obs_in),
+                                              reinterpret_cast<uint16_t*>(S.obs_out), S.total_obs, r0, r1, (int)t0,
+                                              (int)stride);
+    shift_rows_f16<T1_NPRIV, T1_CHIST, true, U>(reinterpret_cast<const uint16_t*>(S.priv_in),
+                                                reinterpret_cast<uint16_t*>(S.priv_out), S.total_priv, r0, r1, (int)t0,
+                                                (int)stride);
     return;
   }
-  const int64_t n4o = (S.total_obs + 3) / 4, n4p = (S.total_priv + 3) / 4;
-  const int64_t ho = (r1 * RO + 3) / 4, hp = (r1 * RP + 3) / 4;
-  shift_range<T1_NOBS, T1_HIST, true>(S.obs_in, S.obs_out, S.total_obs, r0 * RO / 4, ho < n4o ? ho : n4o, t0,
-                                      stride);
-  shift_range<T1_NPRIV, T1_CHIST, true>(S.priv_in, S.priv_out, S.total_priv, r0 * RP / 4, hp < n4p ? hp : n4p, t0,
-                                        stride);
+  shift_rows_f32<T1_NOBS, T1_HIST, true, U>(S.obs_in, S.obs_out, S.total_obs, r0, r1, (int)t0, (int)stride);
+  shift_rows_f32<T1_NPRIV, T1_CHIST, true, U>(S.priv_in, S.priv_out, S.total_priv, r0, r1, (int)t0, (int)stride);
 }
 
 // zero `count` elements of row `row` (row width `width`) of a history buffer, fp32 or fp16

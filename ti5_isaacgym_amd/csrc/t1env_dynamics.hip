@@ -93,6 +93,11 @@ constexpr int DYN_BLOCK = 2 * DYN_ENVS;
 constexpr int D4_BLOCK = 4 * DYN_ENVS;
 constexpr int XCH = 27;  // Sym6 (21) + rhs (6)
 constexpr int SHIFT_UNIT = 8;  // rows per shift/zeroing unit (a multiple of 4: unit boundaries are 16-B aligned)
+// chunks per lane in flight in the in-launch shift: the shift workgroups run one wave per SIMD on the CUs the dynamics
+// leave idle, so they need deep per-lane batches (r02u: 8 -> 16 took the shift alone from 114 to 106 us at 8192 envs)
+#ifndef T1_FUSED_SHIFT_UNROLL
+#define T1_FUSED_SHIFT_UNROLL 16
+#endif
 static_assert(DYN_ENVS % SHIFT_UNIT == 0, "a dynamics workgroup owns whole shift units");
 
 // Handoff word of a shift unit: [epoch tag : 22][reset mask : 8][dynamics done : 1][shift done : 1].  Set
@@ -128,22 +133,29 @@ __device__ __forceinline__ void shift_workgroup(const ShiftArgs& S, const FusedA
   if constexpr (!FUSED) {
     shift_history(S, (int64_t)j * BS + threadIdx.x, (int64_t)nsw * BS);
   } else {
+    // a contiguous run of units per workgroup, shifted as one flat row range: each lane keeps
+    // T1_FUSED_SHIFT_UNROLL x 32 B of loads in flight, enough for HBM rate from one workgroup per CU on the CUs
+    // the dynamics leave idle (a per-unit loop re-starts its unrolled batches every 8 rows and wastes their tails)
     const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
-    for (int u = j; u < units; u += nsw) {
-      const int64_t r0 = (int64_t)u * SHIFT_UNIT, r1 = r0 + SHIFT_UNIT < N ? r0 + SHIFT_UNIT : N;
-      shift_rows_range_sc1(S, r0, r1, threadIdx.x, BS);
+    const int per = (units + nsw - 1) / nsw;
+    const int u0 = j * per < units ? j * per : units, u1 = u0 + per < units ? u0 + per : units;
+    const int mine = u1 - u0;  // units of this workgroup
+#ifndef T1_WHATIF_NO_SHIFT  // timing-only what-if build: the history is not shifted (handoff and zeroing kept)
+    if (mine > 0) {
+      const int64_t r0 = (int64_t)u0 * SHIFT_UNIT, r1 = (int64_t)u1 * SHIFT_UNIT < N ? (int64_t)u1 * SHIFT_UNIT : N;
+      shift_rows_range_sc1<T1_FUSED_SHIFT_UNROLL>(S, r0, r1, threadIdx.x, BS);
     }
+#endif
     // every lane's sc1 stores complete (visible at agent scope) before any handoff
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    const int mine = units > j ? (units - j + nsw - 1) / nsw : 0;  // units of this workgroup
     for (int k0 = 0; k0 < mine; k0 += BS) {
       const int k = k0 + (int)threadIdx.x;
-      if (k < mine) words[threadIdx.x] = unit_handoff(FA.unit_state + j + k * nsw, FA.epoch, HANDOFF_SHIFT);
+      if (k < mine) words[threadIdx.x] = unit_handoff(FA.unit_state + u0 + k, FA.epoch, HANDOFF_SHIFT);
       __syncthreads();
       const int cnt = mine - k0 < BS ? mine - k0 : BS;
       for (int i = 0; i < cnt; ++i)
-        if (handoff_complete(words[i])) zero_unit_resets(S, j + (k0 + i) * nsw, words[i], threadIdx.x, BS);
+        if (handoff_complete(words[i])) zero_unit_resets(S, u0 + k0 + i, words[i], threadIdx.x, BS);
       __syncthreads();
     }
   }
@@ -457,8 +469,10 @@ __device__ __forceinline__ void body_terms(const DynModel& M, const Terrain& T, 
   float Vb[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) Vb[i] = P[12 + i][lane];
+#ifndef T1_WHATIF_NO_HELPER_CONTACT  // timing-only what-if build: the leg's shank / foot contact terms left zero
   body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pb.z + abs.z - M.contact_radius[b], bound, M.contact_start[b], Rb, pb,
                                          abs, Vb, mu, dt, Cc, cc);
+#endif
   lds_put_sym(dst, lane, Cc, cc);
 }
 
@@ -892,6 +906,19 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
       lds_get_sym(lds.ct[leg], lane, Csh, csh);
       lds_get_sym(lds.ct[leg] + XCH, lane, Cft, cft);
       leg_apply_contacts<K_SHANK, K_FOOT>(Csh, csh, Cft, cft, tau, dt, st, lb, Ab, g6);
+#ifdef T1_WHATIF_FOLD2  // timing-only: the fold-in and elimination run twice (second result scaled by 0 and added)
+      {
+        LegBlock<float> lb2 = lb;
+        Sym6<float> Ab2 = Ab;
+        float g2[6], rb2[6];
+        for (int i = 0; i < 6; ++i) g2[i] = g6[i];
+        leg_apply_contacts<K_SHANK, K_FOOT>(Csh, csh, Cft, cft, tau, dt, st, lb2, Ab2, g2);
+        for (int i = 0; i < 6; ++i) rb2[i] = -g2[i];
+        eliminate_leg(lb2, Ab2, rb2);
+        for (int i = 0; i < 21; ++i) Ab.a[i] += 0.0f * Ab2.a[i];
+        for (int i = 0; i < 6; ++i) g6[i] += 0.0f * rb2[i];
+      }
+#endif
     }
     float rb[6];
 #pragma unroll
@@ -1003,6 +1030,7 @@ int t1_dyn_waves_default() { return 4; }
 
 constexpr int MIN_SHIFT_BLOCKS = 64;
 bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg) {
+  if (cfg.shift_blocks < 0) return true;   // forced stand-alone shift (tuning: T1ENV_SHIFT_BLOCKS=-1)
   if (cfg.shift_blocks > 0) return false;  // explicit shift-workgroup count (tuning)
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
   const int per_cu = cfg.waves == 4 ? 1 : 2;
