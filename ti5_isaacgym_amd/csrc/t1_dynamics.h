@@ -355,9 +355,87 @@ T1_HD void contact_point(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[
   moments_add(fric, dt * ct, x);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device, fp32: contact_point for two points of a body at once, every arithmetic step on float2 (v_pk_fma/mul/add_f32:
+// the pair shares the body velocity, so nothing needs shuffling) into pair accumulators folded once per body.  A
+// point not in contact (c0/c1 false) contributes exactly zero.  The same algebra as contact_point; only the
+// summation order of the per-body sums differs.
+typedef float t1f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ t1f2 t1f2_of(float a, float b) { return t1f2{a, b}; }
+struct PairAcc {
+  t1f2 A[21];  // dt J^T C J, packed upper triangle (sidx), summed over the pair halves at the end
+  t1f2 g[6];   // dt * [torque; force] of the points
+  t1f2 m, hx, hy, hz, sxx, syy, szz, sxy, sxz, syz;  // friction point-mass moments (PointMoments)
+};
+__device__ __forceinline__ void pair_acc_zero(PairAcc& P) {
+#pragma unroll
+  for (int k = 0; k < 21; ++k) P.A[k] = t1f2{0.0f, 0.0f};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) P.g[k] = t1f2{0.0f, 0.0f};
+  P.m = P.hx = P.hy = P.hz = P.sxx = P.syy = P.szz = P.sxy = P.sxz = P.syz = t1f2{0.0f, 0.0f};
+}
+__device__ __forceinline__ void contact_pair(const DynModel& M, const V3<float> x0, const V3<float> x1, const V3<float> n0,
+                                             const V3<float> n1, float pen0, float pen1, bool c0, bool c1,
+                                             const float Vb[6], float mu, float dt, PairAcc& P) {
+  const float k = M.k_contact, d = M.d_contact;
+  const t1f2 xx = t1f2_of(x0.x, x1.x), xy = t1f2_of(x0.y, x1.y), xz = t1f2_of(x0.z, x1.z);
+  const t1f2 nx = t1f2_of(n0.x, n1.x), ny = t1f2_of(n0.y, n1.y), nz = t1f2_of(n0.z, n1.z);
+  const t1f2 pen = t1f2_of(c0 ? pen0 : 0.0f, c1 ? pen1 : 0.0f);
+  // vp = v_O + omega x x
+  const t1f2 vpx = Vb[3] + (Vb[1] * xz - Vb[2] * xy);
+  const t1f2 vpy = Vb[4] + (Vb[2] * xx - Vb[0] * xz);
+  const t1f2 vpz = Vb[5] + (Vb[0] * xy - Vb[1] * xx);
+  const t1f2 vn = nx * vpx + ny * vpy + nz * vpz;
+  const t1f2 vtx = vpx - vn * nx, vty = vpy - vn * ny, vtz = vpz - vn * nz;
+  const t1f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
+  const float vs = M.friction_vs;
+  const float vtn0 = fsqrt(vt2.x), vtn1 = fsqrt(vt2.y);
+  const bool ap0 = vn.x < 0.0f, ap1 = vn.y < 0.0f;  // approaching: implicit normal damping
+  const t1f2 cn = t1f2_of(c0 && ap0 ? dt * k + d : 0.0f, c1 && ap1 ? dt * k + d : 0.0f);
+  const t1f2 fn_est = k * pen + t1f2_of(ap0 ? -d * vn.x : 0.0f, ap1 ? -d * vn.y : 0.0f);
+  const t1f2 ct = mu * fn_est * t1f2_of(c0 ? rcp(vtn0 > vs ? vtn0 : vs) : 0.0f, c1 ? rcp(vtn1 > vs ? vtn1 : vs) : 0.0f);
+  // force at the current velocity f = (k pen - cn vn) n - ct vt, and its moment about O
+  const t1f2 fs = k * pen - cn * vn;
+  const t1f2 fx = fs * nx - ct * vtx, fy = fs * ny - ct * vty, fz = fs * nz - ct * vtz;
+  P.g[0] += dt * (xy * fz - xz * fy);
+  P.g[1] += dt * (xz * fx - xx * fz);
+  P.g[2] += dt * (xx * fy - xy * fx);
+  P.g[3] += dt * fx;
+  P.g[4] += dt * fy;
+  P.g[5] += dt * fz;
+  // (cn - ct) w_n w_n^T with w_n = [x cross n; n]
+  const t1f2 w[6] = {xy * nz - xz * ny, xz * nx - xx * nz, xx * ny - xy * nx, nx, ny, nz};
+  const t1f2 cc = dt * (cn - ct);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const t1f2 ci = cc * w[i];
+#pragma unroll
+    for (int j = i; j < 6; ++j) P.A[sidx(i, j)] += ci * w[j];
+  }
+  // friction stiffness ct (I - n n^T) folded as point-mass moments of weight dt ct
+  const t1f2 cm = dt * ct, cx = cm * xx, cy = cm * xy, cz = cm * xz;
+  P.m += cm; P.hx += cx; P.hy += cy; P.hz += cz;
+  P.sxx += cx * xx; P.syy += cy * xy; P.szz += cz * xz;
+  P.sxy += cx * xy; P.sxz += cx * xz; P.syz += cy * xz;
+}
+// fold the pair accumulators into A (Sym6) and g (subtracted, like contact_point)
+__device__ __forceinline__ void pair_acc_flush(const PairAcc& P, Sym6<float>& A, float g[6]) {
+#pragma unroll
+  for (int k = 0; k < 21; ++k) A.a[k] += P.A[k].x + P.A[k].y;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) g[k] -= P.g[k].x + P.g[k].y;
+  PointMoments<float> F;
+  F.m = P.m.x + P.m.y; F.hx = P.hx.x + P.hx.y; F.hy = P.hy.x + P.hy.y; F.hz = P.hz.x + P.hz.y;
+  F.sxx = P.sxx.x + P.sxx.y; F.syy = P.syy.x + P.syy.y; F.szz = P.szz.x + P.szz.y;
+  F.sxy = P.sxy.x + P.sxy.y; F.sxz = P.sxz.x + P.sxz.y; F.syz = P.syz.x + P.syz.y;
+  moments_flush(F, A);
+}
+#endif
+
 // NP points known at compile time: phase 1 transforms every point and queries the terrain with no branch
 // in between, so all coordinate (scalar) and height-field (vector) loads issue together and the body pays
-// one memory latency instead of one per point; phase 2 runs the contact math for the points in contact.
+// one memory latency instead of one per point; phase 2 runs the contact math for the points in contact
+// (on the device in fp32: two points per packed instruction, contact_pair).
 #ifndef T1_CONTACT_BATCH
 #define T1_CONTACT_BATCH 8
 #endif
@@ -368,6 +446,10 @@ T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, con
   static_assert(NP % CH == 0, "contact points per body must be a multiple of the batch");
   PointMoments<R> fric;
   moments_zero(fric);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(T1_SCALAR_CONTACT)
+  PairAcc pacc;
+  if constexpr (std::is_same<R, float>::value && CH % 2 == 0) pair_acc_zero(pacc);
+#endif
 #pragma unroll
   for (int c0 = 0; c0 < NP; c0 += CH) {
     V3<R> xs[CH];
@@ -384,14 +466,79 @@ T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, con
     __builtin_amdgcn_s_waitcnt(0);  // profiling build: separate the height loads' latency from the math
     T1_PROF_MARK(17);
 #endif
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(T1_SCALAR_CONTACT)
+    if constexpr (std::is_same<R, float>::value && CH % 2 == 0) {
 #pragma unroll
-    for (int i = 0; i < CH; ++i)
-      if (dz[i] > R(0)) {  // below the surface (the normal's z is positive)
-        const V3<R> n = terrain_normal<HF>(gxs[i], gys[i]);
-        contact_point(M, xs[i], n, dz[i] * n.z, Vb, mu, dt, A, g, fric);
+      for (int i = 0; i < CH; i += 2) {
+        const bool c0 = dz[i] > R(0), c1 = dz[i + 1] > R(0);  // below the surface (the normal's z is positive)
+        if (c0 || c1) {
+          const V3<R> n0 = terrain_normal<HF>(gxs[i], gys[i]), n1 = terrain_normal<HF>(gxs[i + 1], gys[i + 1]);
+          contact_pair(M, xs[i], xs[i + 1], n0, n1, dz[i] * n0.z, dz[i + 1] * n1.z, c0, c1, Vb, mu, dt, pacc);
+        }
       }
+    } else
+#endif
+    {
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        if (dz[i] > R(0)) {  // below the surface (the normal's z is positive)
+          const V3<R> n = terrain_normal<HF>(gxs[i], gys[i]);
+          contact_point(M, xs[i], n, dz[i] * n.z, Vb, mu, dt, A, g, fric);
+        }
+    }
     T1_PROF_MARK(18);
   }
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(T1_SCALAR_CONTACT)
+  if constexpr (std::is_same<R, float>::value && CH % 2 == 0) pair_acc_flush(pacc, A, g);
+#endif
+  moments_flush(fric, A);
+}
+
+// The same body contact split into its two phases, for callers that batch the queries of several bodies before any
+// contact math (one memory latency for all of them): contact_query transforms the NP points and queries the
+// terrain, contact_terms accumulates their contact terms into (A, g) exactly as body_contact_np does.
+template <int NP, typename R> struct ContactQuery {
+  V3<R> xs[NP];
+  R dz[NP], gx[NP], gy[NP];
+};
+template <bool HF, int NP, typename R>
+T1_HD void contact_query(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb, V3<R> base_abs,
+                         ContactQuery<NP, R>& Q) {
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int c = c_begin + i;
+    Q.xs[i] = pb + mul(Rb, v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]));
+    const V3<R> X = Q.xs[i] + base_abs;
+    Q.dz[i] = terrain_height<HF>(T, X.x, X.y, Q.gx[i], Q.gy[i]) - X.z;
+  }
+}
+template <bool HF, int NP, typename R>
+T1_HD void contact_terms(const DynModel& M, const ContactQuery<NP, R>& Q, const R Vb[6], R mu, R dt, Sym6<R>& A,
+                         R g[6]) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(T1_SCALAR_CONTACT)
+  if constexpr (std::is_same<R, float>::value && NP % 2 == 0) {
+    PairAcc pacc;
+    pair_acc_zero(pacc);
+#pragma unroll
+    for (int i = 0; i < NP; i += 2) {
+      const bool c0 = Q.dz[i] > R(0), c1 = Q.dz[i + 1] > R(0);
+      if (c0 || c1) {
+        const V3<R> n0 = terrain_normal<HF>(Q.gx[i], Q.gy[i]), n1 = terrain_normal<HF>(Q.gx[i + 1], Q.gy[i + 1]);
+        contact_pair(M, Q.xs[i], Q.xs[i + 1], n0, n1, Q.dz[i] * n0.z, Q.dz[i + 1] * n1.z, c0, c1, Vb, mu, dt, pacc);
+      }
+    }
+    pair_acc_flush(pacc, A, g);
+    return;
+  }
+#endif
+  PointMoments<R> fric;
+  moments_zero(fric);
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+    if (Q.dz[i] > R(0)) {
+      const V3<R> n = terrain_normal<HF>(Q.gx[i], Q.gy[i]);
+      contact_point(M, Q.xs[i], n, Q.dz[i] * n.z, Vb, mu, dt, A, g, fric);
+    }
   moments_flush(fric, A);
 }
 

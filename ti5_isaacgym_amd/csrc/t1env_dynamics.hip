@@ -476,6 +476,33 @@ __device__ __forceinline__ void body_terms(const DynModel& M, const Terrain& T, 
   lds_put_sym(dst, lane, Cc, cc);
 }
 
+// the shank and foot contact terms of leg `leg` with both bodies' terrain queries issued before any contact math
+template <bool HF>
+__device__ __forceinline__ void helper_two_bodies(const DynModel& M, const Terrain& T, const float (*P)[DYN_ENVS],
+                                                  int lane, int leg, V3<float> abs, float mu, float dt,
+                                                  float (*ct)[DYN_ENVS]) {
+  ContactQuery<T1_POINTS_PER_BODY, float> Q[2];
+  float Vb[2][6];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {  // 0 shank, 1 foot (the ct rows: shank at 0, foot at XCH)
+    const float (*D)[DYN_ENVS] = P + POSE_F + s * POSE_B;
+    const int b = 1 + 6 * leg + (s ? K_FOOT : K_SHANK);
+    const M3<float> Rb = lds_get_m3(D, lane);
+    const V3<float> pb = v3<float>(D[9][lane], D[10][lane], D[11][lane]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) Vb[s][i] = D[12 + i][lane];
+    contact_query<HF, T1_POINTS_PER_BODY>(M, T, M.contact_start[b], Rb, pb, abs, Q[s]);
+  }
+#pragma unroll
+  for (int s = 1; s >= 0; --s) {  // foot first, like the unmerged order
+    Sym6<float> Cc;
+    float cc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    sym_zero(Cc);
+    contact_terms<HF, T1_POINTS_PER_BODY>(M, Q[s], Vb[s], mu, dt, Cc, cc);
+    lds_put_sym(ct + (s ? XCH : 0), lane, Cc, cc);
+  }
+}
+
 // ---- fused-epilogue staging by the two helper waves (STAGE_NT threads).  Rows [nb, nb + nv) of the workgroup;
 // a row-major source is read as one contiguous run (consecutive threads, consecutive words: coalesced) and
 // transposed into [value][env].  All loads of a thread are issued before the first LDS write (stage_ld for
@@ -815,8 +842,15 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
       const float (*Psh)[DYN_ENVS] = P + POSE_F;
       const int32_t bound_sh = terrain_bound_raw_any(T, Psh[9][lane] + abs.x, Psh[10][lane] + abs.y);
       const int32_t bound_base = terrain_bound_raw_any(T, abs.x, abs.y);
+#ifdef T1_HELPER_MERGED_QUERIES
+      // foot and shank queried in one batch (one memory latency), the shank without its bound test
+      (void)bound_sh;
+      if (T.type == 0) helper_two_bodies<false>(M, T, P, lane, leg, abs, mu, dt, lds.ct[leg]);
+      else helper_two_bodies<true>(M, T, P, lane, leg, abs, mu, dt, lds.ct[leg]);
+#else
       body_terms(M, T, P + POSE_F + POSE_B, lane, 1 + 6 * leg + K_FOOT, abs, mu, dt, lds.ct[leg] + XCH, T1_NO_BOUND);
       body_terms(M, T, Psh, lane, 1 + 6 * leg + K_SHANK, abs, mu, dt, lds.ct[leg], bound_sh);
+#endif
       T1_PROF_MARK(3);
       __syncthreads();  // S2: contact terms published
       T1_PROF_MARK(11);
