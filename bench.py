@@ -33,6 +33,9 @@ sys.path.insert(0, REPO)
 
 B_ALG = 30678          # algorithmic bytes per env-step (fp32, default t1 config)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SHADER_GHZ = 2.4       # MI355X peak engine clock
+LONE_WAVE_VALU_PER_CYCLE = 0.25  # one VALU instruction per 4 cycles for a wave alone on its SIMD (MI355X_MICROARCH.md,
+                                 # 'vector-instruction ISSUE cost'); k_dyn4 runs one wave per SIMD (363+ VGPRs)
 # timer slots of include/t1env.h: slot "k_dynamics" brackets the dynamics launch, which on a normal step is the
 # whole fused step (k_dyn4: dynamics + post-physics epilogue + history-shift workgroups, t1env_dynamics.hip);
 # k_post_a / k_post_b only launch on the split (command-curriculum, 1 in 2400) steps
@@ -72,8 +75,10 @@ def parse():
                         "0 = never, 1 = every step)")
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02a.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02x.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
+    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r02x_sq_counters.json"),
+                   help="SQ instruction counters of the fused kernel (tools/pmc_sq_summary.py): the VALU-issue roofline")
     return p.parse_args()
 
 
@@ -192,6 +197,25 @@ def main():
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
+    # the bound that binds: the fused kernel's dynamics waves are latency / VALU-issue bound at one wave per SIMD
+    # (DESIGN.md §3).  VALU-issue roofline of a dynamics wave: its VALU instructions (SQ counters, committed
+    # profile of the same workload) over its lifetime = the live launch duration, against one instruction per 4
+    # cycles.
+    issue = None
+    if fused and dom == FUSED_KERNEL and os.path.exists(args.sq_json) and dk["avg_ms"] > 0:
+        try:
+            sq = json.load(open(args.sq_json))
+            if sq.get("envs") == N and args.mesh == "trimesh" and args.state_dtype == "fp32" and not args.push:
+                insts = sq["derived"]["valu_insts_per_dyn_wave"]
+                cyc = dk["avg_ms"] * 1e-3 * SHADER_GHZ * 1e9
+                ach = insts / cyc
+                issue = {"bound": "valu_issue", "unit": "VALU instr/cycle per dynamics wave",
+                         "achieved": round(ach, 4), "peak": LONE_WAVE_VALU_PER_CYCLE,
+                         "frac": round(ach / LONE_WAVE_VALU_PER_CYCLE, 4),
+                         "valu_insts_per_dyn_wave": round(insts), "wave_cycles": round(cyc),
+                         "source": os.path.relpath(args.sq_json, REPO)}
+        except Exception:
+            issue = None
     line = {
         "metric": "env-steps/sec at 8192 envs, t1_dh_stand, 1/2/4/8 MI355X; obs/reward parity",
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
@@ -209,6 +233,9 @@ def main():
                      "alg_bytes_per_step": b_alg * N, "alg_bytes_per_env_step": b_alg,
                      "wall_clock_GBs": round(value / world * b_alg / 1e9, 1),
                      "step_span_ms_timed": round(step_span_ms, 4) if step_span_ms else None,
+                     "binding": "dynamics waves: dependent-latency / VALU-issue chain at one wave per SIMD, not HBM "
+                                "(HBM frac above is how much of 8 TB/s the step's algorithmic bytes use)",
+                     "issue": issue,
                      "kernels": per_kernel},
         "finite": ok,
     }
