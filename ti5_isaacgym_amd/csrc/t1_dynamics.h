@@ -1103,6 +1103,38 @@ T1_HD void leg_forward_nc(const DynModel& M, const LegParams<R>& P, const BaseFr
   st.pk = pk;
 }
 
+// The contact bodies' poses and spatial velocities from the joint state, by the operations leg_forward_nc uses for
+// them (no RNEA bias, no inertia): lets the contact helper wave of k_dyn4 start from the substep's state instead of
+// waiting for the leg wave's forward pass.  pub(kconst<k>, R_k, p_k, V_k) for every contact body k of CM.
+template <int CM, typename R, typename Pub>
+T1_HD void leg_contact_kinematics(const DynModel& M, const BaseFrame<R>& F, const R q[NLEG], const R qd[NLEG], int leg,
+                                  Pub&& pub) {
+  M3<R> Rk = F.R0;
+  V3<R> pk = v3<R>(0, 0, 0);
+  R V[6], Sk[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) V[i] = F.V0[i];
+  auto fwd = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int AX = T1_LEG_AXIS[k];
+    const int b = 1 + 6 * leg + k;
+    pk = pk + mul(Rk, v3<R>(M.joint_offset[b][0], M.joint_offset[b][1], M.joint_offset[b][2]));
+    R sn, cs;
+    fsincos(R(M.axis_sign[b]) * q[k], &sn, &cs);
+    Rk = joint_rot<AX>(M, b, Rk, cs, sn);
+    joint_subspace<AX>(M, b, Rk, pk, Sk);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) V[i] += Sk[i] * qd[k];
+    if constexpr ((CM >> k) & 1) pub(kc, Rk, pk, V);
+  };
+  fwd(kconst<0>{});
+  fwd(kconst<1>{});
+  fwd(kconst<2>{});
+  fwd(kconst<3>{});
+  fwd(kconst<4>{});
+  fwd(kconst<5>{});
+}
+
 // backward pass (leaf to root) without contact and without the joint torque: D0, H0, F0 = Bl, r0 and the
 // contact-free leg composite; stores each S_k for leg_apply_contacts
 template <typename R>

@@ -88,6 +88,14 @@ using namespace t1;
 //     placement-independent, and without an L2 write-back fence (buffer_wbl2 per unit cost the concurrently
 //     running dynamics ~8 %).
 // ---------------------------------------------------------------------------------------------------
+// The contact helper waves compute the shank / foot poses themselves from the substep state the leg wave publishes
+// after integrating (leg_contact_kinematics), so their contact terms start in parallel with the leg's forward pass
+// (+2.5 % env-steps/s at 8192 envs, r02ab).  -DT1_HELPER_POSES_FROM_LEG: the previous schedule (poses published by
+// the leg's forward pass), for A/B.
+#ifndef T1_HELPER_POSES_FROM_LEG
+#define T1_HELPER_KIN 1
+#endif
+
 constexpr int DYN_ENVS = 64;
 constexpr int DYN_BLOCK = 2 * DYN_ENVS;
 constexpr int D4_BLOCK = 4 * DYN_ENVS;
@@ -503,6 +511,31 @@ __device__ __forceinline__ void helper_two_bodies(const DynModel& M, const Terra
   }
 }
 
+// body_terms for a pose held in registers (the helper's own kinematics, T1_HELPER_KIN)
+__device__ __forceinline__ void body_terms_at(const DynModel& M, const Terrain& T, const M3<float>& Rb, V3<float> pb,
+                                              const float Vb[6], int lane, int b, V3<float> abs, float mu, float dt,
+                                              float (*dst)[DYN_ENVS], int32_t bound) {
+  Sym6<float> Cc;
+  float cc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  sym_zero(Cc);
+  body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pb.z + abs.z - M.contact_radius[b], bound, M.contact_start[b], Rb, pb,
+                                         abs, Vb, mu, dt, Cc, cc);
+  lds_put_sym(dst, lane, Cc, cc);
+}
+// The substep state the leg wave publishes for its helper (T1_HELPER_KIN): base pos, quat, omega, v_O, and the leg's
+// q, qd -- rows of the leg's pose region, written after integration, read by the helper between S1 and S2.
+enum : int { ST_POS = 0, ST_QUAT = 3, ST_W = 7, ST_VO = 10, ST_Q = 13, ST_QD = 19, ST_N = 25 };
+static_assert(ST_N <= POSE_N, "the substep state fits the pose rows");
+__device__ __forceinline__ void publish_state(float (*P)[DYN_ENVS], int lane, const BaseState<float>& sb,
+                                              const float q[NLEG], const float qd[NLEG]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { P[ST_POS + i][lane] = sb.pos[i]; P[ST_W + i][lane] = sb.w[i]; P[ST_VO + i][lane] = sb.vo[i]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) P[ST_QUAT + i][lane] = sb.quat[i];
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) { P[ST_Q + k][lane] = q[k]; P[ST_QD + k][lane] = qd[k]; }
+}
+
 // ---- fused-epilogue staging by the two helper waves (STAGE_NT threads).  Rows [nb, nb + nv) of the workgroup;
 // a row-major source is read as one contiguous run (consecutive threads, consecutive words: coalesced) and
 // transposed into [value][env].  All loads of a thread are issued before the first LDS write (stage_ld for
@@ -833,8 +866,54 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
     if constexpr (FUSED) stage_epilogue_inputs(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, lds.epi);
     for (int sub = 0; sub < C.decimation; ++sub) {
       T1_PROF_MARK(7);
-      __syncthreads();  // S1: poses of this substep published
+      __syncthreads();  // S1: poses (T1_HELPER_KIN: the substep state) published
       T1_PROF_MARK(8);
+#ifdef T1_HELPER_KIN
+      BaseFrame<float> F;
+      M3<float> Rc[2];
+      V3<float> pc[2];
+      float Vc[2][6];
+      {
+        BaseState<float> sb;
+        float qh[NLEG], qdh[NLEG];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { sb.pos[i] = P[ST_POS + i][lane]; sb.w[i] = P[ST_W + i][lane]; sb.vo[i] = P[ST_VO + i][lane]; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sb.quat[i] = P[ST_QUAT + i][lane];
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) { qh[k] = P[ST_Q + k][lane]; qdh[k] = P[ST_QD + k][lane]; }
+        base_frame(sb, F);
+        leg_contact_kinematics<T1_LEG_CONTACT_MASK>(M, F, qh, qdh, leg,
+                                                    [&](auto kc, const M3<float>& Rk, V3<float> pk, const float* V) {
+                                                      constexpr int i = decltype(kc)::value == K_FOOT ? 1 : 0;
+                                                      Rc[i] = Rk;
+                                                      pc[i] = pk;
+#pragma unroll
+                                                      for (int j = 0; j < 6; ++j) Vc[i][j] = V[j];
+                                                    });
+      }
+      const V3<float> abs = F.abs;
+      const int32_t bound_sh = terrain_bound_raw_any(T, pc[0].x + abs.x, pc[0].y + abs.y);
+      const int32_t bound_base = terrain_bound_raw_any(T, abs.x, abs.y);
+      body_terms_at(M, T, Rc[1], pc[1], Vc[1], lane, 1 + 6 * leg + K_FOOT, abs, mu, dt, lds.ct[leg] + XCH, T1_NO_BOUND);
+      body_terms_at(M, T, Rc[0], pc[0], Vc[0], lane, 1 + 6 * leg + K_SHANK, abs, mu, dt, lds.ct[leg], bound_sh);
+      T1_PROF_MARK(3);
+      __syncthreads();  // S2: contact terms published
+      T1_PROF_MARK(11);
+      {  // base-box contact share of this leg, straight into the base system
+        Sym6<float> Cb;
+        float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        sym_zero(Cb);
+        body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - M.contact_radius[0], bound_base, cb, F.R0,
+                                                   v3<float>(0, 0, 0), F.abs, F.V0, mu, dt, Cb, gw);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) gw[i] = -gw[i];
+        lds_put_sym(lds.xch[2 + leg], lane, Cb, gw);
+      }
+      T1_PROF_MARK(5);
+      __syncthreads();  // S3: base system complete
+      T1_PROF_MARK(12);
+#else
       const V3<float> abs = v3<float>(P[9][lane], P[10][lane], P[11][lane]);
       // the height bounds of the shank and of the base box are loaded first, so their latency hides under the
       // foot's contact terms; the foot goes without a bound test (some foot among a wave's 64 envs is always
@@ -872,6 +951,7 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
       T1_PROF_MARK(5);
       __syncthreads();  // S3: base system complete
       T1_PROF_MARK(12);
+#endif
     }
     T1_PROF_MARK(7);
     __syncthreads();  // R1: end-of-step poses published
@@ -903,8 +983,21 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
     for (int k = 0; k < NLEG; ++k)
       CAP[CAP_ACT + k][lane] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
   T1_PROF_MARK(10);
+#ifdef T1_HELPER_KIN
+  publish_state(P, lane, sb, q, qd);  // the helpers start each substep from the state (their own kinematics)
+#endif
   for (int sub = 0; sub < C.decimation; ++sub) {
     T1_PROF_MARK(7);
+#ifdef T1_HELPER_KIN
+    __syncthreads();  // S1: the substep state published
+    T1_PROF_MARK(8);
+    BaseFrame<float> F;
+    base_frame(sb, F);
+    LegPass<float> st;
+    leg_forward_nc<T1_LEG_CONTACT_MASK>(M, PL, F, q, qd, leg, dt, st,
+                                        [&](auto, const M3<float>&, V3<float>, const float*) {});
+    T1_PROF_MARK(1);
+#else
     BaseFrame<float> F;
     base_frame(sb, F);
     lds_put_m3(P, lane, F.R0);
@@ -924,6 +1017,7 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
     T1_PROF_MARK(1);
     __syncthreads();  // S1
     T1_PROF_MARK(8);
+#endif
     pd_torques_staged(M, C, PD, lane, K, ctr, sub, L.lag, j0, q, qd, tau);
     T1_PROF_MARK(0);
     LegBlock<float> lb;
@@ -1010,6 +1104,9 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
 #pragma unroll
       for (int i = 0; i < 3; ++i) CAP[2 * NLEG + 4 + i][lane] = sb.w[i];
     }
+#ifdef T1_HELPER_KIN
+    if (sub + 1 < C.decimation) publish_state(P, lane, sb, q, qd);  // the helper read the previous one before S2
+#endif
   }
   T1_PROF_MARK(7);
   if (active) {

@@ -593,12 +593,14 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
         rand_float(C.armature_range[j][0], C.armature_range[j][1], K, SLOT_DR_ARMATURE + j);
   }
   // randomize_lag_props: zero the lag rings, redraw lag lengths
+#ifndef T1_WHATIF_NO_RING_ZERO  // timing-only what-if build
 #pragma unroll
   for (int i = 0; i < 48; ++i) B.act_hist[(size_t)n * 48 + i] = 0.0f;
 #pragma unroll
   for (int i = 0; i < 96; ++i) B.dof_hist[(size_t)n * 96 + i] = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) B.imu_hist[(size_t)n * 16 + i] = 0.0f;
+#endif
   B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, K, SLOT_LAG_ACTION);
   B.dof_lag_timestep[n] = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, K, SLOT_LAG_DOF);
   B.imu_lag_timestep[n] = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, K, SLOT_LAG_IMU);
