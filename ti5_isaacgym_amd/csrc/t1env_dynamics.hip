@@ -771,7 +771,7 @@ __device__ __forceinline__ void leg_report_rigid(const DynModel& M, const t1env_
     motion_subspace(M, b, Bk[k], S6);
 #pragma unroll
     for (int i = 0; i < 6; ++i) V[i] += S6[i] * qd[k];
-    if (k == K_SHANK || k == K_FOOT) {
+    if (P && (k == K_SHANK || k == K_FOOT)) {
       float (*D)[DYN_ENVS] = P + POSE_F + (k == K_FOOT ? POSE_B : 0);
       lds_put_m3(D, lane, Bk[k].Rot);
       D[9][lane] = Bk[k].p.x; D[10][lane] = Bk[k].p.y; D[11][lane] = Bk[k].p.z;
@@ -822,6 +822,30 @@ __device__ __forceinline__ void helper_report_contacts(const DynModel& M, const 
 #pragma unroll
     for (int i = 0; i < 6; ++i) V0[i] = P[12 + i][lane];
     const V3<float> f = body_contact_force(M, T, 0, lds_get_m3(P, lane), v3<float>(0, 0, 0), abs, V0, mu);
+    if (active) { cf[0] = f.x; cf[1] = f.y; cf[2] = f.z; }
+    if (FR) { FR[F_CFB][lane] = f.x; FR[F_CFB + 1][lane] = f.y; FR[F_CFB + 2][lane] = f.z; }
+  }
+}
+
+// the contact-force report from poses the helper computed itself (T1_HELPER_KIN: from the end-of-step state)
+__device__ __forceinline__ void helper_report_contacts_at(const DynModel& M, const Terrain& T, const t1env_buffers& B,
+                                                          const BaseFrame<float>& F, const M3<float> (&Rc)[2],
+                                                          const V3<float> (&pc)[2], const float (&Vc)[2][6], int n,
+                                                          int leg, float mu, int lane, bool active,
+                                                          float (*FR)[DYN_ENVS]) {
+  float* cf = B.contact_forces + (size_t)n * 39;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int b = 1 + 6 * leg + (s == 0 ? K_SHANK : K_FOOT);
+    const V3<float> f = body_contact_force(M, T, b, Rc[s], pc[s], F.abs, Vc[s], mu);
+    if (active) { cf[b * 3 + 0] = f.x; cf[b * 3 + 1] = f.y; cf[b * 3 + 2] = f.z; }
+    if (FR && s == 1) {
+      const int r = leg == 0 ? F_C0 : F_C1;
+      FR[r][lane] = f.x; FR[r + 1][lane] = f.y; FR[r + 2][lane] = f.z;
+    }
+  }
+  if (leg == 0) {
+    const V3<float> f = body_contact_force(M, T, 0, F.R0, v3<float>(0, 0, 0), F.abs, F.V0, mu);
     if (active) { cf[0] = f.x; cf[1] = f.y; cf[2] = f.z; }
     if (FR) { FR[F_CFB][lane] = f.x; FR[F_CFB + 1][lane] = f.y; FR[F_CFB + 2][lane] = f.z; }
   }
@@ -954,10 +978,37 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
 #endif
     }
     T1_PROF_MARK(7);
-    __syncthreads();  // R1: end-of-step poses published
+    __syncthreads();  // R1: end-of-step poses (T1_HELPER_KIN: the end-of-step state) published
     T1_PROF_MARK(8);
     float (*FR)[DYN_ENVS] = FUSED ? reinterpret_cast<float (*)[DYN_ENVS]>(&lds.ct[0][0][0]) : nullptr;
+#ifdef T1_HELPER_KIN
+    {  // the contact-force report beside the leg wave's rigid-state report
+      BaseFrame<float> F;
+      M3<float> Rc[2];
+      V3<float> pc[2];
+      float Vc[2][6];
+      BaseState<float> sb;
+      float qh[NLEG], qdh[NLEG];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { sb.pos[i] = P[ST_POS + i][lane]; sb.w[i] = P[ST_W + i][lane]; sb.vo[i] = P[ST_VO + i][lane]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sb.quat[i] = P[ST_QUAT + i][lane];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { qh[k] = P[ST_Q + k][lane]; qdh[k] = P[ST_QD + k][lane]; }
+      base_frame(sb, F);
+      leg_contact_kinematics<T1_LEG_CONTACT_MASK>(M, F, qh, qdh, leg,
+                                                  [&](auto kc, const M3<float>& Rk, V3<float> pk, const float* V) {
+                                                    constexpr int i = decltype(kc)::value == K_FOOT ? 1 : 0;
+                                                    Rc[i] = Rk;
+                                                    pc[i] = pk;
+#pragma unroll
+                                                    for (int j = 0; j < 6; ++j) Vc[i][j] = V[j];
+                                                  });
+      helper_report_contacts_at(M, T, B, F, Rc, pc, Vc, n, leg, mu, lane, active, FR);
+    }
+#else
     helper_report_contacts(M, T, B, P, n, leg, mu, lane, active, FR);
+#endif
     T1_PROF_MARK(11);
     if constexpr (FUSED) __syncthreads();  // the epilogue barrier
     T1_PROF_END();
@@ -1105,9 +1156,13 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
       for (int i = 0; i < 3; ++i) CAP[2 * NLEG + 4 + i][lane] = sb.w[i];
     }
 #ifdef T1_HELPER_KIN
-    if (sub + 1 < C.decimation) publish_state(P, lane, sb, q, qd);  // the helper read the previous one before S2
+    publish_state(P, lane, sb, q, qd);  // the helper read the previous one before S2; after the last substep: the
+                                        // end-of-step state its contact-force report starts from
 #endif
   }
+#ifdef T1_HELPER_KIN
+  __syncthreads();  // R1: the end-of-step state published (the helpers compute the contact forces meanwhile)
+#endif
   T1_PROF_MARK(7);
   if (active) {
     if (L.s_dof < C.decimation) {  // the sensor-lag samples captured in the loop
@@ -1138,6 +1193,11 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
   {
     BaseFrame<float> F;
     base_frame(sb, F);
+#ifdef T1_HELPER_KIN
+    leg_report_rigid(M, B, PB, sb, F, q, qd, n, leg, active, nullptr, lane, FR);
+  }
+  T1_PROF_MARK(11);
+#else
     lds_put_m3(P, lane, F.R0);
     P[9][lane] = F.abs.x; P[10][lane] = F.abs.y; P[11][lane] = F.abs.z;
 #pragma unroll
@@ -1146,6 +1206,7 @@ __global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ 
   }
   T1_PROF_MARK(11);
   __syncthreads();  // R1: end-of-step poses published (the helpers write the contact forces)
+#endif
   if constexpr (FUSED) {
     __syncthreads();  // all four waves: every output of the workgroup is in memory
     T1_PROF_MARK(12);

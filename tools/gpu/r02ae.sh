@@ -1,0 +1,8 @@
+# r02ae: world inertia / COM of each leg body kept from the forward pass (stash): correctness + A/B
+set -e
+out=gpurun_out/r02ae
+mkdir -p $out
+T1ENV_LIB=$PWD/ti5_isaacgym_amd/_lib/var/stash.so timeout -k 10 600 python -u -m pytest tests/test_gpu_dynamics.py \
+  tests/test_gpu_fused.py tests/test_gpu_product_parity.py -x -q --timeout 300 \
+  --timeout-method thread > $out/stash.tests.log 2>&1
+bash tools/gpu/ab.sh r02ae base stash
