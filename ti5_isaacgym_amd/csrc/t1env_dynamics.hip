@@ -681,7 +681,12 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
                    (uint32_t)__float_as_int(E[E_PL][lane]));
   X.gstart = E[E_GS][lane];
   BaseQ bq;
+#ifdef T1_WHATIF_EPI_NO_POSTA  // timing-only what-if build: no post_a (no rewards, termination, callback)
+  const bool do_reset = false;
+  base_quantities_r(X.root, bq);
+#else
   const bool do_reset = post_a_core<PART>(M, C, B, A, n0, X, bq);
+#endif
   T1_PROF_MARK(13);
   if constexpr (PART == POST_A_REWARDS) {
     epilogue_handoff(C, S, FA, lane, do_reset, active);
@@ -716,7 +721,9 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
     Ex.cfz[0] = X.c0[2]; Ex.cfz[1] = X.c1[2];
     Ex.fric = E[E_FRIC][lane];
     Ex.mass = E[E_MASS][lane];
+#ifndef T1_WHATIF_EPI_NO_POSTB  // timing-only what-if build: no reset / observations
     post_b_core(M, C, B, A, n, do_reset, do_reset, O, Ex, /*zero_reward_state=*/false);
+#endif
   }
   T1_PROF_MARK(14);
   // the terrain-level sum reads the levels reset_idx may just have changed
