@@ -862,7 +862,12 @@ __device__ __forceinline__ void helper_report_contacts_at(const DynModel& M, con
 // post-substep (q, qd), leg wave 0 the post-substep root row; a separate instantiation, so the product kernel is
 // unchanged by it.
 template <bool HF, bool FUSED, bool LOG = false>
-__global__ __launch_bounds__(D4_BLOCK) void k_dyn4(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
+#ifdef T1_DYN4_WAVES_PER_EU1  // A/B: tell the scheduler one wave per SIMD is the target (it is, by registers)
+#define T1_DYN4_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
+#else
+#define T1_DYN4_ATTR
+#endif
+__global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
                                                    t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
                                                    t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA,
                                                    SubLog LG) {

@@ -716,8 +716,18 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
   const float* ldp = B.dof_hist + ((size_t)n * 4 + ((A.counter - (uint32_t)(X.dl / 10)) & 3u)) * 24;
   const float* lip = B.imu_hist + ((size_t)n * 2 + ((A.counter - (uint32_t)(X.il / 10)) & 1u)) * 8;
   float ld[24], lraw[8], li[6];
+#ifdef T1_WHATIF_NO_LAG_LOADS  // timing-only what-if build: the lagged sensor samples not loaded
+  (void)ldp;
+  (void)lip;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) ld[i] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) lraw[i] = 0.0f;
+  lraw[3] = 1.0f;
+#else
   ldrow(ld, ldp);
   ldrow(lraw, lip);
+#endif
   imu_sample(lraw, li);
   // ---- compute_observations
   const float* cmd = X.cmd;
