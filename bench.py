@@ -69,6 +69,9 @@ def parse():
     p.add_argument("--state-dtype", default="fp32", choices=["fp32", "fp16"],
                    help="storage dtype of the obs / critic histories (fp16: BASELINE config 5's fp16 state)")
     p.add_argument("--push", action="store_true", help="domain_rand.push_robots on (BASELINE config 5), every 6 s")
+    p.add_argument("--repeats", type=int, default=1,
+                   help="time the K steps R times (each bracketed by barrier + synchronize) and report the median "
+                        "(SURVEY §8(d): median of 5); the per-repeat values go to repeat_values")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--time-every", type=int, default=8,
                    help="record per-kernel HIP events on every k-th timed step (event records cost host time; "
@@ -139,22 +142,26 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
-    barrier()
-    t0 = time.perf_counter()
     te = args.time_every
-    for i in range(args.steps):
-        if te:
-            env.set_timing(i % te == 0, reset=False)  # sampled live per-kernel timing inside the timed region
-        env.step(pool[i % 8])
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
+    reps = []
+    for r in range(max(1, args.repeats)):
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            if te:
+                env.set_timing(i % te == 0, reset=False)  # sampled live per-kernel timing inside the timed region
+            env.step(pool[i % 8])
+        torch.cuda.synchronize(dev)
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        reps.append(el)
     kt = env.get_timing()
     env.set_timing(False)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = sorted(reps)[len(reps) // 2]  # the median repeat (the only one at --repeats 1)
     ok = bool(torch.isfinite(env.root_states).all() and torch.isfinite(env.obs_buf).all())
     if rank != 0:
         if world > 1:
@@ -239,6 +246,9 @@ def main():
                      "kernels": per_kernel},
         "finite": ok,
     }
+    if len(reps) > 1:
+        line["repeats"] = len(reps)
+        line["repeat_values"] = [round(N * world * steps / e, 1) for e in reps]
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(env, args)
     print(json.dumps(line), flush=True)
