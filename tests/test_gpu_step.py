@@ -27,7 +27,7 @@ def _push_hook(cfg):
 
 @pytest.mark.parametrize("n,mesh,hook", [(8192, "trimesh", None), (777, "plane", None),
                                          (32768, "heightfield", _push_hook)],
-                         ids=["config2_8192_trimesh", "ragged777_plane", "config4_32768_hf_push"])
+                         ids=["config3_8192_trimesh", "ragged777_plane", "config5_fp32_32768_hf_push"])
 def test_step_history_shift_and_invariants(n, mesh, hook):
     from ti5_isaacgym_amd import make_t1_env
     env = make_t1_env(num_envs=n, mesh_type=mesh, seed=3, device="cuda:0", cfg_hook=hook)
