@@ -641,6 +641,13 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   base_quantities(B, n);
 }
 
+// the actor-frame noise of observation i (legged_robot.py compute_observations: (2 u - 1) * noise_vec * level, u keyed
+// by the env's post-physics key)
+__device__ __forceinline__ float obs_noise(const t1env_config& C, RngKey K, int i) {
+  const float u = uniform01(K, SLOT_OBS_NOISE + i);
+  return ((2.0f * u - 1.0f) * C.noise_vec[i]) * C.noise_level;
+}
+
 // =====================================================================================================
 // post-physics phase B: reset + observations (legged_robot.py:490-502, t1:368-481)
 // =====================================================================================================
@@ -823,8 +830,11 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
     for (int i = 0; i < 3; ++i) v[k++] = li[3 + i] * C.quat_obs_scale;
 #pragma unroll
     for (int i = 0; i < T1_NOBS; ++i) {
-      const float u = uniform01(K, SLOT_OBS_NOISE + i);
-      const float nz = ((2.0f * u - 1.0f) * C.noise_vec[i]) * C.noise_level;
+#ifdef T1_WHATIF_NO_NOISE_DRAWS  // timing-only what-if build
+      const float nz = 0.0f;
+#else
+      const float nz = obs_noise(C, K, i);
+#endif
       v[i] = clampf(v[i] + nz, -clipo, clipo);
     }
     if (C.obs_half) {
