@@ -32,19 +32,26 @@ def wgrad_splitk(gy, x):
     if S < 2:
         return gy.t().mm(x)
     c = S * SPLITK_ROWS
-    gw = torch.bmm(gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1)).sum(0)
+    # the slices' partial products are summed in at least fp32 (they are bf16 under the opt-in bf16 update,
+    # DHPPO.amp_dtype)
+    wide = lambda t: t if t.dtype in (torch.float32, torch.float64) else t.float()  # noqa: E731
+    gw = wide(torch.bmm(gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1))).sum(0)
     if c < K:
-        gw = gw.addmm(gy[c:].t(), x[c:])
+        gw = gw + wide(gy[c:].t().mm(x[c:]))
     return gw
 
 
 class _LinearSplitK(torch.autograd.Function):
+    # custom_fwd / custom_bwd: under torch.autocast (the opt-in bf16 update) the GEMMs run in the autocast dtype in
+    # both passes; autograd casts the returned gradients to the fp32 parameters' dtype
     @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         return torch.addmm(b, x, w.t())
 
     @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gy = gy.contiguous()
@@ -195,7 +202,7 @@ class ActorCriticDH(nn.Module):
         return torch.cat((short, self.state_estimator(short), code), dim=-1)
 
     def update_distribution(self, actor_obs):
-        mean = self.actor(actor_obs)
+        mean = self.actor(actor_obs).float()   # fp32 distribution under the opt-in bf16 update (no-op in fp32)
         self.distribution = Normal(mean, mean * 0.0 + self.std)
 
     def act(self, observations, **kwargs):
@@ -209,4 +216,4 @@ class ActorCriticDH(nn.Module):
         return self.actor(self.actor_input(observations))
 
     def evaluate(self, critic_observations, **kwargs):
-        return self.critic(critic_observations)
+        return self.critic(critic_observations).float()

@@ -11,6 +11,7 @@ On a HIP device the rollout's act() (policy sample, value, log-prob) replays a c
 pair of observation buffers the env hands out (its ping-pong buffers): the same kernels as the eager call,
 without the per-kernel launch cost that dominates at one call per env step.
 """
+import contextlib
 import warnings
 
 import torch
@@ -28,8 +29,12 @@ class DHPPO:
 
     def __init__(self, actor_critic, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998,
                  lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
-                 lin_vel_idx=45, use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu"):
+                 lin_vel_idx=45, use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
+                 amp_dtype=None):
         self.device = device
+        # opt-in mixed precision of the update (not in the reference): torch.bfloat16 runs the update's forward and
+        # backward GEMMs in bf16 (fp32 accumulation, fp32 weights, optimizer and losses); None = fp32 as the reference
+        self.amp_dtype = amp_dtype
         self.desired_kl, self.schedule, self.learning_rate = desired_kl, schedule, learning_rate
         self.actor_critic = actor_critic
         self.actor_critic.to(self.device)
@@ -147,29 +152,14 @@ class DHPPO:
         sums = torch.zeros(3, device=self.device)  # value, surrogate, state-estimator losses
         mse = nn.MSELoss()
         gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        amp = (torch.autocast(device_type="cuda", dtype=self.amp_dtype)
+               if self.amp_dtype is not None and torch.device(self.device).type == "cuda" else contextlib.nullcontext())
         for (obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b,
              hid_b, masks_b) in gen:
-            ac.act(obs_b, masks=masks_b, hidden_states=hid_b[0])
-            est_lin_vel = ac.state_estimator(obs_b[:, -self.num_short_obs:])
-            ref_lin_vel = critic_b[:, self.lin_vel_idx:self.lin_vel_idx + 3].clone()
-            logp_b = ac.get_actions_log_prob(actions_b)
-            value_b = ac.evaluate(critic_b, masks=masks_b, hidden_states=hid_b[1])
-            mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
-            if self.desired_kl is not None and self.schedule == "adaptive":
-                self._adapt_lr(mu_b, sigma_b, old_mu_b, old_sigma_b)
-            # clipped surrogate
-            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
-            adv = torch.squeeze(adv_b)
-            surrogate_loss = torch.max(-adv * ratio,
-                                       -adv * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)).mean()
-            # value loss
-            if self.use_clipped_value_loss:
-                v_clip = target_values_b + (value_b - target_values_b).clamp(-self.clip_param, self.clip_param)
-                value_loss = torch.max((value_b - returns_b).pow(2), (v_clip - returns_b).pow(2)).mean()
-            else:
-                value_loss = (returns_b - value_b).pow(2).mean()
-            se_loss = mse(est_lin_vel, ref_lin_vel)
-            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean() + se_loss
+            with amp:
+                loss, value_loss, surrogate_loss, se_loss = self._losses(
+                    ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
+                    old_sigma_b, hid_b, masks_b, mse)
             self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
             loss.backward()
             self.grads.all_reduce_()
@@ -180,3 +170,29 @@ class DHPPO:
         self.storage.clear()
         mv, ms, mse_ = (sums / n).tolist()
         return mv, ms, mse_
+
+    def _losses(self, ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
+                old_sigma_b, hid_b, masks_b, mse):
+        """The reference's minibatch losses (dh_ppo.py:130-178); the distribution terms in fp32 under autocast."""
+        ac.act(obs_b, masks=masks_b, hidden_states=hid_b[0])
+        est_lin_vel = ac.state_estimator(obs_b[:, -self.num_short_obs:])
+        ref_lin_vel = critic_b[:, self.lin_vel_idx:self.lin_vel_idx + 3].clone()
+        logp_b = ac.get_actions_log_prob(actions_b)
+        value_b = ac.evaluate(critic_b, masks=masks_b, hidden_states=hid_b[1])
+        mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
+        if self.desired_kl is not None and self.schedule == "adaptive":
+            self._adapt_lr(mu_b, sigma_b, old_mu_b, old_sigma_b)
+        # clipped surrogate
+        ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+        adv = torch.squeeze(adv_b)
+        surrogate_loss = torch.max(-adv * ratio,
+                                   -adv * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)).mean()
+        # value loss
+        if self.use_clipped_value_loss:
+            v_clip = target_values_b + (value_b - target_values_b).clamp(-self.clip_param, self.clip_param)
+            value_loss = torch.max((value_b - returns_b).pow(2), (v_clip - returns_b).pow(2)).mean()
+        else:
+            value_loss = (returns_b - value_b).pow(2).mean()
+        se_loss = mse(est_lin_vel.float(), ref_lin_vel)
+        loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean() + se_loss
+        return loss, value_loss, surrogate_loss, se_loss

@@ -33,6 +33,7 @@ p.add_argument("--conv-search", action="store_true", help="torch.backends.cudnn.
 p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                help="gloo + --one-gpu: rehearse the data-parallel path with every rank on cuda:0 (one-GPU box)")
 p.add_argument("--one-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal only; not a scaling number)")
+p.add_argument("--bf16", action="store_true", help="opt-in bf16 PPO update (DHPPO.amp_dtype; tools/ppo_amp_check.py)")
 a = p.parse_args()
 world = int(os.environ.get("WORLD_SIZE", "1"))
 rank = int(os.environ.get("RANK", "0"))
@@ -52,6 +53,7 @@ cfg = class_to_dict(tc)
 torch.manual_seed(rank)
 r = DHOnPolicyRunner(env, cfg, None, device=str(dev))
 r.alg.graph_act = not a.no_graph
+r.alg.amp_dtype = torch.bfloat16 if a.bf16 else None
 
 
 def barrier():
@@ -105,7 +107,8 @@ for _ in range(a.iters):
     t_roll += t1 - t0
 t_roll, t_env, t_upd = (max_over_ranks(x) for x in (t_roll, t_env, t_upd))
 line = {"bench": "ppo_iteration", "n_gpus": 1 if a.one_gpu else world, "ranks": world, "num_envs_per_gpu": N,
-        "global_envs": N * world, "mesh": a.mesh, "iters": a.iters, "graph_act": r.alg.graph_act, "env_steps_per_s_incl_update": round(steps / dt, 1),
+        "global_envs": N * world, "mesh": a.mesh, "iters": a.iters, "graph_act": r.alg.graph_act,
+        "update_dtype": "bf16" if a.bf16 else "fp32", "env_steps_per_s_incl_update": round(steps / dt, 1),
         "env_steps_per_s_per_gpu": round(steps / dt / world, 1), "s_per_iter": round(dt / a.iters, 4),
         "phases_s_per_iter": {"rollout": round(t_roll / a.iters, 4), "env_step_in_rollout": round(t_env / a.iters, 4),
                               "update": round(t_upd / a.iters, 4)},
