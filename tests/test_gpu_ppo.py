@@ -67,3 +67,32 @@ def test_graphed_act_matches_eager():
         m3 = alg._graphed_act(obs, cobs)[3]
         torch.testing.assert_close(m3, ac.actor(ac.actor_input(obs)), **tol)
     assert len(alg._act_graphs) == 1
+
+
+def test_bf16_update_tracks_fp32():
+    """The opt-in bf16 update (DHPPO.amp_dtype) against the fp32 update from the same weights, optimizer state,
+    rollout and minibatch permutation (tools/ppo_amp_check.py): the three mean losses within 5 % (+1e-4) and the
+    weight updates within 5 % relative L2 (measured 0.8-1.0 % at 8192 envs, profiles/r02ap_ppo_bf16.md)."""
+    import importlib.util
+    import os
+    from ti5_isaacgym_amd import make_t1_env, task_registry
+    from ti5_isaacgym_amd.algo import DHOnPolicyRunner
+    from ti5_isaacgym_amd.utils.helpers import class_to_dict
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "ppo_amp_check.py")
+    spec = importlib.util.spec_from_file_location("ppo_amp_check", path)
+    chk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(chk)
+    env = make_t1_env(num_envs=1024, mesh_type="plane", seed=5, device="cuda:0")
+    _, train_cfg = task_registry.get_cfgs("t1_dh_stand")
+    torch.manual_seed(0)
+    r = DHOnPolicyRunner(env, class_to_dict(train_cfg), None, device="cuda:0")
+    r.alg.actor_critic.train()
+    obs, priv = env.reset()
+    critic = priv if priv is not None else obs
+    for it in range(2):
+        obs, critic = chk.rollout(r, obs, critic)
+        ls32, ls16, rel, _, _ = chk.compare_updates(r, 1000 + it)
+        for a, b in zip(ls16, ls32):
+            assert abs(a - b) <= 0.05 * abs(b) + 1e-4, (ls16, ls32)
+        assert rel < 0.05, rel
+    assert r.alg.amp_dtype is None   # compare_updates leaves the fp32 update in place

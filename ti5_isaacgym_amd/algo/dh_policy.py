@@ -35,7 +35,11 @@ def wgrad_splitk(gy, x):
     # the slices' partial products are summed in at least fp32 (they are bf16 under the opt-in bf16 update,
     # DHPPO.amp_dtype)
     wide = lambda t: t if t.dtype in (torch.float32, torch.float64) else t.float()  # noqa: E731
-    gw = wide(torch.bmm(gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1))).sum(0)
+    if M < 8 and gy.dtype != wide(gy).dtype:
+        # the value head (M = 1): hipBLASLt's bf16 batched GEMM spends ~11 ms of host time per call on a 1-row
+        # output (profiles/r02ap_ppo_bf16.md); the product is a few MB, so widen and take one fp32 GEMM
+        return wide(gy).t().mm(wide(x))
+    gw =wide(torch.bmm(gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1))).sum(0)
     if c < K:
         gw = gw + wide(gy[c:].t().mm(x[c:]))
     return gw

@@ -1,0 +1,48 @@
+"""Dev probe: host and device time of the split-K weight-gradient GEMM (dh_policy.wgrad_splitk's shape: K = 49,152
+batch rows in slices of 2048, M x N = 512 x 256) in fp32 and bf16 through the BLAS routes PyTorch offers on ROCm.
+
+    python tools/bf16_wgrad_probe.py
+
+Per variant: wall time of 50 back-to-back calls with a sync only at the end (host-bound if the per-call host time
+exceeds the device time) and the host time of the enqueue loop alone.
+"""
+import time
+
+import torch
+
+
+def run(name, fn, n=50):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"{name:44s} enqueue {(t1 - t0) / n * 1e6:8.1f} us/call   wall {(t2 - t0) / n * 1e6:8.1f} us/call", flush=True)
+
+
+def main():
+    K, M, N, R = 49152, 512, 256, 2048
+    S = K // R
+    for dt in (torch.float32, torch.bfloat16):
+        gy = torch.randn(K, M, device="cuda", dtype=dt)
+        x = torch.randn(K, N, device="cuda", dtype=dt)
+        a, b = gy.view(S, R, M).transpose(1, 2), x.view(S, R, N)
+        tag = str(dt).split(".")[-1]
+        for lib in ("cublaslt", "cublas"):
+            torch.backends.cuda.preferred_blas_library(lib)
+            run(f"{tag} {lib} bmm+sum", lambda: torch.bmm(a, b).float().sum(0))
+            run(f"{tag} {lib} mm", lambda: gy.t().mm(x))
+            if dt == torch.bfloat16:
+                run(f"{tag} {lib} bmm out fp32 +sum", lambda: torch.bmm(a, b, out_dtype=torch.float32).sum(0))
+                run(f"{tag} {lib} mm out fp32", lambda: torch.mm(gy.t(), x, out_dtype=torch.float32))
+                ac = a.contiguous()
+                run(f"{tag} {lib} bmm contig-A +sum", lambda: torch.bmm(ac, b).float().sum(0))
+    torch.backends.cuda.preferred_blas_library("cublaslt")
+
+
+if __name__ == "__main__":
+    main()

@@ -27,8 +27,9 @@ def snapshot_storage(st):
 
 
 def restore_storage(st, snap):
-    for k, v in snap.items():
-        getattr(st, k).copy_(v)
+    with torch.inference_mode():   # the rollout wrote some storage rows as inference tensors
+        for k, v in snap.items():
+            getattr(st, k).copy_(v)
 
 
 def timed_update(alg, dtype, seed):
@@ -40,6 +41,46 @@ def timed_update(alg, dtype, seed):
     e1.record()
     torch.cuda.synchronize()
     return losses, e0.elapsed_time(e1)
+
+
+def compare_updates(r, seed):
+    """bf16 then fp32 DHPPO.update() from the same weights, optimizer state, storage and minibatch seed; the fp32
+    result is kept.  Returns (losses_fp32, losses_bf16, relative L2 difference of the weight updates, ms fp32,
+    ms bf16)."""
+    alg = r.alg
+    snap = snapshot_storage(alg.storage)
+    w0 = [q.detach().clone() for q in alg.actor_critic.parameters()]
+    opt0 = copy.deepcopy(alg.optimizer.state_dict())
+    lr0 = alg.learning_rate
+    ls_bf16, ms_bf16 = timed_update(alg, torch.bfloat16, seed)
+    w_bf16 = [q.detach().clone() for q in alg.actor_critic.parameters()]
+    # back to the start of the iteration, then the fp32 update (kept)
+    with torch.no_grad():
+        for q, q0 in zip(alg.actor_critic.parameters(), w0):
+            q.copy_(q0)
+    alg.optimizer.load_state_dict(opt0)
+    alg.learning_rate = lr0
+    for g in alg.optimizer.param_groups:
+        g["lr"] = lr0
+    restore_storage(alg.storage, snap)
+    alg.storage.step = r.num_steps_per_env
+    ls_fp32, ms_fp32 = timed_update(alg, None, seed)
+    w_fp32 = [q.detach() for q in alg.actor_critic.parameters()]
+    num = sum(((wb - wf) ** 2).sum() for wb, wf in zip(w_bf16, w_fp32)) ** 0.5
+    den = sum(((wf - w) ** 2).sum() for wf, w in zip(w_fp32, w0)) ** 0.5
+    return ls_fp32, ls_bf16, float(num / den), ms_fp32, ms_bf16
+
+
+def rollout(r, obs, critic):
+    alg = r.alg
+    with torch.inference_mode():
+        for _ in range(r.num_steps_per_env):
+            actions = alg.act(obs, critic)
+            obs, priv, rew, dones, infos = r.env.step(actions)
+            critic = priv if priv is not None else obs
+            alg.process_env_step(rew, dones, infos)
+        alg.compute_returns(critic)
+    return obs, critic
 
 
 def main():
@@ -57,37 +98,12 @@ def main():
     critic = priv if priv is not None else obs
     out = []
     for it in range(a.iters + 1):   # iteration 0 warms the libraries up (not reported)
-        with torch.inference_mode():
-            for _ in range(r.num_steps_per_env):
-                actions = alg.act(obs, critic)
-                obs, priv, rew, dones, infos = env.step(actions)
-                critic = priv if priv is not None else obs
-                alg.process_env_step(rew, dones, infos)
-            alg.compute_returns(critic)
-        snap = snapshot_storage(alg.storage)
-        w0 = [q.detach().clone() for q in alg.actor_critic.parameters()]
-        opt0 = copy.deepcopy(alg.optimizer.state_dict())
-        lr0 = alg.learning_rate
-        ls_bf16, ms_bf16 = timed_update(alg, torch.bfloat16, 1000 + it)
-        w_bf16 = [q.detach().clone() for q in alg.actor_critic.parameters()]
-        # back to the start of the iteration, then the fp32 update (kept)
-        with torch.no_grad():
-            for q, q0 in zip(alg.actor_critic.parameters(), w0):
-                q.copy_(q0)
-        alg.optimizer.load_state_dict(opt0)
-        alg.learning_rate = lr0
-        for g in alg.optimizer.param_groups:
-            g["lr"] = lr0
-        restore_storage(alg.storage, snap)
-        alg.storage.step = r.num_steps_per_env
-        ls_fp32, ms_fp32 = timed_update(alg, None, 1000 + it)
-        w_fp32 = [q.detach() for q in alg.actor_critic.parameters()]
-        num = sum(((wb - wf) ** 2).sum() for wb, wf in zip(w_bf16, w_fp32)) ** 0.5
-        den = sum(((wf - w) ** 2).sum() for wf, w in zip(w_fp32, w0)) ** 0.5
+        obs, critic = rollout(r, obs, critic)
+        ls_fp32, ls_bf16, rel, ms_fp32, ms_bf16 = compare_updates(r, 1000 + it)
         if it > 0:
             out.append({"iter": it, "losses_fp32": [round(x, 6) for x in ls_fp32],
                         "losses_bf16": [round(x, 6) for x in ls_bf16],
-                        "rel_weight_update_diff": round(float(num / den), 5),
+                        "rel_weight_update_diff": round(rel, 5),
                         "update_ms_fp32": round(ms_fp32, 2), "update_ms_bf16": round(ms_bf16, 2)})
     print(json.dumps({"num_envs": a.num_envs, "minibatches": alg.num_mini_batches, "epochs": alg.num_learning_epochs,
                       "iters": out}))
