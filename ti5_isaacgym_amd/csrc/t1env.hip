@@ -67,6 +67,7 @@ struct t1env {
   uint32_t* d_unit_state; // per shift unit handoff word (fused step)
   int step_timer;         // timing slot of the current step span (phase A start .. phase B end)
   unsigned* d_done;       // k_post_b block-completion counter (its last block finalises the extras)
+  float* d_ep_part;       // k_dyn4's per-workgroup partial extras sums (FusedArgs::ep_part)
   int16_t* d_hmax;        // coarse terrain height bound (Terrain::hmax), built by t1env_set_terrain
   float max_contact_radius;
   SubLog log;             // t1env_set_substep_log (tests): fused steps write it
@@ -377,6 +378,9 @@ extern "C" {
 const char* t1env_last_error(void) { return g_err; }
 const char* t1env_version(void) { return "t1env-hip 0.1 (gfx950)"; }
 
+// one EP_PART_ROW-float row per k_dyn4 dynamics workgroup
+static size_t ep_part_bytes(int num_envs) { return sizeof(float) * EP_PART_ROW * (size_t)((num_envs + 63) / 64); }
+
 int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_buffers* bufs, t1env** out) {
   if (!model || !cfg || !bufs || !out) return fail(T1ENV_E_ARG, "t1env_create: null argument");
   if (cfg->num_envs <= 0) return fail(T1ENV_E_SHAPE, "t1env_create: num_envs must be > 0");
@@ -402,7 +406,8 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   if ((err = hipMalloc(&e->d_model, sizeof(DynModel))) != hipSuccess ||
       (err = hipMalloc(&e->d_cfg, sizeof(t1env_config))) != hipSuccess ||
       (err = hipMalloc(&e->d_done, sizeof(unsigned))) != hipSuccess ||
-      (err = hipMalloc(&e->d_unit_state, sizeof(uint32_t) * (size_t)(cfg->num_envs / 8 + 1))) != hipSuccess) {
+      (err = hipMalloc(&e->d_unit_state, sizeof(uint32_t) * (size_t)(cfg->num_envs / 8 + 1))) != hipSuccess ||
+      (err = hipMalloc(&e->d_ep_part, ep_part_bytes(cfg->num_envs))) != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "t1env_create: hipMalloc: %s", hipGetErrorString(err));
     free(e);
     return (int)err;
@@ -412,6 +417,7 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
   HIP_TRY(hipMemset(e->buf.ep_accum, 0, 32 * sizeof(float)));
   HIP_TRY(hipMemset(e->d_done, 0, sizeof(unsigned)));
   HIP_TRY(hipMemset(e->d_unit_state, 0, sizeof(uint32_t) * (size_t)(cfg->num_envs / 8 + 1)));
+  HIP_TRY(hipMemset(e->d_ep_part, 0, ep_part_bytes(cfg->num_envs)));
   e->fused = 1;
   {
     int dev = 0, cus = 256;
@@ -436,6 +442,7 @@ int t1env_destroy(t1env* e) {
   (void)hipFree(e->d_cfg);
   (void)hipFree(e->d_done);
   (void)hipFree(e->d_unit_state);
+  (void)hipFree(e->d_ep_part);
   if (e->d_hmax) (void)hipFree(e->d_hmax);
   for (int i = 0; i < e->n_events; ++i) {
     (void)hipEventDestroy(e->ev_start[i]);
@@ -566,7 +573,7 @@ static int launch_fused(t1env* e, const float* actions, const t1env_step_args* a
   if (pre)
     if (int rc = launch_shift(e, a, s)) return rc;
   const int t = t_begin(e, 0, s);
-  const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch, pre ? 1 : 0};
+  const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch, pre ? 1 : 0, e->d_ep_part};
   HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, e->cfg.num_envs,
                                          shift_args(e, a), e->dyn, &FA, s, pre, e->log_on ? &e->log : nullptr));
   t_end(e, t, s);

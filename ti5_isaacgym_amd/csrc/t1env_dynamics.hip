@@ -232,6 +232,59 @@ __device__ __forceinline__ void epilogue_finalize(const t1env_config& C, const t
     if (lane == 0) __hip_atomic_store(FA.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+// k_dyn4's finaliser: every dynamics workgroup stored one row of partial sums (FusedArgs::ep_part, agent-scope
+// stores completed before its counter increment); the last one sums the rows in a fixed order after an acquire
+// fence (no same-address atomics: 25 per workgroup into one row cost 3.6% of the step, r02ar).  Lane l reads the
+// float4 l % 8 of rows l / 8, l / 8 + 8, ...; the 8 lanes of a float4 are then summed across the wave.
+__device__ __forceinline__ void epilogue_finalize_parts(const t1env_config& C, const t1env_buffers& B,
+                                                        const t1env_step_args& A, const FusedArgs& FA, int dyn_blocks,
+                                                        int lane) {
+  unsigned prev = 0;
+  if (lane == 0) prev = __hip_atomic_fetch_add(FA.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  prev = __shfl(prev, 0, 64);
+  if (prev != (unsigned)dyn_blocks - 1u) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  static_assert(EP_PART_ROW == 32, "8 float4 per row");
+  const float4* P = reinterpret_cast<const float4*>(FA.ep_part);
+  const int q = lane & 7;
+  float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  constexpr int BATCH = 8;  // loads in flight per lane
+  for (int r0 = lane >> 3; r0 < dyn_blocks; r0 += 8 * BATCH) {
+    float4 v[BATCH];
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) {
+      const int r = r0 + 8 * j;
+      v[j] = r < dyn_blocks ? P[(size_t)r * 8 + q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
+  }
+#pragma unroll
+  for (int off = 8; off < 64; off <<= 1) {
+    s.x += __shfl_xor(s.x, off, 64); s.y += __shfl_xor(s.y, off, 64);
+    s.z += __shfl_xor(s.z, off, 64); s.w += __shfl_xor(s.w, off, 64);
+  }
+  // sum t (t < 32) sits in component t % 4 of lane t / 4
+  const int src = (lane & 31) >> 2;
+  const float c0 = __shfl(s.x, src, 64), c1 = __shfl(s.y, src, 64), c2 = __shfl(s.z, src, 64), c3 = __shfl(s.w, src, 64);
+  const int c = lane & 3;
+  const float mine = c == 0 ? c0 : c == 1 ? c1 : c == 2 ? c2 : c3;
+  const float cnt = __shfl(mine, 24, 64);    // reset count
+  const float lvl = __shfl(mine, 25, 64);    // terrain-level sum
+  const int slot = (int)((A.counter + 1u) % T1ENV_EXTRAS_RING);
+  float* ex = B.extras + (size_t)slot * 32;
+  const float* prevx = B.extras + (size_t)((slot + T1ENV_EXTRAS_RING - 1) % T1ENV_EXTRAS_RING) * 32;
+  if (lane < 32) {  // finalize_extras' formulas
+    float v = prevx[lane];
+    if (cnt > 0.0f) {
+      if (lane < T1_NREW) v = (mine / cnt) / C.episode_length_s;
+      else if (lane == 24) v = lvl / (float)C.num_envs;
+    }
+    ex[lane] = v;
+  }
+  if (lane == 0) __hip_atomic_store(FA.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const t1env_buffers& B,
                                                     const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
                                                     int dyn_blocks, int lane, bool do_reset, bool active, int n) {
@@ -685,14 +738,15 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
   const bool do_reset = false;
   base_quantities_r(X.root, bq);
 #else
-  const bool do_reset = post_a_core<PART>(M, C, B, A, n0, X, bq);
+  float* const ep_row = FA.ep_part + (size_t)blockIdx.x * EP_PART_ROW;  // this workgroup's partial extras sums
+  const bool do_reset = post_a_core<PART>(M, C, B, A, n0, X, bq, PART == POST_A_REWARDS ? ep_row : nullptr);
 #endif
   T1_PROF_MARK(13);
   if constexpr (PART == POST_A_REWARDS) {
     epilogue_handoff(C, S, FA, lane, do_reset, active);
     __builtin_amdgcn_s_waitcnt(0);  // this wave's atomics (extras sums) complete
     __syncthreads();                // E2: wave 1's terrain-level sum complete
-    epilogue_finalize(C, B, A, FA, dyn_blocks, lane);
+    epilogue_finalize_parts(C, B, A, FA, dyn_blocks, lane);
     T1_PROF_MARK(15);
     return;
   }
@@ -727,7 +781,7 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
   }
   T1_PROF_MARK(14);
   // the terrain-level sum reads the levels reset_idx may just have changed
-  if (C.custom_origins) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
+  wave_sum_store(ep_row + 25, (C.custom_origins && active) ? (float)B.terrain_levels[n] : 0.0f);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();  // E2
   T1_PROF_MARK(15);

@@ -14,7 +14,10 @@ struct FusedArgs {
   uint32_t epoch;                  // launch number (unique per fused step)
   int32_t shift_done;              // 1: the history shift ran as its own launch before this one (large N):
                                    //    the epilogue zeroes its reset rows directly, no handoff
+  float* ep_part;                  // k_dyn4: per dynamics workgroup one row of EP_PART_ROW partial extras sums
+                                   //    ([0,24) episode sums over reset envs, [24] reset count, [25] terrain levels)
 };
+constexpr int EP_PART_ROW = 32;
 
 // substep log of the fused k_dyn4 (t1env_substep_log; all null = off)
 struct SubLog {

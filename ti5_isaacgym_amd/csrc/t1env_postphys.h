@@ -110,6 +110,13 @@ __device__ __forceinline__ void wave_atomic_add(float* dst, float v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   if ((threadIdx.x & 63) == 0 && v != 0.0f) atomicAdd(dst, v);
 }
+// The wave sum of v, stored by lane 0 as an agent-scope (sc1) store: visible past the XCD's L2 once the store has
+// completed (the fused step's per-workgroup partial extras, read by the last workgroup after its acquire fence)
+__device__ __forceinline__ void wave_sum_store(float* dst, float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // K wave sums at once: each butterfly round issues the K cross-lane moves back to back (one LDS-latency wait
 // per round instead of one per value and round), then lane 0 adds the non-zero sums to dst[0..K)
 template <int K>
@@ -127,6 +134,25 @@ __device__ __forceinline__ void wave_atomic_add_n(float* dst, float (&v)[K]) {
     for (int k = 0; k < K; ++k)
       if (v[k] != 0.0f) atomicAdd(dst + k, v[k]);
   }
+}
+// The same K wave sums stored to row[0..K) without atomics: lane k keeps sum k and stores it (one agent-scope store
+// instruction for the wave, no same-address atomics across workgroups)
+template <int K>
+__device__ __forceinline__ void wave_sum_store_n(float* row, float (&v)[K]) {
+  static_assert(K <= 64, "one lane per sum");
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    float t[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) t[k] = __shfl_xor(v[k], off, 64);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += t[k];
+  }
+  const int lane = threadIdx.x & 63;
+  float mine = v[0];
+#pragma unroll
+  for (int k = 1; k < K; ++k) mine = lane == k ? v[k] : mine;
+  if (lane < K) __hip_atomic_store(row + lane, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // extras["episode"] of one step (legged_robot.py:560-569 via reset_idx): means over the envs reset this step
@@ -214,7 +240,8 @@ __device__ __forceinline__ void load_post_a_in(const t1env_buffers& B, size_t N,
 enum : int { POST_A_ALL = 0, POST_A_REWARDS = 1, POST_A_STATE = 2 };
 template <int PART = POST_A_ALL>
 __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
-                                            const t1env_step_args& A, int n0, PostAIn& X, BaseQ& bq) {
+                                            const t1env_step_args& A, int n0, PostAIn& X, BaseQ& bq,
+                                            float* ep_row = nullptr) {
   const bool live = n0 < C.num_envs;
   const int n = live ? n0 : C.num_envs - 1;
   const uint32_t genv = (uint32_t)(C.env_offset + n);
@@ -522,7 +549,10 @@ __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_confi
 #pragma unroll
     for (int k = 0; k < T1_NREW; ++k) part[k] = contrib[k];
     part[T1_NREW] = do_reset ? 1.0f : 0.0f;
-    wave_atomic_add_n(B.ep_accum, part);  // ep_accum[0..23] episode sums, [24] reset count
+    if (ep_row)  // the fused k_dyn4 step: this workgroup's partial row (FusedArgs::ep_part)
+      wave_sum_store_n(ep_row, part);
+    else
+      wave_atomic_add_n(B.ep_accum, part);  // ep_accum[0..23] episode sums, [24] reset count
   }
   X.el = el;
   X.pl = pl;
