@@ -135,11 +135,11 @@ __device__ __forceinline__ void wave_atomic_add_n(float* dst, float (&v)[K]) {
       if (v[k] != 0.0f) atomicAdd(dst + k, v[k]);
   }
 }
-// The same K wave sums stored to row[0..K) without atomics: lane k keeps sum k and stores it (one agent-scope store
-// instruction for the wave, no same-address atomics across workgroups)
+// The same K wave sums stored to row[0..K) by lane 0 as agent-scope stores (no same-address atomics across
+// workgroups).  Lane 0 stores them one by one: a lane-k-keeps-sum-k select chain is turned into a dynamically
+// indexed array in scratch by the compiler.
 template <int K>
 __device__ __forceinline__ void wave_sum_store_n(float* row, float (&v)[K]) {
-  static_assert(K <= 64, "one lane per sum");
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     float t[K];
@@ -148,11 +148,10 @@ __device__ __forceinline__ void wave_sum_store_n(float* row, float (&v)[K]) {
 #pragma unroll
     for (int k = 0; k < K; ++k) v[k] += t[k];
   }
-  const int lane = threadIdx.x & 63;
-  float mine = v[0];
+  if ((threadIdx.x & 63) == 0) {
 #pragma unroll
-  for (int k = 1; k < K; ++k) mine = lane == k ? v[k] : mine;
-  if (lane < K) __hip_atomic_store(row + lane, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < K; ++k) __hip_atomic_store(row + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // extras["episode"] of one step (legged_robot.py:560-569 via reset_idx): means over the envs reset this step
