@@ -8,8 +8,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-# translation unit -> optimisation level.  The dynamics unit is built at -O1, its fastest level (-O2/-O3 are correct
-# and 6-7 % slower).  Round 1's -O2/-O3 wrong dynamics bisected to the load/store vectorizer over the __restrict__
+# translation unit -> optimisation level.  The dynamics unit is built at -O1 (round 1's fastest level; on the round-2
+# kernel -O1/-O2/-O3 measure the same, profiles/r02bc_opt_levels.json).  Round 1's -O2/-O3 wrong dynamics bisected to the load/store vectorizer over the __restrict__
 # model-pointer loads; the -O3 guard build (OUT_O3) keeps every level under the fp64 check.
 UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1")]
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")

@@ -1,7 +1,7 @@
 // t1env_dynamics.hip -- the env step's main launch: the decimation loop with the articulated-body solver
 // (legged_robot.py:399-434 + Isaac Gym simulate()), the history shift, and in the fused step post-physics.
-// Its own translation unit because it is compiled at -O1 (build.py), the fastest level for it; -O2/-O3 are correct
-// too (tests/test_gpu_opt_levels.py runs the -O3 build through the fp64 dynamics check and the product replay).
+// Its own translation unit because it is compiled at -O1 (build.py; -O2/-O3 measure the same since round 2 and are
+// correct too (tests/test_gpu_opt_levels.py runs the -O3 build through the fp64 dynamics check and the product replay).
 #include <hip/hip_runtime.h>
 
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py): lane 0 of every dynamics wave accumulates shader-clock
