@@ -96,3 +96,29 @@ def test_bf16_update_tracks_fp32():
             assert abs(a - b) <= 0.05 * abs(b) + 1e-4, (ls16, ls32)
         assert rel < 0.05, rel
     assert r.alg.amp_dtype is None   # compare_updates leaves the fp32 update in place
+
+
+def test_bf16_update_obs_cast_once_is_exact():
+    """The bf16 update's actor observations cast to bf16 once per update (RolloutStorage.mini_batch_generator
+    obs_dtype) against autocast's per-minibatch casts: the same bf16 operands reach the same GEMMs, so the losses and
+    weights agree to the bit (a GEMM library picking another solution for the other layout would show here)."""
+    import importlib.util
+    import os
+    from ti5_isaacgym_amd import make_t1_env, task_registry
+    from ti5_isaacgym_amd.algo import DHOnPolicyRunner
+    from ti5_isaacgym_amd.utils.helpers import class_to_dict
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "ppo_amp_check.py")
+    spec = importlib.util.spec_from_file_location("ppo_amp_check", path)
+    chk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(chk)
+    env = make_t1_env(num_envs=1024, mesh_type="plane", seed=5, device="cuda:0")
+    _, train_cfg = task_registry.get_cfgs("t1_dh_stand")
+    torch.manual_seed(0)
+    r = DHOnPolicyRunner(env, class_to_dict(train_cfg), None, device="cuda:0")
+    r.alg.actor_critic.train()
+    obs, priv = env.reset()
+    critic = priv if priv is not None else obs
+    obs, critic = chk.rollout(r, obs, critic)
+    ls_off, ls_on, diff, _, _ = chk.compare_cast_once(r, 77)
+    assert list(ls_off) == list(ls_on), (ls_off, ls_on)
+    assert diff == 0.0, diff

@@ -35,6 +35,7 @@ class DHPPO:
         # opt-in mixed precision of the update (not in the reference): torch.bfloat16 runs the update's forward and
         # backward GEMMs in bf16 (fp32 accumulation, fp32 weights, optimizer and losses); None = fp32 as the reference
         self.amp_dtype = amp_dtype
+        self.cast_obs_once = True
         self.desired_kl, self.schedule, self.learning_rate = desired_kl, schedule, learning_rate
         self.actor_critic = actor_critic
         self.actor_critic.to(self.device)
@@ -151,9 +152,12 @@ class DHPPO:
         ac = self.actor_critic
         sums = torch.zeros(3, device=self.device)  # value, surrogate, state-estimator losses
         mse = nn.MSELoss()
-        gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
-        amp = (torch.autocast(device_type="cuda", dtype=self.amp_dtype)
-               if self.amp_dtype is not None and torch.device(self.device).type == "cuda" else contextlib.nullcontext())
+        use_amp = self.amp_dtype is not None and torch.device(self.device).type == "cuda"
+        amp = torch.autocast(device_type="cuda", dtype=self.amp_dtype) if use_amp else contextlib.nullcontext()
+        # under the bf16 update every consumer of the actor observations is a bf16 GEMM: cast them once per update
+        # (same values as autocast's per-minibatch casts) unless cast_obs_once is switched off (A/B)
+        gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs,
+                                                obs_dtype=self.amp_dtype if use_amp and self.cast_obs_once else None)
         for (obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b,
              hid_b, masks_b) in gen:
             with amp:

@@ -92,12 +92,17 @@ class RolloutStorage:
         idx = torch.cat((flat.new_tensor([-1], dtype=torch.int64), flat.nonzero(as_tuple=False)[:, 0]))
         return (idx[1:] - idx[:-1]).float().mean(), self.rewards.mean()
 
-    def mini_batch_generator(self, num_mini_batches, num_epochs=8):
+    def mini_batch_generator(self, num_mini_batches, num_epochs=8, obs_dtype=None):
+        """The reference's generator (rollout_storage.py:153-173).  obs_dtype (not in the reference): the actor
+        observations are cast once per update to that dtype (the opt-in bf16 update, DHPPO.amp_dtype, whose GEMMs
+        cast every obs-fed operand to bf16 anyway), so each minibatch gathers, unfolds and saves half the bytes."""
         batch = self.num_envs * self.num_transitions_per_env
         mb = batch // num_mini_batches
         perm = torch.randperm(num_mini_batches * mb, requires_grad=False, device=self.device)
         flat = lambda x: x.flatten(0, 1)  # noqa: E731
         obs = flat(self.observations)
+        if obs_dtype is not None and obs.dtype != obs_dtype:
+            obs = obs.to(obs_dtype)
         critic = flat(self.privileged_observations) if self.privileged_observations is not None else obs
         cols = [flat(self.actions), flat(self.values), flat(self.advantages), flat(self.returns),
                 flat(self.actions_log_prob), flat(self.mu), flat(self.sigma)]

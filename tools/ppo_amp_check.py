@@ -71,6 +71,34 @@ def compare_updates(r, seed):
     return ls_fp32, ls_bf16, float(num / den), ms_fp32, ms_bf16
 
 
+def compare_cast_once(r, seed):
+    """The bf16 update with the actor observations cast per minibatch by autocast (cast_obs_once off) and then
+    cast once per update (on, the default), from the same weights, optimizer state, storage and minibatch seed;
+    the second result is kept.  Returns (losses off, losses on, max |dW| difference, ms off, ms on)."""
+    alg = r.alg
+    snap = snapshot_storage(alg.storage)
+    w0 = [q.detach().clone() for q in alg.actor_critic.parameters()]
+    opt0 = copy.deepcopy(alg.optimizer.state_dict())
+    lr0 = alg.learning_rate
+    alg.cast_obs_once = False
+    ls_off, ms_off = timed_update(alg, torch.bfloat16, seed)
+    w_off = [q.detach().clone() for q in alg.actor_critic.parameters()]
+    with torch.no_grad():
+        for q, q0 in zip(alg.actor_critic.parameters(), w0):
+            q.copy_(q0)
+    alg.optimizer.load_state_dict(opt0)
+    alg.learning_rate = lr0
+    for g in alg.optimizer.param_groups:
+        g["lr"] = lr0
+    restore_storage(alg.storage, snap)
+    alg.storage.step = r.num_steps_per_env
+    alg.cast_obs_once = True
+    ls_on, ms_on = timed_update(alg, torch.bfloat16, seed)
+    alg.amp_dtype = None
+    diff = max(float((a - b.detach()).abs().max()) for a, b in zip(w_off, alg.actor_critic.parameters()))
+    return ls_off, ls_on, diff, ms_off, ms_on
+
+
 def rollout(r, obs, critic):
     alg = r.alg
     with torch.inference_mode():
@@ -87,6 +115,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--num-envs", type=int, default=8192)
     p.add_argument("--iters", type=int, default=3)
+    p.add_argument("--cast-ab", action="store_true",
+                   help="bf16 update: actor observations cast per minibatch (autocast) vs once per update")
     a = p.parse_args()
     dev = torch.device("cuda:0")
     env = make_t1_env(num_envs=a.num_envs, mesh_type="trimesh", seed=5, device=str(dev))
@@ -99,6 +129,13 @@ def main():
     out = []
     for it in range(a.iters + 1):   # iteration 0 warms the libraries up (not reported)
         obs, critic = rollout(r, obs, critic)
+        if a.cast_ab:
+            ls_off, ls_on, diff, ms_off, ms_on = compare_cast_once(r, 1000 + it)
+            if it > 0:
+                out.append({"iter": it, "losses_cast_per_minibatch": ls_off, "losses_cast_once": ls_on,
+                            "max_abs_weight_diff": diff, "update_ms_cast_per_minibatch": round(ms_off, 2),
+                            "update_ms_cast_once": round(ms_on, 2)})
+            continue
         ls_fp32, ls_bf16, rel, ms_fp32, ms_bf16 = compare_updates(r, 1000 + it)
         if it > 0:
             out.append({"iter": it, "losses_fp32": [round(x, 6) for x in ls_fp32],
