@@ -36,9 +36,12 @@ def wgrad_splitk(gy, x):
     # DHPPO.amp_dtype)
     wide = lambda t: t if t.dtype in (torch.float32, torch.float64) else t.float()  # noqa: E731
     if M < 8 and gy.dtype != wide(gy).dtype:
-        # the value head (M = 1): hipBLASLt's bf16 batched GEMM spends ~11 ms of host time per call on a 1-row
-        # output (profiles/r02ap_ppo_bf16.md); the product is a few MB, so widen and take one fp32 GEMM
-        return wide(gy).t().mm(wide(x))
+        # the heads (M = 1, 3, 12 outputs): hipBLASLt's bf16 batched GEMM spends ~11 ms of host time per call on a
+        # 1-row output (profiles/r02ap_ppo_bf16.md), and one GEMM over all K rows has a single output tile (141 us for
+        # M = 3, N = 64).  Widen (a few MB) and take the split-K batched GEMM in fp32, outside autocast (which would
+        # narrow it again): 28-57 us (profiles/r02bf_small_m_wgrad.txt)
+        with torch.autocast(device_type="cuda", enabled=False):
+            return wgrad_splitk(wide(gy), wide(x))
     gw =wide(torch.bmm(gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1))).sum(0)
     if c < K:
         gw = gw + wide(gy[c:].t().mm(x[c:]))
