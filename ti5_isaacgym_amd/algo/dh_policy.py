@@ -178,6 +178,7 @@ class ActorCriticDH(nn.Module):
         self.critic = _mlp([num_critic_obs, *critic_hidden_dims, 1], act)
         self.std = nn.Parameter(init_noise_std * torch.ones(num_actions))
         self.distribution = None
+        self.validate_args = None
         Normal.set_default_validate_args = False
         self.long_history = _history_encoder(in_channels, num_proprio_obs, filter_size, kernel_size, stride_size,
                                              lh_output_dim)
@@ -210,7 +211,9 @@ class ActorCriticDH(nn.Module):
 
     def update_distribution(self, actor_obs):
         mean = self.actor(actor_obs).float()   # fp32 distribution under the opt-in bf16 update (no-op in fp32)
-        self.distribution = Normal(mean, mean * 0.0 + self.std)
+        # validate_args None = torch's default, as the reference; DHPPO.update turns it off on the device, where each
+        # argument check is a host sync (it checks the losses' finiteness once per update instead)
+        self.distribution = Normal(mean, mean * 0.0 + self.std, validate_args=self.validate_args)
 
     def act(self, observations, **kwargs):
         self.update_distribution(self.actor_input(observations))

@@ -12,6 +12,7 @@ pair of observation buffers the env hands out (its ping-pong buffers): the same 
 without the per-kernel launch cost that dominates at one call per env step.
 """
 import contextlib
+import math
 import warnings
 
 import torch
@@ -158,21 +159,31 @@ class DHPPO:
         # (same values as autocast's per-minibatch casts) unless cast_obs_once is switched off (A/B)
         gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs,
                                                 obs_dtype=self.amp_dtype if use_amp and self.cast_obs_once else None)
-        for (obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b,
-             hid_b, masks_b) in gen:
-            with amp:
-                loss, value_loss, surrogate_loss, se_loss = self._losses(
-                    ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
-                    old_sigma_b, hid_b, masks_b, mse)
-            self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
-            loss.backward()
-            self.grads.all_reduce_()
-            nn.utils.clip_grad_norm_(ac.parameters(), self.max_grad_norm)
-            self.optimizer.step()
-            sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), se_loss.detach()])
+        # the distribution's argument checks are host syncs (three per minibatch) on the device: off for the update,
+        # replaced by one finiteness check of the losses below (the reference would raise at the first non-finite mean)
+        validate = ac.validate_args
+        if torch.device(self.device).type == "cuda":
+            ac.validate_args = False
+        try:
+            for (obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b,
+                 hid_b, masks_b) in gen:
+                with amp:
+                    loss, value_loss, surrogate_loss, se_loss = self._losses(
+                        ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
+                        old_sigma_b, hid_b, masks_b, mse)
+                self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
+                loss.backward()
+                self.grads.all_reduce_()
+                nn.utils.clip_grad_norm_(ac.parameters(), self.max_grad_norm)
+                self.optimizer.step()
+                sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), se_loss.detach()])
+        finally:
+            ac.validate_args = validate
         n = self.num_learning_epochs * self.num_mini_batches
         self.storage.clear()
         mv, ms, mse_ = (sums / n).tolist()
+        if not all(map(math.isfinite, (mv, ms, mse_))):
+            raise ValueError(f"DHPPO.update: non-finite losses (value {mv}, surrogate {ms}, state estimator {mse_})")
         return mv, ms, mse_
 
     def _losses(self, ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
