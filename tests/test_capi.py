@@ -73,3 +73,15 @@ def test_env_refuses_cpu_device():
     import ti5_isaacgym_amd as t
     with pytest.raises(RuntimeError):
         t.make_t1_env(num_envs=4, mesh_type="plane", device="cpu")
+
+
+def test_policy_header_exports(lib):
+    """include/t1policy.h's entry points are exported by the same library, and _lib binds them."""
+    src = open(os.path.join(REPO, "include", "t1policy.h")).read()
+    names = sorted(set(re.findall(r"^\s*int\s+(t1policy_\w+)\s*\(", src, re.M)))
+    from ti5_isaacgym_amd import _lib
+    assert names == sorted(_lib.POLICY_EXPORTS) and names
+    for n in names:
+        assert hasattr(lib, n), n
+    # argument errors are reported without touching the GPU
+    assert lib.t1policy_conv1d_forward(None, None, None, None, 1, 66, 47, 32, 6, 3, None) == -1

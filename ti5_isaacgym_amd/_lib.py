@@ -92,6 +92,9 @@ EXPORTS = ["t1env_create", "t1env_destroy", "t1env_init", "t1env_set_terrain", "
            "t1env_set_fused", "t1env_set_timing", "t1env_get_timing", "t1env_last_error", "t1env_version",
            "t1env_measure_heights", "t1env_critic_heights", "t1env_reset_idx", "t1env_set_substep_log"]
 
+# include/t1policy.h: the DH policy's HIP kernels, in the same library
+POLICY_EXPORTS = ["t1policy_conv1d_forward"]
+
 _lib = None
 
 
@@ -124,6 +127,7 @@ def load():
         "t1env_measure_heights": ([vp, vp, i32, vp, vp], C.c_int),
         "t1env_reset_idx": ([vp, vp, P(StepArgs), vp], C.c_int),
         "t1env_critic_heights": ([vp, i32, i32, f32, vp, vp, vp, vp], C.c_int),
+        "t1policy_conv1d_forward": ([vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -106,6 +106,29 @@ def _mlp(sizes, act):
     return nn.Sequential(*layers)
 
 
+def conv1d_direct(x, conv):
+    """Inference forward of a (B, C, L) Conv1d as the HIP direct-conv kernel (include/t1policy.h), channels-last
+    (B, Lout, O) like conv1d_as_gemm: one pass over x instead of the unfolded-row copy plus a GEMM.  Returns None for
+    a shape the library has no instance of (the caller keeps the GEMM path)."""
+    from .. import _lib
+    lib = _lib.load()
+    k, st = conv.kernel_size[0], conv.stride[0]
+    x = x.contiguous()
+    B, C, L = x.shape
+    O = conv.out_channels
+    lout = (L - k) // st + 1
+    wt = conv.weight.detach().permute(1, 2, 0).contiguous()   # tap-major: wt[c, t, o]
+    bias = conv.bias.detach().contiguous()
+    y = torch.empty(B, lout, O, device=x.device, dtype=torch.float32)
+    rc = lib.t1policy_conv1d_forward(x.data_ptr(), wt.data_ptr(), bias.data_ptr(), y.data_ptr(), B, C, L, O, k, st,
+                                     torch.cuda.current_stream(x.device).cuda_stream)
+    if rc == 1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"t1policy_conv1d_forward failed (rc={rc})")
+    return y
+
+
 def conv1d_as_gemm(x, conv, channels_last=False):
     """nn.Conv1d (no padding / dilation / groups) as one GEMM over unfolded windows.  x: (B, C, L), or (B, L, C) with
     channels_last; returns (B, Lout, O) (channels last).  The windows x[b, :, s*l : s*l + k] become rows of a
@@ -131,7 +154,8 @@ class HistoryEncoder(nn.Sequential):
     names (so checkpoints load either way).  On the host the layers run as written (nn.Conv1d, bit-identical to the
     reference's CPU path); on the MI355X the two Conv1d run as unfold + GEMM (conv1d_as_gemm) with the activations
     kept channels-last: MIOpen's Conv1d kernels for this shape (66-channel, length-47 input, batch 49,152 in the PPO
-    update) were the update's dominant cost.  Same arithmetic up to fp32 summation order."""
+    update) were the update's dominant cost.  Without autograd (the rollout's act()) the first conv is the HIP
+    direct-conv kernel (conv1d_direct).  Same arithmetic up to fp32 summation order."""
 
     def forward(self, x):
         if not x.is_cuda:
@@ -139,7 +163,10 @@ class HistoryEncoder(nn.Sequential):
         last = False   # x is (B, C, L) until the first conv; channels-last after it
         for m in self:
             if isinstance(m, nn.Conv1d):
-                x = conv1d_as_gemm(x, m, channels_last=last)
+                y = None
+                if not last and not torch.is_grad_enabled() and x.dtype == torch.float32 and m.weight.dtype == x.dtype:
+                    y = conv1d_direct(x, m)   # inference (the rollout's act()): the HIP direct conv
+                x = y if y is not None else conv1d_as_gemm(x, m, channels_last=last)
                 last = True
             elif isinstance(m, nn.Flatten) and last:
                 x = x.transpose(1, 2).reshape(x.shape[0], -1)   # (B, O, Lout) order, as nn.Flatten of NCL

@@ -11,13 +11,14 @@ CSRC = os.path.join(HERE, "csrc")
 # translation unit -> optimisation level.  The dynamics unit is built at -O1 (round 1's fastest level; on the round-2
 # kernel -O1/-O2/-O3 measure the same, profiles/r02bc_opt_levels.json).  Round 1's -O2/-O3 wrong dynamics bisected to the load/store vectorizer over the __restrict__
 # model-pointer loads; the -O3 guard build (OUT_O3) keeps every level under the fp64 check.
-UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1")]
+UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1"), ("t1policy.hip", "-O3")]
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
 # guard build: the dynamics unit at -O3 (tests/test_gpu_opt_levels.py keeps it under the fp64 dynamics check)
 OUT_O3 = os.path.join(HERE, "_lib", "var", "libt1env_hip_dyn_o3.so")
 DEPS = [os.path.join(CSRC, f) for f in ("t1env.hip", "t1env_dynamics.hip", "t1_dynamics.h", "t1_common.h", "t1env_post.h",
                                        "t1_model_conv.h", "t1env_device.h", "t1env_internal.h")] + \
-    [os.path.join(os.path.dirname(HERE), "include", "t1env.h")]
+    [os.path.join(CSRC, "t1policy.hip")] + \
+    [os.path.join(os.path.dirname(HERE), "include", h) for h in ("t1env.h", "t1policy.h")]
 ARCH = os.environ.get("T1ENV_ARCH", "gfx950")
 
 
