@@ -78,7 +78,7 @@ def parse():
                         "0 = never, 1 = every step)")
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02ax.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02bn.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
     p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r02ax_sq_counters.json"),
                    help="SQ instruction counters of the fused kernel (tools/pmc_sq_summary.py): the VALU-issue roofline")
