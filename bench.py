@@ -76,8 +76,9 @@ def parse():
     p.add_argument("--time-every", type=int, default=8,
                    help="record per-kernel HIP events on every k-th timed step (event records cost host time; "
                         "0 = never, 1 = every step)")
-    p.add_argument("--cpu-envs", type=int, default=256)
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-envs", type=int, default=4096,
+                   help="CPU-baseline sample size (BASELINE configs[1]'s 4096 envs; 256 understated the CPU by ~2x)")
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02bn.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
     p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r02ax_sq_counters.json"),
@@ -108,9 +109,14 @@ def cpu_baseline(env, args):
         model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
     except Exception:
         model = "unknown"
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count()
     return {"value": round(args.cpu_envs * n / dt, 1), "unit": "env-steps/s", "cores": cpu.threads(), "kind": "port",
             "sample": f"{args.cpu_envs} envs x {n} steps ({dt:.1f} s), same cfg/terrain as the GPU run; "
-                      f"numpy oracle post-physics + OpenMP fp32 dynamics on {cpu.threads()} threads of {model}"}
+                      f"numpy oracle post-physics (one thread) + OpenMP fp32 dynamics on {cpu.threads()} threads "
+                      f"(OMP_NUM_THREADS; {aff} cores in this process's affinity) of {model}"}
 
 
 def main():
@@ -214,15 +220,33 @@ def main():
             sq = json.load(open(args.sq_json))
             if sq.get("envs") == N and args.mesh == "trimesh" and args.state_dtype == "fp32" and not args.push:
                 insts = sq["derived"]["valu_insts_per_dyn_wave"]
-                cyc = dk["avg_ms"] * 1e-3 * SHADER_GHZ * 1e9
+                # the shader clock the SQ pass measured (SQ_BUSY_CYCLES per SE / traced duration), else the peak clock
+                ghz = sq["derived"].get("shader_clock_ghz", SHADER_GHZ)
+                cyc = dk["avg_ms"] * 1e-3 * ghz * 1e9
                 ach = insts / cyc
                 issue = {"bound": "valu_issue", "unit": "VALU instr/cycle per dynamics wave",
                          "achieved": round(ach, 4), "peak": LONE_WAVE_VALU_PER_CYCLE,
                          "frac": round(ach / LONE_WAVE_VALU_PER_CYCLE, 4),
                          "valu_insts_per_dyn_wave": round(insts), "wave_cycles": round(cyc),
+                         "shader_clock_ghz": round(ghz, 3),
+                         "sq_profile_dyn_wave_issue_frac": sq["derived"].get("dyn_wave_issue_frac"),
+                         "wait_any_frac_all_waves": sq["derived"].get("wait_any_frac"),
                          "source": os.path.relpath(args.sq_json, REPO)}
         except Exception:
             issue = None
+    # the bound: the roofline this kernel sits closest to.  HBM (achieved / peak below) unless the dynamics waves'
+    # VALU-issue fraction is higher; when neither is near 1, SQ_WAIT_ANY says the rest is dependent latency
+    hbm_frac = achieved / HBM_PEAK_GBS
+    bound = "hbm"
+    if issue is not None and issue["frac"] > hbm_frac:
+        bound = "valu_issue"
+    binding = {"hbm": f"HBM: {hbm_frac:.3f} of 8 TB/s"}
+    if issue is not None:
+        binding["valu_issue"] = f"VALU issue of a dynamics wave: {issue['frac']:.3f} of 1 instr / 4 cycles"
+        if max(hbm_frac, issue["frac"]) < 0.7:
+            binding["note"] = ("neither roofline binds: dependent-latency / barrier waits of the leg wave's chain at one "
+                               f"wave per SIMD (SQ_WAIT_ANY {issue['wait_any_frac_all_waves']:.2f} of wave cycles)"
+                               if issue.get("wait_any_frac_all_waves") else "neither roofline binds: latency")
     line = {
         "metric": "env-steps/sec at 8192 envs, t1_dh_stand, 1/2/4/8 MI355X; obs/reward parity",
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
@@ -234,14 +258,13 @@ def main():
                                f"10 substeps/step, {args.state_dtype} obs/critic histories",
                    "state_dtype": args.state_dtype,
                    "num_envs_per_gpu": N, "global_envs": N * world, "mesh": args.mesh, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "basis": basis,
+        "roofline": {"bound": bound, "kernel": dom, "basis": basis,
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_step": b_alg * N, "alg_bytes_per_env_step": b_alg,
                      "wall_clock_GBs": round(value / world * b_alg / 1e9, 1),
                      "step_span_ms_timed": round(step_span_ms, 4) if step_span_ms else None,
-                     "binding": "dynamics waves: dependent-latency / VALU-issue chain at one wave per SIMD, not HBM "
-                                "(HBM frac above is how much of 8 TB/s the step's algorithmic bytes use)",
+                     "binding": binding,
                      "issue": issue,
                      "kernels": per_kernel},
         "finite": ok,

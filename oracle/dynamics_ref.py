@@ -75,7 +75,9 @@ class Robot:
                 Jw[b, :, k] = [W[2, 1], W[0, 2], W[1, 0]]
         return Jv, Jw
 
-    def accel(self, p, quat, w, v, q, qd, tau, g=9.81, eps=1e-5):
+    def accel(self, p, quat, w, v, q, qd, tau, g=9.81, eps=1e-5, f_base=None):
+        """generalized accelerations; f_base: an external world-frame force on the base body at its COM (Isaac Gym
+        apply_rigid_body_force_tensors without positions), entering as Jv_base^T f."""
         R = quat_to_R(quat)
         u = np.concatenate([w, v, qd])
         Jv, Jw = self.jacobians(p, R, q)
@@ -94,4 +96,6 @@ class Robot:
             h += Jv[b].T @ (self.mass[b] * (Jvd_u - grav)) + Jw[b].T @ (Ib @ Jwd_u + np.cross(wb, Ib @ wb))
         M[6:, 6:] += np.diag(self.arm)
         f = np.concatenate([np.zeros(6), tau])
+        if f_base is not None:
+            f = f + Jv[0].T @ np.asarray(f_base, float)
         return np.linalg.solve(M, f - h), M

@@ -313,8 +313,9 @@ class T1Oracle:
         return self.obs_buf, self.priv_buf, self.rew_buf, self.reset_buf, self.extras
 
     def reset(self, physics):
-        """legged_robot.py:450-455"""
-        self.reset_idx(np.arange(self.N))
+        """legged_robot.py:450-455.  After the first step the draws take the between-step key domain: the plain
+        counter would repeat the draws of every env the last step reset (t1env.hip k_reset_all)."""
+        self.reset_idx(np.arange(self.N), between_steps=self.common_step_counter > 0)
         self.step(np.zeros((self.N, 12), f32), physics)
         return self.obs_buf, self.priv_buf
 

@@ -2,7 +2,7 @@
 
 The reference outputs (tests/golden/*.npz) were produced by the reference's own env code running on the
 same synthetic physics states (tests/golden/synth.py) with the same counter-RNG draws.  Tolerance: 1e-4
-relative with a 1e-4 absolute floor (north_star), exact for bool / integer buffers.
+relative with a 1e-6 absolute floor (golden_util.RTOL / ATOL), exact for bool / integer buffers.
 """
 import copy
 
@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 import synth
-from golden_util import assert_close, load, measures_heights, mid_reset, push_interval_s, terrain_curriculum
+from golden_util import assert_close, load, torque_atol, measures_heights, mid_reset, push_interval_s, terrain_curriculum
 
 REWARD_NAMES = sorted(["joint_pos", "feet_clearance", "feet_contact_number", "feet_air_time", "foot_slip",
                        "feet_distance", "knee_distance", "feet_rotation", "feet_contact_forces",
@@ -157,7 +157,8 @@ def compare(name, fx, outs):
         np.testing.assert_array_equal(s["imu_lag"], fx["step_imu_lag_timestep"][t], err_msg="imu_lag" + ctx)
         np.testing.assert_array_equal(s["lag"], fx["step_lag_timestep"][t], err_msg="lag" + ctx)
         assert_close("gait_start", s["gait_start"], fx["step_gait_start"][t], ctx=ctx)
-        for k in ("torques", "commands", "ref_dof_pos", "feet_air_time", "feet_height", "ext_forces",
+        assert_close("torques", s["torques"], fx["step_torques"][t], atol=torque_atol(), ctx=ctx)
+        for k in ("commands", "ref_dof_pos", "feet_air_time", "feet_height", "ext_forces",
                   "env_origins", "root_states", "episode_sums", "dof_state"):
             assert_close(k, s[k], fx["step_" + k][t], ctx=ctx)
         assert_close("kp", s["kp"], fx["step_randomized_p_gains"][t], ctx=ctx)

@@ -85,3 +85,14 @@ def test_policy_header_exports(lib):
         assert hasattr(lib, n), n
     # argument errors are reported without touching the GPU
     assert lib.t1policy_conv1d_forward(None, None, None, None, 1, 66, 47, 32, 6, 3, None) == -1
+
+
+def test_env_refuses_external_torques():
+    """ext_torque_max != 0 would draw torques into the critic frame that the HIP dynamics never applies: it raises
+    (the reference applies them, t1_dh_stand_env.py:243-247; DHT1StandCfg uses 0, t1_dh_stand_config.py:201)."""
+    import ti5_isaacgym_amd as t
+
+    def hook(cfg):
+        cfg.domain_rand.ext_torque_max = 2.0
+    with pytest.raises(NotImplementedError, match="ext_torque_max"):
+        t.make_t1_env(num_envs=4, mesh_type="plane", device="cpu", cfg_hook=hook)

@@ -5,13 +5,16 @@ reference is oracle/dynamics_ref.py (Kane's projected Newton-Euler equations fro
 plain forward kinematics: nothing shared with the product's CRBA / RNEA / LTDL code).  PhysX itself is absent, so
 this pins the equations of motion, not PhysX parity.
 
-Airborne robots (base 5 m up, joints inside their limits, speeds well below the velocity limits, no external
-force): no contact and no joint-limit term enters, so one substep of the semi-implicit integrator changes the
+Airborne robots (base 5 m up, joints inside their limits, speeds well below the velocity limits): no contact and no joint-limit term enters, so one substep of the semi-implicit integrator changes the
 generalized speeds by exactly dt times the accelerations at the substep's start state.  The kernel's substep log
 (t1env_set_substep_log) gives the state after substep 0 and the PD torques of substep 0; the test recovers the
 kernel's velocity change from the logged root / dof rows (undoing the COM-velocity report and the base-origin
 velocity update of integrate_base) and compares delta_u / dt with Kane's accelerations for the same state, torques
 and per-env randomized masses, COM displacement, inertia scales and armatures.
+
+The second case also sets a random base force in `applied_force` (the _add_ext_force force the next simulate applies,
+t1_dh_stand_env.py:233-247; the kernel applies it on the step's first substep at the base COM), which enters Kane's
+equations as Jv_base^T f.
 
 Tolerance: |gpu - ref| <= 2e-4 (1 + |ref|_max) per env (the fp32 velocity change divided by dt = 1 ms; measured
 worst 1.2e-5 on the MI355X, profiles/r02am_gpu_kane.log).
@@ -31,7 +34,8 @@ def _skew(w):
     return np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
 
 
-def test_one_substep_matches_kane_equations():
+@pytest.mark.parametrize("ext_force", [False, True], ids=["no_force", "base_ext_force"])
+def test_one_substep_matches_kane_equations(ext_force):
     from ti5_isaacgym_amd import make_t1_env
     from ti5_isaacgym_amd.utils.urdf import load_model
 
@@ -59,7 +63,11 @@ def test_one_substep_matches_kane_equations():
     root[:, 10:13] = rng.normal(0, 0.8, (N, 3))
     env.root_states.copy_(torch.from_numpy(root))
     env.dof_state.copy_(torch.from_numpy(np.stack([q0, qd0], -1).reshape(N * 12, 2).astype(np.float32)))
-    env.applied_force.zero_()
+    fb = np.zeros((N, 3))
+    if ext_force:   # the t1 cfg's ranges: x U(-300, 600), y U(-400, 400), z U(-5, 5)
+        fb = np.stack([rng.uniform(-300, 600, N), rng.uniform(-400, 400, N), rng.uniform(-5, 5, N)], 1)
+    env.applied_force.copy_(torch.from_numpy(fb.astype(np.float32)))
+    fb = fb.astype(np.float32).astype(np.float64)
     env.step(torch.from_numpy(rng.normal(0, 0.5, (N, 12)).astype(np.float32)).to("cuda:0"))
     lg = {k: v.cpu().numpy().astype(np.float64) for k, v in env.substep_log.items()}
     env.set_substep_log(False)
@@ -82,7 +90,8 @@ def test_one_substep_matches_kane_equations():
         R0, w0 = quat_to_R(r0[n, 3:7]), r0[n, 10:13]
         vo0 = r0[n, 7:10] - np.cross(w0, R0 @ (com_base + com_disp[n]))
         tau = lg["torque"][0, n]
-        ref, _ = Robot(tab, mass, isc, com_disp[n], arm[n]).accel(r0[n, 0:3], r0[n, 3:7], w0, vo0, q0[n], qd0[n], tau)
+        ref, _ = Robot(tab, mass, isc, com_disp[n], arm[n]).accel(r0[n, 0:3], r0[n, 3:7], w0, vo0, q0[n], qd0[n], tau,
+                                                                  f_base=fb[n])
         ref_sp = ref.copy()
         ref_sp[3:6] = ref[3:6] - np.cross(w0, vo0)   # classical -> spatial acceleration of the base origin
         # the kernel's velocity change over substep 0 (integrate_base: vb = vO_new + dt w_new x vO_new, reported at

@@ -16,16 +16,20 @@ same states, so what is compared is k_dyn4's own arithmetic around the solver:
     feet_air_time, feet_height, ref_dof_pos, episode sums, gait times, episode lengths, terrain levels, origins,
     root / dof state after resets and pushes).
 
-Tolerance: 1e-4 relative with a 1e-4 absolute floor (north_star), exact for bool / integer buffers.  Every 7th env
-starts near its time-out so the reset path runs inside the fused epilogue.  Cases: BASELINE configs[1] (4096 envs,
-plane), configs[2] (8192 envs, trimesh curriculum + full DR) and configs[4] (32768 envs, height field, pushes),
-plus a ragged 777-env trimesh run (last workgroup partly empty).
+Tolerance: 1e-4 relative with a 1e-6 absolute floor (golden_util.RTOL / ATOL), exact for bool / integer buffers.
+Every 7th env starts near its time-out so the reset path runs inside the fused epilogue.  Cases: BASELINE configs[1]
+(4096 envs, plane), configs[2] (8192 envs, trimesh curriculum + full DR) and configs[4] (32768 envs, height field,
+pushes), plus a ragged 777-env trimesh run (last workgroup partly empty).  Two more cases start the step counter just
+before an external-force window (`counter % 400 <= duration`, t1_dh_stand_env.py:205-215): at 400 (duration 0: the
+forces are drawn, enter the critic frame and are never applied) and at 96,400 (duration index 1 = 0.05 s: drawn at
+96,400, applied to the base of standing envs from 96,401 to 96,405, t1_dh_stand_env.py:233-247,
+t1_dh_stand_config.py:197-204), so k_dyn4's fused draw, its critic-frame terms and `applied_force` are compared.
 """
 import numpy as np
 import pytest
 import torch
 
-from golden_util import assert_close
+from golden_util import assert_close, torque_atol
 from oracle.t1_oracle import DECIMATION, REWARD_NAMES, T1Oracle
 
 pytestmark = pytest.mark.gpu
@@ -76,7 +80,7 @@ def np_(t):
 def compare(env, o, rp, step):
     ctx = f" [step {step}]"
     assert rp.s == DECIMATION
-    assert_close("torques", np.stack(o.torque_log), rp.torque, ctx=ctx)
+    assert_close("torques", np.stack(o.torque_log), rp.torque, atol=torque_atol(), ctx=ctx)
     np.testing.assert_array_equal(np_(env.reset_buf), o.reset_buf, err_msg="reset" + ctx)
     np.testing.assert_array_equal(np_(env.time_out_buf), o.time_out_buf, err_msg="time_out" + ctx)
     np.testing.assert_array_equal(np_(env.episode_length_buf), o.episode_length_buf, err_msg="episode_length" + ctx)
@@ -95,6 +99,13 @@ def compare(env, o, rp, step):
         assert_close(name, np_(a), b, ctx=ctx)
     assert_close("episode_sums", np.stack([np_(env.episode_sums[k]) for k in REWARD_NAMES]),
                  np.stack([o.episode_sums[k] for k in REWARD_NAMES]), ctx=ctx)
+    # the external-force draw (_add_ext_force) and the base force the next step's first substep applies
+    assert_close("ext_forces", np_(env.ext_forces), o.ext_forces, ctx=ctx)
+    assert_close("ext_torques", np_(env.ext_torques), o.ext_torques, ctx=ctx)
+    # (the library writes the force for the next simulate every step, zeros outside a window; the oracle keeps its
+    # last _add_ext_force value, consumed by the next step's first substep: force_pending)
+    af = o.applied_force[:, 0, :] if o.force_pending else np.zeros((env.num_envs, 3), np.float32)
+    assert_close("applied_force", np_(env.applied_force), af, ctx=ctx)
     # the lag sample k_dyn4 captured (ring slot of step ctr - lag // 10) vs the dof_lag_buffer entry the observation
     # reads (index dof_lag_timestep): (q, qd) of substep 9 - lag % 10
     ctr = env.common_step_counter - 1
@@ -105,11 +116,12 @@ def compare(env, o, rp, step):
     assert_close("dof_lag_sample", got, ref, ctx=ctx)
 
 
-@pytest.mark.parametrize("n,mesh,push,steps", [(4096, "plane", False, 6), (8192, "trimesh", False, 6),
-                                               (32768, "heightfield", True, 4), (777, "trimesh", True, 5)],
-                         ids=["config2_4096_plane", "config3_8192_trimesh", "config5_32768_hf_push",
-                              "ragged777_trimesh_push"])
-def test_product_kernel_matches_oracle(n, mesh, push, steps):
+@pytest.mark.parametrize("n,mesh,push,steps,counter0", [
+    (4096, "plane", False, 6, None), (8192, "trimesh", False, 6, None), (32768, "heightfield", True, 4, None),
+    (777, "trimesh", True, 5, None), (4096, "trimesh", False, 4, 398), (8192, "trimesh", False, 9, 96398)],
+    ids=["config2_4096_plane", "config3_8192_trimesh", "config5_32768_hf_push", "ragged777_trimesh_push",
+         "extforce_window_400", "extforce_window_96400_applied"])
+def test_product_kernel_matches_oracle(n, mesh, push, steps, counter0):
     from ti5_isaacgym_amd import make_t1_env
     env = make_t1_env(num_envs=n, mesh_type=mesh, seed=3, device="cuda:0", cfg_hook=_push_hook if push else None)
     o = oracle_for(env, push)
@@ -131,8 +143,11 @@ def test_product_kernel_matches_oracle(n, mesh, push, steps):
     el[::7] = int(env.max_episode_length) - 3 - np.arange(0, n, 7) % 4
     env.episode_length_buf = torch.from_numpy(el)
     o.episode_length_buf[:] = el
+    if counter0 is not None:   # jump to just before an external-force window (both sides: is_first_add_force stays True)
+        assert env.is_first_add_force and o.is_first_add_force
+        env.common_step_counter = o.common_step_counter = counter0
     g = torch.Generator(device="cuda:0").manual_seed(0)
-    resets = pushes = 0
+    resets = pushes = applied = drawn = 0
     for t in range(steps):
         a = torch.randn(n, 12, device="cuda:0", generator=g)
         env.step(a)
@@ -142,6 +157,11 @@ def test_product_kernel_matches_oracle(n, mesh, push, steps):
         compare(env, o, rp, t + 1)
         resets += int(o.reset_buf.sum())
         pushes += int(push and env.common_step_counter % env.push_interval == 0)
+        drawn += int(np.abs(o.ext_forces).max() > 0)
+        applied += int(o.force_pending and np.abs(o.applied_force).max() > 0)
     env.set_substep_log(False)
     assert resets > 0, "no env reset: the fused epilogue's reset path was not exercised"
     assert pushes > 0 or not push
+    if counter0 is not None:
+        assert drawn > 0, "the external-force window was not reached"
+        assert (applied > 0) == (counter0 >= 96000), (applied, counter0)

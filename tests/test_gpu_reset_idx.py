@@ -63,3 +63,21 @@ def test_reset_idx_after_in_step_reset_draws_fresh_values():
     assert (env.randomized_p_gains[r] != kp[r]).all(dim=1).all(), "reset_idx reused the in-step reset's draws"
     assert not torch.equal(env.lag_timestep[r], lag[r]) or not torch.equal(env.gait_time[r], gs[r])
     assert torch.equal(env.randomized_p_gains[~r], kp[~r])
+
+
+def test_reset_after_stepping_draws_fresh_values():
+    """env.reset() on an env that has stepped (reset_idx of every env between steps): the envs the last step reset
+    must not redraw that step's values -- t1env_reset_all keys on counter | BETWEEN_STEP_SALT once counter > 0, like
+    the oracle's reset()."""
+    from ti5_isaacgym_amd import make_t1_env
+    n = 256
+    env = make_t1_env(num_envs=n, mesh_type="plane", seed=9, device="cuda:0")
+    env.reset()
+    env.episode_length_buf[::5] = int(env.max_episode_length)   # these envs time out in the next step
+    env.step(torch.zeros(n, 12, device="cuda:0"))
+    r = env.reset_buf.bool()
+    assert r[::5].all()
+    kp = env.randomized_p_gains.clone()
+    env.reset_idx_all()
+    torch.cuda.synchronize()
+    assert (env.randomized_p_gains[r] != kp[r]).all(dim=1).all(), "reset() reused the in-step reset's draws"

@@ -1,0 +1,52 @@
+"""The substep log must not change the product kernel's results -- needs the MI355X.
+
+tests/test_gpu_product_parity.py pins k_dyn4 through its substep log (t1env_set_substep_log), i.e. the `LOG=true`
+instantiation of the fused step kernel; bench.py, the runner and every other caller execute the `LOG=false` code
+object.  The two are separate compilations of a unit with a history of optimiser-dependent results,
+so this test steps two identically seeded envs -- one with the log on, one with it off -- through the same actions
+and requires every buffer the step writes to be BIT-identical, at BASELINE configs[2] (8192 envs, trimesh curriculum
++ full DR) through in-epilogue resets and an applied external-force window (counter 96,400, t1_dh_stand_env.py:205-247).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("obs_buf", "privileged_obs_buf", "rew_buf", "reset_buf", "time_out_buf", "root_states", "dof_state",
+          "rigid_state", "contact_forces", "torques", "commands", "episode_length_buf", "phase_length_buf",
+          "feet_air_time", "feet_height", "last_feet_z", "last_contacts", "ref_dof_pos", "gait_time", "ext_forces",
+          "ext_torques", "applied_force", "env_origins", "terrain_levels", "last_actions", "last_dof_vel",
+          "last_root_vel", "base_lin_vel", "base_ang_vel", "projected_gravity", "base_euler_xyz",
+          "randomized_p_gains", "lag_timestep", "dof_lag_timestep", "_act_hist", "_dof_hist", "_imu_hist",
+          "_episode_sums", "_extras_ring")
+
+
+@pytest.mark.parametrize("n,mesh", [(8192, "trimesh"), (777, "heightfield")], ids=["config3_8192_trimesh", "ragged777_hf"])
+def test_substep_log_does_not_change_results(n, mesh):
+    from ti5_isaacgym_amd import make_t1_env
+    envs = [make_t1_env(num_envs=n, mesh_type=mesh, seed=4, device="cuda:0") for _ in range(2)]
+    envs[0].set_substep_log(True)
+    for e in envs:
+        e.reset()
+        el = e.episode_length_buf.cpu().numpy().copy()
+        el[::5] = int(e.max_episode_length) - 2 - np.arange(0, n, 5) % 3   # in-epilogue resets
+        e.episode_length_buf = torch.from_numpy(el)
+        e.common_step_counter = 96398   # an applied external-force window: 96,400 draw, 96,401.. apply
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    resets, applied = 0, 0.0
+    for t in range(8):
+        a = torch.randn(n, 12, device="cuda:0", generator=g)
+        for e in envs:
+            e.step(a)
+        torch.cuda.synchronize()
+        for f in FIELDS:
+            x, y = getattr(envs[0], f), getattr(envs[1], f)
+            assert torch.equal(x, y) or (x.is_floating_point() and torch.equal(torch.nan_to_num(x, 7.0),
+                                                                               torch.nan_to_num(y, 7.0))), \
+                f"{f} differs at step {t}: max |d| {(x.double() - y.double()).abs().nan_to_num(0).max().item():.3g}"
+        resets += int(envs[0].reset_buf.sum())
+        applied = max(applied, float(envs[0].applied_force.abs().max()))
+    assert resets > 0, "no in-epilogue reset"
+    assert applied > 0, "no external force was applied"
+    envs[0].set_substep_log(False)

@@ -1,6 +1,6 @@
 """Pin the CPU oracle (oracle/t1_oracle.py) against the reference's own outputs (tests/golden/*.npz).
 
-Tolerance: 1e-4 relative (north_star) with a 1e-4 absolute floor for values near zero; exact for
+Tolerance: 1e-4 relative (north_star) with a 1e-6 absolute floor for values near zero; exact for
 bool / integer state.  Obs/priv are compared after clipping, as returned by step().
 """
 import numpy as np

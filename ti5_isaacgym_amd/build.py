@@ -2,6 +2,7 @@
 
     python -m ti5_isaacgym_amd.build [--out=PATH] [--dyn-opt=-O3] [extra hipcc flags]
 """
+import glob
 import os
 import subprocess
 import sys
@@ -15,10 +16,9 @@ UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1"), ("t1policy.hip", "
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
 # guard build: the dynamics unit at -O3 (tests/test_gpu_opt_levels.py keeps it under the fp64 dynamics check)
 OUT_O3 = os.path.join(HERE, "_lib", "var", "libt1env_hip_dyn_o3.so")
-DEPS = [os.path.join(CSRC, f) for f in ("t1env.hip", "t1env_dynamics.hip", "t1_dynamics.h", "t1_common.h", "t1env_post.h",
-                                       "t1_model_conv.h", "t1env_device.h", "t1env_internal.h")] + \
-    [os.path.join(CSRC, "t1policy.hip")] + \
-    [os.path.join(os.path.dirname(HERE), "include", h) for h in ("t1env.h", "t1policy.h")]
+# every source and header the units include (a hand-kept list missed t1env_postphys.h)
+DEPS = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h")) +
+              glob.glob(os.path.join(os.path.dirname(HERE), "include", "*.h")))
 ARCH = os.environ.get("T1ENV_ARCH", "gfx950")
 
 
@@ -39,9 +39,9 @@ def build(force=False, extra=(), out=None, dyn_opt=None):
         obj = os.path.join(os.path.dirname(out), os.path.splitext(src)[0] + ".o")
         procs.append(subprocess.Popen([hipcc, opt, *common, "-c", "-o", obj, os.path.join(CSRC, src)]))
         objs.append(obj)
-    for pr in procs:
-        if pr.wait() != 0:
-            raise subprocess.CalledProcessError(pr.returncode, pr.args)
+    failed = [pr for pr in procs if pr.wait() != 0]   # wait for every unit before reporting a failure
+    if failed:
+        raise subprocess.CalledProcessError(failed[0].returncode, failed[0].args)
     subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs], check=True)
     os.replace(out + ".tmp", out)
     return out

@@ -319,9 +319,10 @@ __global__ __launch_bounds__(BLOCK) void k_reset_all(const DynModel* __restrict_
   wave_atomic_add(B.ep_accum + 24, live ? 1.0f : 0.0f);
   if (!live) return;
   const uint32_t genv = (uint32_t)(C.env_offset + n);
-  // t1env_reset_idx (mask): the between-step key domain, so an env reset in the step that produced A.counter draws
-  // fresh values here (t1_common.h T1_BETWEEN_STEP_SALT)
-  const uint32_t key_ctr = mask ? (A.counter | T1_BETWEEN_STEP_SALT) : A.counter;
+  // t1env_reset_idx (mask), and t1env_reset_all after the first step (env.reset() on a stepped env): the between-step
+  // key domain, so an env reset in the step that produced A.counter draws fresh values here (t1_common.h
+  // T1_BETWEEN_STEP_SALT; oracle T1Oracle.reset)
+  const uint32_t key_ctr = (mask || A.counter > 0) ? (A.counter | T1_BETWEEN_STEP_SALT) : A.counter;
   reset_env(*Mp, C, B, A, n, genv, key_ctr, true);
   resample_commands(C, B, A, n, genv, key_ctr);
 }

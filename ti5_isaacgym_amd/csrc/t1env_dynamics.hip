@@ -240,6 +240,14 @@ __device__ __forceinline__ void epilogue_finalize_parts(const t1env_config& C, c
                                                         const t1env_step_args& A, const FusedArgs& FA, int dyn_blocks,
                                                         int lane) {
   unsigned prev = 0;
+  // Ordering: the increment is RELAXED and no release fence precedes it.  What orders the ep_part rows
+  // before it is gfx950 hardware behaviour, not the HIP memory model: every row element is a relaxed agent-scope
+  // store (global_store ... sc1, which writes through past this XCD's L2 and drops the line), every storing wave ran
+  // s_waitcnt vmcnt(0) after its stores and joined the barrier before lane 0's agent-scope atomic add; the workgroup
+  // whose add returns dyn_blocks - 1 then reads the rows after an agent acquire (buffer_inv sc1).  That is the
+  // hand-off MI355X_MICROARCH.md measures safe on gfx950 / ROCm 7.2 ("one lane of each storing workgroup ... an
+  // agent-scope atomic add", sc1 stores); an agent release here would be buffer_wbl2 sc1 per workgroup, ~1.7-6.5 us
+  // on the step's tail (same guide).  Porting this off gfx950 needs __ATOMIC_RELEASE on the add.
   if (lane == 0) prev = __hip_atomic_fetch_add(FA.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   prev = __shfl(prev, 0, 64);
   if (prev != (unsigned)dyn_blocks - 1u) return;
@@ -734,11 +742,13 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
                    (uint32_t)__float_as_int(E[E_PL][lane]));
   X.gstart = E[E_GS][lane];
   BaseQ bq;
+  float* const ep_row = FA.ep_part + (size_t)blockIdx.x * EP_PART_ROW;  // this workgroup's partial extras sums
 #ifdef T1_WHATIF_EPI_NO_POSTA  // timing-only what-if build: no post_a (no rewards, termination, callback)
   const bool do_reset = false;
   base_quantities_r(X.root, bq);
+  if (PART == POST_A_REWARDS && lane < 25)  // the finaliser still sums every row (agent-scope stores, as wave_sum_store)
+    __hip_atomic_store(ep_row + lane, 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
-  float* const ep_row = FA.ep_part + (size_t)blockIdx.x * EP_PART_ROW;  // this workgroup's partial extras sums
   const bool do_reset = post_a_core<PART>(M, C, B, A, n0, X, bq, PART == POST_A_REWARDS ? ep_row : nullptr);
 #endif
   T1_PROF_MARK(13);

@@ -99,9 +99,20 @@ def build_model(cfg, urdf_path=None):
     return m, tab, default, kp, kd
 
 
+def check_supported(cfg):
+    """Configuration switches the HIP path does not implement raise here, before any device work."""
+    dr = cfg.domain_rand
+    if dr.add_ext_force and dr.ext_torque_max != 0:
+        # the reference applies the drawn torques to the base too (apply_torques, t1_dh_stand_env.py:243-247); the
+        # HIP dynamics applies the base force only (ext_torque_max = 0 in DHT1StandCfg, t1_dh_stand_config.py:201)
+        raise NotImplementedError("domain_rand.ext_torque_max != 0: external base torques are not applied by the HIP "
+                                  "dynamics (t1_dh_stand uses 0)")
+
+
 class T1DHStandEnv(VecEnv):
     def __init__(self, cfg, sim_params=None, physics_engine=None, sim_device="cuda:0", headless=True,
                  env_offset=0, num_envs_total=None, urdf_path=None):
+        check_supported(cfg)
         lib = _lib.load()
         self.cfg = cfg
         self.sim_params = sim_params if sim_params is not None else _SimDt(cfg.sim.dt)
