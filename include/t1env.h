@@ -65,6 +65,14 @@ typedef struct t1env_model {
   float k_contact, d_contact, friction_vs, k_limit, d_limit, gravity;
   float ground_friction, ground_restitution;
   float base_init_state[13];    /* pos(3) quat xyzw(4) linvel(3) angvel(3) -- cfg.init_state */
+  /* self-collision (asset.self_collisions = 0: enabled, t1_dh_stand_config.py:51) between the legs' contact bodies:
+   * the shank collision boxes (t1.urdf:265-272, 625-632) and the feet's ankle-roll STL hulls as their bounding boxes
+   * (t1.urdf:390-398, 750-758), each in its link frame: center (3), half extents (3); order left shank, left foot,
+   * right shank, right foot.  Restitution acts above bounce_threshold (sim.physx.bounce_threshold_velocity,
+   * t1_dh_stand_config.py:171) with the per-env coefficient of DR (restitution_range, :185). */
+  int32_t self_collisions;      /* 1: enabled */
+  float self_box[4][6];
+  float bounce_threshold;       /* [m/s] */
 } t1env_model;
 
 /* Scalar config (DHT1StandCfg values that shape the step; see t1_dh_stand_config.py). */
@@ -171,6 +179,10 @@ typedef struct t1env_buffers {
                                (t1env_reset_all: c % RING); a step without resets carries the previous slot */
   float* ep_accum;          /* (32,) per-step reduction scratch: [0,24) sums over reset envs, [24] count,
                                [25] terrain level sum; zeroed by the library */
+  float* contact_vimp;      /* (N,6) restitution episodes of the contact bodies (left shank, left foot, right shank,
+                               right foot, base-box halves of the left / right leg): the approach speed a body's
+                               current terrain contact began with, 0 when it touches nothing; zeroed at reset
+                               (physics state PhysX keeps inside its contact cache) */
 } t1env_buffers;
 
 /* Per-step host-side schedule (no device->host sync needed to build it). */

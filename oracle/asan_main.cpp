@@ -21,7 +21,7 @@ int main(int argc, char** argv) {
   for (auto& h : hf) h = (int16_t)(rnd() * 40.0f - 20.0f);
   for (int flags = 0; flags < 4; ++flags) {
     std::vector<float> root(N * 13, 0.0f), dof(N * 24, 0.0f), tau(N * 12), bm(N), ls(N * 12, 1.0f), cd(N * 3, 0.0f),
-        arm(N * 12, 0.1f), fr(N, 0.8f), rigid(N * 169), contact(N * 39), ext(N * 3, 0.0f);
+        arm(N * 12, 0.1f), fr(N, 0.8f), rst(N, 0.3f), vimp(N * 6, 0.0f), rigid(N * 169), contact(N * 39), ext(N * 3, 0.0f);
     const float q0[6] = {0.0f, 0.0f, -0.3f, 0.6f, -0.3f, 0.0f};
     for (int n = 0; n < N; ++n) {
       root[n * 13 + 0] = 1.5f + rnd();
@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
       ext[n * 3 + 0] = 100.0f * rnd();
     }
     const int rc = t1dyn_substeps(&model, N, flags, root.data(), dof.data(), tau.data(), bm.data(), ls.data(), cd.data(),
-                                  arm.data(), fr.data(), ext.data(), 0.001f, 20, hf.data(), rows, cols, 0.1f, 0.005f,
+                                  arm.data(), fr.data(), rst.data(), vimp.data(), ext.data(), 0.001f, 20, hf.data(), rows, cols, 0.1f, 0.005f,
                                   1.0f, 2, rigid.data(), contact.data());
     if (rc) return 4;
     for (float v : root)

@@ -28,6 +28,7 @@ class CpuT1Env:
             self.hf = np.zeros((2, 2), np.int16)
             self.tparams = (2, 2, 0.1, 0.005, 0.0, 0)
         self.rigid = np.zeros((num_envs, 13, 13), np.float32)
+        self.vimp = np.zeros((num_envs, 6), np.float32)   # the contact bodies' restitution episodes (t1_dynamics.h)
         self.contact = np.zeros((num_envs, 13, 3), np.float32)
 
     def threads(self):
@@ -37,12 +38,14 @@ class CpuT1Env:
         fp = C.POINTER(C.c_float)
         f = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
         root, dof = f(o.root.copy()), f(o.dof.reshape(self.N, 24).copy())
-        args = [f(torques), f(o.body_mass), f(o.link_mass_scale), f(o.com_disp), f(o.armature), f(o.friction)]
+        args = [f(torques), f(o.body_mass), f(o.link_mass_scale), f(o.com_disp), f(o.armature), f(o.friction),
+                f(o.restitution)]
         ext = f(o.applied_force[:, 0, :]) if o.force_pending else None
         rows, cols, hs, vs, border, mesh = self.tparams
         rc = self.lib.t1dyn_substeps(
             C.byref(self.model), self.N, self.fp64, root.ctypes.data_as(fp), dof.ctypes.data_as(fp),
-            *[a.ctypes.data_as(fp) for a in args], ext.ctypes.data_as(fp) if ext is not None else None,
+            *[a.ctypes.data_as(fp) for a in args], self.vimp.ctypes.data_as(fp),
+            ext.ctypes.data_as(fp) if ext is not None else None,
             C.c_float(0.001), 1, self.hf.ctypes.data_as(C.POINTER(C.c_int16)), rows, cols, C.c_float(hs),
             C.c_float(vs), C.c_float(border), mesh, self.rigid.ctypes.data_as(fp), self.contact.ctypes.data_as(fp))
         assert rc == 0

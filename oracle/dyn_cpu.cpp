@@ -16,11 +16,13 @@ namespace {
 template <typename R>
 void load(const DynModel& M, int n, const float* root, const float* dof, const float* body_mass,
           const float* link_scale, const float* com_disp, const float* armature, const float* friction,
-          EnvParams<R>& P, EnvState<R>& s) {
+          const float* restitution, const float* vimp, EnvParams<R>& P, EnvState<R>& s) {
   P.base.mass = body_mass[n];
   P.base.inertia_scale = P.base.mass / R(M.mass[0]);
   for (int k = 0; k < 3; ++k) P.base.com_disp[k] = com_disp[n * 3 + k];
   P.base.friction = R(0.5) * (R(friction[n]) + R(M.ground_friction));
+  P.base.self_friction = R(friction[n]);
+  P.base.restitution = restitution ? R(restitution[n]) : R(0);
   for (int j = 0; j < ND; ++j) {
     LegParams<R>& L = P.leg[j / 6];
     L.mass[j % 6] = R(M.mass[1 + j]) * link_scale[n * 12 + j];
@@ -36,6 +38,7 @@ void load(const DynModel& M, int n, const float* root, const float* dof, const f
   V3<R> vo = v3<R>(r[7], r[8], r[9]) - cross(w, c0);
   s.w[0] = w.x; s.w[1] = w.y; s.w[2] = w.z; s.vo[0] = vo.x; s.vo[1] = vo.y; s.vo[2] = vo.z;
   for (int j = 0; j < ND; ++j) { s.q[j] = dof[(size_t)n * 24 + 2 * j]; s.qd[j] = dof[(size_t)n * 24 + 2 * j + 1]; }
+  for (int i = 0; i < NVIMP; ++i) s.vimp[i] = vimp ? R(vimp[(size_t)n * NVIMP + i]) : R(0);
 }
 
 template <typename R> struct Writer {
@@ -48,8 +51,9 @@ template <typename R> struct Writer {
 template <typename R>
 int substep_batch(const t1env_model* model, int N, float* root, float* dof, const float* tau, const float* body_mass,
                   const float* link_scale, const float* com_disp, const float* armature, const float* friction,
-                  const float* ext_force, float dt, int nsub, const int16_t* hf, int rows, int cols, float hs, float vs,
-                  float border, int mesh, float* rigid, float* contact, bool split) {
+                  const float* restitution, float* vimp, const float* ext_force, float dt, int nsub, const int16_t* hf,
+                  int rows, int cols, float hs, float vs, float border, int mesh, float* rigid, float* contact,
+                  bool split) {
   DynModel M;
   if (make_dyn_model(model, &M)) return -1;
   Terrain T = make_terrain(hf, rows, cols, mesh, hs, vs, border);
@@ -57,7 +61,7 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
   for (int n = 0; n < N; ++n) {
     EnvParams<R> P;
     EnvState<R> s;
-    load<R>(M, n, root, dof, body_mass, link_scale, com_disp, armature, friction, P, s);
+    load<R>(M, n, root, dof, body_mass, link_scale, com_disp, armature, friction, restitution, vimp, P, s);
     R t[ND];
     for (int j = 0; j < ND; ++j) t[j] = tau[(size_t)n * 12 + j];
     for (int k = 0; k < nsub; ++k) {
@@ -67,6 +71,8 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
     Writer<R> W{root + (size_t)n * 13, rigid ? rigid + (size_t)n * 169 : nullptr, contact ? contact + (size_t)n * 39 : nullptr};
     report(M, T, P, s, W);
     for (int j = 0; j < ND; ++j) { dof[(size_t)n * 24 + 2 * j] = (float)s.q[j]; dof[(size_t)n * 24 + 2 * j + 1] = (float)s.qd[j]; }
+    if (vimp)
+      for (int i = 0; i < NVIMP; ++i) vimp[(size_t)n * NVIMP + i] = (float)s.vimp[i];
   }
   return 0;
 }
@@ -75,17 +81,20 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
 extern "C" {
 // Advance N envs by nsub substeps with constant joint torques (root: Gym layout, COM velocity).
 // flags: bit 0 = fp64, bit 1 = the k_dyn4 split composition (compute_delta_split) instead of compute_delta.
+// restitution: the envs' shape restitution (null: 0); vimp: (N, 6) restitution episodes of the contact bodies, read
+// and updated (null: none carried across calls).
 int t1dyn_substeps(const t1env_model* model, int N, int flags, float* root, float* dof, const float* tau,
                    const float* body_mass, const float* link_scale, const float* com_disp, const float* armature,
-                   const float* friction, const float* ext_force, float dt, int nsub, const int16_t* hf, int rows,
-                   int cols, float hs, float vs, float border, int mesh, float* rigid, float* contact) {
+                   const float* friction, const float* restitution, float* vimp, const float* ext_force, float dt, int nsub,
+                   const int16_t* hf, int rows, int cols, float hs, float vs, float border, int mesh, float* rigid,
+                   float* contact) {
   const bool split = (flags & 2) != 0;
   return (flags & 1) ? substep_batch<double>(model, N, root, dof, tau, body_mass, link_scale, com_disp, armature,
-                                             friction, ext_force, dt, nsub, hf, rows, cols, hs, vs, border, mesh, rigid,
-                                             contact, split)
+                                             friction, restitution, vimp, ext_force, dt, nsub, hf, rows, cols, hs, vs, border,
+                                             mesh, rigid, contact, split)
                      : substep_batch<float>(model, N, root, dof, tau, body_mass, link_scale, com_disp, armature,
-                                            friction, ext_force, dt, nsub, hf, rows, cols, hs, vs, border, mesh, rigid,
-                                            contact, split);
+                                            friction, restitution, vimp, ext_force, dt, nsub, hf, rows, cols, hs, vs, border,
+                                            mesh, rigid, contact, split);
 }
 
 // Solver accelerations in fp64 for one env with internal state (pos, quat, w, v_O, q, qd): returns
@@ -100,6 +109,8 @@ int t1dyn_accel(const t1env_model* model, const double* mass, const double* iner
   P.base.inertia_scale = inertia_scale[0];
   for (int k = 0; k < 3; ++k) P.base.com_disp[k] = com_disp[k];
   P.base.friction = 0.5;
+  P.base.self_friction = 0.5;
+  P.base.restitution = 0.0;
   for (int j = 0; j < ND; ++j) {
     P.leg[j / 6].mass[j % 6] = mass[1 + j];
     P.leg[j / 6].inertia_scale[j % 6] = inertia_scale[1 + j];
@@ -110,6 +121,7 @@ int t1dyn_accel(const t1env_model* model, const double* mass, const double* iner
   for (int i = 0; i < 4; ++i) s.quat[i] = state[3 + i];
   for (int i = 0; i < 3; ++i) { s.w[i] = state[7 + i]; s.vo[i] = state[10 + i]; }
   for (int j = 0; j < ND; ++j) { s.q[j] = state[13 + j]; s.qd[j] = state[25 + j]; }
+  for (int i = 0; i < NVIMP; ++i) s.vimp[i] = 0.0;
   double d[18];
   compute_delta(M, T, P, s, tau, v3<double>(0, 0, 0), 1.0, d);
   V3<double> w{s.w[0], s.w[1], s.w[2]}, v{s.vo[0], s.vo[1], s.vo[2]};

@@ -99,3 +99,147 @@ class Robot:
         if f_base is not None:
             f = f + Jv[0].T @ np.asarray(f_base, float)
         return np.linalg.solve(M, f - h), M
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# One implicit substep WITH contact, written independently of the product's assembly (TEST INFRASTRUCTURE).
+#
+# The product (t1_dynamics.h) folds its contact and joint-limit terms into a tree-sparse LTDL; this restates the
+# same discrete law densely from plain kinematics:
+#   * point Jacobians J_x (velocity of a body-fixed point w.r.t. u = [omega, v_O, qd]) by central differences of
+#     forward kinematics -- no spatial algebra shared with the product;
+#   * terrain: the plane z = 0 (normal +z), contact candidates = the model's contact points below it;
+#   * self-collision: the legs' boxes (model self_box: left shank, left foot, right shank, right foot), every corner of
+#     one box inside another, depth / normal of that box's nearest face; pairs {l, r} x {shank, foot} across the
+#     legs and shank-foot within a leg; each body gets the force at the corner, the other body the reaction;
+#   * the law per contact: normal spring k pen, damper d while approaching (implicit: cn = dt k + d) and,
+#     with a restitution target v_tgt, while separating slower than it (cn = d, f_n += d v_tgt), regularised Coulomb friction ct = mu fn_est / max(|v_t|, v_s) as an implicit tangential
+#     damper: C = cn n n^T + ct (I - n n^T), f = (k pen - cn v_n + d v_tgt) n - ct v_t;
+#   * restitution: each terrain-contact body (shanks, feet, the base box's two halves) keeps the approach speed v_imp
+#     of its contact episode; v_tgt = e v_imp above the bounce threshold, else 0 (self-contacts: 0);
+#   * soft joint limits k_l, d_l (implicit damper when moving further out);
+#   * implicit Euler in the contact / limit velocities with each body's own terms implicit (a self-contact's other
+#     body enters through its current velocity):
+#       (M + dt sum J^T C J + dt diag(c_l)) du = dt (tau - h + sum J^T f + f_limit).
+# ---------------------------------------------------------------------------------------------------------------
+SELF_BODIES = (4, 6, 10, 12)
+
+
+def _box_corners(box):
+    c, h = np.asarray(box[:3], float), np.asarray(box[3:], float)
+    return np.array([c + np.array([sx, sy, sz]) * h for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)])
+
+
+def _inside(box, R, p, x):
+    """x (world) inside the box of a body at (R, p): (depth, outward unit normal of the nearest face) or None"""
+    c, h = np.asarray(box[:3], float), np.asarray(box[3:], float)
+    loc = R.T @ (x - p) - c
+    d = h - np.abs(loc)
+    if np.all(d > 0):
+        k = int(np.argmin(d))
+        return d[k], np.sign(loc[k]) * R[:, k]
+    return None
+
+
+class ContactRobot(Robot):
+    def __init__(self, tab, mass=None, inertia_scale=None, com_disp=(0, 0, 0), armature=None, solver=None,
+                 limits=None):
+        super().__init__(tab, mass, inertia_scale, com_disp, armature)
+        self.tab = tab
+        self.sv = dict(solver)
+        lim = np.asarray(tab["limits"], float) if limits is None else np.asarray(limits, float)
+        self.lo, self.hi = lim[:, 0], lim[:, 1]
+
+    def _points(self, Rs, ps, b, local):
+        return ps[b] + Rs[b] @ local
+
+    def point_jacobian(self, p, R, q, b, local, eps=1e-6):
+        """d x / d u of the body-fixed point `local` of body b (world position x)"""
+        J = np.zeros((3, 18))
+        for k in range(18):
+            e = np.zeros(18)
+            e[k] = 1.0
+            Rp, pp, _ = self.fk(*self._move(p, R, q, e, eps))
+            Rm, pm, _ = self.fk(*self._move(p, R, q, e, -eps))
+            J[:, k] = (self._points(Rp, pp, b, local) - self._points(Rm, pm, b, local)) / (2 * eps)
+        return J
+
+    def contacts(self, p, R, q, u, mu_ground, e_ground, mu_self, e_self, self_collision=True):
+        """[(body, local point, normal, pen, other body's point or None, mu, episode slot or None)] of the state;
+        episode slots: 2 leg + (0 shank, 1 foot), 4 + leg for the base box half the point belongs to"""
+        Rs, ps, _ = self.fk(p, R, q)
+        out = []
+        pts = np.asarray(self.tab["contact_point"], float)
+        for b in range(13):
+            s, n = self.tab["contact_start"][b], self.tab["contact_count"][b]
+            for c in range(s, s + n):
+                x = self._points(Rs, ps, b, pts[c])
+                if x[2] < 0:
+                    slot = 4 + (c - s) * 2 // n if b == 0 else 2 * ((b - 1) // 6) + (1 if (b - 1) % 6 == 5 else 0)
+                    out.append((b, pts[c], np.array([0.0, 0.0, 1.0]), -x[2], None, mu_ground, slot))
+        if self_collision:
+            boxes = dict(zip(SELF_BODIES, self.tab["self_box"]))
+            pairs = [(4, 10), (4, 12), (6, 10), (6, 12), (4, 6), (10, 12)]
+            for a, bb in pairs:
+                for own, oth in ((a, bb), (bb, a)):
+                    for corner in _box_corners(boxes[own]):
+                        x = self._points(Rs, ps, own, corner)
+                        hit = _inside(boxes[oth], Rs[oth], ps[oth], x)
+                        if hit is None:
+                            continue
+                        pen, n = hit
+                        # the corner's body is pushed out along n; the other body gets the reaction at the same point
+                        loc_oth = Rs[oth].T @ (x - ps[oth])
+                        out.append((own, corner, n, pen, (oth, loc_oth), mu_self, None))
+                        out.append((oth, loc_oth, -n, pen, (own, corner), mu_self, None))
+        return out
+
+    def step(self, p, quat, w, v, q, qd, tau, dt, mu_ground, e_ground, mu_self, e_self, f_base=None,
+             self_collision=True, g=9.81, vimp=None):
+        """(du over one substep (u = [omega, v_O, qd]), the restitution episodes after it)"""
+        sv = self.sv
+        k, d, vs = sv["k_contact"], sv["d_contact"], sv["friction_vs"]
+        R = quat_to_R(quat)
+        u = np.concatenate([w, v, qd])
+        acc, Mm = self.accel(p, quat, w, v, q, qd, np.zeros(12), g=g, f_base=f_base)
+        # accel() gives the classical acceleration of the (moving) base origin; the substep's du is taken about the point
+        # O fixed where the base origin is at the substep's start: the spatial acceleration a_O - w x v_O
+        acc = acc.copy()
+        acc[3:6] -= np.cross(w, v)
+        f0 = Mm @ acc                        # the generalized force without tau: J_base^T f_base - h(q, u)
+        A = Mm.copy()
+        rhs = dt * (np.concatenate([np.zeros(6), tau]) + f0)
+        vimp = np.zeros(6) if vimp is None else np.asarray(vimp, float)
+        amax = np.full(6, -1.0)
+        for b, local, n, pen, other, mu, slot in self.contacts(p, R, q, u, mu_ground, e_ground, mu_self, e_self,
+                                                               self_collision):
+            J = self.point_jacobian(p, R, q, b, local)
+            vp = J @ u
+            if other is not None:
+                vp = vp - self.point_jacobian(p, R, q, other[0], other[1]) @ u
+            vn = n @ vp
+            vt = vp - vn * n
+            vtg = 0.0
+            if slot is not None:
+                vtg = e_ground * vimp[slot] if vimp[slot] > sv["bounce_threshold"] else 0.0
+                amax[slot] = max(amax[slot], max(-vn, 0.0))
+            approach, below = vn < 0, 0 <= vn < vtg
+            cn = dt * k + d if approach else (d if below else 0.0)
+            fn_est = k * pen + (-d * vn if approach else (d * (vtg - vn) if below else 0.0))
+            ct = mu * fn_est / max(np.linalg.norm(vt), vs)
+            f = (k * pen - cn * vn + (d * vtg if below else 0.0)) * n - ct * vt
+            C = cn * np.outer(n, n) + ct * (np.eye(3) - np.outer(n, n))
+            A += dt * J.T @ C @ J
+            rhs += dt * J.T @ f
+        for j in range(12):
+            kl, dl = sv["k_limit"], sv["d_limit"]
+            if q[j] < self.lo[j]:
+                cl = dt * kl + dl if qd[j] < 0 else 0.0
+                A[6 + j, 6 + j] += dt * cl
+                rhs[6 + j] += dt * (kl * (self.lo[j] - q[j]) - cl * qd[j])
+            elif q[j] > self.hi[j]:
+                cl = dt * kl + dl if qd[j] > 0 else 0.0
+                A[6 + j, 6 + j] += dt * cl
+                rhs[6 + j] += dt * (kl * (self.hi[j] - q[j]) - cl * qd[j])
+        new = np.where(amax < 0, 0.0, np.where(vimp > 0, vimp, np.maximum(amax, 1e-6)))
+        return np.linalg.solve(A, rhs), new   # du = change of [omega, v_O (spatial, about O), qd]; episodes

@@ -42,6 +42,8 @@ def model():
     for k, v in SOLVER.items():
         setattr(m, k, v)
     m.ground_friction = 0.6
+    from ti5_isaacgym_amd.envs.t1_env import set_self_collision
+    set_self_collision(m, tab, enabled=True, bounce_threshold=0.5)
     return m, tab
 
 
@@ -89,6 +91,8 @@ class Sim:
         self.cd = np.zeros((n, 3), np.float32)
         self.arm = np.full((n, 12), 0.1, np.float32)
         self.fr = np.full(n, 0.8, np.float32)
+        self.rst = np.zeros(n, np.float32)
+        self.vimp = np.zeros((n, 6), np.float32)
         self.rigid = np.zeros((n, 13, 13), np.float32)
         self.contact = np.zeros((n, 13, 3), np.float32)
         self.hf = np.zeros((2, 2), np.int16)
@@ -99,7 +103,8 @@ class Sim:
         rc = self.dyn.t1dyn_substeps(C.byref(self.m), self.n, 1, self.root.ctypes.data_as(fp), self.dof.ctypes.data_as(fp),
                                      tau.ctypes.data_as(fp), self.bm.ctypes.data_as(fp), self.ls.ctypes.data_as(fp),
                                      self.cd.ctypes.data_as(fp), self.arm.ctypes.data_as(fp), self.fr.ctypes.data_as(fp),
-                                     None, C.c_float(dt), nsub, self.hf.ctypes.data_as(C.POINTER(C.c_int16)), 2, 2,
+                                     self.rst.ctypes.data_as(fp), self.vimp.ctypes.data_as(fp), None,
+                                     C.c_float(dt), nsub, self.hf.ctypes.data_as(C.POINTER(C.c_int16)), 2, 2,
                                      C.c_float(0.1), C.c_float(0.005), C.c_float(0.0), 0,
                                      self.rigid.ctypes.data_as(fp), self.contact.ctypes.data_as(fp))
         assert rc == 0
@@ -203,13 +208,15 @@ def _run_flags(dyn, m, flags, root, dof, tau, hf, mesh, nsub):
     cd = rng.uniform(-0.05, 0.05, (n, 3)).astype(np.float32)
     arm = rng.uniform(0.05, 0.5, (n, 12)).astype(np.float32)
     fr = rng.uniform(0.2, 1.3, n).astype(np.float32)
+    rst = rng.uniform(0.0, 0.4, n).astype(np.float32)
     rigid = np.zeros((n, 13, 13), np.float32)
     contact = np.zeros((n, 13, 3), np.float32)
     tau = np.ascontiguousarray(tau, np.float32)
     hf = np.ascontiguousarray(hf)
     rc = dyn.t1dyn_substeps(C.byref(m), n, flags, root.ctypes.data_as(fp), dof.ctypes.data_as(fp),
                             tau.ctypes.data_as(fp), bm.ctypes.data_as(fp), ls.ctypes.data_as(fp), cd.ctypes.data_as(fp),
-                            arm.ctypes.data_as(fp), fr.ctypes.data_as(fp), None, C.c_float(0.001), nsub,
+                            arm.ctypes.data_as(fp), fr.ctypes.data_as(fp), rst.ctypes.data_as(fp),
+                            np.zeros((n, 6), np.float32).ctypes.data_as(fp), None, C.c_float(0.001), nsub,
                             hf.ctypes.data_as(C.POINTER(C.c_int16)), hf.shape[0], hf.shape[1], C.c_float(0.1),
                             C.c_float(0.005), C.c_float(1.0), mesh, rigid.ctypes.data_as(fp), contact.ctypes.data_as(fp))
     assert rc == 0

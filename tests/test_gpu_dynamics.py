@@ -1,5 +1,5 @@
-"""The HIP dynamics kernels (articulated-body solver + PD loop: k_dyn4, the default, and the 2-wave
-k_dynamics) against an independent host replica in fp64.
+"""The HIP dynamics kernel (articulated-body solver + PD loop, k_dyn4, with terrain contact, self-collision and
+restitution) against the same algorithm on the host in fp64.
 
 PhysX itself cannot run anywhere here, so the simulator step is checked against the same algorithm run in
 double precision on the host (oracle/cpu_env.py: numpy oracle PD/post-physics + oracle/dyn_cpu.cpp fp64),
@@ -41,10 +41,9 @@ def _state(root, dof):
             "q": dof[..., 0], "qd": dof[..., 1]}
 
 
-@pytest.fixture(params=["4", "2"], ids=["dyn4", "dyn2"])
-def dyn_waves(request, monkeypatch):
-    monkeypatch.setenv("T1ENV_DYN_WAVES", request.param)  # read by t1env_create
-    return request.param
+@pytest.fixture(params=["4"], ids=["dyn4"])
+def dyn_waves(request):
+    return request.param   # k_dyn4 is the only dynamics kernel since round 3 (the 2-wave k_dynamics was retired)
 
 
 @pytest.mark.parametrize("mesh", ["plane", "trimesh"])
@@ -64,8 +63,10 @@ def test_dynamics_one_step_matches_fp64_host(mesh, dyn_waves):
         root, dof = c64.o.root.copy(), c64.o.dof.copy()
         env.root_states.copy_(torch.from_numpy(root))
         env.dof_state.copy_(torch.from_numpy(dof.reshape(N * 12, 2)))
+        env.contact_vimp.copy_(torch.from_numpy(c64.vimp))   # the restitution episodes are physics state too
         c32.o.root[:] = root
         c32.o.dof[:] = dof
+        c32.vimp[:] = c64.vimp
         env.step(torch.from_numpy(a).to("cuda:0"))
         c64.step(a)
         c32.step(a)

@@ -43,10 +43,9 @@ def _env(n, mesh, fused):
     return env
 
 
-@pytest.fixture(params=["4", "2"], ids=["dyn4", "dyn2"])
-def dyn_waves(request, monkeypatch):
-    monkeypatch.setenv("T1ENV_DYN_WAVES", request.param)  # read by t1env_create
-    return request.param
+@pytest.fixture(params=["4"], ids=["dyn4"])
+def dyn_waves(request):
+    return request.param   # k_dyn4 is the only dynamics kernel since round 3 (the 2-wave k_dynamics was retired)
 
 
 # 16384 envs: k_dyn4 fills every CU, so the history shift runs as its own launch ahead of the fused kernel and

@@ -25,6 +25,7 @@ class Model(C.Structure):
         ("n_contact", i32),
         ("k_contact", f32), ("d_contact", f32), ("friction_vs", f32), ("k_limit", f32), ("d_limit", f32),
         ("gravity", f32), ("ground_friction", f32), ("ground_restitution", f32), ("base_init_state", f32 * 13),
+        ("self_collisions", i32), ("self_box", (f32 * 6) * 4), ("bounce_threshold", f32),
     ]
 
 
@@ -67,6 +68,7 @@ BUFFER_FIELDS = [
     ("link_mass_scale", fp), ("com_disp", fp), ("lag_timestep", i32p), ("dof_lag_timestep", i32p),
     ("imu_lag_timestep", i32p), ("act_hist", fp), ("dof_hist", fp), ("imu_hist", fp), ("env_origins", fp),
     ("terrain_levels", i32p), ("terrain_types", i32p), ("terrain_origins", fp), ("extras", fp), ("ep_accum", fp),
+    ("contact_vimp", fp),
 ]
 
 

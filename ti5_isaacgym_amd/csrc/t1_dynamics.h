@@ -48,6 +48,11 @@ constexpr int T1_POINTS_PER_BODY = 8;
 constexpr int T1_LEG_AXIS[NLEG] = {2, 0, 1, 1, 1, 0};
 
 
+// A self-collision box in its link frame: center and half extents (t1env_model.self_box).
+struct SelfBox {
+  float c[3], h[3];
+};
+
 // Model in the form the kernels consume (built from t1env_model at create time).
 struct DynModel {
   float joint_offset[NB][3];
@@ -64,6 +69,9 @@ struct DynModel {
   float k_contact, d_contact, friction_vs, k_limit, d_limit, gravity;
   float ground_friction, ground_restitution;
   float base_init_state[13];
+  SelfBox self_box[2][2];  // [leg][0 shank, 1 foot]
+  int32_t self_collisions;
+  float bounce_threshold;  // restitution acts on contacts approaching faster than this [m/s]
 };
 
 // Terrain: plane (type 0) or height field sampled like the trimesh the reference builds from it
@@ -86,8 +94,13 @@ inline Terrain make_terrain(const int16_t* h, int32_t rows, int32_t cols, int32_
 
 template <typename R> struct BaseParams {
   R mass, inertia_scale, com_disp[3];
-  R friction;  // combined shape/ground friction coefficient
+  R friction;       // combined shape/ground friction coefficient
+  R restitution;    // the env's shape restitution (DR, restitution_range); ground contacts combine it with the ground's
+  R self_friction;  // the env's shape friction (a self-contact is between two shapes of the same env)
 };
+// PhysX's default combine mode (average) for a robot shape against the ground: friction (load_base_params) and
+// restitution alike (third-party semantics, unpinned)
+template <typename R> T1_HD R ground_restitution(const DynModel& M, R e_env) { return R(0.5) * (e_env + R(M.ground_restitution)); }
 template <typename R> struct LegParams {
   R mass[NLEG], inertia_scale[NLEG], armature[NLEG];
 };
@@ -331,20 +344,43 @@ template <typename R> T1_HD void moments_flush(const PointMoments<R>& P, Sym6<R>
   A.a[sidx(3, 3)] += P.m; A.a[sidx(4, 4)] += P.m; A.a[sidx(5, 5)] += P.m;
 }
 
+// Restitution (PhysX's bounce: sim.physx.bounce_threshold_velocity and the shapes' restitution e).  A contact body
+// keeps the approach speed v_imp its contact episode began with (the fastest approaching point of the episode's
+// first substep; 0 while the body touches nothing, t1env_buffers.contact_vimp).  When v_imp exceeds the threshold,
+// the points' normal damper, which otherwise acts only while they approach, also acts while they separate slower than
+// v_tgt = e v_imp, pushing them out toward that speed -- PhysX's restitution target (exit) velocity, as a set point of
+// the damper in the separation phase:  approaching (v_n < 0): cn = dt k + d, f_n = k pen - cn v_n (unchanged);
+// separating below the target (0 <= v_n < v_tgt): cn = d, f_n = k pen - d (v_n - v_tgt); otherwise no damper.  The
+// compliant law's own rebound (the spring's stored energy) comes on top: the exit speed is at least ~e v_imp.
+// v_tgt = 0 is the plain compliant law.
+template <typename R> T1_HD R restitution_target(const DynModel& M, R e, R vimp) {
+  return vimp > R(M.bounce_threshold) ? e * vimp : R(0);
+}
+// the episode after this substep: amax = the fastest approach among the body's points in contact (< 0: none)
+template <typename R> T1_HD R restitution_episode(R vimp, R amax) {
+  return amax < R(0) ? R(0) : (vimp > R(0) ? vimp : (amax > R(1e-6) ? amax : R(1e-6)));
+}
+
+// One contact point of a body: x (about O), unit normal n pushing the body out, depth pen, the body's spatial velocity
+// Vb, friction mu, restitution target speed vtg; vs = the velocity of the surface it touches at x (zero for the
+// terrain, the other body's point velocity for a self-contact, whose own-side terms are implicit and the other side's
+// motion explicit).  amax (optional): raised to this point's approach speed max(-v_n, 0).
 template <typename R>
-T1_HD void contact_point(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[6], R mu, R dt, Sym6<R>& A,
-                         R g[6], PointMoments<R>& fric) {
+T1_HD void contact_point(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[6], R mu, R vtg, R dt, Sym6<R>& A,
+                         R g[6], PointMoments<R>& fric, V3<R> vs = V3<R>{R(0), R(0), R(0)}, R* amax = nullptr) {
   const R k = R(M.k_contact), d = R(M.d_contact);
   V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
-  V3<R> vp = vo + cross(om, x);
+  V3<R> vp = vo + cross(om, x) - vs;
   R vn = dot(n, vp);
   V3<R> vt = vp - vn * n;
   R vtn = fsqrt(dot(vt, vt));
-  R cn = vn < R(0) ? dt * k + d : R(0);
-  R fn_est = k * pen + (vn < R(0) ? -d * vn : R(0));
+  const bool ap = vn < R(0), rs = !ap && vn < vtg;  // approaching; separating below the restitution target
+  R cn = ap ? dt * k + d : (rs ? d : R(0));
+  R fn_est = k * pen + (ap ? -d * vn : (rs ? d * (vtg - vn) : R(0)));
   R ct = mu * fn_est * rcp(vtn > R(M.friction_vs) ? vtn : R(M.friction_vs));
-  // force at the current velocity (explicit part) f = k pen n - C vp, C = cn nn^T + ct (I - nn^T)
-  V3<R> f = (k * pen - cn * vn) * n - ct * vt;
+  if (amax) *amax = *amax > -vn ? *amax : (-vn > R(0) ? -vn : R(0));
+  // force at the current velocity (explicit part) f = (k pen - cn vn + d vtg) n - ct vt, C = cn nn^T + ct (I - nn^T)
+  V3<R> f = (k * pen - cn * vn + (rs ? d * vtg : R(0))) * n - ct * vt;
   V3<R> tq = cross(x, f);
   g[0] -= dt * tq.x; g[1] -= dt * tq.y; g[2] -= dt * tq.z;
   g[3] -= dt * f.x;  g[4] -= dt * f.y;  g[5] -= dt * f.z;
@@ -376,7 +412,8 @@ __device__ __forceinline__ void pair_acc_zero(PairAcc& P) {
 }
 __device__ __forceinline__ void contact_pair(const DynModel& M, const V3<float> x0, const V3<float> x1, const V3<float> n0,
                                              const V3<float> n1, float pen0, float pen1, bool c0, bool c1,
-                                             const float Vb[6], float mu, float dt, PairAcc& P) {
+                                             const float Vb[6], float mu, float vtg, float dt, PairAcc& P,
+                                             float& amax) {
   const float k = M.k_contact, d = M.d_contact;
   const t1f2 xx = t1f2_of(x0.x, x1.x), xy = t1f2_of(x0.y, x1.y), xz = t1f2_of(x0.z, x1.z);
   const t1f2 nx = t1f2_of(n0.x, n1.x), ny = t1f2_of(n0.y, n1.y), nz = t1f2_of(n0.z, n1.z);
@@ -390,12 +427,17 @@ __device__ __forceinline__ void contact_pair(const DynModel& M, const V3<float> 
   const t1f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
   const float vs = M.friction_vs;
   const float vtn0 = fsqrt(vt2.x), vtn1 = fsqrt(vt2.y);
-  const bool ap0 = vn.x < 0.0f, ap1 = vn.y < 0.0f;  // approaching: implicit normal damping
-  const t1f2 cn = t1f2_of(c0 && ap0 ? dt * k + d : 0.0f, c1 && ap1 ? dt * k + d : 0.0f);
-  const t1f2 fn_est = k * pen + t1f2_of(ap0 ? -d * vn.x : 0.0f, ap1 ? -d * vn.y : 0.0f);
+  // approaching; separating below the restitution target (contact_point)
+  const bool ap0 = vn.x < 0.0f, ap1 = vn.y < 0.0f, rs0 = !ap0 && vn.x < vtg, rs1 = !ap1 && vn.y < vtg;
+  const t1f2 cn = t1f2_of(c0 ? (ap0 ? dt * k + d : (rs0 ? d : 0.0f)) : 0.0f, c1 ? (ap1 ? dt * k + d : (rs1 ? d : 0.0f)) : 0.0f);
+  const t1f2 fn_est = k * pen + t1f2_of(ap0 ? -d * vn.x : (rs0 ? d * (vtg - vn.x) : 0.0f),
+                                        ap1 ? -d * vn.y : (rs1 ? d * (vtg - vn.y) : 0.0f));
   const t1f2 ct = mu * fn_est * t1f2_of(c0 ? rcp(vtn0 > vs ? vtn0 : vs) : 0.0f, c1 ? rcp(vtn1 > vs ? vtn1 : vs) : 0.0f);
-  // force at the current velocity f = (k pen - cn vn) n - ct vt, and its moment about O
-  const t1f2 fs = k * pen - cn * vn;
+  if (c0) amax = fmaxf(amax, fmaxf(-vn.x, 0.0f));
+  if (c1) amax = fmaxf(amax, fmaxf(-vn.y, 0.0f));
+  // force at the current velocity f = (k pen - cn vn + d vtg) n - ct vt, and its moment about O
+  const float dv = d * vtg;
+  const t1f2 fs = k * pen - cn * vn + t1f2_of(c0 && rs0 ? dv : 0.0f, c1 && rs1 ? dv : 0.0f);
   const t1f2 fx = fs * nx - ct * vtx, fy = fs * ny - ct * vty, fz = fs * nz - ct * vtz;
   P.g[0] += dt * (xy * fz - xz * fy);
   P.g[1] += dt * (xz * fx - xx * fz);
@@ -441,7 +483,7 @@ __device__ __forceinline__ void pair_acc_flush(const PairAcc& P, Sym6<float>& A,
 #endif
 template <bool HF, int NP, typename R>
 T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb,
-                           V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
+                           V3<R> base_abs, const R Vb[6], R mu, R vtg, R dt, Sym6<R>& A, R g[6], R& amax) {
   constexpr int CH = NP < T1_CONTACT_BATCH ? NP : T1_CONTACT_BATCH;  // points in flight (bounds live registers)
   static_assert(NP % CH == 0, "contact points per body must be a multiple of the batch");
   PointMoments<R> fric;
@@ -473,7 +515,7 @@ T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, con
         const bool c0 = dz[i] > R(0), c1 = dz[i + 1] > R(0);  // below the surface (the normal's z is positive)
         if (c0 || c1) {
           const V3<R> n0 = terrain_normal<HF>(gxs[i], gys[i]), n1 = terrain_normal<HF>(gxs[i + 1], gys[i + 1]);
-          contact_pair(M, xs[i], xs[i + 1], n0, n1, dz[i] * n0.z, dz[i + 1] * n1.z, c0, c1, Vb, mu, dt, pacc);
+          contact_pair(M, xs[i], xs[i + 1], n0, n1, dz[i] * n0.z, dz[i + 1] * n1.z, c0, c1, Vb, mu, vtg, dt, pacc, amax);
         }
       }
     } else
@@ -483,7 +525,7 @@ T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, con
       for (int i = 0; i < CH; ++i)
         if (dz[i] > R(0)) {  // below the surface (the normal's z is positive)
           const V3<R> n = terrain_normal<HF>(gxs[i], gys[i]);
-          contact_point(M, xs[i], n, dz[i] * n.z, Vb, mu, dt, A, g, fric);
+          contact_point(M, xs[i], n, dz[i] * n.z, Vb, mu, vtg, dt, A, g, fric, V3<R>{R(0), R(0), R(0)}, &amax);
         }
     }
     T1_PROF_MARK(18);
@@ -494,60 +536,12 @@ T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, con
   moments_flush(fric, A);
 }
 
-// The same body contact split into its two phases, for callers that batch the queries of several bodies before any
-// contact math (one memory latency for all of them): contact_query transforms the NP points and queries the
-// terrain, contact_terms accumulates their contact terms into (A, g) exactly as body_contact_np does.
-template <int NP, typename R> struct ContactQuery {
-  V3<R> xs[NP];
-  R dz[NP], gx[NP], gy[NP];
-};
-template <bool HF, int NP, typename R>
-T1_HD void contact_query(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb, V3<R> base_abs,
-                         ContactQuery<NP, R>& Q) {
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int c = c_begin + i;
-    Q.xs[i] = pb + mul(Rb, v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]));
-    const V3<R> X = Q.xs[i] + base_abs;
-    Q.dz[i] = terrain_height<HF>(T, X.x, X.y, Q.gx[i], Q.gy[i]) - X.z;
-  }
-}
-template <bool HF, int NP, typename R>
-T1_HD void contact_terms(const DynModel& M, const ContactQuery<NP, R>& Q, const R Vb[6], R mu, R dt, Sym6<R>& A,
-                         R g[6]) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(T1_SCALAR_CONTACT)
-  if constexpr (std::is_same<R, float>::value && NP % 2 == 0) {
-    PairAcc pacc;
-    pair_acc_zero(pacc);
-#pragma unroll
-    for (int i = 0; i < NP; i += 2) {
-      const bool c0 = Q.dz[i] > R(0), c1 = Q.dz[i + 1] > R(0);
-      if (c0 || c1) {
-        const V3<R> n0 = terrain_normal<HF>(Q.gx[i], Q.gy[i]), n1 = terrain_normal<HF>(Q.gx[i + 1], Q.gy[i + 1]);
-        contact_pair(M, Q.xs[i], Q.xs[i + 1], n0, n1, Q.dz[i] * n0.z, Q.dz[i + 1] * n1.z, c0, c1, Vb, mu, dt, pacc);
-      }
-    }
-    pair_acc_flush(pacc, A, g);
-    return;
-  }
-#endif
-  PointMoments<R> fric;
-  moments_zero(fric);
-#pragma unroll
-  for (int i = 0; i < NP; ++i)
-    if (Q.dz[i] > R(0)) {
-      const V3<R> n = terrain_normal<HF>(Q.gx[i], Q.gy[i]);
-      contact_point(M, Q.xs[i], n, Q.dz[i] * n.z, Vb, mu, dt, A, g, fric);
-    }
-  moments_flush(fric, A);
-}
-
 template <bool HF, typename R>
 T1_HD void body_contact_t(const DynModel& M, const Terrain& T, int c_begin, int c_end, const M3<R>& Rb, V3<R> pb,
-                          V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
+                          V3<R> base_abs, const R Vb[6], R mu, R vtg, R dt, Sym6<R>& A, R g[6], R& amax) {
   // the T1 model: 8 points per contact body (base box split 4 + 4 between the legs)
-  if (c_end - c_begin == 8) return body_contact_np<HF, 8>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
-  if (c_end - c_begin == 4) return body_contact_np<HF, 4>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+  if (c_end - c_begin == 8) return body_contact_np<HF, 8>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
+  if (c_end - c_begin == 4) return body_contact_np<HF, 4>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
   PointMoments<R> fric;
   moments_zero(fric);
   for (int c = c_begin; c < c_end; ++c) {
@@ -556,34 +550,39 @@ T1_HD void body_contact_t(const DynModel& M, const Terrain& T, int c_begin, int 
     V3<R> n;
     R h = terrain_height<HF>(T, X.x, X.y, n);
     R pen = (h - X.z) * n.z;
-    if (pen > R(0)) contact_point(M, x, n, pen, Vb, mu, dt, A, g, fric);
+    if (pen > R(0)) contact_point(M, x, n, pen, Vb, mu, vtg, dt, A, g, fric, V3<R>{R(0), R(0), R(0)}, &amax);
   }
   moments_flush(fric, A);
 }
+// a body's terrain contact (generic layout, host builds) with its restitution episode vimp (updated)
 template <typename R>
 T1_HD void body_contact(const DynModel& M, const Terrain& T, int c_begin, int c_end, const M3<R>& Rb, V3<R> pb,
-                        V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A, R g[6]) {
-  if (T.type == 0) body_contact_t<false>(M, T, c_begin, c_end, Rb, pb, base_abs, Vb, mu, dt, A, g);
-  else body_contact_t<true>(M, T, c_begin, c_end, Rb, pb, base_abs, Vb, mu, dt, A, g);
+                        V3<R> base_abs, const R Vb[6], R mu, R e, R& vimp, R dt, Sym6<R>& A, R g[6]) {
+  const R vtg = restitution_target(M, e, vimp);
+  R amax = R(-1);
+  if (T.type == 0) body_contact_t<false>(M, T, c_begin, c_end, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
+  else body_contact_t<true>(M, T, c_begin, c_end, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
+  vimp = restitution_episode(vimp, amax);
 }
 
 // contact force (world) a body receives at velocity Vb (used for the net-contact-force report)
 template <typename R>
-T1_HD V3<R> point_contact_force(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[6], R mu) {
+T1_HD V3<R> point_contact_force(const DynModel& M, V3<R> x, V3<R> n, R pen, const R Vb[6], R mu, R vtg,
+                                V3<R> vs = V3<R>{R(0), R(0), R(0)}) {
   const R k = R(M.k_contact), d = R(M.d_contact);
   V3<R> om{Vb[0], Vb[1], Vb[2]}, vo{Vb[3], Vb[4], Vb[5]};
-  V3<R> vp = vo + cross(om, x);
+  V3<R> vp = vo + cross(om, x) - vs;
   R vn = dot(n, vp);
   V3<R> vt = vp - vn * n;
   R vtn = fsqrt(dot(vt, vt));
-  R fn = k * pen - (vn < R(0) ? d * vn : R(0));
+  R fn = k * pen - (vn < vtg ? d * (vn - vtg) : R(0));  // approaching, or separating below the restitution target
   fn = fn > R(0) ? fn : R(0);
   R ct = mu * fn * rcp(vtn > R(M.friction_vs) ? vtn : R(M.friction_vs));
   return fn * n - ct * vt;
 }
 template <bool HF, typename R>
 T1_HD V3<R> body_contact_force_t(const DynModel& M, const Terrain& T, int b, const M3<R>& Rb, V3<R> pb,
-                                 V3<R> base_abs, const R Vb[6], R mu) {
+                                 V3<R> base_abs, const R Vb[6], R mu, R vtg) {
   const int c0 = M.contact_start[b], nc = M.contact_count[b];
   V3<R> F = v3<R>(0, 0, 0);
   const V3<R> W = pb + base_abs;
@@ -603,7 +602,7 @@ T1_HD V3<R> body_contact_force_t(const DynModel& M, const Terrain& T, int b, con
     for (int i = 0; i < NP; ++i)
       if (dz[i] > R(0)) {
         const V3<R> n = terrain_normal<HF>(gxs[i], gys[i]);
-        F = F + point_contact_force(M, xs[i], n, dz[i] * n.z, Vb, mu);
+        F = F + point_contact_force(M, xs[i], n, dz[i] * n.z, Vb, mu, vtg);
       }
     return F;
   }
@@ -614,15 +613,172 @@ T1_HD V3<R> body_contact_force_t(const DynModel& M, const Terrain& T, int b, con
     V3<R> n;
     R h = terrain_height<HF>(T, X.x, X.y, n);
     R pen = (h - X.z) * n.z;
-    if (pen > R(0)) F = F + point_contact_force(M, x, n, pen, Vb, mu);
+    if (pen > R(0)) F = F + point_contact_force(M, x, n, pen, Vb, mu, vtg);
   }
   return F;
 }
 template <typename R>
 T1_HD V3<R> body_contact_force(const DynModel& M, const Terrain& T, int b, const M3<R>& Rb, V3<R> pb,
-                               V3<R> base_abs, const R Vb[6], R mu) {
-  return T.type == 0 ? body_contact_force_t<false>(M, T, b, Rb, pb, base_abs, Vb, mu)
-                     : body_contact_force_t<true>(M, T, b, Rb, pb, base_abs, Vb, mu);
+                               V3<R> base_abs, const R Vb[6], R mu, R vtg) {
+  return T.type == 0 ? body_contact_force_t<false>(M, T, b, Rb, pb, base_abs, Vb, mu, vtg)
+                     : body_contact_force_t<true>(M, T, b, Rb, pb, base_abs, Vb, mu, vtg);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Self-collision between the legs' collision bodies (asset.self_collisions = 0 enables it in the reference,
+// t1_dh_stand_config.py:51; PhysX collides every non-adjacent pair of shapes of the articulation).  The bodies that
+// carry shapes are the base box, the shanks and the feet; the base box cannot be reached by a shank or a foot within
+// the joint limits, which leaves the pairs {left, right} x {shank, foot} across the legs and the
+// shank-foot pair within a leg (not adjacent: the ankle-pitch link lies between them).  Volumes: the shank boxes
+// themselves and the foot hulls' bounding boxes (SelfBox).  Contacts: every corner of one box inside the other,
+// with the depth and normal of the nearest face of the box it is in, under the same compliant law as the terrain
+// (contact_point, with the other body's point velocity as the surface velocity): each body's own terms are
+// implicit (folded into its composite like a terrain contact), the other body's motion enters explicitly.
+// ---------------------------------------------------------------------------------------------------
+template <typename R> struct BoxPose {
+  M3<R> Rb;   // the body's (= the box's) rotation, world axes
+  V3<R> c;    // box center about O
+  R h[3];     // half extents
+};
+template <typename R> T1_HD BoxPose<R> box_pose(const SelfBox& b, const M3<R>& Rb, V3<R> pb) {
+  BoxPose<R> P;
+  P.Rb = Rb;
+  P.c = pb + mul(Rb, v3<R>(R(b.c[0]), R(b.c[1]), R(b.c[2])));
+  P.h[0] = R(b.h[0]); P.h[1] = R(b.h[1]); P.h[2] = R(b.h[2]);
+  return P;
+}
+template <typename R> T1_HD V3<R> mat_col(const M3<R>& A, int i) { return v3<R>(A.m[i], A.m[3 + i], A.m[6 + i]); }
+template <typename R> T1_HD R fabs_r(R x) { return x < R(0) ? -x : x; }
+// separating-axis test over the 6 face normals: false when the boxes are certainly apart (the 9 edge-edge axes are
+// not tested, so "may touch" can be true for boxes that an edge axis separates: the corner tests then find nothing)
+template <typename R> T1_HD bool boxes_may_touch(const BoxPose<R>& A, const BoxPose<R>& B) {
+  R C[3][3], t[3];
+  const V3<R> d = B.c - A.c;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const V3<R> ai = mat_col(A.Rb, i);
+    t[i] = dot(ai, d);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) C[i][j] = fabs_r(dot(ai, mat_col(B.Rb, j)));
+  }
+  bool sep = false;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    sep = sep || fabs_r(t[i]) > A.h[i] + B.h[0] * C[i][0] + B.h[1] * C[i][1] + B.h[2] * C[i][2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const R tj = t[0] * dot(mat_col(A.Rb, 0), mat_col(B.Rb, j)) + t[1] * dot(mat_col(A.Rb, 1), mat_col(B.Rb, j)) +
+                 t[2] * dot(mat_col(A.Rb, 2), mat_col(B.Rb, j));
+    sep = sep || fabs_r(tj) > A.h[0] * C[0][j] + A.h[1] * C[1][j] + A.h[2] * C[2][j] + B.h[j];
+  }
+  return !sep;
+}
+// every corner x of box P strictly inside box T: hit(x, n, pen), n the unit normal of T's nearest face (pushing the
+// corner out of T), pen the corner's distance to that face.  The corners are c +- u0 +- u1 +- u2 (u_i = h_i axis_i),
+// and their coordinates in T's frame follow from four matrix-vector products.
+template <typename R, typename Hit> T1_HD void corners_in_box(const BoxPose<R>& P, const BoxPose<R>& T, Hit&& hit) {
+  V3<R> u[3], lu[3];
+  const V3<R> dc = P.c - T.c;
+  const V3<R> lc = v3<R>(dot(mat_col(T.Rb, 0), dc), dot(mat_col(T.Rb, 1), dc), dot(mat_col(T.Rb, 2), dc));
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    u[i] = P.h[i] * mat_col(P.Rb, i);
+    lu[i] = v3<R>(dot(mat_col(T.Rb, 0), u[i]), dot(mat_col(T.Rb, 1), u[i]), dot(mat_col(T.Rb, 2), u[i]));
+  }
+  // a rolled loop: one copy of the hit's contact math per call site (the corner signs are selects, no array index)
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    const R s0 = (k & 1) ? R(1) : R(-1), s1 = (k & 2) ? R(1) : R(-1), s2 = (k & 4) ? R(1) : R(-1);
+    const V3<R> l = lc + s0 * lu[0] + s1 * lu[1] + s2 * lu[2];
+    const R d0 = T.h[0] - fabs_r(l.x), d1 = T.h[1] - fabs_r(l.y), d2 = T.h[2] - fabs_r(l.z);
+    if (d0 > R(0) && d1 > R(0) && d2 > R(0)) {
+      const int ax = (d0 <= d1 && d0 <= d2) ? 0 : (d1 <= d2 ? 1 : 2);
+      const R pen = ax == 0 ? d0 : (ax == 1 ? d1 : d2);
+      const R sg = (ax == 0 ? l.x : (ax == 1 ? l.y : l.z)) < R(0) ? R(-1) : R(1);
+      // the face normal by selects (a runtime index into the rotation's registers would put them in scratch)
+      const V3<R> c0 = mat_col(T.Rb, 0), c1 = mat_col(T.Rb, 1), c2 = mat_col(T.Rb, 2);
+      const V3<R> n = sg * (ax == 0 ? c0 : (ax == 1 ? c1 : c2));
+      hit(P.c + s0 * u[0] + s1 * u[1] + s2 * u[2], n, pen);
+    }
+  }
+}
+template <typename R> T1_HD V3<R> point_velocity(const R V[6], V3<R> x) {
+  return v3<R>(V[3], V[4], V[5]) + cross(v3<R>(V[0], V[1], V[2]), x);
+}
+// the self-contact terms one body (box O, velocity Vo) receives from another (box X, velocity Vx): O's corners in X
+// (normal pushing O out) and X's corners in O (the reaction: normal reversed), accumulated like terrain contacts
+template <typename R>
+T1_HD void self_pair_terms(const DynModel& M, const BoxPose<R>& O, const R Vo[6], const BoxPose<R>& X, const R Vx[6],
+                           R mu, R dt, Sym6<R>& A, R g[6], PointMoments<R>& fric) {
+  if (!boxes_may_touch(O, X)) return;
+  corners_in_box(O, X, [&](V3<R> x, V3<R> n, R pen) {
+    contact_point(M, x, n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
+  });
+  corners_in_box(X, O, [&](V3<R> x, V3<R> n, R pen) {
+    contact_point(M, x, R(-1) * n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
+  });
+}
+// the net self-contact force on body O (the report): the explicit force of each of those contacts
+template <typename R>
+T1_HD V3<R> self_pair_force(const DynModel& M, const BoxPose<R>& O, const R Vo[6], const BoxPose<R>& X, const R Vx[6],
+                            R mu) {
+  V3<R> F = v3<R>(R(0), R(0), R(0));
+  if (!boxes_may_touch(O, X)) return F;
+  corners_in_box(O, X, [&](V3<R> x, V3<R> n, R pen) { F = F + point_contact_force(M, x, n, pen, Vo, mu, R(0), point_velocity(Vx, x)); });
+  corners_in_box(X, O, [&](V3<R> x, V3<R> n, R pen) {
+    F = F + point_contact_force(M, x, R(-1) * n, pen, Vo, mu, R(0), point_velocity(Vx, x));
+  });
+  return F;
+}
+// Pose (rotation, origin about O) and spatial velocity of one contact body, as the kinematics publish them
+template <typename R> struct BodyKin {
+  M3<R> Rb;
+  V3<R> p;
+  R V[6];
+};
+// Self-contact terms of the shank (s = 0) and foot (s = 1) of leg `own` from the contact-body kinematics of that leg
+// (Ko) and of the other leg (Kx): accumulated (contact_point's convention) into C[s] / c[s].  mu: the robot's own
+// shapes' friction (the env's; PhysX's average of two equal values).  Self-contacts keep no restitution episode
+// (v_tgt = 0): a leg striking the other leg faster than the bounce threshold is not given a bounce.
+template <typename R>
+T1_HD void self_terms_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2], const BodyKin<R> (&Kx)[2], R mu, R dt,
+                          Sym6<R> (&C)[2], R (&c)[2][6]) {
+  BoxPose<R> Po[2], Px[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    Po[s] = box_pose(M.self_box[own][s], Ko[s].Rb, Ko[s].p);
+    Px[s] = box_pose(M.self_box[1 - own][s], Kx[s].Rb, Kx[s].p);
+  }
+  // one instantiation per body (a plain loop this large is not unrolled, and its register arrays would go to scratch)
+  auto body = [&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    PointMoments<R> fric;
+    moments_zero(fric);
+    self_pair_terms(M, Po[s], Ko[s].V, Px[0], Kx[0].V, mu, dt, C[s], c[s], fric);
+    self_pair_terms(M, Po[s], Ko[s].V, Px[1], Kx[1].V, mu, dt, C[s], c[s], fric);
+    self_pair_terms(M, Po[s], Ko[s].V, Po[1 - s], Ko[1 - s].V, mu, dt, C[s], c[s], fric);
+    moments_flush(fric, C[s]);
+  };
+  body(std::integral_constant<int, 0>{});
+  body(std::integral_constant<int, 1>{});
+}
+// the net self-contact forces on the shank / foot of leg `own` (report)
+template <typename R>
+T1_HD void self_forces_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2], const BodyKin<R> (&Kx)[2], R mu,
+                           V3<R> (&F)[2]) {
+  BoxPose<R> Po[2], Px[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    Po[s] = box_pose(M.self_box[own][s], Ko[s].Rb, Ko[s].p);
+    Px[s] = box_pose(M.self_box[1 - own][s], Kx[s].Rb, Kx[s].p);
+  }
+  auto body = [&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    F[s] = self_pair_force(M, Po[s], Ko[s].V, Px[0], Kx[0].V, mu) + self_pair_force(M, Po[s], Ko[s].V, Px[1], Kx[1].V, mu) +
+           self_pair_force(M, Po[s], Ko[s].V, Po[1 - s], Ko[1 - s].V, mu);
+  };
+  body(std::integral_constant<int, 0>{});
+  body(std::integral_constant<int, 1>{});
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -636,6 +792,7 @@ template <typename R> struct BaseState {
 };
 template <typename R> struct EnvState : BaseState<R> {
   R q[ND], qd[ND];
+  R vimp[6];  // restitution episodes of the contact bodies (vimp_shank / vimp_foot / vimp_base)
 };
 
 // base quantities of one substep shared by both legs
@@ -728,21 +885,37 @@ template <int AX, typename R> T1_HD void joint_subspace(const DynModel& M, int b
 
 // contact of a body with NP points; `lowest` = its origin height minus its contact radius, `bound` = the
 // terrain_bound at its origin (fetched earlier): skipped when the body cannot reach the terrain
+// terrain: e = the combined restitution, vimp = the body's restitution episode (updated).
 template <int NP, typename R>
 T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, R lowest, int32_t bound_raw, int c_begin,
-                              const M3<R>& Rb, V3<R> pb, V3<R> base_abs, const R Vb[6], R mu, R dt, Sym6<R>& A,
-                              R g[6]) {
-  if (lowest > bound_height<R>(T, bound_raw)) return;
-  if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
-  else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, dt, A, g);
+                              const M3<R>& Rb, V3<R> pb, V3<R> base_abs, const R Vb[6], R mu, R e, R& vimp, R dt,
+                              Sym6<R>& A, R g[6]) {
+  if (lowest > bound_height<R>(T, bound_raw)) {
+    vimp = R(0);  // cannot touch the terrain: no contact episode
+    return;
+  }
+  const R vtg = restitution_target(M, e, vimp);
+  R amax = R(-1);
+  if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
+  else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
+  vimp = restitution_episode(vimp, amax);
 }
+// slots of an env's restitution episodes (t1env_buffers.contact_vimp, EnvState::vimp): the shank and the foot of each
+// leg, and the base box's two halves (one per leg: base_contact_range)
+T1_HD constexpr int vimp_shank(int leg) { return 2 * leg; }
+T1_HD constexpr int vimp_foot(int leg) { return 2 * leg + 1; }
+T1_HD constexpr int vimp_base(int leg) { return 4 + leg; }
+constexpr int NVIMP = 6;
 
 template <int K> using kconst = std::integral_constant<int, K>;
 
+// selfC / selfc: the self-contact terms of the leg's shank [0] and foot [1] (self_terms_leg), or null
+// vimp_leg: the restitution episodes of the leg's shank [0] and foot [1] (updated)
 template <int CM, typename R>
-T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>& P, R mu, const BaseFrame<R>& F,
-                        const R q[NLEG], const R qd[NLEG], const R tau[NLEG], int leg, R dt, LegBlock<R>& out,
-                        Sym6<R>& Ac_up, R gc_up[6]) {
+T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>& P, R mu, R e, R (&vimp_leg)[2],
+                        const BaseFrame<R>& F, const R q[NLEG], const R qd[NLEG], const R tau[NLEG], int leg, R dt,
+                        LegBlock<R>& out, Sym6<R>& Ac_up, R gc_up[6], const Sym6<R>* selfC = nullptr,
+                        const R (*selfc)[6] = nullptr) {
   R sn[NLEG], cs[NLEG], g[NLEG][6];
   M3<R> Rk = F.R0;
   V3<R> pk = v3<R>(0, 0, 0);
@@ -814,12 +987,27 @@ T1_HD void leg_assemble(const DynModel& M, const Terrain& T, const LegParams<R>&
       if constexpr ((CM >> k) & 1) {
         T1_PROF_MARK(2);
         body_contact_fixed<T1_POINTS_PER_BODY>(M, T, lowest[k], bound[k], M.contact_start[b], Rk, pk, F.abs, V, mu,
-                                               dt, Ac, gc);
+                                               e, vimp_leg[k == NLEG - 1 ? 1 : 0], dt, Ac, gc);
+        if (selfC) {
+          constexpr int sfs = k == NLEG - 1 ? 1 : 0;  // shank (k = 3) -> 0, foot (k = 5) -> 1
+          sym_add(Ac, selfC[sfs]);
+#pragma unroll
+          for (int i = 0; i < 6; ++i) gc[i] += selfc[sfs][i];
+        }
         T1_PROF_MARK(3);
       }
     } else {
       const int c0 = M.contact_start[b], nc = M.contact_count[b];
-      if (nc > 0) body_contact(M, T, c0, c0 + nc, Rk, pk, F.abs, V, mu, dt, Ac, gc);
+      if (nc > 0) {  // the T1's contact bodies of a leg are the shank and the foot; others keep no episode
+        R dummy = R(0);
+        R& vi = k == 3 ? vimp_leg[0] : (k == NLEG - 1 ? vimp_leg[1] : dummy);
+        body_contact(M, T, c0, c0 + nc, Rk, pk, F.abs, V, mu, e, vi, dt, Ac, gc);
+      }
+      if (selfC && (k == 3 || k == NLEG - 1)) {  // the T1's self-collision bodies: shank, foot
+        const int sfs = k == NLEG - 1 ? 1 : 0;
+        sym_add(Ac, selfC[sfs]);
+        for (int i = 0; i < 6; ++i) gc[i] += selfc[sfs][i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < 6; ++i) gc[i] += g[k][i];
@@ -945,11 +1133,16 @@ template <typename R> T1_HD void backsub_leg(const LegBlock<R>& lb, const R xb[6
 template <int CM = -1, typename R>
 T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParams<R>& PB, const LegParams<R>& PL,
                             const BaseFrame<R>& F, const R q[NLEG], const R qd[NLEG], const R tau[NLEG], int leg,
-                            R dt, LegBlock<R>& lb, Sym6<R>& Ab, R rb[6]) {
+                            R dt, LegBlock<R>& lb, Sym6<R>& Ab, R rb[6], R (&vimp)[NVIMP],
+                            const Sym6<R>* selfC = nullptr, const R (*selfc)[6] = nullptr) {
   sym_zero(Ab);
   R g[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+  const R e = ground_restitution(M, PB.restitution);
   const int32_t base_bound = CM >= 0 ? terrain_bound_raw_any(T, F.abs.x, F.abs.y) : 0;  // tested after the leg pass
-  leg_assemble<CM>(M, T, PL, PB.friction, F, q, qd, tau, leg, dt, lb, Ab, g);
+  R vl[2] = {vimp[vimp_shank(leg)], vimp[vimp_foot(leg)]};
+  leg_assemble<CM>(M, T, PL, PB.friction, e, vl, F, q, qd, tau, leg, dt, lb, Ab, g, selfC, selfc);
+  vimp[vimp_shank(leg)] = vl[0];
+  vimp[vimp_foot(leg)] = vl[1];
   T1_PROF_MARK(2);
 #pragma unroll
   for (int i = 0; i < 6; ++i) rb[i] = -g[i];
@@ -960,9 +1153,11 @@ T1_HD void leg_contribution(const DynModel& M, const Terrain& T, const BaseParam
   R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
   if constexpr (CM >= 0) {
     body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - R(M.contact_radius[0]), base_bound, cb, F.R0,
-                                               v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
+                                               v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, e, vimp[vimp_base(leg)], dt,
+                                               Ab, gw);
   } else {
-    if (ce > cb) body_contact(M, T, cb, ce, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, dt, Ab, gw);
+    if (ce > cb)
+      body_contact(M, T, cb, ce, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, PB.friction, e, vimp[vimp_base(leg)], dt, Ab, gw);
   }
 #pragma unroll
   for (int i = 0; i < 6; ++i) rb[i] -= gw[i];
@@ -1135,6 +1330,51 @@ T1_HD void leg_contact_kinematics(const DynModel& M, const BaseFrame<R>& F, cons
   fwd(kconst<5>{});
 }
 
+// one leg's contact-body kinematics (shank [0], foot [1]) from its joint state
+template <typename R>
+T1_HD void leg_body_kinematics(const DynModel& M, const BaseFrame<R>& F, const R q[NLEG], const R qd[NLEG], int leg,
+                               BodyKin<R> (&K)[2]) {
+  leg_contact_kinematics<T1_LEG_CONTACT_MASK>(M, F, q, qd, leg, [&](auto kc, const M3<R>& Rk, V3<R> pk, const R* V) {
+    constexpr int i = decltype(kc)::value == NLEG - 1 ? 1 : 0;
+    K[i].Rb = Rk;
+    K[i].p = pk;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) K[i].V[j] = V[j];
+  });
+}
+// both legs' contact-body kinematics (shank [0], foot [1]) from the env's joint state
+template <typename R>
+T1_HD void contact_body_kinematics(const DynModel& M, const BaseFrame<R>& F, const R q[ND], const R qd[ND],
+                                   BodyKin<R> (&K)[2][2]) {
+  for (int leg = 0; leg < 2; ++leg)
+    leg_contact_kinematics<T1_LEG_CONTACT_MASK>(M, F, q + 6 * leg, qd + 6 * leg, leg,
+                                                [&](auto kc, const M3<R>& Rk, V3<R> pk, const R* V) {
+                                                  constexpr int i = decltype(kc)::value == NLEG - 1 ? 1 : 0;
+                                                  K[leg][i].Rb = Rk;
+                                                  K[leg][i].p = pk;
+                                                  for (int j = 0; j < 6; ++j) K[leg][i].V[j] = V[j];
+                                                });
+}
+// self-contact terms of all four contact bodies [leg][shank, foot] (zero when self-collision is off)
+template <typename R> struct SelfTerms {
+  Sym6<R> C[2][2];
+  R c[2][2][6];
+};
+template <typename R>
+T1_HD void self_terms_env(const DynModel& M, const BaseFrame<R>& F, const R q[ND], const R qd[ND],
+                          const BaseParams<R>& PB, R dt, SelfTerms<R>& S) {
+  for (int l = 0; l < 2; ++l)
+    for (int i = 0; i < 2; ++i) {
+      sym_zero(S.C[l][i]);
+      for (int j = 0; j < 6; ++j) S.c[l][i][j] = R(0);
+    }
+  if (!M.self_collisions) return;
+  BodyKin<R> K[2][2];
+  contact_body_kinematics(M, F, q, qd, K);
+  for (int leg = 0; leg < 2; ++leg)
+    self_terms_leg(M, leg, K[leg], K[1 - leg], PB.self_friction, dt, S.C[leg], S.c[leg]);
+}
+
 // backward pass (leaf to root) without contact and without the joint torque: D0, H0, F0 = Bl, r0 and the
 // contact-free leg composite; stores each S_k for leg_apply_contacts
 template <typename R>
@@ -1279,7 +1519,7 @@ T1_HD void integrate_leg(const DynModel& M, int leg, R q[NLEG], R qd[NLEG], cons
 // about the fixed point O), qd] over dt, including implicit contact / joint-limit terms.
 // ---------------------------------------------------------------------------------------------------
 template <typename R>
-T1_HD void compute_delta(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s,
+T1_HD void compute_delta(const DynModel& M, const Terrain& T, const EnvParams<R>& P, EnvState<R>& s,
                          const R tau[ND], V3<R> ext_f, R dt, R delta[6 + ND]) {
   BaseFrame<R> F;
   base_frame(s, F);
@@ -1290,10 +1530,13 @@ T1_HD void compute_delta(const DynModel& M, const Terrain& T, const EnvParams<R>
 #pragma unroll
   for (int i = 0; i < 6; ++i) rb[i] = -gc[i];
   LegBlock<R> lb[2];
+  SelfTerms<R> S;
+  self_terms_env(M, F, s.q, s.qd, P.base, dt, S);
   for (int leg = 0; leg < 2; ++leg) {
     Sym6<R> Ab;
     R r[6];
-    leg_contribution(M, T, P.base, P.leg[leg], F, s.q + 6 * leg, s.qd + 6 * leg, tau + 6 * leg, leg, dt, lb[leg], Ab, r);
+    leg_contribution(M, T, P.base, P.leg[leg], F, s.q + 6 * leg, s.qd + 6 * leg, tau + 6 * leg, leg, dt, lb[leg], Ab, r,
+                     s.vimp, M.self_collisions ? S.C[leg] : nullptr, S.c[leg]);
     sym_add(Ac, Ab);
     for (int i = 0; i < 6; ++i) rb[i] += r[i];
   }
@@ -1307,7 +1550,7 @@ T1_HD void compute_delta(const DynModel& M, const Terrain& T, const EnvParams<R>
 // (leg_apply_contacts), the elimination, and the base-box contact share of the leg; summed base block, solve,
 // back-substitution.  Host builds run it to check the split algebra against compute_delta (tests/test_dynamics.py).
 template <typename R>
-T1_HD void compute_delta_split(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s,
+T1_HD void compute_delta_split(const DynModel& M, const Terrain& T, const EnvParams<R>& P, EnvState<R>& s,
                                const R tau[ND], V3<R> ext_f, R dt, R delta[6 + ND]) {
   constexpr int KS = 3, KF = 5;
   static_assert(T1_LEG_CONTACT_MASK == ((1 << KS) | (1 << KF)), "split composition assumes shank + foot contacts");
@@ -1320,7 +1563,9 @@ T1_HD void compute_delta_split(const DynModel& M, const Terrain& T, const EnvPar
 #pragma unroll
   for (int i = 0; i < 6; ++i) rb[i] = -gc[i];
   LegBlock<R> lb[2];
-  const R mu = P.base.friction;
+  const R mu = P.base.friction, e = ground_restitution(M, P.base.restitution);
+  SelfTerms<R> S;
+  self_terms_env(M, F, s.q, s.qd, P.base, dt, S);
   for (int leg = 0; leg < 2; ++leg) {
     const R* q = s.q + 6 * leg;
     const R* qd = s.qd + 6 * leg;
@@ -1343,11 +1588,12 @@ T1_HD void compute_delta_split(const DynModel& M, const Terrain& T, const EnvPar
     R cc[2][6];
     for (int i = 0; i < 2; ++i) {
       const int b = 1 + 6 * leg + (i ? KF : KS);
-      sym_zero(Cc[i]);
-      for (int j = 0; j < 6; ++j) cc[i][j] = R(0);
+      Cc[i] = S.C[leg][i];  // the self-contact terms (zero without self-collision), then the terrain's
+      for (int j = 0; j < 6; ++j) cc[i][j] = S.c[leg][i][j];
       const int32_t bound = terrain_bound_raw_any(T, pc[i].x + F.abs.x, pc[i].y + F.abs.y);
       body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pc[i].z + F.abs.z - R(M.contact_radius[b]), bound,
-                                             M.contact_start[b], Rc[i], pc[i], F.abs, Vc[i], mu, dt, Cc[i], cc[i]);
+                                             M.contact_start[b], Rc[i], pc[i], F.abs, Vc[i], mu, e,
+                                             s.vimp[i ? vimp_foot(leg) : vimp_shank(leg)], dt, Cc[i], cc[i]);
     }
     leg_apply_contacts<KS, KF>(Cc[0], cc[0], Cc[1], cc[1], tau + 6 * leg, dt, st, lb[leg], Ab, g6);
     R r[6];
@@ -1362,7 +1608,7 @@ T1_HD void compute_delta_split(const DynModel& M, const Terrain& T, const EnvPar
     sym_zero(Cb);
     const int32_t bound = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
     body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - R(M.contact_radius[0]), bound, cb, F.R0,
-                                               v3<R>(0, 0, 0), F.abs, F.V0, mu, dt, Cb, gw);
+                                               v3<R>(0, 0, 0), F.abs, F.V0, mu, e, s.vimp[vimp_base(leg)], dt, Cb, gw);
     sym_add(Ac, Ab);
     sym_add(Ac, Cb);
 #pragma unroll
@@ -1389,7 +1635,7 @@ T1_HD void substep(const DynModel& M, const Terrain& T, const EnvParams<R>& P, E
 // ---------------------------------------------------------------------------------------------------
 template <typename R, typename Writer>
 T1_HD void report_base(const DynModel& M, const Terrain& T, const BaseParams<R>& P, const BaseState<R>& s,
-                       const BaseFrame<R>& F, Writer& W) {
+                       const BaseFrame<R>& F, Writer& W, const R vimp_b[2]) {
   V3<R> c0 = base_com(M, P, F.R0);
   V3<R> vcom = v3<R>(s.vo[0], s.vo[1], s.vo[2]) + cross(v3<R>(s.w[0], s.w[1], s.w[2]), c0);
   R body[13];
@@ -1399,11 +1645,15 @@ T1_HD void report_base(const DynModel& M, const Terrain& T, const BaseParams<R>&
   body[10] = s.w[0]; body[11] = s.w[1]; body[12] = s.w[2];
   W.root(body);
   W.rigid(0, body);
-  W.contact(0, body_contact_force(M, T, 0, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, P.friction));
+  // the base box's halves keep separate episodes; the report uses the stronger set point of the two
+  const R e = ground_restitution(M, P.restitution);
+  const R vt0 = restitution_target(M, e, vimp_b[0]), vt1 = restitution_target(M, e, vimp_b[1]);
+  W.contact(0, body_contact_force(M, T, 0, F.R0, v3<R>(0, 0, 0), F.abs, F.V0, P.friction, vt0 > vt1 ? vt0 : vt1));
 }
+// fself: the self-contact forces on the leg's shank [0] and foot [1] (self_forces_leg), added to their net force
 template <typename R, typename Writer>
-T1_HD void report_leg(const DynModel& M, const Terrain& T, R mu, const BaseFrame<R>& F, const R q[NLEG],
-                      const R qd[NLEG], int leg, Writer& W) {
+T1_HD void report_leg(const DynModel& M, const Terrain& T, R mu, R e, const R vimp_leg[2], const BaseFrame<R>& F,
+                      const R q[NLEG], const R qd[NLEG], int leg, Writer& W, const V3<R>* fself = nullptr) {
   BodyState<R> B[NLEG];
   leg_fk(M, leg, F.R0, q, B);
   R V[6];
@@ -1424,16 +1674,31 @@ T1_HD void report_leg(const DynModel& M, const Terrain& T, R mu, const BaseFrame
     R out[13] = {B[k].p.x + F.abs.x, B[k].p.y + F.abs.y, B[k].p.z + F.abs.z, qb[0], qb[1], qb[2], qb[3],
                  vc.x, vc.y, vc.z, om.x, om.y, om.z};
     W.rigid(b, out);
-    W.contact(b, M.contact_count[b] > 0 ? body_contact_force(M, T, b, B[k].Rot, B[k].p, F.abs, V, mu)
-                                        : v3<R>(0, 0, 0));
+    const R vtg = restitution_target(M, e, k == 3 ? vimp_leg[0] : (k == NLEG - 1 ? vimp_leg[1] : R(0)));
+    V3<R> fc = M.contact_count[b] > 0 ? body_contact_force(M, T, b, B[k].Rot, B[k].p, F.abs, V, mu, vtg) : v3<R>(0, 0, 0);
+    if (fself && (k == 3 || k == NLEG - 1)) fc = fc + fself[k == NLEG - 1 ? 1 : 0];
+    W.contact(b, fc);
   }
 }
 template <typename R, typename Writer>
 T1_HD void report(const DynModel& M, const Terrain& T, const EnvParams<R>& P, const EnvState<R>& s, Writer& W) {
   BaseFrame<R> F;
   base_frame(s, F);
-  report_base(M, T, P.base, s, F, W);
-  for (int leg = 0; leg < 2; ++leg) report_leg(M, T, P.base.friction, F, s.q + 6 * leg, s.qd + 6 * leg, leg, W);
+  const R vb[2] = {s.vimp[vimp_base(0)], s.vimp[vimp_base(1)]};
+  report_base(M, T, P.base, s, F, W, vb);
+  V3<R> fs[2][2];
+  for (int l = 0; l < 2; ++l) fs[l][0] = fs[l][1] = v3<R>(R(0), R(0), R(0));
+  if (M.self_collisions) {
+    BodyKin<R> K[2][2];
+    contact_body_kinematics(M, F, s.q, s.qd, K);
+    for (int leg = 0; leg < 2; ++leg)
+      self_forces_leg(M, leg, K[leg], K[1 - leg], P.base.self_friction, fs[leg]);
+  }
+  const R e = ground_restitution(M, P.base.restitution);
+  for (int leg = 0; leg < 2; ++leg) {
+    const R vl[2] = {s.vimp[vimp_shank(leg)], s.vimp[vimp_foot(leg)]};
+    report_leg(M, T, P.base.friction, e, vl, F, s.q + 6 * leg, s.qd + 6 * leg, leg, W, fs[leg]);
+  }
 }
 
 }  // namespace t1

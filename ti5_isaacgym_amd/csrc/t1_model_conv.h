@@ -60,6 +60,15 @@ inline const char* make_dyn_model(const t1env_model* model, DynModel* dm) {
   dm->k_limit = model->k_limit; dm->d_limit = model->d_limit; dm->gravity = model->gravity;
   dm->ground_friction = model->ground_friction; dm->ground_restitution = model->ground_restitution;
   for (int i = 0; i < 13; ++i) dm->base_init_state[i] = model->base_init_state[i];
+  dm->self_collisions = model->self_collisions != 0;
+  for (int i = 0; i < 4; ++i)
+    for (int k = 0; k < 3; ++k) {
+      dm->self_box[i / 2][i % 2].c[k] = model->self_box[i][k];
+      dm->self_box[i / 2][i % 2].h[k] = model->self_box[i][3 + k];
+      if (dm->self_collisions && !(model->self_box[i][3 + k] > 0.0f)) return "self_box half extents must be positive";
+    }
+  dm->bounce_threshold = model->bounce_threshold;
+  if (!(dm->bounce_threshold >= 0.0f)) return "bounce_threshold must be >= 0";
   return nullptr;
 }
 

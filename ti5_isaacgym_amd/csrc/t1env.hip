@@ -426,8 +426,6 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
         hipSuccess) cus = 256;
     e->dyn.cus = cus;
     e->dyn.waves = t1_dyn_waves_default();
-    if (const char* w = getenv("T1ENV_DYN_WAVES"))
-      if (atoi(w) == 2 || atoi(w) == 4) e->dyn.waves = atoi(w);
     e->dyn.shift_blocks = 0;
     if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))  // > 0: shift workgroups in the launch; -1: stand-alone shift
       if (atoi(sb) > 0 || atoi(sb) == -1) e->dyn.shift_blocks = atoi(sb);
@@ -598,7 +596,6 @@ int t1env_set_substep_log(t1env* e, const t1env_substep_log* log) {
     return 0;
   }
   if (!log->root || !log->dof || !log->torque) return fail(T1ENV_E_ARG, "t1env_set_substep_log: null buffer");
-  if (e->dyn.waves != 4) return fail(T1ENV_E_STATE, "t1env_set_substep_log: the log is written by k_dyn4 only");
   e->log = SubLog{log->root, log->dof, log->torque};
   e->log_on = 1;
   return 0;

@@ -36,6 +36,8 @@ __device__ __forceinline__ void load_base_params(const DynModel& M, const t1env_
 #pragma unroll
   for (int i = 0; i < 3; ++i) P.com_disp[i] = B.com_disp[n * 3 + i];
   P.friction = 0.5f * (B.friction[n] + M.ground_friction);
+  P.self_friction = B.friction[n];
+  P.restitution = B.restitution[n];
 }
 __device__ __forceinline__ void load_leg_params(const DynModel& M, const t1env_buffers& B, int n, int j0,
                                                 LegParams<float>& P) {

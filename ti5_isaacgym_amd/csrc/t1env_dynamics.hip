@@ -54,22 +54,19 @@ __device__ __forceinline__ void t1_prof_end() {
 using namespace t1;
 
 // ---------------------------------------------------------------------------------------------------
-// Two kernels share the launch layout: ceil(N/64) dynamics workgroups of 64 envs, then history-shift
-// workgroups (blockIdx >= dyn_blocks, t1env_device.h).  The dynamics fill at most half the CUs at 8192 envs,
-// so the HBM-bound shift streams on the rest of the chip inside the same launch -- no second stream, no
-// cross-stream events on the step path.
+// The launch: ceil(N/64) dynamics workgroups of 64 envs, then history-shift workgroups (blockIdx >= dyn_blocks,
+// t1env_device.h).  The dynamics fill at most half the CUs at 8192 envs, so the HBM-bound shift streams on the rest
+// of the chip inside the same launch -- no second stream, no cross-stream events on the step path.
 //
-//   k_dynamics (2 waves / 64 envs): wave 0 runs every env's left leg, wave 1 the right leg (the leg index is
-//     wave-uniform, so model reads are scalar loads).  Per substep each wave eliminates its leg into a
-//     27-float base-block contribution (t1_dynamics.h leg_contribution), the two contributions meet in LDS
-//     (double-buffered by substep parity -> one barrier per substep), and both waves solve the 6x6 base system
-//     redundantly, so the base state stays bit-identical in both without further exchange.
-//   k_dyn4 (4 waves / 64 envs, the default): waves 0/1 are the leg waves as above, but run the articulated-
-//     body passes without contact (leg_forward_nc / leg_backward_nc); waves 2/3 are their contact helpers:
-//     from the poses the leg wave publishes after its forward pass they compute the shank / foot contact
-//     terms while the leg wave runs its backward pass, then the base-box contact terms while the leg wave
-//     folds the contact terms in (leg_apply_contacts) and eliminates.  Three barriers per substep; all four
-//     SIMDs of the CU work on the same 64 envs (+34 % env-steps/s over k_dynamics at 8192 envs).
+//   k_dyn4 (4 waves / 64 envs): waves 0/1 are the leg waves -- wave 0 runs every env's left leg, wave 1 the right
+//     leg (the leg index is wave-uniform, so model reads are scalar loads) -- running the articulated-body passes
+//     without contact (leg_forward_nc / leg_backward_nc); waves 2/3 are their contact helpers: from the substep
+//     state the leg waves publish they compute the shank / foot contact terms (terrain and self-collision) while
+//     the leg wave runs its passes, then the base-box contact terms while the leg wave folds the contact terms in
+//     (leg_apply_contacts) and eliminates its leg into a 27-float base-block contribution.  The contributions meet
+//     in LDS and both leg waves solve the 6x6 base system redundantly, so the base state stays bit-identical in
+//     both.  Three barriers per substep; all four SIMDs of the CU work on the same 64 envs.  (Round 1's 2-wave
+//     k_dynamics, with contacts inside the leg waves, ran 34 % slower and was retired in round 3.)
 //
 // FUSED (t1env_step on every step that needs no host decision between the phases): the whole env step is
 // one launch.  After its dynamics, wave 0 of each dynamics workgroup runs post-physics for its 64 envs
@@ -88,16 +85,12 @@ using namespace t1;
 //     placement-independent, and without an L2 write-back fence (buffer_wbl2 per unit cost the concurrently
 //     running dynamics ~8 %).
 // ---------------------------------------------------------------------------------------------------
-// The contact helper waves compute the shank / foot poses themselves from the substep state the leg wave publishes
+// The contact helper waves compute the shank / foot poses themselves from the substep state the leg waves publish
 // after integrating (leg_contact_kinematics), so their contact terms start in parallel with the leg's forward pass
-// (+2.5 % env-steps/s at 8192 envs, r02ab).  -DT1_HELPER_POSES_FROM_LEG: the previous schedule (poses published by
-// the leg's forward pass), for A/B.
-#ifndef T1_HELPER_POSES_FROM_LEG
-#define T1_HELPER_KIN 1
-#endif
+// (+2.5 % env-steps/s at 8192 envs, r02ab); with self-collision on, each helper also computes the other leg's
+// contact-body kinematics from that leg's published state.
 
 constexpr int DYN_ENVS = 64;
-constexpr int DYN_BLOCK = 2 * DYN_ENVS;
 constexpr int D4_BLOCK = 4 * DYN_ENVS;
 constexpr int XCH = 27;  // Sym6 (21) + rhs (6)
 constexpr int SHIFT_UNIT = 8;  // rows per shift/zeroing unit (a multiple of 4: unit boundaries are 16-B aligned)
@@ -169,27 +162,6 @@ __device__ __forceinline__ void shift_workgroup(const ShiftArgs& S, const FusedA
   }
 }
 
-__device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const t1env_buffers& B,
-                                                    const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
-                                                    int dyn_blocks, int lane, bool do_reset, bool active, int n);
-
-// The fused step's post-physics for one dynamics workgroup's 64 envs, run by one whole wave after the
-// dynamics outputs of the workgroup are in memory (t1env_postphys.h: the same code as k_post_a / k_post_b),
-// then the reset-row handoff and the extras finalisation.
-__device__ __forceinline__ void fused_epilogue(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
-                                               const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
-                                               int dyn_blocks, int lane) {
-  const int N = C.num_envs;
-  const int n0 = blockIdx.x * DYN_ENVS + lane;
-  const bool active = n0 < N;
-  const int n = active ? n0 : N - 1;
-  const bool do_reset = post_a_env(M, C, B, A, n0);
-  T1_PROF_MARK(13);
-  if (active) post_b_env(M, C, B, A, n, do_reset, do_reset);
-  T1_PROF_MARK(14);
-  fused_epilogue_tail(C, B, A, S, FA, dyn_blocks, lane, do_reset, active, n);
-}
-
 // after post-physics: the terrain-level sum, the reset-row handoff and the extras finalisation
 __device__ __forceinline__ void epilogue_handoff(const t1env_config& C, const ShiftArgs& S, const FusedArgs& FA, int lane,
                                                  bool do_reset, bool active) {
@@ -215,21 +187,6 @@ __device__ __forceinline__ void epilogue_handoff(const t1env_config& C, const Sh
     const int l = __ffsll((unsigned long long)todo) - 1;
     todo &= todo - 1;
     zero_unit_resets(S, blockIdx.x * (DYN_ENVS / SHIFT_UNIT) + l, __shfl(w, l, 64), lane, DYN_ENVS);
-  }
-}
-// The last dynamics workgroup to finish finalises the step's extras.  Only atomics cross workgroups here (the
-// ep_accum sums and this counter; agent-scope atomics are performed past the L2s), so once every atomic of the
-// workgroup has completed (the caller's s_waitcnt, and a barrier when two waves contributed) the increment is
-// ordered after them; the finaliser reads ep_accum through atomics as well.
-__device__ __forceinline__ void epilogue_finalize(const t1env_config& C, const t1env_buffers& B,
-                                                  const t1env_step_args& A, const FusedArgs& FA, int dyn_blocks,
-                                                  int lane) {
-  unsigned prev = 0;
-  if (lane == 0) prev = __hip_atomic_fetch_add(FA.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  prev = __shfl(prev, 0, 64);
-  if (prev == (unsigned)dyn_blocks - 1u) {
-    finalize_extras(B, C, (int)((A.counter + 1u) % T1ENV_EXTRAS_RING));
-    if (lane == 0) __hip_atomic_store(FA.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 // k_dyn4's finaliser: every dynamics workgroup stored one row of partial sums (FusedArgs::ep_part, agent-scope
@@ -293,16 +250,6 @@ __device__ __forceinline__ void epilogue_finalize_parts(const t1env_config& C, c
   if (lane == 0) __hip_atomic_store(FA.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void fused_epilogue_tail(const t1env_config& C, const t1env_buffers& B,
-                                                    const t1env_step_args& A, const ShiftArgs& S, const FusedArgs& FA,
-                                                    int dyn_blocks, int lane, bool do_reset, bool active, int n) {
-  if (C.custom_origins) wave_atomic_add(B.ep_accum + 25, active ? (float)B.terrain_levels[n] : 0.0f);
-  epilogue_handoff(C, S, FA, lane, do_reset, active);
-  __builtin_amdgcn_s_waitcnt(0);
-  epilogue_finalize(C, B, A, FA, dyn_blocks, lane);
-  T1_PROF_MARK(15);
-}
-
 // per-leg setup shared by both kernels: clipped actions into the step's action slot, sensor-lag capture
 // slots, per-env parameters, base state and the leg's joint state
 struct LegSetup {
@@ -343,114 +290,6 @@ __device__ __forceinline__ LegSetup leg_setup(const DynModel& M, const t1env_con
   return L;
 }
 
-// the step's outputs of one leg wave (Gym-shaped root / rigid / contact / dof / torque buffers)
-__device__ __forceinline__ void leg_report(const DynModel& M, const Terrain& T, const t1env_buffers& B,
-                                           const BaseParams<float>& PB, const BaseState<float>& sb,
-                                           const float q[NLEG], const float qd[NLEG], const float tau[NLEG], int n,
-                                           int leg, int j0) {
-  BaseFrame<float> F;
-  base_frame(sb, F);
-  DevWriter W{B.root_states + (size_t)n * 13, B.rigid_state + (size_t)n * 169, B.contact_forces + (size_t)n * 39};
-  if (leg == 0) report_base(M, T, PB, sb, F, W);
-  report_leg(M, T, PB.friction, F, q, qd, leg, W);
-#pragma unroll
-  for (int k = 0; k < NLEG; ++k) {
-    B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
-    B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
-    B.torques[n * 12 + j0 + k] = tau[k];
-  }
-}
-
-// HF: height-field terrain (mesh heightfield/trimesh) or plane; one instantiation each so the contact code
-// of the other terrain kind is folded away (it is uniform per launch).
-template <bool HF, bool FUSED>
-__global__ __launch_bounds__(DYN_BLOCK) void k_dynamics(const DynModel* __restrict__ Mp,
-                                                        const t1env_config* __restrict__ Cp, t1env_buffers B,
-                                                        Terrain Tin, const float* __restrict__ actions,
-                                                        t1env_step_args A, ShiftArgs S, int dyn_blocks,
-                                                        FusedArgs FA, SubLog) {
-  __shared__ float xch[2][2][XCH][DYN_ENVS];  // [substep parity][leg][value][env]
-  if ((int)blockIdx.x >= dyn_blocks) {
-    shift_workgroup<FUSED, DYN_BLOCK>(S, FA, Cp->num_envs, blockIdx.x - dyn_blocks, gridDim.x - dyn_blocks,
-                                      reinterpret_cast<uint32_t*>(&xch[0][0][0][0]));
-    return;
-  }
-  Terrain T = Tin;
-  T.type = HF ? 2 : 0;
-  const t1env_config& C = *Cp;
-  const DynModel& M = *Mp;
-  const int leg = __builtin_amdgcn_readfirstlane((int)threadIdx.x / DYN_ENVS);
-  T1_PROF_BEGIN();
-  const int lane = threadIdx.x % DYN_ENVS;
-  const int N = C.num_envs;
-  const bool active = (int)(blockIdx.x * DYN_ENVS) + lane < N;
-  const int n = active ? blockIdx.x * DYN_ENVS + lane : N - 1;  // inactive lanes shadow a valid env, never store
-  const int j0 = 6 * leg;
-  const uint32_t genv = (uint32_t)(C.env_offset + n);
-  const uint32_t ctr = A.counter;
-  const float dt = C.sim_dt;
-  BaseParams<float> PB;
-  LegParams<float> PL;
-  BaseState<float> sb;
-  float q[NLEG], qd[NLEG], tau[NLEG];
-  const LegSetup L = leg_setup(M, C, B, actions, ctr, n, active, j0, PB, PL, sb, q, qd);
-  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
-  T1_PROF_MARK(10);
-  for (int sub = 0; sub < C.decimation; ++sub) {
-    T1_PROF_MARK(7);
-    pd_torques<NLEG>(M, C, B, n, genv, ctr, sub, L.lag, j0, q, qd, tau);
-    BaseFrame<float> F;
-    base_frame(sb, F);
-    T1_PROF_MARK(0);
-    LegBlock<float> lb;
-    {
-      Sym6<float> Ab;
-      float rb[6];
-      leg_contribution<T1_LEG_CONTACT_MASK>(M, T, PB, PL, F, q, qd, tau, leg, dt, lb, Ab, rb);
-      float* X = &xch[sub & 1][leg][0][lane];
-#pragma unroll
-      for (int i = 0; i < 21; ++i) X[i * DYN_ENVS] = Ab.a[i];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) X[(21 + i) * DYN_ENVS] = rb[i];
-    }
-    Sym6<float> Ac;
-    float r[6];
-    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) r[i] = -r[i];
-    T1_PROF_MARK(6);
-    __syncthreads();
-    T1_PROF_MARK(8);
-#pragma unroll
-    for (int l = 0; l < 2; ++l) {
-      const float* Y = &xch[sub & 1][l][0][lane];
-#pragma unroll
-      for (int i = 0; i < 21; ++i) Ac.a[i] += Y[i * DYN_ENVS];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) r[i] += Y[(21 + i) * DYN_ENVS];
-    }
-    solve_base(Ac, r);
-    float dq[NLEG];
-    backsub_leg(lb, r, dq);
-    integrate_base(sb, r, dt);
-    integrate_leg(M, leg, q, qd, dq, dt);
-    T1_PROF_MARK(9);
-    if (active && sub == L.s_dof) {
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) { L.dof_dst[j0 + k] = q[k]; L.dof_dst[12 + j0 + k] = qd[k]; }
-    }
-    if (active && leg == 0 && sub == L.s_imu) capture_imu(sb.quat, sb.w, L.imu_dst);
-  }
-  T1_PROF_MARK(7);
-  if (active) leg_report(M, T, B, PB, sb, q, qd, tau, n, leg, j0);
-  T1_PROF_MARK(11);
-  if constexpr (FUSED) {
-    __syncthreads();  // both legs' outputs are in memory (same workgroup: visible after the barrier)
-    T1_PROF_MARK(12);
-    if (leg == 0) fused_epilogue(M, C, B, A, S, FA, dyn_blocks, lane);
-  }
-  T1_PROF_END();
-}
 
 // ---------------------------------------------------------------------------------------------------
 // k_dyn4: 4 waves per 64 envs (see the top of the file).  Per substep, leg wave | contact helper wave:
@@ -498,6 +337,7 @@ struct Dyn4Lds {
   PdStage<DYN_ENVS> pd[2];
   float cap[2][CAP_N][DYN_ENVS];
   float epi[EPI_N][DYN_ENVS];
+  float vib[2][DYN_ENVS];  // the base-box halves' end-of-step restitution episodes (helpers, for the report)
 };
 static_assert(FR_N <= 2 * CT_N, "the fresh outputs fit the contact-term region");
 
@@ -524,69 +364,43 @@ __device__ __forceinline__ void lds_get_sym(const float (*src)[DYN_ENVS], int la
   for (int i = 0; i < 6; ++i) g[i] = src[21 + i][lane];
 }
 
-// contact terms (Sym6 + wrench) of a leg contact body from its published pose; `bound` = its terrain height
-// bound sample (terrain_bound_raw_any, loaded by the caller ahead of time) or T1_NO_BOUND
 constexpr int32_t T1_NO_BOUND = 0x7fffffff;  // bound_height() = +inf: the body is always evaluated
-__device__ __forceinline__ void body_terms(const DynModel& M, const Terrain& T, const float (*P)[DYN_ENVS], int lane,
-                                           int b, V3<float> abs, float mu, float dt, float (*dst)[DYN_ENVS],
-                                           int32_t bound) {
-  Sym6<float> Cc;
-  float cc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  sym_zero(Cc);
-  const M3<float> Rb = lds_get_m3(P, lane);
-  const V3<float> pb = v3<float>(P[9][lane], P[10][lane], P[11][lane]);
-  float Vb[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) Vb[i] = P[12 + i][lane];
-#ifndef T1_WHATIF_NO_HELPER_CONTACT  // timing-only what-if build: the leg's shank / foot contact terms left zero
-  body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pb.z + abs.z - M.contact_radius[b], bound, M.contact_start[b], Rb, pb,
-                                         abs, Vb, mu, dt, Cc, cc);
-#endif
+
+
+// a contact body's terrain terms (from its pose held in registers) added to its self-contact terms (Cc, cc), then
+// published to LDS for the leg wave's fold-in
+__device__ __forceinline__ void body_terms_at(const DynModel& M, const Terrain& T, const BodyKin<float>& K, int lane,
+                                              int b, V3<float> abs, float mu, float e, float& vimp, float dt,
+                                              Sym6<float>& Cc, float (&cc)[6], float (*dst)[DYN_ENVS], int32_t bound) {
+  body_contact_fixed<T1_POINTS_PER_BODY>(M, T, K.p.z + abs.z - M.contact_radius[b], bound, M.contact_start[b], K.Rb,
+                                         K.p, abs, K.V, mu, e, vimp, dt, Cc, cc);
   lds_put_sym(dst, lane, Cc, cc);
 }
-
-// the shank and foot contact terms of leg `leg` with both bodies' terrain queries issued before any contact math
-template <bool HF>
-__device__ __forceinline__ void helper_two_bodies(const DynModel& M, const Terrain& T, const float (*P)[DYN_ENVS],
-                                                  int lane, int leg, V3<float> abs, float mu, float dt,
-                                                  float (*ct)[DYN_ENVS]) {
-  ContactQuery<T1_POINTS_PER_BODY, float> Q[2];
-  float Vb[2][6];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {  // 0 shank, 1 foot (the ct rows: shank at 0, foot at XCH)
-    const float (*D)[DYN_ENVS] = P + POSE_F + s * POSE_B;
-    const int b = 1 + 6 * leg + (s ? K_FOOT : K_SHANK);
-    const M3<float> Rb = lds_get_m3(D, lane);
-    const V3<float> pb = v3<float>(D[9][lane], D[10][lane], D[11][lane]);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) Vb[s][i] = D[12 + i][lane];
-    contact_query<HF, T1_POINTS_PER_BODY>(M, T, M.contact_start[b], Rb, pb, abs, Q[s]);
-  }
-#pragma unroll
-  for (int s = 1; s >= 0; --s) {  // foot first, like the unmerged order
-    Sym6<float> Cc;
-    float cc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    sym_zero(Cc);
-    contact_terms<HF, T1_POINTS_PER_BODY>(M, Q[s], Vb[s], mu, dt, Cc, cc);
-    lds_put_sym(ct + (s ? XCH : 0), lane, Cc, cc);
-  }
-}
-
-// body_terms for a pose held in registers (the helper's own kinematics, T1_HELPER_KIN)
-__device__ __forceinline__ void body_terms_at(const DynModel& M, const Terrain& T, const M3<float>& Rb, V3<float> pb,
-                                              const float Vb[6], int lane, int b, V3<float> abs, float mu, float dt,
-                                              float (*dst)[DYN_ENVS], int32_t bound) {
-  Sym6<float> Cc;
-  float cc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  sym_zero(Cc);
-  body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pb.z + abs.z - M.contact_radius[b], bound, M.contact_start[b], Rb, pb,
-                                         abs, Vb, mu, dt, Cc, cc);
-  lds_put_sym(dst, lane, Cc, cc);
-}
-// The substep state the leg wave publishes for its helper (T1_HELPER_KIN): base pos, quat, omega, v_O, and the leg's
-// q, qd -- rows of the leg's pose region, written after integration, read by the helper between S1 and S2.
+// The substep state each leg wave publishes for the helpers: base pos, quat, omega, v_O, and the leg's q, qd -- rows
+// of the leg's pose region, written after integration, read by the helpers between S1 and S2 (and after R1).
 enum : int { ST_POS = 0, ST_QUAT = 3, ST_W = 7, ST_VO = 10, ST_Q = 13, ST_QD = 19, ST_N = 25 };
 static_assert(ST_N <= POSE_N, "the substep state fits the pose rows");
+// a helper's kinematics of one published state: the base frame and the contact bodies of leg `leg` (own state P), and
+// with self-collision on (wave-uniform) those of the other leg too (its state Po: the same base rows)
+__device__ __forceinline__ void helper_kinematics(const DynModel& M, const float (*P)[DYN_ENVS],
+                                                  const float (*Po)[DYN_ENVS], int lane, int leg, BaseFrame<float>& F,
+                                                  BodyKin<float> (&Ko)[2], BodyKin<float> (&Kx)[2]) {
+  BaseState<float> sb;
+  float qh[NLEG], qdh[NLEG];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { sb.pos[i] = P[ST_POS + i][lane]; sb.w[i] = P[ST_W + i][lane]; sb.vo[i] = P[ST_VO + i][lane]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sb.quat[i] = P[ST_QUAT + i][lane];
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) { qh[k] = P[ST_Q + k][lane]; qdh[k] = P[ST_QD + k][lane]; }
+  base_frame(sb, F);
+  leg_body_kinematics(M, F, qh, qdh, leg, Ko);
+  if (M.self_collisions) {
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) { qh[k] = Po[ST_Q + k][lane]; qdh[k] = Po[ST_QD + k][lane]; }
+    leg_body_kinematics(M, F, qh, qdh, 1 - leg, Kx);
+  }
+}
 __device__ __forceinline__ void publish_state(float (*P)[DYN_ENVS], int lane, const BaseState<float>& sb,
                                               const float q[NLEG], const float qd[NLEG]) {
 #pragma unroll
@@ -868,47 +682,21 @@ __device__ __forceinline__ void leg_report_rigid(const DynModel& M, const t1env_
     if (k != K_SHANK && k != K_FOOT) { cf[b * 3 + 0] = 0.0f; cf[b * 3 + 1] = 0.0f; cf[b * 3 + 2] = 0.0f; }
   }
 }
-__device__ __forceinline__ void helper_report_contacts(const DynModel& M, const Terrain& T, const t1env_buffers& B,
-                                                       const float (*P)[DYN_ENVS], int n, int leg, float mu, int lane,
-                                                       bool active, float (*FR)[DYN_ENVS]) {
-  float* cf = B.contact_forces + (size_t)n * 39;
-  const V3<float> abs = v3<float>(P[9][lane], P[10][lane], P[11][lane]);
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const float (*D)[DYN_ENVS] = P + POSE_F + s * POSE_B;
-    const int b = 1 + 6 * leg + (s == 0 ? K_SHANK : K_FOOT);
-    float Vb[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) Vb[i] = D[12 + i][lane];
-    const V3<float> f = body_contact_force(M, T, b, lds_get_m3(D, lane), v3<float>(D[9][lane], D[10][lane], D[11][lane]),
-                                           abs, Vb, mu);
-    if (active) { cf[b * 3 + 0] = f.x; cf[b * 3 + 1] = f.y; cf[b * 3 + 2] = f.z; }
-    if (FR && s == 1) {
-      const int r = leg == 0 ? F_C0 : F_C1;
-      FR[r][lane] = f.x; FR[r + 1][lane] = f.y; FR[r + 2][lane] = f.z;
-    }
-  }
-  if (leg == 0) {
-    float V0[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) V0[i] = P[12 + i][lane];
-    const V3<float> f = body_contact_force(M, T, 0, lds_get_m3(P, lane), v3<float>(0, 0, 0), abs, V0, mu);
-    if (active) { cf[0] = f.x; cf[1] = f.y; cf[2] = f.z; }
-    if (FR) { FR[F_CFB][lane] = f.x; FR[F_CFB + 1][lane] = f.y; FR[F_CFB + 2][lane] = f.z; }
-  }
-}
 
-// the contact-force report from poses the helper computed itself (T1_HELPER_KIN: from the end-of-step state)
+// the contact-force report from the poses the helper computes itself from the end-of-step state: terrain forces plus
+// the self-contact forces fself of the shank / foot
+// (vt: the restitution set points of the shank, foot and base half; the base box's whole report uses the larger of
+// its two halves', the other half's being the other helper's)
 __device__ __forceinline__ void helper_report_contacts_at(const DynModel& M, const Terrain& T, const t1env_buffers& B,
-                                                          const BaseFrame<float>& F, const M3<float> (&Rc)[2],
-                                                          const V3<float> (&pc)[2], const float (&Vc)[2][6], int n,
-                                                          int leg, float mu, int lane, bool active,
+                                                          const BaseFrame<float>& F, const BodyKin<float> (&Kc)[2],
+                                                          const V3<float> (&fself)[2], int n, int leg, float mu,
+                                                          const float (&vt)[3], float vt_base, int lane, bool active,
                                                           float (*FR)[DYN_ENVS]) {
   float* cf = B.contact_forces + (size_t)n * 39;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int b = 1 + 6 * leg + (s == 0 ? K_SHANK : K_FOOT);
-    const V3<float> f = body_contact_force(M, T, b, Rc[s], pc[s], F.abs, Vc[s], mu);
+    const V3<float> f = body_contact_force(M, T, b, Kc[s].Rb, Kc[s].p, F.abs, Kc[s].V, mu, vt[s]) + fself[s];
     if (active) { cf[b * 3 + 0] = f.x; cf[b * 3 + 1] = f.y; cf[b * 3 + 2] = f.z; }
     if (FR && s == 1) {
       const int r = leg == 0 ? F_C0 : F_C1;
@@ -916,7 +704,7 @@ __device__ __forceinline__ void helper_report_contacts_at(const DynModel& M, con
     }
   }
   if (leg == 0) {
-    const V3<float> f = body_contact_force(M, T, 0, F.R0, v3<float>(0, 0, 0), F.abs, F.V0, mu);
+    const V3<float> f = body_contact_force(M, T, 0, F.R0, v3<float>(0, 0, 0), F.abs, F.V0, mu, vt_base);
     if (active) { cf[0] = f.x; cf[1] = f.y; cf[2] = f.z; }
     if (FR) { FR[F_CFB][lane] = f.x; FR[F_CFB + 1][lane] = f.y; FR[F_CFB + 2][lane] = f.z; }
   }
@@ -956,47 +744,43 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
   const float dt = C.sim_dt;
   if (helper) {
     // ---------------- contact helper of leg `leg`
-    const float mu = 0.5f * (B.friction[n] + M.ground_friction);
+    const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // robot shape vs ground (PhysX average)
+    const float mu_self = B.friction[n];                          // robot shape vs robot shape
+    const float e_self = B.restitution[n];
+    const float e = ground_restitution(M, e_self);
     int cb, ce;
     base_contact_range(M, leg, cb, ce);
     const float (*P)[DYN_ENVS] = lds.pose[leg];
+    const float (*Po)[DYN_ENVS] = lds.pose[1 - leg];  // the other leg's published state (self-collision)
+    // this helper's restitution episodes: its leg's shank, foot and base-box half (include/t1env.h contact_vimp)
+    float* const vimp_row = B.contact_vimp + (size_t)n * NVIMP;
+    float vi_sh = vimp_row[vimp_shank(leg)], vi_ft = vimp_row[vimp_foot(leg)], vi_b = vimp_row[vimp_base(leg)];
     T1_PROF_MARK(10);
     // the epilogue's inputs the step does not change, staged while the leg waves set up and run the first
     // forward pass (nothing writes them before the epilogue)
     if constexpr (FUSED) stage_epilogue_inputs(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, lds.epi);
     for (int sub = 0; sub < C.decimation; ++sub) {
       T1_PROF_MARK(7);
-      __syncthreads();  // S1: poses (T1_HELPER_KIN: the substep state) published
+      __syncthreads();  // S1: the substep states published
       T1_PROF_MARK(8);
-#ifdef T1_HELPER_KIN
       BaseFrame<float> F;
-      M3<float> Rc[2];
-      V3<float> pc[2];
-      float Vc[2][6];
-      {
-        BaseState<float> sb;
-        float qh[NLEG], qdh[NLEG];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) { sb.pos[i] = P[ST_POS + i][lane]; sb.w[i] = P[ST_W + i][lane]; sb.vo[i] = P[ST_VO + i][lane]; }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sb.quat[i] = P[ST_QUAT + i][lane];
-#pragma unroll
-        for (int k = 0; k < NLEG; ++k) { qh[k] = P[ST_Q + k][lane]; qdh[k] = P[ST_QD + k][lane]; }
-        base_frame(sb, F);
-        leg_contact_kinematics<T1_LEG_CONTACT_MASK>(M, F, qh, qdh, leg,
-                                                    [&](auto kc, const M3<float>& Rk, V3<float> pk, const float* V) {
-                                                      constexpr int i = decltype(kc)::value == K_FOOT ? 1 : 0;
-                                                      Rc[i] = Rk;
-                                                      pc[i] = pk;
-#pragma unroll
-                                                      for (int j = 0; j < 6; ++j) Vc[i][j] = V[j];
-                                                    });
-      }
+      BodyKin<float> Ko[2], Kx[2];
+      helper_kinematics(M, P, Po, lane, leg, F, Ko, Kx);
       const V3<float> abs = F.abs;
-      const int32_t bound_sh = terrain_bound_raw_any(T, pc[0].x + abs.x, pc[0].y + abs.y);
+      const int32_t bound_sh = terrain_bound_raw_any(T, Ko[0].p.x + abs.x, Ko[0].p.y + abs.y);
       const int32_t bound_base = terrain_bound_raw_any(T, abs.x, abs.y);
-      body_terms_at(M, T, Rc[1], pc[1], Vc[1], lane, 1 + 6 * leg + K_FOOT, abs, mu, dt, lds.ct[leg] + XCH, T1_NO_BOUND);
-      body_terms_at(M, T, Rc[0], pc[0], Vc[0], lane, 1 + 6 * leg + K_SHANK, abs, mu, dt, lds.ct[leg], bound_sh);
+      Sym6<float> Cs[2];
+      float cs[2][6];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        sym_zero(Cs[i]);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) cs[i][j] = 0.0f;
+      }
+      if (M.self_collisions) self_terms_leg(M, leg, Ko, Kx, mu_self, dt, Cs, cs);
+      body_terms_at(M, T, Ko[1], lane, 1 + 6 * leg + K_FOOT, abs, mu, e, vi_ft, dt, Cs[1], cs[1], lds.ct[leg] + XCH,
+                    T1_NO_BOUND);
+      body_terms_at(M, T, Ko[0], lane, 1 + 6 * leg + K_SHANK, abs, mu, e, vi_sh, dt, Cs[0], cs[0], lds.ct[leg], bound_sh);
       T1_PROF_MARK(3);
       __syncthreads();  // S2: contact terms published
       T1_PROF_MARK(11);
@@ -1005,7 +789,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
         float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         sym_zero(Cb);
         body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - M.contact_radius[0], bound_base, cb, F.R0,
-                                                   v3<float>(0, 0, 0), F.abs, F.V0, mu, dt, Cb, gw);
+                                                   v3<float>(0, 0, 0), F.abs, F.V0, mu, e, vi_b, dt, Cb, gw);
 #pragma unroll
         for (int i = 0; i < 6; ++i) gw[i] = -gw[i];
         lds_put_sym(lds.xch[2 + leg], lane, Cb, gw);
@@ -1013,78 +797,25 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
       T1_PROF_MARK(5);
       __syncthreads();  // S3: base system complete
       T1_PROF_MARK(12);
-#else
-      const V3<float> abs = v3<float>(P[9][lane], P[10][lane], P[11][lane]);
-      // the height bounds of the shank and of the base box are loaded first, so their latency hides under the
-      // foot's contact terms; the foot goes without a bound test (some foot among a wave's 64 envs is always
-      // near the ground, so the test would never skip it and would only add a dependent memory round trip)
-      const float (*Psh)[DYN_ENVS] = P + POSE_F;
-      const int32_t bound_sh = terrain_bound_raw_any(T, Psh[9][lane] + abs.x, Psh[10][lane] + abs.y);
-      const int32_t bound_base = terrain_bound_raw_any(T, abs.x, abs.y);
-#ifdef T1_HELPER_MERGED_QUERIES
-      // foot and shank queried in one batch (one memory latency), the shank without its bound test
-      (void)bound_sh;
-      if (T.type == 0) helper_two_bodies<false>(M, T, P, lane, leg, abs, mu, dt, lds.ct[leg]);
-      else helper_two_bodies<true>(M, T, P, lane, leg, abs, mu, dt, lds.ct[leg]);
-#else
-      body_terms(M, T, P + POSE_F + POSE_B, lane, 1 + 6 * leg + K_FOOT, abs, mu, dt, lds.ct[leg] + XCH, T1_NO_BOUND);
-      body_terms(M, T, Psh, lane, 1 + 6 * leg + K_SHANK, abs, mu, dt, lds.ct[leg], bound_sh);
-#endif
-      T1_PROF_MARK(3);
-      __syncthreads();  // S2: contact terms published
-      T1_PROF_MARK(11);
-      {  // base-box contact share of this leg, straight into the base system
-        BaseFrame<float> F;
-        F.R0 = lds_get_m3(P, lane);
-        F.abs = abs;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) F.V0[i] = P[12 + i][lane];
-        Sym6<float> Cb;
-        float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-        sym_zero(Cb);
-        body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - M.contact_radius[0], bound_base, cb, F.R0,
-                                                   v3<float>(0, 0, 0), F.abs, F.V0, mu, dt, Cb, gw);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) gw[i] = -gw[i];
-        lds_put_sym(lds.xch[2 + leg], lane, Cb, gw);
-      }
-      T1_PROF_MARK(5);
-      __syncthreads();  // S3: base system complete
-      T1_PROF_MARK(12);
-#endif
     }
     T1_PROF_MARK(7);
-    __syncthreads();  // R1: end-of-step poses (T1_HELPER_KIN: the end-of-step state) published
+    lds.vib[leg][lane] = vi_b;
+    if (active) { vimp_row[vimp_shank(leg)] = vi_sh; vimp_row[vimp_foot(leg)] = vi_ft; vimp_row[vimp_base(leg)] = vi_b; }
+    __syncthreads();  // R1: the end-of-step states published
     T1_PROF_MARK(8);
     float (*FR)[DYN_ENVS] = FUSED ? reinterpret_cast<float (*)[DYN_ENVS]>(&lds.ct[0][0][0]) : nullptr;
-#ifdef T1_HELPER_KIN
     {  // the contact-force report beside the leg wave's rigid-state report
       BaseFrame<float> F;
-      M3<float> Rc[2];
-      V3<float> pc[2];
-      float Vc[2][6];
-      BaseState<float> sb;
-      float qh[NLEG], qdh[NLEG];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) { sb.pos[i] = P[ST_POS + i][lane]; sb.w[i] = P[ST_W + i][lane]; sb.vo[i] = P[ST_VO + i][lane]; }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sb.quat[i] = P[ST_QUAT + i][lane];
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) { qh[k] = P[ST_Q + k][lane]; qdh[k] = P[ST_QD + k][lane]; }
-      base_frame(sb, F);
-      leg_contact_kinematics<T1_LEG_CONTACT_MASK>(M, F, qh, qdh, leg,
-                                                  [&](auto kc, const M3<float>& Rk, V3<float> pk, const float* V) {
-                                                    constexpr int i = decltype(kc)::value == K_FOOT ? 1 : 0;
-                                                    Rc[i] = Rk;
-                                                    pc[i] = pk;
-#pragma unroll
-                                                    for (int j = 0; j < 6; ++j) Vc[i][j] = V[j];
-                                                  });
-      helper_report_contacts_at(M, T, B, F, Rc, pc, Vc, n, leg, mu, lane, active, FR);
+      BodyKin<float> Ko[2], Kx[2];
+      helper_kinematics(M, P, Po, lane, leg, F, Ko, Kx);
+      V3<float> fself[2] = {v3<float>(0.0f, 0.0f, 0.0f), v3<float>(0.0f, 0.0f, 0.0f)};
+      if (M.self_collisions) self_forces_leg(M, leg, Ko, Kx, mu_self, fself);
+      const float vt[3] = {restitution_target(M, e, vi_sh), restitution_target(M, e, vi_ft),
+                           restitution_target(M, e, vi_b)};
+      const float vt_o = restitution_target(M, e, lds.vib[1 - leg][lane]);  // the other base half (leg 0 reports)
+      const float vt_base = vt_o > vt[2] ? vt_o : vt[2];
+      helper_report_contacts_at(M, T, B, F, Ko, fself, n, leg, mu, vt, vt_base, lane, active, FR);
     }
-#else
-    helper_report_contacts(M, T, B, P, n, leg, mu, lane, active, FR);
-#endif
     T1_PROF_MARK(11);
     if constexpr (FUSED) __syncthreads();  // the epilogue barrier
     T1_PROF_END();
@@ -1110,12 +841,9 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     for (int k = 0; k < NLEG; ++k)
       CAP[CAP_ACT + k][lane] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
   T1_PROF_MARK(10);
-#ifdef T1_HELPER_KIN
   publish_state(P, lane, sb, q, qd);  // the helpers start each substep from the state (their own kinematics)
-#endif
   for (int sub = 0; sub < C.decimation; ++sub) {
     T1_PROF_MARK(7);
-#ifdef T1_HELPER_KIN
     __syncthreads();  // S1: the substep state published
     T1_PROF_MARK(8);
     BaseFrame<float> F;
@@ -1124,27 +852,6 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     leg_forward_nc<T1_LEG_CONTACT_MASK>(M, PL, F, q, qd, leg, dt, st,
                                         [&](auto, const M3<float>&, V3<float>, const float*) {});
     T1_PROF_MARK(1);
-#else
-    BaseFrame<float> F;
-    base_frame(sb, F);
-    lds_put_m3(P, lane, F.R0);
-    P[9][lane] = F.abs.x; P[10][lane] = F.abs.y; P[11][lane] = F.abs.z;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) P[12 + i][lane] = F.V0[i];
-    LegPass<float> st;
-    leg_forward_nc<T1_LEG_CONTACT_MASK>(M, PL, F, q, qd, leg, dt, st,
-                                        [&](auto kc, const M3<float>& Rk, V3<float> pk, const float* V) {
-                                          constexpr int k = decltype(kc)::value;
-                                          float (*D)[DYN_ENVS] = P + POSE_F + (k == K_FOOT ? POSE_B : 0);
-                                          lds_put_m3(D, lane, Rk);
-                                          D[9][lane] = pk.x; D[10][lane] = pk.y; D[11][lane] = pk.z;
-#pragma unroll
-                                          for (int i = 0; i < 6; ++i) D[12 + i][lane] = V[i];
-                                        });
-    T1_PROF_MARK(1);
-    __syncthreads();  // S1
-    T1_PROF_MARK(8);
-#endif
     pd_torques_staged(M, C, PD, lane, K, ctr, sub, L.lag, j0, q, qd, tau);
     T1_PROF_MARK(0);
     LegBlock<float> lb;
@@ -1231,14 +938,10 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
 #pragma unroll
       for (int i = 0; i < 3; ++i) CAP[2 * NLEG + 4 + i][lane] = sb.w[i];
     }
-#ifdef T1_HELPER_KIN
     publish_state(P, lane, sb, q, qd);  // the helper read the previous one before S2; after the last substep: the
                                         // end-of-step state its contact-force report starts from
-#endif
   }
-#ifdef T1_HELPER_KIN
   __syncthreads();  // R1: the end-of-step state published (the helpers compute the contact forces meanwhile)
-#endif
   T1_PROF_MARK(7);
   if (active) {
     if (L.s_dof < C.decimation) {  // the sensor-lag samples captured in the loop
@@ -1269,20 +972,9 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
   {
     BaseFrame<float> F;
     base_frame(sb, F);
-#ifdef T1_HELPER_KIN
     leg_report_rigid(M, B, PB, sb, F, q, qd, n, leg, active, nullptr, lane, FR);
   }
   T1_PROF_MARK(11);
-#else
-    lds_put_m3(P, lane, F.R0);
-    P[9][lane] = F.abs.x; P[10][lane] = F.abs.y; P[11][lane] = F.abs.z;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) P[12 + i][lane] = F.V0[i];
-    leg_report_rigid(M, B, PB, sb, F, q, qd, n, leg, active, P, lane, FR);
-  }
-  T1_PROF_MARK(11);
-  __syncthreads();  // R1: end-of-step poses published (the helpers write the contact forces)
-#endif
   if constexpr (FUSED) {
     __syncthreads();  // all four waves: every output of the workgroup is in memory
     T1_PROF_MARK(12);
@@ -1301,8 +993,7 @@ bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg) {
   if (cfg.shift_blocks < 0) return true;   // forced stand-alone shift (tuning: T1ENV_SHIFT_BLOCKS=-1)
   if (cfg.shift_blocks > 0) return false;  // explicit shift-workgroup count (tuning)
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
-  const int per_cu = cfg.waves == 4 ? 1 : 2;
-  return per_cu * cfg.cus - dyn_blocks < MIN_SHIFT_BLOCKS;
+  return cfg.cus - dyn_blocks < MIN_SHIFT_BLOCKS;
 }
 
 int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
@@ -1310,11 +1001,10 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
                        const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s, bool shift_prelaunched,
                        const SubLog* log) {
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
-  // history-shift workgroups: the workgroup slots the dynamics leave free (a wave of either kernel holds a
-  // whole SIMD's registers: 2 workgroups/CU for k_dynamics, 1 for k_dyn4), at least MIN_SHIFT_BLOCKS; none
-  // when the caller ran the shift as its own launch (t1_shift_prelaunch)
-  const int per_cu = cfg.waves == 4 ? 1 : 2;
-  int shift_blocks = cfg.shift_blocks > 0 ? cfg.shift_blocks : per_cu * cfg.cus - dyn_blocks;
+  // history-shift workgroups: the workgroup slots the dynamics leave free (a k_dyn4 wave holds a whole SIMD's
+  // registers: one workgroup per CU), at least MIN_SHIFT_BLOCKS; none when the caller ran the shift as its own
+  // launch (t1_shift_prelaunch)
+  int shift_blocks = cfg.shift_blocks > 0 ? cfg.shift_blocks : cfg.cus - dyn_blocks;
   if (shift_blocks < MIN_SHIFT_BLOCKS) shift_blocks = MIN_SHIFT_BLOCKS;
   if (shift_prelaunched) shift_blocks = 0;
   const FusedArgs FA = fused ? *fused : FusedArgs{};
@@ -1322,7 +1012,7 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
   const dim3 grid(dyn_blocks + shift_blocks);
   const bool hf = T.type != 0;
   if (log) {  // the substep log: fused k_dyn4 only (the caller checks)
-    if (cfg.waves != 4 || !fused) return (int)hipErrorInvalidValue;
+    if (!fused) return (int)hipErrorInvalidValue;
     if (hf)
       hipLaunchKernelGGL((k_dyn4<true, true, true>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S,
                          dyn_blocks, FA, LG);
@@ -1331,15 +1021,10 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
                          dyn_blocks, FA, LG);
     return (int)hipGetLastError();
   }
-#define T1_LAUNCH(KERNEL, BS, HF, FU) \
-  hipLaunchKernelGGL((KERNEL<HF, FU>), grid, dim3(BS), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA, LG)
-  if (cfg.waves == 4) {
-    if (fused) { if (hf) T1_LAUNCH(k_dyn4, D4_BLOCK, true, true); else T1_LAUNCH(k_dyn4, D4_BLOCK, false, true); }
-    else { if (hf) T1_LAUNCH(k_dyn4, D4_BLOCK, true, false); else T1_LAUNCH(k_dyn4, D4_BLOCK, false, false); }
-  } else {
-    if (fused) { if (hf) T1_LAUNCH(k_dynamics, DYN_BLOCK, true, true); else T1_LAUNCH(k_dynamics, DYN_BLOCK, false, true); }
-    else { if (hf) T1_LAUNCH(k_dynamics, DYN_BLOCK, true, false); else T1_LAUNCH(k_dynamics, DYN_BLOCK, false, false); }
-  }
+#define T1_LAUNCH(HF, FU) \
+  hipLaunchKernelGGL((k_dyn4<HF, FU>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA, LG)
+  if (fused) { if (hf) T1_LAUNCH(true, true); else T1_LAUNCH(false, true); }
+  else { if (hf) T1_LAUNCH(true, false); else T1_LAUNCH(false, false); }
 #undef T1_LAUNCH
   return (int)hipGetLastError();
 }

@@ -28,7 +28,7 @@ struct SubLog {
 
 // launch shape of the dynamics kernel
 struct DynLaunch {
-  int waves;         // 4: k_dyn4 (leg waves + contact helper waves, default), 2: k_dynamics
+  int waves;         // 4: k_dyn4 (leg waves + contact helper waves; the only kernel since round 3)
   int cus;           // compute units of the device (default history-shift grid)
   int shift_blocks;  // > 0: history-shift workgroups override (tuning)
 };

@@ -591,6 +591,9 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
     B.env_origins[n * 3 + 1] = to[1];
     B.env_origins[n * 3 + 2] = to[2];
   }
+  // the new episode starts in the air as far as restitution is concerned (no contact episode carried over)
+#pragma unroll
+  for (int i = 0; i < NVIMP; ++i) B.contact_vimp[(size_t)n * NVIMP + i] = 0.0f;
   // _reset_dofs
 #pragma unroll
   for (int j = 0; j < 12; ++j) {

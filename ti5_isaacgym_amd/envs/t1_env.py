@@ -96,7 +96,20 @@ def build_model(cfg, urdf_path=None):
         list(cfg.init_state.ang_vel)
     for i in range(13):
         m.base_init_state[i] = init[i]
+    # asset.self_collisions is Isaac Gym's bitwise filter: 0 enables self-collision (t1_dh_stand_config.py:51)
+    set_self_collision(m, tab, enabled=int(cfg.asset.self_collisions) == 0,
+                       bounce_threshold=cfg.sim.physx.bounce_threshold_velocity)
     return m, tab, default, kp, kd
+
+
+def set_self_collision(m, tab, enabled=True, bounce_threshold=0.5):
+    """The model's self-collision boxes (utils/urdf.py self_box: left shank, left foot, right shank, right foot) and
+    the restitution bounce threshold (sim.physx.bounce_threshold_velocity, t1_dh_stand_config.py:171)."""
+    m.self_collisions = int(bool(enabled))
+    for i, box in enumerate(tab["self_box"]):
+        for k in range(6):
+            m.self_box[i][k] = box[k]
+    m.bounce_threshold = float(bounce_threshold)
 
 
 def check_supported(cfg):
@@ -227,6 +240,7 @@ class T1DHStandEnv(VecEnv):
         self.terrain_levels, self.terrain_types = z(N, dtype=i32), z(N, dtype=i32)
         self.terrain_origins = z(1, 1, 3)
         self._extras_ring = torch.full((EXTRAS_RING, 32), float("nan"), device=d)
+        self.contact_vimp = z(N, 6)   # restitution episodes of the contact bodies (include/t1env.h)
         self._ep_accum = z(32)
         # views mirroring the reference's attribute names
         self.dof_pos = self.dof_state.view(N, 12, 2)[..., 0]
@@ -411,6 +425,7 @@ class T1DHStandEnv(VecEnv):
             "act_hist": self._act_hist, "dof_hist": self._dof_hist, "imu_hist": self._imu_hist,
             "env_origins": self.env_origins, "terrain_levels": self.terrain_levels, "terrain_types": self.terrain_types,
             "terrain_origins": self.terrain_origins, "extras": self._extras_ring, "ep_accum": self._ep_accum,
+            "contact_vimp": self.contact_vimp,
         }
         types = dict(_lib.BUFFER_FIELDS)
         for name, t in m.items():

@@ -9,7 +9,8 @@ theorem), leaving 13 bodies / 12 revolute DOF in Isaac Gym's depth-first order:
 
 Collision geometry (contact candidates): the base box, the two shank boxes and the
 two ankle-roll STL meshes (t1.urdf:42-51, 265-272, 390-398, 625-632, 750-758).  The mesh is replaced by
-support points of its convex hull (sole corners, toe/heel edges), the box by its 8 corners.
+support points of its convex hull (sole corners, toe/heel edges), the box by its 8 corners.  Self-collision
+volumes (``self_box``): the shank boxes themselves and the foot hulls' bounding boxes, in the link frame.
 """
 import os
 import struct
@@ -19,6 +20,7 @@ import numpy as np
 
 BODY_NAMES = ["base_link"] + [f"leg_{s}{i}_link" for s in "lr" for i in range(1, 7)]
 DOF_NAMES = [f"leg_{s}{i}_joint" for s in "lr" for i in range(1, 7)]
+SELF_BODIES = [4, 6, 10, 12]   # leg_l4 (shank), leg_l6 (foot), leg_r4, leg_r6: the legs' collision bodies
 FOOT_POINT_DIRS = [(1, 1, -1), (1, -1, -1), (-1, 1, -1), (-1, -1, -1),
                    (1, 0, -1), (-1, 0, -1), (1, 0, 0), (-1, 0, 0)]
 
@@ -136,14 +138,22 @@ class Articulation:
     def _contact_points(self):
         mesh_dir = os.path.dirname(self.urdf_path)
         pts, bodies = [], []
+        self.self_box = {}   # body -> [center (3), half extents (3)] in the link frame (self-collision volumes)
         for b, name in enumerate(BODY_NAMES):
             for tag, attr, xyz, R in self.collisions[name]:
                 if tag == "box":
                     c = box_corners(_vec(attr["size"]), xyz, R)
+                    if not np.allclose(R, np.eye(3)) and b != 0:
+                        raise ValueError("rotated leg collision boxes are not supported")
+                    self.self_box[b] = list(xyz) + list(_vec(attr["size"]) / 2)
                 elif tag == "mesh":
                     v = load_stl(os.path.normpath(os.path.join(mesh_dir, attr["filename"])))
                     v = v @ R.T + xyz
                     c = np.array([v[np.argmax(v @ np.asarray(d, float))] for d in FOOT_POINT_DIRS])
+                    # the hull's axis-aligned bounding box in the link frame stands in for the hull as a self-collision
+                    # volume (PhysX collides the convex hull itself)
+                    lo, hi = v.min(0), v.max(0)
+                    self.self_box[b] = list((lo + hi) / 2) + list((hi - lo) / 2)
                 else:
                     raise ValueError(f"unsupported collision geometry {tag}")
                 pts.extend(c)
@@ -174,6 +184,8 @@ def compile_model(urdf_path):
         "limits": a.limits.tolist(),  # lower, upper, effort, velocity
         "contact_body": a.contact_body.tolist(), "contact_point": a.contact_point.tolist(),
         "contact_start": a.contact_start.tolist(), "contact_count": a.contact_count.tolist(),
+        # self-collision boxes of left shank, left foot, right shank, right foot (center, half extents; link frame)
+        "self_box": [[float(x) for x in a.self_box[b]] for b in SELF_BODIES],
     }
 
 
