@@ -58,9 +58,12 @@ class DHPPO:
         self.graph_act = torch.device(device).type == "cuda"
         self._act_graphs = {}
 
-    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
+    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape,
+                     history=None):
+        """history=(frame, frames): the actor observations are a frame history the env shifts every step (the T1
+        env's, T1DHStandEnv.obs_frame_history): stored as frames (RolloutStorage)."""
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
-                                      action_shape, None, self.device)
+                                      action_shape, None, self.device, history=history)
 
     def test_mode(self):
         self.actor_critic.test()

@@ -1,11 +1,16 @@
 """RolloutStorage: on-device PPO rollout buffer + GAE (reference humanoid/algo/ppo/rollout_storage.py:3-173).
 
 Same API (``Transition``, ``add_transitions``, ``compute_returns``, ``mini_batch_generator``,
-``get_statistics``, ``clear``) and the same arithmetic.  Everything stays resident in HBM: at 8192 envs x 24
-steps the actor observations are 24 x 8192 x 3102 fp32 = 2.4 GB, a small fraction of the 288 GB of one MI355X,
-so no host staging or reduced-precision storage is needed.  With data-parallel training the advantage
-normalisation uses the mean / std over all ranks, which equals the single-GPU statistics
-of the concatenated rollout.
+``get_statistics``, ``clear``) and the same arithmetic.  Everything stays resident in HBM.  With data-parallel
+training the advantage normalisation uses the mean / std over all ranks, which equals the
+single-GPU statistics of the concatenated rollout.
+
+Frame-history storage (``history=(frame, frames)``): the actor observation of the T1 env is a stack of
+`frames` frames of `frame` features, oldest first, which the env shifts by one frame per step and clears (zeros)
+when an env resets (t1_dh_stand_env.py:368-481, 548-558).  Storing all 24 x 8192 x 3102 fp32 (2.4 GB) costs a
+101 MB copy per rollout step; with `history` the storage keeps the first step's full history plus each later step's
+newest frame (137 MB in all), and the minibatch generator rebuilds every sampled history from them and the stored
+dones -- the same bits as the full rows.  Callers whose observations are not such a history keep the full storage.
 """
 import torch
 
@@ -25,7 +30,7 @@ class RolloutStorage:
                 setattr(self, k, None)
 
     def __init__(self, num_envs, num_transitions_per_env, obs_shape, privileged_obs_shape, actions_shape,
-                 num_single_obs=None, device="cpu"):
+                 num_single_obs=None, device="cpu", history=None):
         T, N, d = num_transitions_per_env, num_envs, device
         self.device = device
         self.obs_shape, self.privileged_obs_shape, self.actions_shape = obs_shape, privileged_obs_shape, actions_shape
@@ -34,7 +39,17 @@ class RolloutStorage:
         def buf(*shape, dtype=torch.float32):
             return torch.zeros(T, N, *shape, device=d, dtype=dtype)
 
-        self.observations = buf(*obs_shape)
+        self.history = None
+        if history is not None:
+            frame, frames = (int(x) for x in history)
+            if tuple(obs_shape) != (frame * frames,):
+                raise ValueError(f"history {history} does not match obs_shape {tuple(obs_shape)}")
+            self.history = (frame, frames)
+            self.obs0 = torch.zeros(N, frame * frames, device=d)   # the first step's whole history
+            self.frames = buf(frame)                                # each step's newest frame
+            self.observations = None
+        else:
+            self.observations = buf(*obs_shape)
         self.privileged_observations = buf(*privileged_obs_shape) if privileged_obs_shape[0] is not None else None
         self.rewards = buf(1)
         self.actions = buf(*actions_shape)
@@ -54,7 +69,12 @@ class RolloutStorage:
         if self.step >= self.num_transitions_per_env:
             raise AssertionError("Rollout buffer overflow")
         k = self.step
-        self.observations[k].copy_(t.observations)
+        if self.history is not None:
+            if k == 0:
+                self.obs0.copy_(t.observations)
+            self.frames[k].copy_(t.observations[:, -self.history[0]:])
+        else:
+            self.observations[k].copy_(t.observations)
         if self.privileged_observations is not None:
             self.privileged_observations[k].copy_(t.critic_observations)
         self.actions[k].copy_(t.actions)
@@ -100,9 +120,12 @@ class RolloutStorage:
         mb = batch // num_mini_batches
         perm = torch.randperm(num_mini_batches * mb, requires_grad=False, device=self.device)
         flat = lambda x: x.flatten(0, 1)  # noqa: E731
-        obs = flat(self.observations)
-        if obs_dtype is not None and obs.dtype != obs_dtype:
-            obs = obs.to(obs_dtype)
+        if self.history is not None:
+            obs = _HistoryRows(self, obs_dtype)
+        else:
+            obs = flat(self.observations)
+            if obs_dtype is not None and obs.dtype != obs_dtype:
+                obs = obs.to(obs_dtype)
         critic = flat(self.privileged_observations) if self.privileged_observations is not None else obs
         cols = [flat(self.actions), flat(self.values), flat(self.advantages), flat(self.returns),
                 flat(self.actions_log_prob), flat(self.mu), flat(self.sigma)]
@@ -118,3 +141,37 @@ class RolloutStorage:
                            logp, mu, sigma, (None, None), None)
                 else:
                     yield obs[idx], critic[idx], actions, values, advantages, returns, logp, mu, sigma, (None, None), None
+
+
+class _HistoryRows:
+    """Rows [idx] of the flattened (T * N, frame * frames) observations, rebuilt from the frame-history storage.
+
+    Per env the frames form one sequence: the first step's history (frames oldest..newest = times -frames+1..0), then
+    the newest frame of steps 1..T-1 (times 1..T-1).  Step k's history is the window of times k-frames+1..k, with the
+    frames older than the env's latest reset at or before step k zeroed: obs k is post-reset when dones[k-1] is set
+    (the env zeroes the history and appends the new frame), and the zeros stay until the frames shift out."""
+
+    def __init__(self, st, dtype=None):
+        frame, frames = st.history
+        T, N = st.num_transitions_per_env, st.num_envs
+        dt = dtype if dtype is not None else st.obs0.dtype
+        self.frame, self.frames, self.N = frame, frames, N
+        seq = torch.empty(N, frames + T - 1, frame, device=st.obs0.device, dtype=dt)
+        seq[:, :frames] = st.obs0.view(N, frames, frame)
+        if T > 1:
+            seq[:, frames:] = st.frames[1:].transpose(0, 1)
+        self.seq = seq
+        # first time step whose frame is valid for step k's history (frames of earlier times are zero)
+        dn = st.dones.view(T, N) > 0
+        steps = torch.arange(T, device=st.obs0.device).view(T, 1).expand(T, N)
+        reset_at = torch.where(torch.cat([torch.zeros(1, N, dtype=torch.bool, device=dn.device), dn[:-1]]),
+                               steps, torch.full_like(steps, -(frames + T)))
+        self.first = torch.cummax(reset_at, 0).values
+        self.win = torch.arange(frames, device=st.obs0.device)
+
+    def __getitem__(self, idx):
+        k, n = idx // self.N, idx % self.N
+        pos = k.unsqueeze(1) + self.win.unsqueeze(0)                     # seq index = time + frames - 1
+        rows = self.seq[n.unsqueeze(1), pos]                              # (M, frames, frame)
+        old = (pos - (self.frames - 1)) < self.first[k, n].unsqueeze(1)   # frame time before the latest reset
+        return rows.masked_fill_(old.unsqueeze(2), 0).reshape(idx.numel(), self.frames * self.frame)

@@ -71,7 +71,10 @@ class DHOnPolicyRunner:
         self.alg = alg_cls(actor_critic, device=self.device, **self.alg_cfg)
         self.num_steps_per_env = self.cfg["num_steps_per_env"]
         self.save_interval = self.cfg["save_interval"]
-        self.alg.init_storage(env.num_envs, self.num_steps_per_env, [env.num_obs], [num_critic_obs], [env.num_actions])
+        # an env whose actor observations are a shifted frame history (T1DHStandEnv.obs_frame_history) lets the
+        # storage keep frames instead of whole histories (rollout.py)
+        self.alg.init_storage(env.num_envs, self.num_steps_per_env, [env.num_obs], [num_critic_obs], [env.num_actions],
+                              history=getattr(env, "obs_frame_history", None))
         self.log_dir = log_dir if self.rank0 else None
         self.writer = None
         self.current_learning_iteration = 0

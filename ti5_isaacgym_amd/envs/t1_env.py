@@ -143,6 +143,9 @@ class T1DHStandEnv(VecEnv):
         self.num_privileged_obs = int(e.num_privileged_obs)
         self.num_actions = int(e.num_actions)
         self.num_single_obs = int(e.num_single_obs)
+        # the actor observation is frame_stack frames of num_single_obs, shifted one frame per step and zeroed at
+        # reset (t1_dh_stand_env.py:368-481, 548-558): the runner's rollout storage keeps frames (algo/rollout.py)
+        self.obs_frame_history = (self.num_single_obs, int(e.frame_stack))
         if (self.num_single_obs, e.single_num_privileged_obs, e.frame_stack, e.c_frame_stack, self.num_actions) != \
                 (_lib.NOBS, _lib.NPRIV, _lib.HIST, _lib.CHIST, _lib.ND):
             raise ValueError("the HIP kernels are specialised for the t1_dh_stand layout (47 x 66 obs, 73 x 3 priv)")
