@@ -73,6 +73,8 @@ def parse():
                    help="time the K steps R times (each bracketed by barrier + synchronize) and report the median "
                         "(SURVEY §8(d): median of 5); the per-repeat values go to repeat_values")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-self-collision", action="store_true",
+                   help="A/B only (not the metric's config): asset.self_collisions = 1 (Isaac Gym's filter: disabled)")
     p.add_argument("--time-every", type=int, default=8,
                    help="record per-kernel HIP events on every k-th timed step (event records cost host time; "
                         "0 = never, 1 = every step)")
@@ -133,6 +135,8 @@ def main():
     def hook(cfg):
         cfg.env.state_dtype = args.state_dtype
         cfg.domain_rand.push_robots = bool(args.push)
+        if args.no_self_collision:
+            cfg.asset.self_collisions = 1
     env = make_t1_env(num_envs=N, mesh_type=args.mesh, seed=5, device=str(dev), env_offset=rank * N,
                       num_envs_total=N * world, cfg_hook=hook)
     b_alg, shift_bytes = alg_bytes(args.state_dtype)

@@ -66,12 +66,13 @@ typedef struct t1env_model {
   float ground_friction, ground_restitution;
   float base_init_state[13];    /* pos(3) quat xyzw(4) linvel(3) angvel(3) -- cfg.init_state */
   /* self-collision (asset.self_collisions = 0: enabled, t1_dh_stand_config.py:51) between the legs' contact bodies:
-   * the shank collision boxes (t1.urdf:265-272, 625-632) and the feet's ankle-roll STL hulls as their bounding boxes
-   * (t1.urdf:390-398, 750-758), each in its link frame: center (3), half extents (3); order left shank, left foot,
-   * right shank, right foot.  Restitution acts above bounce_threshold (sim.physx.bounce_threshold_velocity,
-   * t1_dh_stand_config.py:171) with the per-env coefficient of DR (restitution_range, :185). */
+   * the shank collision boxes (t1.urdf:265-272, 625-632) and the feet's ankle-roll STL hulls (t1.urdf:390-398,
+   * 750-758) as capsules along their long axes (utils/urdf.py self_capsules), each in its link frame: segment end a (3),
+   * end b (3), radius (1); order left shank, left foot, right shank, right foot.  Restitution acts above
+   * bounce_threshold (sim.physx.bounce_threshold_velocity, t1_dh_stand_config.py:171) with the per-env coefficient of
+   * DR (restitution_range, :185). */
   int32_t self_collisions;      /* 1: enabled */
-  float self_box[4][6];
+  float self_capsule[4][7];
   float bounce_threshold;       /* [m/s] */
 } t1env_model;
 

@@ -109,9 +109,11 @@ class Robot:
 #   * point Jacobians J_x (velocity of a body-fixed point w.r.t. u = [omega, v_O, qd]) by central differences of
 #     forward kinematics -- no spatial algebra shared with the product;
 #   * terrain: the plane z = 0 (normal +z), contact candidates = the model's contact points below it;
-#   * self-collision: the legs' boxes (model self_box: left shank, left foot, right shank, right foot), every corner of
-#     one box inside another, depth / normal of that box's nearest face; pairs {l, r} x {shank, foot} across the
-#     legs and shank-foot within a leg; each body gets the force at the corner, the other body the reaction;
+#   * self-collision: the legs' capsules (utils/urdf.py self_capsules: left shank, left foot, right shank, right foot);
+#     per overlapping pair one contact at the middle of the overlap along the segments' closest points (found here by
+#     enumerating the 2-parameter problem's interior stationary point and its four edges; near-parallel segments,
+#     sin^2 < 1e-3, by the overlap-midpoint rule the product documents); pairs {l, r} x {shank, foot} across the legs
+#     and shank-foot within a leg; each body gets the force at that point, the other body the reaction;
 #   * the law per contact: normal spring k pen, damper d while approaching (implicit: cn = dt k + d) and,
 #     with a restitution target v_tgt, while separating slower than it (cn = d, f_n += d v_tgt), regularised Coulomb friction ct = mu fn_est / max(|v_t|, v_s) as an implicit tangential
 #     damper: C = cn n n^T + ct (I - n n^T), f = (k pen - cn v_n + d v_tgt) n - ct v_t;
@@ -125,20 +127,40 @@ class Robot:
 SELF_BODIES = (4, 6, 10, 12)
 
 
-def _box_corners(box):
-    c, h = np.asarray(box[:3], float), np.asarray(box[3:], float)
-    return np.array([c + np.array([sx, sy, sz]) * h for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)])
+def _capsules(tab):
+    """{body: (a, b, r)}: each self-collision box (tab["self_box"], link frame) as the capsule along its longest axis,
+    radius the smaller cross-section half extent, ends inset by the radius (the model's definition)"""
+    out = {}
+    for body, box in zip(SELF_BODIES, tab["self_box"]):
+        c, h = np.asarray(box[:3], float), np.asarray(box[3:], float)
+        ax = int(np.argmax(h))
+        r = float(np.min(np.delete(h, ax)))
+        e = np.eye(3)[ax] * max(h[ax] - r, 1e-3)
+        out[body] = (c - e, c + e, r)
+    return out
 
 
-def _inside(box, R, p, x):
-    """x (world) inside the box of a body at (R, p): (depth, outward unit normal of the nearest face) or None"""
-    c, h = np.asarray(box[:3], float), np.asarray(box[3:], float)
-    loc = R.T @ (x - p) - c
-    d = h - np.abs(loc)
-    if np.all(d > 0):
-        k = int(np.argmin(d))
-        return d[k], np.sign(loc[k]) * R[:, k]
-    return None
+def _closest_segments(p1, q1, p2, q2):
+    """closest points of the segments p1-q1, p2-q2: min over the interior stationary point (if inside [0,1]^2) and the
+    best point of each edge of the parameter square; near-parallel segments: the overlap-midpoint rule"""
+    d1, d2 = q1 - p1, q2 - p2
+    a, e, b = d1 @ d1, d2 @ d2, d1 @ d2
+    clip = lambda x: min(max(x, 0.0), 1.0)  # noqa: E731
+    if a * e - b * b < 1e-3 * a * e:
+        s0, s1 = sorted(((p2 - p1) @ d1 / a, (q2 - p1) @ d1 / a))
+        c1 = p1 + 0.5 * (clip(s0) + clip(s1)) * d1
+        return c1, p2 + clip((c1 - p2) @ d2 / e) * d2
+    cands = []
+    st = np.linalg.solve(np.array([[a, -b], [-b, e]]), np.array([-(p1 - p2) @ d1, (p1 - p2) @ d2]))
+    if 0 <= st[0] <= 1 and 0 <= st[1] <= 1:
+        cands.append(tuple(st))
+    for sv in (0.0, 1.0):
+        cands.append((sv, clip((p1 + sv * d1 - p2) @ d2 / e)))
+    for tv in (0.0, 1.0):
+        cands.append((clip((p2 + tv * d2 - p1) @ d1 / a), tv))
+    dist = [np.linalg.norm(p1 + sv * d1 - p2 - tv * d2) for sv, tv in cands]
+    sv, tv = cands[int(np.argmin(dist))]
+    return p1 + sv * d1, p2 + tv * d2
 
 
 class ContactRobot(Robot):
@@ -178,20 +200,21 @@ class ContactRobot(Robot):
                     slot = 4 + (c - s) * 2 // n if b == 0 else 2 * ((b - 1) // 6) + (1 if (b - 1) % 6 == 5 else 0)
                     out.append((b, pts[c], np.array([0.0, 0.0, 1.0]), -x[2], None, mu_ground, slot))
         if self_collision:
-            boxes = dict(zip(SELF_BODIES, self.tab["self_box"]))
+            caps = _capsules(self.tab)
             pairs = [(4, 10), (4, 12), (6, 10), (6, 12), (4, 6), (10, 12)]
             for a, bb in pairs:
-                for own, oth in ((a, bb), (bb, a)):
-                    for corner in _box_corners(boxes[own]):
-                        x = self._points(Rs, ps, own, corner)
-                        hit = _inside(boxes[oth], Rs[oth], ps[oth], x)
-                        if hit is None:
-                            continue
-                        pen, n = hit
-                        # the corner's body is pushed out along n; the other body gets the reaction at the same point
-                        loc_oth = Rs[oth].T @ (x - ps[oth])
-                        out.append((own, corner, n, pen, (oth, loc_oth), mu_self, None))
-                        out.append((oth, loc_oth, -n, pen, (own, corner), mu_self, None))
+                (a0, a1, ra), (b0, b1, rb) = caps[a], caps[bb]
+                ca, cb = _closest_segments(self._points(Rs, ps, a, a0), self._points(Rs, ps, a, a1),
+                                           self._points(Rs, ps, bb, b0), self._points(Rs, ps, bb, b1))
+                dist = np.linalg.norm(ca - cb)
+                if dist >= ra + rb:
+                    continue
+                n = (ca - cb) / dist            # pushes a out of b
+                pen = ra + rb - dist
+                x = cb + (rb - 0.5 * pen) * n   # the middle of the overlap
+                la, lb = Rs[a].T @ (x - ps[a]), Rs[bb].T @ (x - ps[bb])
+                out.append((a, la, n, pen, (bb, lb), mu_self, None))
+                out.append((bb, lb, -n, pen, (a, la), mu_self, None))
         return out
 
     def step(self, p, quat, w, v, q, qd, tau, dt, mu_ground, e_ground, mu_self, e_self, f_base=None,

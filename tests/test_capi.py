@@ -51,7 +51,7 @@ int main(void) {
   printf("%zu %zu %zu %zu %zu\n", sizeof(t1env_model), sizeof(t1env_config), sizeof(t1env_buffers),
          sizeof(t1env_step_args), sizeof(t1env_injected));
   printf("%zu %zu %zu %zu %zu %zu\n", offsetof(t1env_config, reset_xy_range), offsetof(t1env_buffers, ep_accum),
-         offsetof(t1env_model, base_init_state), offsetof(t1env_buffers, contact_vimp), offsetof(t1env_model, self_box),
+         offsetof(t1env_model, base_init_state), offsetof(t1env_buffers, contact_vimp), offsetof(t1env_model, self_capsule),
          offsetof(t1env_model, bounce_threshold));
   return 0;
 }
@@ -68,7 +68,7 @@ int main(void) {
     assert sizes[5] == _lib.Config.reset_xy_range.offset
     assert sizes[6] == _lib.Buffers.ep_accum.offset
     assert sizes[7] == _lib.Model.base_init_state.offset
-    assert sizes[8:] == [_lib.Buffers.contact_vimp.offset, _lib.Model.self_box.offset, _lib.Model.bounce_threshold.offset]
+    assert sizes[8:] == [_lib.Buffers.contact_vimp.offset, _lib.Model.self_capsule.offset, _lib.Model.bounce_threshold.offset]
 
 
 def test_env_refuses_cpu_device():

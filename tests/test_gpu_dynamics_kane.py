@@ -41,6 +41,10 @@ def test_one_substep_matches_kane_equations(ext_force):
 
     def hook(cfg):
         cfg.domain_rand.push_robots = False
+        # Kane's equations here have no contact terms: self-collision off (asset.self_collisions is Isaac Gym's
+        # filter, 1 = disabled), since random joint offsets of +-0.15 rad can press the feet into each other
+        # (tests/test_gpu_dynamics_contact.py checks those contacts)
+        cfg.asset.self_collisions = 1
 
     env = make_t1_env(num_envs=N, mesh_type="plane", seed=11, device="cuda:0", cfg_hook=hook)
     tab = load_model()

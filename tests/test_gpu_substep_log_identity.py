@@ -1,11 +1,12 @@
 """The substep log must not change the product kernel's results -- needs the MI355X.
 
-tests/test_gpu_product_parity.py pins k_dyn4 through its substep log (t1env_set_substep_log), i.e. the `LOG=true`
-instantiation of the fused step kernel; bench.py, the runner and every other caller execute the `LOG=false` code
-object.  The two are separate compilations of a unit with a history of optimiser-dependent results,
-so this test steps two identically seeded envs -- one with the log on, one with it off -- through the same actions
-and requires every buffer the step writes to be BIT-identical, at BASELINE configs[2] (8192 envs, trimesh curriculum
-+ full DR) through in-epilogue resets and an applied external-force window (counter 96,400, t1_dh_stand_env.py:205-247).
+tests/test_gpu_product_parity.py pins k_dyn4 through its substep log (t1env_set_substep_log), while bench.py, the
+runner and every other caller step with the log off.  Round 2 compiled the logged step as a separate template
+instantiation, and this test found it differing from the product's by up to 2.5e-5 in obs (the compiler contracted
+the two differently); the log is now a run-time switch of the one product code object.  The test steps two
+identically seeded envs -- one with the log on, one with it off -- through the same actions and requires every buffer
+the step writes to be BIT-identical, at BASELINE configs[2] (8192 envs, trimesh curriculum + full DR) through
+in-epilogue resets and an applied external-force window (counter 96,400, t1_dh_stand_env.py:205-247).
 """
 import numpy as np
 import pytest
@@ -32,21 +33,27 @@ def test_substep_log_does_not_change_results(n, mesh):
         el = e.episode_length_buf.cpu().numpy().copy()
         el[::5] = int(e.max_episode_length) - 2 - np.arange(0, n, 5) % 3   # in-epilogue resets
         e.episode_length_buf = torch.from_numpy(el)
-        e.common_step_counter = 96398   # an applied external-force window: 96,400 draw, 96,401.. apply
+        e.common_step_counter = 96397   # an applied external-force window: 96,400 draw, 96,401.. apply
+        #                                (counter residue mod 4 kept: the lag rings are counter-indexed)
     g = torch.Generator(device="cuda:0").manual_seed(1)
-    resets, applied = 0, 0.0
-    for t in range(8):
+    resets, applied, drawn = 0, 0.0, 0.0
+    for t in range(9):
         a = torch.randn(n, 12, device="cuda:0", generator=g)
         for e in envs:
             e.step(a)
         torch.cuda.synchronize()
+        bad = []
         for f in FIELDS:
             x, y = getattr(envs[0], f), getattr(envs[1], f)
-            assert torch.equal(x, y) or (x.is_floating_point() and torch.equal(torch.nan_to_num(x, 7.0),
-                                                                               torch.nan_to_num(y, 7.0))), \
-                f"{f} differs at step {t}: max |d| {(x.double() - y.double()).abs().nan_to_num(0).max().item():.3g}"
+            if not (torch.equal(x, y) or (x.is_floating_point() and torch.equal(torch.nan_to_num(x, 7.0),
+                                                                                torch.nan_to_num(y, 7.0)))):
+                bad.append(f"{f} (max |d| {(x.double() - y.double()).abs().nan_to_num(0).max().item():.3g})")
+        assert not bad, f"step {t}: " + ", ".join(bad)
         resets += int(envs[0].reset_buf.sum())
         applied = max(applied, float(envs[0].applied_force.abs().max()))
+        drawn = max(drawn, float(envs[0].ext_forces.abs().max()))
     assert resets > 0, "no in-epilogue reset"
-    assert applied > 0, "no external force was applied"
+    assert drawn > 0, "the external-force window was not reached"
+    # forces act on standing envs only; at 777 envs early in their episodes none may stand
+    assert applied > 0 or n < 8192, "no external force was applied"
     envs[0].set_substep_log(False)

@@ -25,7 +25,7 @@ class Model(C.Structure):
         ("n_contact", i32),
         ("k_contact", f32), ("d_contact", f32), ("friction_vs", f32), ("k_limit", f32), ("d_limit", f32),
         ("gravity", f32), ("ground_friction", f32), ("ground_restitution", f32), ("base_init_state", f32 * 13),
-        ("self_collisions", i32), ("self_box", (f32 * 6) * 4), ("bounce_threshold", f32),
+        ("self_collisions", i32), ("self_capsule", (f32 * 7) * 4), ("bounce_threshold", f32),
     ]
 
 

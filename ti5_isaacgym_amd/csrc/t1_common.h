@@ -34,7 +34,11 @@ T1_HD float uniform01(uint32_t seed, uint32_t env, uint32_t ctr, uint32_t slot) 
 T1_HD float rand_float(float lo, float hi, uint32_t seed, uint32_t env, uint32_t ctr, uint32_t slot) {
   float u = uniform01(seed, env, ctr, slot);
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __fadd_rn(__fmul_rn(hi - lo, u), lo);
+  // __fmul_rn / __fadd_rn alone are contracted into one v_fmac by the compiler (r03: ext-force draws U(-300, 600)
+  // off by up to 5e-5 from the two-rounding value); the empty asm makes the rounded product opaque to that fusion
+  float p = __fmul_rn(hi - lo, u);
+  asm volatile("" : "+v"(p));
+  return __fadd_rn(p, lo);
 #else
   volatile float p = (hi - lo) * u;
   return p + lo;
@@ -57,7 +61,11 @@ T1_HD float uniform01(RngKey k, uint32_t slot) { return (float)(hash_k(k, slot) 
 T1_HD float rand_float(float lo, float hi, RngKey k, uint32_t slot) {
   float u = uniform01(k, slot);
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __fadd_rn(__fmul_rn(hi - lo, u), lo);
+  // __fmul_rn / __fadd_rn alone are contracted into one v_fmac by the compiler (r03: ext-force draws U(-300, 600)
+  // off by up to 5e-5 from the two-rounding value); the empty asm makes the rounded product opaque to that fusion
+  float p = __fmul_rn(hi - lo, u);
+  asm volatile("" : "+v"(p));
+  return __fadd_rn(p, lo);
 #else
   volatile float p = (hi - lo) * u;
   return p + lo;

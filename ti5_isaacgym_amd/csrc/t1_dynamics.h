@@ -48,9 +48,9 @@ constexpr int T1_POINTS_PER_BODY = 8;
 constexpr int T1_LEG_AXIS[NLEG] = {2, 0, 1, 1, 1, 0};
 
 
-// A self-collision box in its link frame: center and half extents (t1env_model.self_box).
-struct SelfBox {
-  float c[3], h[3];
+// A self-collision capsule in its link frame: segment a-b and radius r (t1env_model.self_capsule).
+struct SelfCapsule {
+  float a[3], b[3], r;
 };
 
 // Model in the form the kernels consume (built from t1env_model at create time).
@@ -69,7 +69,7 @@ struct DynModel {
   float k_contact, d_contact, friction_vs, k_limit, d_limit, gravity;
   float ground_friction, ground_restitution;
   float base_init_state[13];
-  SelfBox self_box[2][2];  // [leg][0 shank, 1 foot]
+  SelfCapsule self_cap[2][2];  // [leg][0 shank, 1 foot]
   int32_t self_collisions;
   float bounce_threshold;  // restitution acts on contacts approaching faster than this [m/s]
 };
@@ -629,106 +629,82 @@ T1_HD V3<R> body_contact_force(const DynModel& M, const Terrain& T, int b, const
 // t1_dh_stand_config.py:51; PhysX collides every non-adjacent pair of shapes of the articulation).  The bodies that
 // carry shapes are the base box, the shanks and the feet; the base box cannot be reached by a shank or a foot within
 // the joint limits, which leaves the pairs {left, right} x {shank, foot} across the legs and the
-// shank-foot pair within a leg (not adjacent: the ankle-pitch link lies between them).  Volumes: the shank boxes
-// themselves and the foot hulls' bounding boxes (SelfBox).  Contacts: every corner of one box inside the other,
-// with the depth and normal of the nearest face of the box it is in, under the same compliant law as the terrain
-// (contact_point, with the other body's point velocity as the surface velocity): each body's own terms are
-// implicit (folded into its composite like a terrain contact), the other body's motion enters explicitly.
+// shank-foot pair within a leg (not adjacent: the ankle-pitch link lies between them).  Volumes: each shank box and
+// each foot hull's bounding box as a capsule along its long axis (SelfCapsule, utils/urdf.py), the representation
+// legged-robot self-collision usually takes: one closest-point query per pair.  A pair whose capsules overlap is one
+// contact at the middle of the overlap, under the same compliant law as the terrain (contact_point, with the other
+// body's point velocity as the surface velocity): each body's own terms are implicit (folded into its composite like
+// a terrain contact), the other body's motion enters explicitly, and each leg's helper evaluates the pair for its own
+// body (the reaction on the other body is the other helper's evaluation of the same pair).
 // ---------------------------------------------------------------------------------------------------
-template <typename R> struct BoxPose {
-  M3<R> Rb;   // the body's (= the box's) rotation, world axes
-  V3<R> c;    // box center about O
-  R h[3];     // half extents
+template <typename R> T1_HD R clamp01(R x) { return x < R(0) ? R(0) : (x > R(1) ? R(1) : x); }
+// Closest points c1, c2 of the segments p1-q1 and p2-q2 (non-degenerate), by selects (no divergent branch).  Crossing
+// segments: the unconstrained minimum, then clamped (the convex 2-parameter problem's solution).  Segments within
+// ~1.8 deg of parallel (sin^2 < 1e-3; the crossing point is ill-conditioned there, and both legs' shanks are parallel
+// whenever the legs mirror each other): the middle of the overlap of segment 2's projection onto segment 1.
+template <typename R>
+T1_HD void closest_segments(V3<R> p1, V3<R> q1, V3<R> p2, V3<R> q2, V3<R>& c1, V3<R>& c2) {
+  const V3<R> d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
+  const R a = dot(d1, d1), e = dot(d2, d2), f = dot(d2, r), c = dot(d1, r), b = dot(d1, d2);
+  const R den = a * e - b * b, ia = R(1) / a;
+  const bool parallel = den < R(1e-3) * a * e;
+  // crossing
+  R sx = clamp01((b * f - c * e) / (parallel ? R(1) : den));
+  const R tx = (b * sx + f) / e;
+  sx = tx < R(0) ? clamp01(-c * ia) : (tx > R(1) ? clamp01((b - c) * ia) : sx);
+  // parallel: segment 2's ends project to s = -c / a and (b - c) / a
+  const R s0 = -c * ia, s1 = (b - c) * ia;
+  const R sp = R(0.5) * (clamp01(s0 < s1 ? s0 : s1) + clamp01(s0 < s1 ? s1 : s0));
+  const R sv = parallel ? sp : sx;
+  c1 = p1 + sv * d1;
+  c2 = p2 + clamp01(dot(c1 - p2, d2) / e) * d2;
+}
+// a capsule in world axes about O: segment p-q, radius r
+template <typename R> struct CapPose {
+  V3<R> p, q;
+  R r;
 };
-template <typename R> T1_HD BoxPose<R> box_pose(const SelfBox& b, const M3<R>& Rb, V3<R> pb) {
-  BoxPose<R> P;
-  P.Rb = Rb;
-  P.c = pb + mul(Rb, v3<R>(R(b.c[0]), R(b.c[1]), R(b.c[2])));
-  P.h[0] = R(b.h[0]); P.h[1] = R(b.h[1]); P.h[2] = R(b.h[2]);
-  return P;
-}
-template <typename R> T1_HD V3<R> mat_col(const M3<R>& A, int i) { return v3<R>(A.m[i], A.m[3 + i], A.m[6 + i]); }
-template <typename R> T1_HD R fabs_r(R x) { return x < R(0) ? -x : x; }
-// separating-axis test over the 6 face normals: false when the boxes are certainly apart (the 9 edge-edge axes are
-// not tested, so "may touch" can be true for boxes that an edge axis separates: the corner tests then find nothing)
-template <typename R> T1_HD bool boxes_may_touch(const BoxPose<R>& A, const BoxPose<R>& B) {
-  R C[3][3], t[3];
-  const V3<R> d = B.c - A.c;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const V3<R> ai = mat_col(A.Rb, i);
-    t[i] = dot(ai, d);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) C[i][j] = fabs_r(dot(ai, mat_col(B.Rb, j)));
-  }
-  bool sep = false;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-    sep = sep || fabs_r(t[i]) > A.h[i] + B.h[0] * C[i][0] + B.h[1] * C[i][1] + B.h[2] * C[i][2];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const R tj = t[0] * dot(mat_col(A.Rb, 0), mat_col(B.Rb, j)) + t[1] * dot(mat_col(A.Rb, 1), mat_col(B.Rb, j)) +
-                 t[2] * dot(mat_col(A.Rb, 2), mat_col(B.Rb, j));
-    sep = sep || fabs_r(tj) > A.h[0] * C[0][j] + A.h[1] * C[1][j] + A.h[2] * C[2][j] + B.h[j];
-  }
-  return !sep;
-}
-// every corner x of box P strictly inside box T: hit(x, n, pen), n the unit normal of T's nearest face (pushing the
-// corner out of T), pen the corner's distance to that face.  The corners are c +- u0 +- u1 +- u2 (u_i = h_i axis_i),
-// and their coordinates in T's frame follow from four matrix-vector products.
-template <typename R, typename Hit> T1_HD void corners_in_box(const BoxPose<R>& P, const BoxPose<R>& T, Hit&& hit) {
-  V3<R> u[3], lu[3];
-  const V3<R> dc = P.c - T.c;
-  const V3<R> lc = v3<R>(dot(mat_col(T.Rb, 0), dc), dot(mat_col(T.Rb, 1), dc), dot(mat_col(T.Rb, 2), dc));
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    u[i] = P.h[i] * mat_col(P.Rb, i);
-    lu[i] = v3<R>(dot(mat_col(T.Rb, 0), u[i]), dot(mat_col(T.Rb, 1), u[i]), dot(mat_col(T.Rb, 2), u[i]));
-  }
-  // a rolled loop: one copy of the hit's contact math per call site (the corner signs are selects, no array index)
-#pragma unroll 1
-  for (int k = 0; k < 8; ++k) {
-    const R s0 = (k & 1) ? R(1) : R(-1), s1 = (k & 2) ? R(1) : R(-1), s2 = (k & 4) ? R(1) : R(-1);
-    const V3<R> l = lc + s0 * lu[0] + s1 * lu[1] + s2 * lu[2];
-    const R d0 = T.h[0] - fabs_r(l.x), d1 = T.h[1] - fabs_r(l.y), d2 = T.h[2] - fabs_r(l.z);
-    if (d0 > R(0) && d1 > R(0) && d2 > R(0)) {
-      const int ax = (d0 <= d1 && d0 <= d2) ? 0 : (d1 <= d2 ? 1 : 2);
-      const R pen = ax == 0 ? d0 : (ax == 1 ? d1 : d2);
-      const R sg = (ax == 0 ? l.x : (ax == 1 ? l.y : l.z)) < R(0) ? R(-1) : R(1);
-      // the face normal by selects (a runtime index into the rotation's registers would put them in scratch)
-      const V3<R> c0 = mat_col(T.Rb, 0), c1 = mat_col(T.Rb, 1), c2 = mat_col(T.Rb, 2);
-      const V3<R> n = sg * (ax == 0 ? c0 : (ax == 1 ? c1 : c2));
-      hit(P.c + s0 * u[0] + s1 * u[1] + s2 * u[2], n, pen);
-    }
-  }
+template <typename R> T1_HD CapPose<R> cap_pose(const SelfCapsule& c, const M3<R>& Rb, V3<R> pb) {
+  return CapPose<R>{pb + mul(Rb, v3<R>(R(c.a[0]), R(c.a[1]), R(c.a[2]))),
+                    pb + mul(Rb, v3<R>(R(c.b[0]), R(c.b[1]), R(c.b[2]))), R(c.r)};
 }
 template <typename R> T1_HD V3<R> point_velocity(const R V[6], V3<R> x) {
   return v3<R>(V[3], V[4], V[5]) + cross(v3<R>(V[0], V[1], V[2]), x);
 }
-// the self-contact terms one body (box O, velocity Vo) receives from another (box X, velocity Vx): O's corners in X
-// (normal pushing O out) and X's corners in O (the reaction: normal reversed), accumulated like terrain contacts
+// The contact of capsule O (own body) with capsule X, if they overlap: x the middle of the overlap, n the unit normal
+// pushing O out, pen the overlap depth.  Returns false when apart.
 template <typename R>
-T1_HD void self_pair_terms(const DynModel& M, const BoxPose<R>& O, const R Vo[6], const BoxPose<R>& X, const R Vx[6],
-                           R mu, R dt, Sym6<R>& A, R g[6], PointMoments<R>& fric) {
-  if (!boxes_may_touch(O, X)) return;
-  corners_in_box(O, X, [&](V3<R> x, V3<R> n, R pen) {
-    contact_point(M, x, n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
-  });
-  corners_in_box(X, O, [&](V3<R> x, V3<R> n, R pen) {
-    contact_point(M, x, R(-1) * n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
-  });
+T1_HD bool capsule_contact(const CapPose<R>& O, const CapPose<R>& X, V3<R>& x, V3<R>& n, R& pen) {
+  V3<R> co, cx;
+  closest_segments(O.p, O.q, X.p, X.q, co, cx);
+  const V3<R> d = co - cx;
+  const R d2 = dot(d, d), rs = O.r + X.r;
+  if (!(d2 < rs * rs)) return false;
+  const R dist = fsqrt(d2);
+  // axes crossing (dist ~ 0): push apart along the line between the segment midpoints (fallback +z)
+  const V3<R> m = R(0.5) * (O.p + O.q) - R(0.5) * (X.p + X.q);
+  const R mm = dot(m, m);
+  n = dist > R(1e-6) ? (R(1) / dist) * d : (mm > R(1e-12) ? rcp(fsqrt(mm)) * m : v3<R>(R(0), R(0), R(1)));
+  pen = rs - dist;
+  x = cx + (X.r - R(0.5) * pen) * n;
+  return true;
 }
-// the net self-contact force on body O (the report): the explicit force of each of those contacts
+// the self-contact terms one body (capsule O, velocity Vo) receives from another (capsule X, velocity Vx)
 template <typename R>
-T1_HD V3<R> self_pair_force(const DynModel& M, const BoxPose<R>& O, const R Vo[6], const BoxPose<R>& X, const R Vx[6],
+T1_HD void self_pair_terms(const DynModel& M, const CapPose<R>& O, const R Vo[6], const CapPose<R>& X, const R Vx[6],
+                           R mu, R dt, Sym6<R>& A, R g[6], PointMoments<R>& fric) {
+  V3<R> x, n;
+  R pen;
+  if (capsule_contact(O, X, x, n, pen)) contact_point(M, x, n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
+}
+// the self-contact force on body O (the report): that contact's explicit force
+template <typename R>
+T1_HD V3<R> self_pair_force(const DynModel& M, const CapPose<R>& O, const R Vo[6], const CapPose<R>& X, const R Vx[6],
                             R mu) {
-  V3<R> F = v3<R>(R(0), R(0), R(0));
-  if (!boxes_may_touch(O, X)) return F;
-  corners_in_box(O, X, [&](V3<R> x, V3<R> n, R pen) { F = F + point_contact_force(M, x, n, pen, Vo, mu, R(0), point_velocity(Vx, x)); });
-  corners_in_box(X, O, [&](V3<R> x, V3<R> n, R pen) {
-    F = F + point_contact_force(M, x, R(-1) * n, pen, Vo, mu, R(0), point_velocity(Vx, x));
-  });
-  return F;
+  V3<R> x, n;
+  R pen;
+  if (!capsule_contact(O, X, x, n, pen)) return v3<R>(R(0), R(0), R(0));
+  return point_contact_force(M, x, n, pen, Vo, mu, R(0), point_velocity(Vx, x));
 }
 // Pose (rotation, origin about O) and spatial velocity of one contact body, as the kinematics publish them
 template <typename R> struct BodyKin {
@@ -743,11 +719,11 @@ template <typename R> struct BodyKin {
 template <typename R>
 T1_HD void self_terms_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2], const BodyKin<R> (&Kx)[2], R mu, R dt,
                           Sym6<R> (&C)[2], R (&c)[2][6]) {
-  BoxPose<R> Po[2], Px[2];
+  CapPose<R> Po[2], Px[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    Po[s] = box_pose(M.self_box[own][s], Ko[s].Rb, Ko[s].p);
-    Px[s] = box_pose(M.self_box[1 - own][s], Kx[s].Rb, Kx[s].p);
+    Po[s] = cap_pose(M.self_cap[own][s], Ko[s].Rb, Ko[s].p);
+    Px[s] = cap_pose(M.self_cap[1 - own][s], Kx[s].Rb, Kx[s].p);
   }
   // one instantiation per body (a plain loop this large is not unrolled, and its register arrays would go to scratch)
   auto body = [&](auto sc) {
@@ -766,11 +742,11 @@ T1_HD void self_terms_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2],
 template <typename R>
 T1_HD void self_forces_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2], const BodyKin<R> (&Kx)[2], R mu,
                            V3<R> (&F)[2]) {
-  BoxPose<R> Po[2], Px[2];
+  CapPose<R> Po[2], Px[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    Po[s] = box_pose(M.self_box[own][s], Ko[s].Rb, Ko[s].p);
-    Px[s] = box_pose(M.self_box[1 - own][s], Kx[s].Rb, Kx[s].p);
+    Po[s] = cap_pose(M.self_cap[own][s], Ko[s].Rb, Ko[s].p);
+    Px[s] = cap_pose(M.self_cap[1 - own][s], Kx[s].Rb, Kx[s].p);
   }
   auto body = [&](auto sc) {
     constexpr int s = decltype(sc)::value;

@@ -61,12 +61,18 @@ inline const char* make_dyn_model(const t1env_model* model, DynModel* dm) {
   dm->ground_friction = model->ground_friction; dm->ground_restitution = model->ground_restitution;
   for (int i = 0; i < 13; ++i) dm->base_init_state[i] = model->base_init_state[i];
   dm->self_collisions = model->self_collisions != 0;
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    SelfCapsule& c = dm->self_cap[i / 2][i % 2];
+    float len2 = 0.0f;
     for (int k = 0; k < 3; ++k) {
-      dm->self_box[i / 2][i % 2].c[k] = model->self_box[i][k];
-      dm->self_box[i / 2][i % 2].h[k] = model->self_box[i][3 + k];
-      if (dm->self_collisions && !(model->self_box[i][3 + k] > 0.0f)) return "self_box half extents must be positive";
+      c.a[k] = model->self_capsule[i][k];
+      c.b[k] = model->self_capsule[i][3 + k];
+      len2 += (c.b[k] - c.a[k]) * (c.b[k] - c.a[k]);
     }
+    c.r = model->self_capsule[i][6];
+    if (dm->self_collisions && !(c.r > 0.0f && len2 > 1e-8f))
+      return "self_capsule needs a positive radius and two distinct segment ends";
+  }
   dm->bounce_threshold = model->bounce_threshold;
   if (!(dm->bounce_threshold >= 0.0f)) return "bounce_threshold must be >= 0";
   return nullptr;

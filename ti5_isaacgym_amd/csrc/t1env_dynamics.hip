@@ -710,10 +710,11 @@ __device__ __forceinline__ void helper_report_contacts_at(const DynModel& M, con
   }
 }
 
-// LOG (tests only, fused step): the substep log (t1env_substep_log) -- each leg wave writes its joints' torques and
-// post-substep (q, qd), leg wave 0 the post-substep root row; a separate instantiation, so the product kernel is
-// unchanged by it.
-template <bool HF, bool FUSED, bool LOG = false>
+// The substep log (tests only: t1env_substep_log; LG.root == nullptr when off) -- each leg wave writes its joints'
+// torques and post-substep (q, qd), leg wave 0 the post-substep root row.  A run-time switch, not a template
+// parameter: the logged and the product step are the same code object, so the log cannot change the arithmetic
+// (r03: a separate LOG instantiation differed from the product's by up to 2.5e-5 in obs, compiler contraction).
+template <bool HF, bool FUSED>
 #ifdef T1_DYN4_WAVES_PER_EU1  // A/B: tell the scheduler one wave per SIMD is the target (it is, by registers)
 #define T1_DYN4_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
 #else
@@ -766,6 +767,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
       BaseFrame<float> F;
       BodyKin<float> Ko[2], Kx[2];
       helper_kinematics(M, P, Po, lane, leg, F, Ko, Kx);
+      T1_PROF_MARK(20);
       const V3<float> abs = F.abs;
       const int32_t bound_sh = terrain_bound_raw_any(T, Ko[0].p.x + abs.x, Ko[0].p.y + abs.y);
       const int32_t bound_base = terrain_bound_raw_any(T, abs.x, abs.y);
@@ -778,6 +780,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
         for (int j = 0; j < 6; ++j) cs[i][j] = 0.0f;
       }
       if (M.self_collisions) self_terms_leg(M, leg, Ko, Kx, mu_self, dt, Cs, cs);
+      T1_PROF_MARK(21);
       body_terms_at(M, T, Ko[1], lane, 1 + 6 * leg + K_FOOT, abs, mu, e, vi_ft, dt, Cs[1], cs[1], lds.ct[leg] + XCH,
                     T1_NO_BOUND);
       body_terms_at(M, T, Ko[0], lane, 1 + 6 * leg + K_SHANK, abs, mu, e, vi_sh, dt, Cs[0], cs[0], lds.ct[leg], bound_sh);
@@ -909,7 +912,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     integrate_base(sb, r, dt);
     integrate_leg(M, leg, q, qd, dq, dt);
     T1_PROF_MARK(9);
-    if constexpr (LOG) {
+    if (LG.root != nullptr) {  // wave-uniform (a kernel argument)
       if (active) {
         const size_t row = (size_t)sub * N + n;
 #pragma unroll
@@ -1011,16 +1014,7 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
   const SubLog LG = log ? *log : SubLog{};
   const dim3 grid(dyn_blocks + shift_blocks);
   const bool hf = T.type != 0;
-  if (log) {  // the substep log: fused k_dyn4 only (the caller checks)
-    if (!fused) return (int)hipErrorInvalidValue;
-    if (hf)
-      hipLaunchKernelGGL((k_dyn4<true, true, true>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S,
-                         dyn_blocks, FA, LG);
-    else
-      hipLaunchKernelGGL((k_dyn4<false, true, true>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S,
-                         dyn_blocks, FA, LG);
-    return (int)hipGetLastError();
-  }
+  if (log && !fused) return (int)hipErrorInvalidValue;  // the substep log: fused steps only (the caller checks)
 #define T1_LAUNCH(HF, FU) \
   hipLaunchKernelGGL((k_dyn4<HF, FU>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA, LG)
   if (fused) { if (hf) T1_LAUNCH(true, true); else T1_LAUNCH(false, true); }

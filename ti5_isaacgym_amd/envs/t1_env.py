@@ -23,7 +23,7 @@ from .. import _lib
 from ..algo.vec_env import VecEnv
 from ..utils.helpers import class_to_dict
 from ..utils.terrain import Terrain
-from ..utils.urdf import load_model
+from ..utils.urdf import load_model, self_capsules
 
 REWARD_NAMES = sorted(["action_smoothness", "base_acc", "base_height", "collision", "default_joint_pos", "dof_acc",
                        "dof_vel", "feet_air_time", "feet_clearance", "feet_contact_forces", "feet_contact_number",
@@ -103,12 +103,12 @@ def build_model(cfg, urdf_path=None):
 
 
 def set_self_collision(m, tab, enabled=True, bounce_threshold=0.5):
-    """The model's self-collision boxes (utils/urdf.py self_box: left shank, left foot, right shank, right foot) and
-    the restitution bounce threshold (sim.physx.bounce_threshold_velocity, t1_dh_stand_config.py:171)."""
+    """The model's self-collision capsules (utils/urdf.py self_capsules: left shank, left foot, right shank, right
+    foot) and the restitution bounce threshold (sim.physx.bounce_threshold_velocity, t1_dh_stand_config.py:171)."""
     m.self_collisions = int(bool(enabled))
-    for i, box in enumerate(tab["self_box"]):
-        for k in range(6):
-            m.self_box[i][k] = box[k]
+    for i, cap in enumerate(self_capsules(tab)):
+        for k in range(7):
+            m.self_capsule[i][k] = cap[k]
     m.bounce_threshold = float(bounce_threshold)
 
 

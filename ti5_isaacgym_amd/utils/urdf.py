@@ -189,6 +189,22 @@ def compile_model(urdf_path):
     }
 
 
+def self_capsules(tab):
+    """The self-collision capsules of left shank, left foot, right shank, right foot, from the model's boxes
+    (``self_box``): along the box's longest axis, radius the smaller of its two cross-section half extents (the shank's
+    0.05 m square section; the foot's lateral half width, the direction the feet meet each other in), segment ends
+    inset by the radius so the capsule spans the box's length.  Rows: a (3), b (3), radius, link frame."""
+    out = []
+    for box in tab["self_box"]:
+        c, h = np.asarray(box[:3], float), np.asarray(box[3:], float)
+        ax = int(np.argmax(h))
+        r = float(min(h[k] for k in range(3) if k != ax))
+        e = np.zeros(3)
+        e[ax] = max(h[ax] - r, 1e-3)
+        out.append([float(x) for x in np.concatenate([c - e, c + e, [r]])])
+    return out
+
+
 def load_model(urdf_path=None):
     """Compiled tables: from a URDF when given (and present), else the committed t1_model.json."""
     import json

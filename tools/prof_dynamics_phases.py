@@ -34,7 +34,8 @@ BUCKETS += SUB
 BUCKETS4 += SUB
 # the helper waves reuse ids 16-18 inside body_contact_np (they never run the epilogue)
 HELPER_SUB = {16: "contacts: transforms + height queries (issue)", 17: "contacts: height-load latency",
-              18: "contacts: contact math (points in contact)"}
+              18: "contacts: contact math (points in contact)", 20: "helper kinematics (own + other leg)",
+              21: "self-collision terms"}
 NB = len(BUCKETS)
 NW = 4
 
@@ -46,6 +47,7 @@ def main():
     p.add_argument("--num-envs", type=int, default=8192)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--split", action="store_true", help="time the split path (k_dynamics without epilogue)")
+    p.add_argument("--no-self-collision", action="store_true", help="asset.self_collisions = 1 (A/B)")
     a = p.parse_args()
     sys.path.insert(0, REPO)
     if a.build:
@@ -55,7 +57,10 @@ def main():
     os.environ["T1ENV_LIB"] = PROF_LIB
     import torch
     from ti5_isaacgym_amd import make_t1_env
-    env = make_t1_env(num_envs=a.num_envs, mesh_type=a.mesh, seed=5, device="cuda:0")
+    def hook(cfg):
+        if a.no_self_collision:
+            cfg.asset.self_collisions = 1
+    env = make_t1_env(num_envs=a.num_envs, mesh_type=a.mesh, seed=5, device="cuda:0", cfg_hook=hook)
     env.set_fused(not a.split)
     lib = ctypes.CDLL(PROF_LIB)
     buf = (ctypes.c_ulonglong * (NW * NB))()
