@@ -75,6 +75,12 @@ def scenario(kind, n, rng, tab):
         q[:, 7] = rng.uniform(0.08, 0.17, n)
         q[:, 0] = rng.uniform(-0.3, 0.3, n)
         q[:, 6] = rng.uniform(-0.3, 0.3, n)
+        # every third robot mirrors its legs: the feet (and shanks) run near parallel, the capsules' overlap-midpoint
+        # rule (and the fixed pair order both legs evaluate it in)
+        mir = np.arange(n) % 3 == 0
+        q[mir, 6] = q[mir, 0]
+        q[mir, 7] = -q[mir, 1]
+        q[mir, 8:12] = q[mir, 2:6]
     if kind == "limits":
         lim = np.asarray(tab["limits"])
         j = rng.integers(0, 12, n)
@@ -191,10 +197,17 @@ def test_self_collision_scenario_has_self_contacts(setup):
     rob = ContactRobot(tab, solver={})
     rng = np.random.default_rng(1)
     root, dof = scenario("self", 12, rng, tab)
+    from oracle.dynamics_ref import _capsules
+    caps, parallel = _capsules(tab), 0
     for i in range(12):
         c = rob.contacts(root[i, 0:3] + np.array([0, 0, 5.0]), quat_to_R(root[i, 3:7]), dof[i, :, 0], None,
                          0.5, 0.0, 0.5, 0.0)
         assert len(c) > 0 and all(x[4] is not None for x in c), i
+        Rs, ps, _ = rob.fk(root[i, 0:3], quat_to_R(root[i, 3:7]), dof[i, :, 0])
+        dl, dr = (Rs[b] @ (caps[b][1] - caps[b][0]) for b in (6, 12))
+        touching = any({x[0], x[4][0]} == {6, 12} for x in c)
+        parallel += touching and np.linalg.norm(np.cross(dl, dr)) ** 2 < 1e-3 * (dl @ dl) * (dr @ dr)
+    assert parallel > 0, "no near-parallel foot contact in the scenario"
 
 
 def test_restitution_makes_impacts_bounce(setup):

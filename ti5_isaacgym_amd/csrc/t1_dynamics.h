@@ -672,11 +672,14 @@ template <typename R> T1_HD V3<R> point_velocity(const R V[6], V3<R> x) {
   return v3<R>(V[3], V[4], V[5]) + cross(v3<R>(V[0], V[1], V[2]), x);
 }
 // The contact of capsule O (own body) with capsule X, if they overlap: x the middle of the overlap, n the unit normal
-// pushing O out, pen the overlap depth.  Returns false when apart.
+// pushing O out, pen the overlap depth.  Returns false when apart.  o_first: O is the pair's first body (the left leg's
+// across the legs, the shank within a leg); the segments go to closest_segments in that fixed order, so both bodies'
+// evaluations of a pair use the same closest points (the near-parallel rule is not symmetric in its arguments).
 template <typename R>
-T1_HD bool capsule_contact(const CapPose<R>& O, const CapPose<R>& X, V3<R>& x, V3<R>& n, R& pen) {
-  V3<R> co, cx;
-  closest_segments(O.p, O.q, X.p, X.q, co, cx);
+T1_HD bool capsule_contact(const CapPose<R>& O, const CapPose<R>& X, bool o_first, V3<R>& x, V3<R>& n, R& pen) {
+  V3<R> c1, c2;
+  closest_segments(o_first ? O.p : X.p, o_first ? O.q : X.q, o_first ? X.p : O.p, o_first ? X.q : O.q, c1, c2);
+  const V3<R> co = o_first ? c1 : c2, cx = o_first ? c2 : c1;
   const V3<R> d = co - cx;
   const R d2 = dot(d, d), rs = O.r + X.r;
   if (!(d2 < rs * rs)) return false;
@@ -692,18 +695,18 @@ T1_HD bool capsule_contact(const CapPose<R>& O, const CapPose<R>& X, V3<R>& x, V
 // the self-contact terms one body (capsule O, velocity Vo) receives from another (capsule X, velocity Vx)
 template <typename R>
 T1_HD void self_pair_terms(const DynModel& M, const CapPose<R>& O, const R Vo[6], const CapPose<R>& X, const R Vx[6],
-                           R mu, R dt, Sym6<R>& A, R g[6], PointMoments<R>& fric) {
+                           bool o_first, R mu, R dt, Sym6<R>& A, R g[6], PointMoments<R>& fric) {
   V3<R> x, n;
   R pen;
-  if (capsule_contact(O, X, x, n, pen)) contact_point(M, x, n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
+  if (capsule_contact(O, X, o_first, x, n, pen)) contact_point(M, x, n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
 }
 // the self-contact force on body O (the report): that contact's explicit force
 template <typename R>
 T1_HD V3<R> self_pair_force(const DynModel& M, const CapPose<R>& O, const R Vo[6], const CapPose<R>& X, const R Vx[6],
-                            R mu) {
+                            bool o_first, R mu) {
   V3<R> x, n;
   R pen;
-  if (!capsule_contact(O, X, x, n, pen)) return v3<R>(R(0), R(0), R(0));
+  if (!capsule_contact(O, X, o_first, x, n, pen)) return v3<R>(R(0), R(0), R(0));
   return point_contact_force(M, x, n, pen, Vo, mu, R(0), point_velocity(Vx, x));
 }
 // Pose (rotation, origin about O) and spatial velocity of one contact body, as the kinematics publish them
@@ -730,9 +733,9 @@ T1_HD void self_terms_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2],
     constexpr int s = decltype(sc)::value;
     PointMoments<R> fric;
     moments_zero(fric);
-    self_pair_terms(M, Po[s], Ko[s].V, Px[0], Kx[0].V, mu, dt, C[s], c[s], fric);
-    self_pair_terms(M, Po[s], Ko[s].V, Px[1], Kx[1].V, mu, dt, C[s], c[s], fric);
-    self_pair_terms(M, Po[s], Ko[s].V, Po[1 - s], Ko[1 - s].V, mu, dt, C[s], c[s], fric);
+    self_pair_terms(M, Po[s], Ko[s].V, Px[0], Kx[0].V, own == 0, mu, dt, C[s], c[s], fric);
+    self_pair_terms(M, Po[s], Ko[s].V, Px[1], Kx[1].V, own == 0, mu, dt, C[s], c[s], fric);
+    self_pair_terms(M, Po[s], Ko[s].V, Po[1 - s], Ko[1 - s].V, s == 0, mu, dt, C[s], c[s], fric);
     moments_flush(fric, C[s]);
   };
   body(std::integral_constant<int, 0>{});
@@ -750,8 +753,9 @@ T1_HD void self_forces_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2]
   }
   auto body = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
-    F[s] = self_pair_force(M, Po[s], Ko[s].V, Px[0], Kx[0].V, mu) + self_pair_force(M, Po[s], Ko[s].V, Px[1], Kx[1].V, mu) +
-           self_pair_force(M, Po[s], Ko[s].V, Po[1 - s], Ko[1 - s].V, mu);
+    F[s] = self_pair_force(M, Po[s], Ko[s].V, Px[0], Kx[0].V, own == 0, mu) +
+           self_pair_force(M, Po[s], Ko[s].V, Px[1], Kx[1].V, own == 0, mu) +
+           self_pair_force(M, Po[s], Ko[s].V, Po[1 - s], Ko[1 - s].V, s == 0, mu);
   };
   body(std::integral_constant<int, 0>{});
   body(std::integral_constant<int, 1>{});
