@@ -122,3 +122,100 @@ def test_bf16_update_obs_cast_once_is_exact():
     ls_off, ls_on, diff, _, _ = chk.compare_cast_once(r, 77)
     assert list(ls_off) == list(ls_on), (ls_off, ls_on)
     assert diff == 0.0, diff
+
+
+@pytest.mark.parametrize("amp", [None, torch.bfloat16], ids=["fp32", "bf16"])
+def test_graphed_update_matches_eager(amp):
+    """DHPPO.update with its minibatch step replayed as a captured HIP graph (the default on the device) against the
+    eager step: the same storage, permutation and initial weights, three updates with the adaptive learning rate --
+    weights, Adam state, learning rate and losses bit-identical (the same kernels run), and the graph is captured
+    once and follows the storage's in-place refills."""
+    from ti5_isaacgym_amd import task_registry
+    from ti5_isaacgym_amd.algo.dh_policy import ActorCriticDH
+    from ti5_isaacgym_amd.algo.dh_update import DHPPO
+    from ti5_isaacgym_amd.utils.helpers import class_to_dict
+    _, tc = task_registry.get_cfgs("t1_dh_stand")
+    cfg = class_to_dict(tc)
+    N, T, dev = 1024, 24, torch.device("cuda:0")
+    algs = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        ac = ActorCriticDH(235, 47, 219, 12, **cfg["policy"]).to(dev)
+        alg = DHPPO(ac, device=str(dev), amp_dtype=amp, **cfg["algorithm"])
+        alg.graph_update = graphed
+        alg.init_storage(N, T, [3102], [219], [12], history=(47, 66))
+        algs.append(alg)
+    assert algs[0].schedule == "adaptive"
+    g = torch.Generator(device=dev)
+    lrs = []
+    for it in range(3):
+        losses = []
+        for alg in algs:
+            st = alg.storage
+            g.manual_seed(10 + it)
+            for t in (st.obs0, st.frames, st.privileged_observations, st.actions, st.values, st.returns,
+                      st.actions_log_prob, st.mu):
+                t.normal_(generator=g)
+            st.sigma.uniform_(0.5, 1.5, generator=g)
+            st.dones.copy_((torch.rand(st.dones.shape, generator=g, device=dev) < 0.05).to(torch.uint8))
+            st.rewards.normal_(generator=g)
+            st.step = T
+            alg.compute_returns(torch.randn(N, 219, device=dev, generator=g))
+            alg.actor_critic.train()
+            torch.manual_seed(100 + it)
+            losses.append(alg.update())
+        assert losses[0] == losses[1], (it, losses)
+        lrs.append((algs[0].learning_rate, algs[1].learning_rate))
+        assert lrs[-1][0] == lrs[-1][1]
+        for p0, p1 in zip(algs[0].actor_critic.parameters(), algs[1].actor_critic.parameters()):
+            assert torch.equal(p0, p1)
+        for s0, s1 in zip(algs[0].optimizer.state.values(), algs[1].optimizer.state.values()):
+            assert all(torch.equal(s0[k], s1[k]) for k in ("exp_avg", "exp_avg_sq", "step"))
+    assert algs[1]._upd is not None and algs[0]._upd is None
+    print("learning rates", lrs)
+
+
+def test_graphed_update_follows_optimizer_reload():
+    """The same update twice from one snapshot (weights, optimizer.load_state_dict of the saved state, storage, seed),
+    as tools/ppo_amp_check.py and a checkpoint resume do: the loaded Adam state replaces the tensors a captured graph
+    held, so the graph is recaptured and both runs give the same losses and weights."""
+    import copy
+    from ti5_isaacgym_amd import task_registry
+    from ti5_isaacgym_amd.algo.dh_policy import ActorCriticDH
+    from ti5_isaacgym_amd.algo.dh_update import DHPPO
+    from ti5_isaacgym_amd.utils.helpers import class_to_dict
+    _, tc = task_registry.get_cfgs("t1_dh_stand")
+    cfg = class_to_dict(tc)
+    N, T, dev = 512, 24, torch.device("cuda:0")
+    torch.manual_seed(0)
+    ac = ActorCriticDH(235, 47, 219, 12, **cfg["policy"]).to(dev)
+    alg = DHPPO(ac, device=str(dev), **cfg["algorithm"])
+    alg.init_storage(N, T, [3102], [219], [12], history=(47, 66))
+    st = alg.storage
+    g = torch.Generator(device=dev).manual_seed(3)
+    for t in (st.obs0, st.frames, st.privileged_observations, st.actions, st.values, st.returns, st.actions_log_prob,
+              st.mu, st.rewards):
+        t.normal_(generator=g)
+    st.sigma.uniform_(0.5, 1.5, generator=g)
+    alg.compute_returns(torch.randn(N, 219, device=dev, generator=g))
+    for first in (True, False):   # the second snapshot has Adam state (the first has none yet)
+        snap = {k: v.clone() for k, v in vars(st).items() if torch.is_tensor(v)}
+        w0 = [p.detach().clone() for p in ac.parameters()]
+        opt0 = copy.deepcopy(alg.optimizer.state_dict())
+        lr0 = alg.learning_rate
+        runs = []
+        for rep in range(3):
+            with torch.no_grad():
+                for p, p0 in zip(ac.parameters(), w0):
+                    p.copy_(p0)
+            # a copy: load_state_dict adopts device tensors as they are, and the update then changes them in place
+            alg.optimizer.load_state_dict(copy.deepcopy(opt0))
+            alg.learning_rate = lr0
+            for k, v in snap.items():
+                getattr(st, k).copy_(v)
+            st.step = T
+            torch.manual_seed(9)
+            runs.append((alg.update(), [p.detach().clone() for p in ac.parameters()]))
+        for ls, w in runs[1:]:
+            assert ls == runs[0][0], (first, [r[0] for r in runs])
+            assert all(torch.equal(a, b) for a, b in zip(w, runs[0][1]))

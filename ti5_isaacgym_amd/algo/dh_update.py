@@ -9,7 +9,12 @@ backward() and clip_grad_norm_, the KL mean all-reduced before the adaptive lear
 rank-0 weights broadcast at start.  Losses are accumulated on the device and read once per update.
 On a HIP device the rollout's act() (policy sample, value, log-prob) replays a captured HIP graph, one per
 pair of observation buffers the env hands out (its ping-pong buffers): the same kernels as the eager call,
-without the per-kernel launch cost that dominates at one call per env step.
+without the per-kernel launch cost that dominates at one call per env step.  The update's minibatch step (gather,
+forward, losses, backward, clipping, the adaptive learning rate, Adam) replays a captured graph as well: Adam keeps
+its step count and learning rate on the device (capturable, a tensor lr), the adaptive schedule's decision
+(dh_ppo.py:141-151) is taken on the device, and the losses are summed there, so an update has no host sync until its
+mean losses are read.  The first update's first minibatches run eagerly (the warm-up the capture needs), the rest
+replay the graph; eager and graphed steps run the same kernels (bit-identical, tests/test_gpu_ppo.py).
 """
 import contextlib
 import math
@@ -25,6 +30,25 @@ from .dh_policy import ActorCriticDH
 from .rollout import RolloutStorage
 
 
+_GRAPH_RNG_ANCHOR = {}
+
+
+def _init_graph_rng(device):
+    """Let the device generator create its graph-capture state (seed / offset tensors) outside inference mode, and
+    keep it: the generator allocates that state when the first live graph registers with it and drops it when the
+    last one is gone.  The rollout's act() is captured under torch.inference_mode, where it would otherwise be made
+    as inference tensors, which a later capture outside inference mode (the update's) may not update in place.  A
+    one-node graph held for the process anchors it."""
+    device = torch.device(device)
+    if device in _GRAPH_RNG_ANCHOR or torch.is_inference_mode_enabled():
+        return
+    x = torch.empty(1, device=device)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        x.normal_()
+    _GRAPH_RNG_ANCHOR[device] = (graph, x)
+
+
 class DHPPO:
     actor_critic: ActorCriticDH
 
@@ -37,11 +61,18 @@ class DHPPO:
         # backward GEMMs in bf16 (fp32 accumulation, fp32 weights, optimizer and losses); None = fp32 as the reference
         self.amp_dtype = amp_dtype
         self.cast_obs_once = True
-        self.desired_kl, self.schedule, self.learning_rate = desired_kl, schedule, learning_rate
+        self.desired_kl, self.schedule = desired_kl, schedule
+        self._lr = float(learning_rate)
         self.actor_critic = actor_critic
         self.actor_critic.to(self.device)
         self.storage = None
-        self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=learning_rate)
+        cuda = torch.device(device).type == "cuda"
+        # the device learning rate (a 0-d tensor Adam reads) on a HIP device; None on the host (the reference's floats)
+        self._lr_t = torch.tensor(float(learning_rate), device=device) if cuda else None
+        if cuda:
+            self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=self._lr_t, capturable=True, foreach=True)
+        else:
+            self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=learning_rate)
         # created (and checkpointed) like the reference's; its separate step is disabled there as well
         self.state_estimator_optimizer = optim.Adam(self.actor_critic.state_estimator.parameters(), lr=learning_rate)
         self.transition = RolloutStorage.Transition()
@@ -55,8 +86,35 @@ class DHPPO:
         self.grads = dist_util.GradientBucket(self.actor_critic.parameters())
         self.grads.broadcast_params_()
         # graphed rollout act(): {(obs ptr, critic obs ptr, shapes): (graph, static outputs)}; None = eager
-        self.graph_act = torch.device(device).type == "cuda"
+        self.graph_act = cuda
         self._act_graphs = {}
+        # graphed update minibatch step (single process; the DP all-reduce stays eager): (key, graph) once captured
+        self.graph_update = cuda
+        if cuda:
+            _init_graph_rng(device)
+        self._upd = None
+        self._upd_warm = 0
+        self._idx = None
+        self._sums = torch.zeros(3, device=device)
+
+    @property
+    def learning_rate(self):
+        """The current learning rate (the adaptive schedule's; on a HIP device read from the device)."""
+        return float(self._lr_t) if self._lr_t is not None else self._lr
+
+    @learning_rate.setter
+    def learning_rate(self, v):
+        self._lr = float(v)
+        if self._lr_t is not None:
+            self._lr_t.fill_(float(v))
+
+    def _bind_lr(self):
+        """Keep every param group's lr the device tensor (a loaded optimizer state or a caller may have put a float or
+        another tensor there: its value is taken over)."""
+        for g in self.optimizer.param_groups:
+            if g["lr"] is not self._lr_t:
+                self._lr_t.fill_(float(g["lr"]))
+                g["lr"] = self._lr_t
 
     def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape,
                      history=None):
@@ -139,11 +197,20 @@ class DHPPO:
         self.storage.compute_returns(last_values, self.gamma, self.lam)
 
     def _adapt_lr(self, mu, sigma, old_mu, old_sigma):
-        with torch.inference_mode():
+        with torch.no_grad():
             kl = torch.sum(torch.log(sigma / old_sigma + 1.0e-5)
                            + (torch.square(old_sigma) + torch.square(old_mu - mu)) / (2.0 * torch.square(sigma)) - 0.5,
                            axis=-1)
             kl_mean = dist_util.all_reduce_mean_(torch.mean(kl).reshape(1))[0]
+            if self._lr_t is not None:
+                # the same decision on the device (no host sync; capturable): lr / 1.5 floored at 1e-5 above twice the
+                # target KL, lr * 1.5 capped at 1e-2 below half of it (a KL of exactly 0 keeps lr)
+                lr = self._lr_t
+                down = torch.clamp(lr / 1.5, min=1e-5)
+                up = torch.clamp(lr * 1.5, max=1e-2)
+                low = (kl_mean > 0.0) & (kl_mean < self.desired_kl / 2.0)
+                lr.copy_(torch.where(kl_mean > self.desired_kl * 2.0, down, torch.where(low, up, lr)))
+                return
             kl_mean = float(kl_mean)
         if kl_mean > self.desired_kl * 2.0:
             self.learning_rate = max(1e-5, self.learning_rate / 1.5)
@@ -152,47 +219,114 @@ class DHPPO:
         for g in self.optimizer.param_groups:
             g["lr"] = self.learning_rate
 
+    def _minibatch_step(self, batch, amp, mse):
+        """One minibatch of the update: losses, backward, gradient all-reduce, clipping, Adam; the losses summed into
+        self._sums on the device."""
+        ac = self.actor_critic
+        (obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b, hid_b,
+         masks_b) = batch
+        with amp:
+            loss, value_loss, surrogate_loss, se_loss = self._losses(
+                ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b,
+                hid_b, masks_b, mse)
+        self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
+        loss.backward()
+        self.grads.all_reduce_()
+        nn.utils.clip_grad_norm_(ac.parameters(), self.max_grad_norm)
+        self.optimizer.step()
+        self._sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), se_loss.detach()])
+
     def update(self):
         ac = self.actor_critic
-        sums = torch.zeros(3, device=self.device)  # value, surrogate, state-estimator losses
         mse = nn.MSELoss()
-        use_amp = self.amp_dtype is not None and torch.device(self.device).type == "cuda"
-        amp = torch.autocast(device_type="cuda", dtype=self.amp_dtype) if use_amp else contextlib.nullcontext()
+        cuda = torch.device(self.device).type == "cuda"
+        use_amp = self.amp_dtype is not None and cuda
+        # cache_enabled=False: a captured graph must not depend on autocast's weight-cast cache (same values)
+        amp = torch.autocast(device_type="cuda", dtype=self.amp_dtype, cache_enabled=False) if use_amp \
+            else contextlib.nullcontext()
         # under the bf16 update every consumer of the actor observations is a bf16 GEMM: cast them once per update
         # (same values as autocast's per-minibatch casts) unless cast_obs_once is switched off (A/B)
-        gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs,
-                                                obs_dtype=self.amp_dtype if use_amp and self.cast_obs_once else None)
+        obs_dtype = self.amp_dtype if use_amp and self.cast_obs_once else None
+        self._sums.zero_()
+        if self._lr_t is not None:
+            self._bind_lr()
         # the distribution's argument checks are host syncs (three per minibatch) on the device: off for the update,
         # replaced by one finiteness check of the losses below (the reference would raise at the first non-finite mean)
         validate = ac.validate_args
-        if torch.device(self.device).type == "cuda":
+        if cuda:
             ac.validate_args = False
         try:
-            for (obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b,
-                 hid_b, masks_b) in gen:
-                with amp:
-                    loss, value_loss, surrogate_loss, se_loss = self._losses(
-                        ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
-                        old_sigma_b, hid_b, masks_b, mse)
-                self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
-                loss.backward()
-                self.grads.all_reduce_()
-                nn.utils.clip_grad_norm_(ac.parameters(), self.max_grad_norm)
-                self.optimizer.step()
-                sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), se_loss.detach()])
+            if cuda and self.graph_update and not dist_util.active():
+                self._update_graphed(amp, mse, obs_dtype)
+            else:
+                for batch in self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs,
+                                                               obs_dtype=obs_dtype):
+                    self._minibatch_step(batch, amp, mse)
         finally:
             ac.validate_args = validate
         n = self.num_learning_epochs * self.num_mini_batches
         self.storage.clear()
-        mv, ms, mse_ = (sums / n).tolist()
+        mv, ms, mse_ = (self._sums / n).tolist()
         if not all(map(math.isfinite, (mv, ms, mse_))):
             raise ValueError(f"DHPPO.update: non-finite losses (value {mv}, surrogate {ms}, state estimator {mse_})")
         return mv, ms, mse_
 
+    WARMUP_STEPS = 2   # eager minibatch steps (on a side stream) before the capture
+
+    def _update_graphed(self, amp, mse, obs_dtype):
+        """The minibatches of mini_batch_generator, each as (copy its indices into a static buffer, replay)."""
+        st = self.storage
+        mb = st.num_envs * st.num_transitions_per_env // self.num_mini_batches
+        perm = torch.randperm(self.num_mini_batches * mb, requires_grad=False, device=self.device)
+        take = st.minibatch_source(obs_dtype)
+        key = self._graph_key(mb, take)
+        if self._upd is None or self._upd[0] != key:
+            # (re)capture after WARMUP_STEPS eager steps, which also create any missing Adam state: a state tensor
+            # created inside the capture would be re-initialised by every replay
+            self._upd, self._upd_warm = None, 0
+        if self._idx is None or self._idx.numel() != mb:
+            self._idx = torch.empty(mb, dtype=torch.int64, device=self.device)
+        cur = torch.cuda.current_stream(self._idx.device)
+        for _ in range(self.num_learning_epochs):
+            for i in range(self.num_mini_batches):
+                self._idx.copy_(perm[i * mb:(i + 1) * mb])
+                if self._upd is not None:
+                    self._upd[1].replay()
+                elif self._upd_warm < self.WARMUP_STEPS or any(len(self.optimizer.state.get(p, {})) == 0
+                                                               for p in self.grads.params):
+                    side = torch.cuda.Stream(device=self._idx.device)
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        self._minibatch_step(take(self._idx), amp, mse)
+                    cur.wait_stream(side)
+                    self._upd_warm += 1
+                else:
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph):
+                        self._minibatch_step(take(self._idx), amp, mse)
+                    self._upd = (self._graph_key(mb, take), graph)
+                    graph.replay()
+
+    def _graph_key(self, mb, take):
+        """Everything a captured minibatch step holds as a constant: the buffers' addresses (storage sources, Adam's
+        state -- replaced by optimizer.load_state_dict, created lazily by the first step --, the learning rate), the
+        update dtype and the loss hyperparameters."""
+        opt = []
+        for g in self.optimizer.param_groups:
+            opt.append(g["lr"].data_ptr() if torch.is_tensor(g["lr"]) else g["lr"])
+            for p in g["params"]:
+                st = self.optimizer.state.get(p, {})
+                opt.extend(st[k].data_ptr() if k in st else None for k in ("step", "exp_avg", "exp_avg_sq"))
+        return (mb, take.key, tuple(opt), str(self.amp_dtype), self.schedule, self.desired_kl, self.clip_param,
+                self.value_loss_coef, self.entropy_coef, self.max_grad_norm, self.use_clipped_value_loss,
+                self.lin_vel_idx)
+
     def _losses(self, ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
                 old_sigma_b, hid_b, masks_b, mse):
         """The reference's minibatch losses (dh_ppo.py:130-178); the distribution terms in fp32 under autocast."""
-        ac.act(obs_b, masks=masks_b, hidden_states=hid_b[0])
+        # the reference calls ac.act() here for its distribution and drops the sample: the distribution alone (a
+        # sample's std >= 0 check is a host sync, which no graph capture allows; the losses do not use it)
+        ac.update_distribution(ac.actor_input(obs_b))
         est_lin_vel = ac.state_estimator(obs_b[:, -self.num_short_obs:])
         ref_lin_vel = critic_b[:, self.lin_vel_idx:self.lin_vel_idx + 3].clone()
         logp_b = ac.get_actions_log_prob(actions_b)

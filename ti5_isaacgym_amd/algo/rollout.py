@@ -64,6 +64,8 @@ class RolloutStorage:
         self.saved_hidden_states_a = None
         self.saved_hidden_states_c = None
         self.step = 0
+        self._rows = None       # the frame-history rows source (_HistoryRows), rebuilt in place every update
+        self._obs_cast = None   # the full storage's observations cast to the update's dtype, in place every update
 
     def add_transitions(self, t):
         if self.step >= self.num_transitions_per_env:
@@ -101,9 +103,10 @@ class RolloutStorage:
             adv = delta + not_done * gamma * lam * adv
             self.returns[k] = adv + self.values[k]
             next_values = self.values[k]
-        self.advantages = self.returns - self.values
+        # in place: the minibatch sources keep their addresses across updates (a captured update graph reads them)
+        torch.sub(self.returns, self.values, out=self.advantages)
         mean, std = dist_util.global_mean_std(self.advantages)
-        self.advantages = (self.advantages - mean) / (std + 1e-8)
+        self.advantages.sub_(mean).div_(std + 1e-8)
 
     def get_statistics(self):
         done = self.dones
@@ -112,35 +115,53 @@ class RolloutStorage:
         idx = torch.cat((flat.new_tensor([-1], dtype=torch.int64), flat.nonzero(as_tuple=False)[:, 0]))
         return (idx[1:] - idx[:-1]).float().mean(), self.rewards.mean()
 
-    def mini_batch_generator(self, num_mini_batches, num_epochs=8, obs_dtype=None):
-        """The reference's generator (rollout_storage.py:153-173).  obs_dtype (not in the reference): the actor
-        observations are cast once per update to that dtype (the opt-in bf16 update, DHPPO.amp_dtype, whose GEMMs
-        cast every obs-fed operand to bf16 anyway), so each minibatch gathers, unfolds and saves half the bytes."""
-        batch = self.num_envs * self.num_transitions_per_env
-        mb = batch // num_mini_batches
-        perm = torch.randperm(num_mini_batches * mb, requires_grad=False, device=self.device)
+    def minibatch_source(self, obs_dtype=None):
+        """take(idx) -> the reference generator's minibatch tuple (rollout_storage.py:153-173) for the flattened rows
+        idx.  Every source is one of this storage's own buffers (the frame-history rows and the obs cast are rebuilt
+        in place), so take() reads the same addresses every update and can sit inside a captured HIP graph;
+        take.key names those addresses.  obs_dtype (not in the reference): the actor observations are cast once per
+        update to that dtype (the opt-in bf16 update, DHPPO.amp_dtype, whose GEMMs cast every obs-fed operand to bf16
+        anyway), so each minibatch gathers, unfolds and saves half the bytes."""
         flat = lambda x: x.flatten(0, 1)  # noqa: E731
         if self.history is not None:
-            obs = _HistoryRows(self, obs_dtype)
+            dt = obs_dtype if obs_dtype is not None else self.obs0.dtype
+            if self._rows is None or self._rows.seq.dtype != dt:
+                self._rows = _HistoryRows(self, dt)
+            self._rows.refresh(self)
+            obs, okey = self._rows, self._rows.seq.data_ptr()
         else:
             obs = flat(self.observations)
             if obs_dtype is not None and obs.dtype != obs_dtype:
-                obs = obs.to(obs_dtype)
+                if self._obs_cast is None or self._obs_cast.dtype != obs_dtype:
+                    self._obs_cast = torch.empty(obs.shape, dtype=obs_dtype, device=obs.device)
+                obs = self._obs_cast.copy_(obs)
+            okey = obs.data_ptr()
         critic = flat(self.privileged_observations) if self.privileged_observations is not None else obs
         cols = [flat(self.actions), flat(self.values), flat(self.advantages), flat(self.returns),
                 flat(self.actions_log_prob), flat(self.mu), flat(self.sigma)]
         extra = None
         if self.next_proprio_obs is not None:
             extra = (flat(self.next_proprio_obs), flat(self.rewards))
+
+        def take(idx):
+            actions, values, advantages, returns, logp, mu, sigma = (c[idx] for c in cols)
+            if extra is not None:
+                return (extra[0][idx], extra[1][idx], obs[idx], critic[idx], actions, values, advantages, returns,
+                        logp, mu, sigma, (None, None), None)
+            return obs[idx], critic[idx], actions, values, advantages, returns, logp, mu, sigma, (None, None), None
+
+        take.key = (okey, obs_dtype, critic.data_ptr(), *(c.data_ptr() for c in cols))
+        return take
+
+    def mini_batch_generator(self, num_mini_batches, num_epochs=8, obs_dtype=None):
+        """The reference's generator (rollout_storage.py:153-173) over minibatch_source(obs_dtype)."""
+        batch = self.num_envs * self.num_transitions_per_env
+        mb = batch // num_mini_batches
+        perm = torch.randperm(num_mini_batches * mb, requires_grad=False, device=self.device)
+        take = self.minibatch_source(obs_dtype)
         for _ in range(num_epochs):
             for i in range(num_mini_batches):
-                idx = perm[i * mb:(i + 1) * mb]
-                actions, values, advantages, returns, logp, mu, sigma = (c[idx] for c in cols)
-                if extra is not None:
-                    yield (extra[0][idx], extra[1][idx], obs[idx], critic[idx], actions, values, advantages, returns,
-                           logp, mu, sigma, (None, None), None)
-                else:
-                    yield obs[idx], critic[idx], actions, values, advantages, returns, logp, mu, sigma, (None, None), None
+                yield take(perm[i * mb:(i + 1) * mb])
 
 
 class _HistoryRows:
@@ -151,23 +172,27 @@ class _HistoryRows:
     frames older than the env's latest reset at or before step k zeroed: obs k is post-reset when dones[k-1] is set
     (the env zeroes the history and appends the new frame), and the zeros stay until the frames shift out."""
 
-    def __init__(self, st, dtype=None):
+    def __init__(self, st, dtype):
         frame, frames = st.history
         T, N = st.num_transitions_per_env, st.num_envs
-        dt = dtype if dtype is not None else st.obs0.dtype
-        self.frame, self.frames, self.N = frame, frames, N
-        seq = torch.empty(N, frames + T - 1, frame, device=st.obs0.device, dtype=dt)
-        seq[:, :frames] = st.obs0.view(N, frames, frame)
+        dev = st.obs0.device
+        self.frame, self.frames, self.N, self.T = frame, frames, N, T
+        self.seq = torch.empty(N, frames + T - 1, frame, device=dev, dtype=dtype)
+        self.first = torch.empty(T, N, dtype=torch.int64, device=dev)
+        self.win = torch.arange(frames, device=dev)
+        self._steps = torch.arange(T, device=dev).view(T, 1).expand(T, N)
+
+    def refresh(self, st):
+        """Rebuild the sequences and reset marks from the storage, in place."""
+        N, T, frames = self.N, self.T, self.frames
+        self.seq[:, :frames] = st.obs0.view(N, frames, self.frame)
         if T > 1:
-            seq[:, frames:] = st.frames[1:].transpose(0, 1)
-        self.seq = seq
+            self.seq[:, frames:] = st.frames[1:].transpose(0, 1)
         # first time step whose frame is valid for step k's history (frames of earlier times are zero)
         dn = st.dones.view(T, N) > 0
-        steps = torch.arange(T, device=st.obs0.device).view(T, 1).expand(T, N)
         reset_at = torch.where(torch.cat([torch.zeros(1, N, dtype=torch.bool, device=dn.device), dn[:-1]]),
-                               steps, torch.full_like(steps, -(frames + T)))
-        self.first = torch.cummax(reset_at, 0).values
-        self.win = torch.arange(frames, device=st.obs0.device)
+                               self._steps, torch.full_like(self._steps, -(frames + T)))
+        self.first.copy_(torch.cummax(reset_at, 0).values)
 
     def __getitem__(self, idx):
         k, n = idx // self.N, idx % self.N

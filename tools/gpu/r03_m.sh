@@ -1,0 +1,11 @@
+# capsule self-collision checks + graphed PPO update: tests, self-collision A/B, phase profile, PPO bench
+set -e
+t=${1:-r03m}
+o=$GRAFT_REPO_ROOT/gpurun_out/$t
+mkdir -p $o
+cd $GRAFT_REPO_ROOT
+timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread -s tests/test_gpu_dynamics_contact.py tests/test_gpu_dynamics.py tests/test_gpu_dynamics_kane.py tests/test_gpu_ppo.py > $o/tests.log 2>&1
+bash tools/gpu/r03_ab_self.sh $t
+timeout -k 10 300 python tools/prof_dynamics_phases.py > $o/phases_self_on.txt 2>&1
+timeout -k 10 300 python tools/bench_ppo.py --bf16 --iters 6 > $o/ppo_bf16.json 2> $o/ppo_bf16.err
+timeout -k 10 300 python tools/bench_ppo.py --iters 6 > $o/ppo_fp32.json 2> $o/ppo_fp32.err

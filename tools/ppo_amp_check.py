@@ -58,7 +58,7 @@ def compare_updates(r, seed):
     with torch.no_grad():
         for q, q0 in zip(alg.actor_critic.parameters(), w0):
             q.copy_(q0)
-    alg.optimizer.load_state_dict(opt0)
+    alg.optimizer.load_state_dict(copy.deepcopy(opt0))   # adopted as is, then changed in place
     alg.learning_rate = lr0
     for g in alg.optimizer.param_groups:
         g["lr"] = lr0
@@ -86,7 +86,7 @@ def compare_cast_once(r, seed):
     with torch.no_grad():
         for q, q0 in zip(alg.actor_critic.parameters(), w0):
             q.copy_(q0)
-    alg.optimizer.load_state_dict(opt0)
+    alg.optimizer.load_state_dict(copy.deepcopy(opt0))   # adopted as is, then changed in place
     alg.learning_rate = lr0
     for g in alg.optimizer.param_groups:
         g["lr"] = lr0
