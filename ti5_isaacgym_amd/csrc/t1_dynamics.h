@@ -51,6 +51,7 @@ constexpr int T1_LEG_AXIS[NLEG] = {2, 0, 1, 1, 1, 0};
 // A self-collision capsule in its link frame: segment a-b and radius r (t1env_model.self_capsule).
 struct SelfCapsule {
   float a[3], b[3], r;
+  float bound;  // radius of the capsule's bounding sphere about the segment's middle: |b - a| / 2 + r
 };
 
 // Model in the form the kernels consume (built from t1env_model at create time).
@@ -662,11 +663,18 @@ T1_HD void closest_segments(V3<R> p1, V3<R> q1, V3<R> p2, V3<R> q2, V3<R>& c1, V
 // a capsule in world axes about O: segment p-q, radius r
 template <typename R> struct CapPose {
   V3<R> p, q;
-  R r;
+  R r, bound;
 };
 template <typename R> T1_HD CapPose<R> cap_pose(const SelfCapsule& c, const M3<R>& Rb, V3<R> pb) {
   return CapPose<R>{pb + mul(Rb, v3<R>(R(c.a[0]), R(c.a[1]), R(c.a[2]))),
-                    pb + mul(Rb, v3<R>(R(c.b[0]), R(c.b[1]), R(c.b[2]))), R(c.r)};
+                    pb + mul(Rb, v3<R>(R(c.b[0]), R(c.b[1]), R(c.b[2]))), R(c.r), R(c.bound)};
+}
+// the capsules' bounding spheres overlap (a necessary condition for contact: a wave whose lanes all fail it skips the
+// pair's closest-point query and contact terms)
+template <typename R> T1_HD bool capsules_near(const CapPose<R>& O, const CapPose<R>& X) {
+  const V3<R> d = R(0.5) * ((O.p + O.q) - (X.p + X.q));
+  const R rs = O.bound + X.bound;
+  return dot(d, d) < rs * rs;
 }
 template <typename R> T1_HD V3<R> point_velocity(const R V[6], V3<R> x) {
   return v3<R>(V[3], V[4], V[5]) + cross(v3<R>(V[0], V[1], V[2]), x);
@@ -696,6 +704,7 @@ T1_HD bool capsule_contact(const CapPose<R>& O, const CapPose<R>& X, bool o_firs
 template <typename R>
 T1_HD void self_pair_terms(const DynModel& M, const CapPose<R>& O, const R Vo[6], const CapPose<R>& X, const R Vx[6],
                            bool o_first, R mu, R dt, Sym6<R>& A, R g[6], PointMoments<R>& fric) {
+  if (!capsules_near(O, X)) return;
   V3<R> x, n;
   R pen;
   if (capsule_contact(O, X, o_first, x, n, pen)) contact_point(M, x, n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
@@ -706,7 +715,7 @@ T1_HD V3<R> self_pair_force(const DynModel& M, const CapPose<R>& O, const R Vo[6
                             bool o_first, R mu) {
   V3<R> x, n;
   R pen;
-  if (!capsule_contact(O, X, o_first, x, n, pen)) return v3<R>(R(0), R(0), R(0));
+  if (!capsules_near(O, X) || !capsule_contact(O, X, o_first, x, n, pen)) return v3<R>(R(0), R(0), R(0));
   return point_contact_force(M, x, n, pen, Vo, mu, R(0), point_velocity(Vx, x));
 }
 // Pose (rotation, origin about O) and spatial velocity of one contact body, as the kinematics publish them
