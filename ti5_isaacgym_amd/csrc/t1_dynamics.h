@@ -51,7 +51,6 @@ constexpr int T1_LEG_AXIS[NLEG] = {2, 0, 1, 1, 1, 0};
 // A self-collision capsule in its link frame: segment a-b and radius r (t1env_model.self_capsule).
 struct SelfCapsule {
   float a[3], b[3], r;
-  float bound;  // radius of the capsule's bounding sphere about the segment's middle: |b - a| / 2 + r
 };
 
 // Model in the form the kernels consume (built from t1env_model at create time).
@@ -647,35 +646,29 @@ template <typename R>
 T1_HD void closest_segments(V3<R> p1, V3<R> q1, V3<R> p2, V3<R> q2, V3<R>& c1, V3<R>& c2) {
   const V3<R> d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
   const R a = dot(d1, d1), e = dot(d2, d2), f = dot(d2, r), c = dot(d1, r), b = dot(d1, d2);
-  const R den = a * e - b * b, ia = R(1) / a;
+  const R den = a * e - b * b, ia = rcp(a), ie = rcp(e);
   const bool parallel = den < R(1e-3) * a * e;
   // crossing
-  R sx = clamp01((b * f - c * e) / (parallel ? R(1) : den));
-  const R tx = (b * sx + f) / e;
+  R sx = clamp01((b * f - c * e) * rcp(parallel ? R(1) : den));
+  const R tx = (b * sx + f) * ie;
   sx = tx < R(0) ? clamp01(-c * ia) : (tx > R(1) ? clamp01((b - c) * ia) : sx);
   // parallel: segment 2's ends project to s = -c / a and (b - c) / a
   const R s0 = -c * ia, s1 = (b - c) * ia;
   const R sp = R(0.5) * (clamp01(s0 < s1 ? s0 : s1) + clamp01(s0 < s1 ? s1 : s0));
   const R sv = parallel ? sp : sx;
   c1 = p1 + sv * d1;
-  c2 = p2 + clamp01(dot(c1 - p2, d2) / e) * d2;
+  c2 = p2 + clamp01(dot(c1 - p2, d2) * ie) * d2;
 }
 // a capsule in world axes about O: segment p-q, radius r
 template <typename R> struct CapPose {
   V3<R> p, q;
-  R r, bound;
+  R r;
 };
 template <typename R> T1_HD CapPose<R> cap_pose(const SelfCapsule& c, const M3<R>& Rb, V3<R> pb) {
   return CapPose<R>{pb + mul(Rb, v3<R>(R(c.a[0]), R(c.a[1]), R(c.a[2]))),
-                    pb + mul(Rb, v3<R>(R(c.b[0]), R(c.b[1]), R(c.b[2]))), R(c.r), R(c.bound)};
+                    pb + mul(Rb, v3<R>(R(c.b[0]), R(c.b[1]), R(c.b[2]))), R(c.r)};
 }
-// the capsules' bounding spheres overlap (a necessary condition for contact: a wave whose lanes all fail it skips the
-// pair's closest-point query and contact terms)
-template <typename R> T1_HD bool capsules_near(const CapPose<R>& O, const CapPose<R>& X) {
-  const V3<R> d = R(0.5) * ((O.p + O.q) - (X.p + X.q));
-  const R rs = O.bound + X.bound;
-  return dot(d, d) < rs * rs;
-}
+
 template <typename R> T1_HD V3<R> point_velocity(const R V[6], V3<R> x) {
   return v3<R>(V[3], V[4], V[5]) + cross(v3<R>(V[0], V[1], V[2]), x);
 }
@@ -695,7 +688,7 @@ T1_HD bool capsule_contact(const CapPose<R>& O, const CapPose<R>& X, bool o_firs
   // axes crossing (dist ~ 0): push apart along the line between the segment midpoints (fallback +z)
   const V3<R> m = R(0.5) * (O.p + O.q) - R(0.5) * (X.p + X.q);
   const R mm = dot(m, m);
-  n = dist > R(1e-6) ? (R(1) / dist) * d : (mm > R(1e-12) ? rcp(fsqrt(mm)) * m : v3<R>(R(0), R(0), R(1)));
+  n = dist > R(1e-6) ? rcp(dist) * d : (mm > R(1e-12) ? rcp(fsqrt(mm)) * m : v3<R>(R(0), R(0), R(1)));
   pen = rs - dist;
   x = cx + (X.r - R(0.5) * pen) * n;
   return true;
@@ -704,7 +697,6 @@ T1_HD bool capsule_contact(const CapPose<R>& O, const CapPose<R>& X, bool o_firs
 template <typename R>
 T1_HD void self_pair_terms(const DynModel& M, const CapPose<R>& O, const R Vo[6], const CapPose<R>& X, const R Vx[6],
                            bool o_first, R mu, R dt, Sym6<R>& A, R g[6], PointMoments<R>& fric) {
-  if (!capsules_near(O, X)) return;
   V3<R> x, n;
   R pen;
   if (capsule_contact(O, X, o_first, x, n, pen)) contact_point(M, x, n, pen, Vo, mu, R(0), dt, A, g, fric, point_velocity(Vx, x));
@@ -715,7 +707,7 @@ T1_HD V3<R> self_pair_force(const DynModel& M, const CapPose<R>& O, const R Vo[6
                             bool o_first, R mu) {
   V3<R> x, n;
   R pen;
-  if (!capsules_near(O, X) || !capsule_contact(O, X, o_first, x, n, pen)) return v3<R>(R(0), R(0), R(0));
+  if (!capsule_contact(O, X, o_first, x, n, pen)) return v3<R>(R(0), R(0), R(0));
   return point_contact_force(M, x, n, pen, Vo, mu, R(0), point_velocity(Vx, x));
 }
 // Pose (rotation, origin about O) and spatial velocity of one contact body, as the kinematics publish them
@@ -737,6 +729,10 @@ T1_HD void self_terms_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2],
     Po[s] = cap_pose(M.self_cap[own][s], Ko[s].Rb, Ko[s].p);
     Px[s] = cap_pose(M.self_cap[1 - own][s], Kx[s].Rb, Kx[s].p);
   }
+  // the shank-foot pair within the leg: one query for both bodies (shank first)
+  V3<R> xi, ni;
+  R peni;
+  const bool intra = capsule_contact(Po[0], Po[1], true, xi, ni, peni);
   // one instantiation per body (a plain loop this large is not unrolled, and its register arrays would go to scratch)
   auto body = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
@@ -744,7 +740,9 @@ T1_HD void self_terms_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2],
     moments_zero(fric);
     self_pair_terms(M, Po[s], Ko[s].V, Px[0], Kx[0].V, own == 0, mu, dt, C[s], c[s], fric);
     self_pair_terms(M, Po[s], Ko[s].V, Px[1], Kx[1].V, own == 0, mu, dt, C[s], c[s], fric);
-    self_pair_terms(M, Po[s], Ko[s].V, Po[1 - s], Ko[1 - s].V, s == 0, mu, dt, C[s], c[s], fric);
+    if (intra)
+      contact_point(M, xi, s == 0 ? ni : R(-1) * ni, peni, Ko[s].V, mu, R(0), dt, C[s], c[s], fric,
+                    point_velocity(Ko[1 - s].V, xi));
     moments_flush(fric, C[s]);
   };
   body(std::integral_constant<int, 0>{});

@@ -70,7 +70,6 @@ inline const char* make_dyn_model(const t1env_model* model, DynModel* dm) {
       len2 += (c.b[k] - c.a[k]) * (c.b[k] - c.a[k]);
     }
     c.r = model->self_capsule[i][6];
-    c.bound = 0.5f * sqrtf(len2) * 1.0001f + c.r + 1e-6f;  // rounded up: the test must be conservative
     if (dm->self_collisions && !(c.r > 0.0f && len2 > 1e-8f))
       return "self_capsule needs a positive radius and two distinct segment ends";
   }
