@@ -354,6 +354,9 @@ template <typename R> T1_HD void moments_flush(const PointMoments<R>& P, Sym6<R>
 // compliant law's own rebound (the spring's stored energy) comes on top: the exit speed is at least ~e v_imp.
 // v_tgt = 0 is the plain compliant law.
 template <typename R> T1_HD R restitution_target(const DynModel& M, R e, R vimp) {
+#ifdef T1_WHATIF_NO_RESTITUTION  // timing-only what-if build: no restitution set point
+  return R(0);
+#endif
   return vimp > R(M.bounce_threshold) ? e * vimp : R(0);
 }
 // the episode after this substep: amax = the fastest approach among the body's points in contact (< 0: none)
@@ -870,6 +873,14 @@ template <int AX, typename R> T1_HD void joint_subspace(const DynModel& M, int b
   }
 }
 
+// true if p holds on any lane of the wave (wave-uniform); the host runs one env at a time
+T1_HD bool t1_wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(p) != 0;
+#else
+  return p;
+#endif
+}
 // contact of a body with NP points; `lowest` = its origin height minus its contact radius, `bound` = the
 // terrain_bound at its origin (fetched earlier): skipped when the body cannot reach the terrain
 // terrain: e = the combined restitution, vimp = the body's restitution episode (updated).
@@ -883,8 +894,15 @@ T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, R lowest, int
   }
   const R vtg = restitution_target(M, e, vimp);
   R amax = R(-1);
-  if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
-  else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
+  // a restitution set point is rare (an episode opened above the bounce threshold): a wave with none anywhere runs the
+  // law with v_tgt = 0 folded in (the same values: the separation branch is empty at v_tgt = 0), -7% of the step
+  if (t1_wave_any(vtg > R(0))) {
+    if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
+    else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, vtg, dt, A, g, amax);
+  } else {
+    if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, R(0), dt, A, g, amax);
+    else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, R(0), dt, A, g, amax);
+  }
   vimp = restitution_episode(vimp, amax);
 }
 // slots of an env's restitution episodes (t1env_buffers.contact_vimp, EnvState::vimp): the shank and the foot of each

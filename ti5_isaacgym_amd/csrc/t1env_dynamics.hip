@@ -380,6 +380,11 @@ __device__ __forceinline__ void body_terms_at(const DynModel& M, const Terrain& 
 // of the leg's pose region, written after integration, read by the helpers between S1 and S2 (and after R1).
 enum : int { ST_POS = 0, ST_QUAT = 3, ST_W = 7, ST_VO = 10, ST_Q = 13, ST_QD = 19, ST_N = 25 };
 static_assert(ST_N <= POSE_N, "the substep state fits the pose rows");
+#ifdef T1_WHATIF_NO_SELF  // timing-only what-if build: the self-collision code compiled out of k_dyn4
+#define T1_SELF_CODE 0
+#else
+#define T1_SELF_CODE 1
+#endif
 // a helper's kinematics of one published state: the base frame and the contact bodies of leg `leg` (own state P), and
 // with self-collision on (wave-uniform) those of the other leg too (its state Po: the same base rows)
 __device__ __forceinline__ void helper_kinematics(const DynModel& M, const float (*P)[DYN_ENVS],
@@ -395,7 +400,7 @@ __device__ __forceinline__ void helper_kinematics(const DynModel& M, const float
   for (int k = 0; k < NLEG; ++k) { qh[k] = P[ST_Q + k][lane]; qdh[k] = P[ST_QD + k][lane]; }
   base_frame(sb, F);
   leg_body_kinematics(M, F, qh, qdh, leg, Ko);
-  if (M.self_collisions) {
+  if (T1_SELF_CODE && M.self_collisions) {
 #pragma unroll
     for (int k = 0; k < NLEG; ++k) { qh[k] = Po[ST_Q + k][lane]; qdh[k] = Po[ST_QD + k][lane]; }
     leg_body_kinematics(M, F, qh, qdh, 1 - leg, Kx);
@@ -779,7 +784,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
 #pragma unroll
         for (int j = 0; j < 6; ++j) cs[i][j] = 0.0f;
       }
-      if (M.self_collisions) self_terms_leg(M, leg, Ko, Kx, mu_self, dt, Cs, cs);
+      if (T1_SELF_CODE && M.self_collisions) self_terms_leg(M, leg, Ko, Kx, mu_self, dt, Cs, cs);
       T1_PROF_MARK(21);
       body_terms_at(M, T, Ko[1], lane, 1 + 6 * leg + K_FOOT, abs, mu, e, vi_ft, dt, Cs[1], cs[1], lds.ct[leg] + XCH,
                     T1_NO_BOUND);
@@ -812,7 +817,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
       BodyKin<float> Ko[2], Kx[2];
       helper_kinematics(M, P, Po, lane, leg, F, Ko, Kx);
       V3<float> fself[2] = {v3<float>(0.0f, 0.0f, 0.0f), v3<float>(0.0f, 0.0f, 0.0f)};
-      if (M.self_collisions) self_forces_leg(M, leg, Ko, Kx, mu_self, fself);
+      if (T1_SELF_CODE && M.self_collisions) self_forces_leg(M, leg, Ko, Kx, mu_self, fself);
       const float vt[3] = {restitution_target(M, e, vi_sh), restitution_target(M, e, vi_ft),
                            restitution_target(M, e, vi_b)};
       const float vt_o = restitution_target(M, e, lds.vib[1 - leg][lane]);  // the other base half (leg 0 reports)
@@ -912,7 +917,11 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     integrate_base(sb, r, dt);
     integrate_leg(M, leg, q, qd, dq, dt);
     T1_PROF_MARK(9);
+#ifdef T1_WHATIF_NO_LOG  // timing-only what-if build: the substep-log branch compiled out
+    if (false) {
+#else
     if (LG.root != nullptr) {  // wave-uniform (a kernel argument)
+#endif
       if (active) {
         const size_t row = (size_t)sub * N + n;
 #pragma unroll
