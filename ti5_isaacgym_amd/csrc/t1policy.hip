@@ -1,49 +1,135 @@
-// Direct Conv1d of the DH policy's long-history encoder, inference forward (include/t1policy.h).
+// Conv1d of the DH policy's long-history encoder, inference forward (include/t1policy.h), on the matrix cores.
 //
 // The reference's first history conv (actor_critic_dh.py:83-96): nn.Conv1d(66 frames -> 32, kernel 6, stride 3)
 // over the 47 features of each frame.  y[b, l, o] = bias[o] + sum_{c, t} w[o, c, t] * x[b, c, S*l + t], written
 // channels-last (B, Lout, O), the layout conv1d_as_gemm returns.
 //
-// One lane per output position (b, l) and group of 8 output channels: the weights are the same for every lane,
-// so they are read with wave-uniform addresses (scalar loads, used as SGPR operands of the FMAs; the caller passes
-// them tap-major, wt[c][t][o], so each (c, t) is O contiguous floats) and the only vector loads are the lane's own
-// K inputs per channel.  That replaces the unfolded-row copy
-// (B * Lout * C * K floats) plus a GEMM over it with one pass over x.  fp32 throughout; the sum runs over (c, t) in
-// order, so the result equals the GEMM's up to fp32 summation order.
+// Per sample it is a (14 positions x 396) . (396 x 32) product: one 16-row MFMA tile (rows 14, 15 discarded) and two
+// 16-column tiles, v_mfma_f32_16x16x32_f16.  fp32 accuracy from fp16 matrix cores by splitting both operands:
+// v = hi + lo with hi = fp16(v) and lo = fp16((v - hi) * 2^11) (the residual scaled up, so it does not underflow fp16),
+// and y = sum hi.hi + 2^-11 sum (hi.lo + lo.hi): three MFMAs per step, fp32 accumulation, the dropped lo.lo term and
+// the residual's rounding are ~2^-22 of each product (the test bound is 1e-5, tests/test_gpu_policy_conv.py).  The
+// fp32 VALU kernel this replaces ran 66 us at 8192 samples (compute-bound: 2.9 GFLOP at <= 157 TFLOP/s fp32); the
+// split runs on the 2.5 PFLOP/s fp16 rate and is bound by the 101.6 MB read of the history instead.
+//
+// K order: 8 slots per channel (its 6 taps and 2 zeros), so a lane's A fragment (row = output position l, 8 slots of
+// one channel) is the 6 contiguous inputs x[c][3l .. 3l+5] and needs no transposition; a K-step of 32 covers 4
+// channels, 17 steps cover the 66 (2 zero channels).  Each workgroup builds the split weight fragments in LDS once;
+// each wave stages one sample (12.4 KB, coalesced) into its own LDS rows while the next sample's loads are in flight.
 #include <hip/hip_runtime.h>
 
 namespace {
 
-template <int C, int L, int O, int K, int S, int OPL>
-__global__ __launch_bounds__(256) void k_conv1d_direct(const float* __restrict__ x, const float* __restrict__ wt,
-                                                       const float* __restrict__ bias, float* __restrict__ y,
-                                                       int positions) {
-  // blockIdx.y picks OPL of the O output channels (uniform per wave: the weights stay scalar loads); 4x the waves of
-  // one lane per position with all O outputs, so the loads of one wave hide behind the FMAs of others
-  constexpr int LOUT = (L - K) / S + 1;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;  // output position b * LOUT + l
-  if (g >= positions) return;
-  const int o0 = blockIdx.y * OPL;
-  const int b = g / LOUT, l = g - b * LOUT;
-  const float* xp = x + (size_t)b * (C * L) + S * l;
-  const float* wp = wt + o0;
-  float acc[OPL];
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int CV_C = 66, CV_L = 47, CV_O = 32, CV_K = 6, CV_S = 3, CV_LOUT = (CV_L - CV_K) / CV_S + 1;  // 14
+constexpr int CV_STEPS = 17;            // K-steps of 32: 4 channels each
+constexpr int CV_CPAD = 4 * CV_STEPS;   // 68 staged channel rows (66 + 2 zero rows)
+constexpr int CV_LPAD = 48;             // staged row length (47 + 1 zero)
+constexpr int CV_WAVES = 6;             // waves per workgroup (LDS: 69.6 KB of fragments + 6 x 13 KB of samples)
+constexpr int CV_PER_LANE = (CV_C * CV_L / 2 + 63) / 64;  // float2 loads per lane per sample (1551 float2)
+constexpr float CV_SPLIT = 2048.0f;
+static_assert(CV_LOUT <= 16 && CV_O == 32, "one 16-row tile, two 16-column tiles");
+
+struct ConvLds {
+  h8 wf[CV_STEPS][2][2][64];               // [step][column tile][hi, lo][lane]
+  float x[CV_WAVES][CV_CPAD][CV_LPAD];     // each wave's staged sample
+};
+
+__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
 #pragma unroll
-  for (int o = 0; o < OPL; ++o) acc[o] = bias[o0 + o];
-#pragma unroll 2
-  for (int c = 0; c < C; ++c) {
-    float xv[K];
-#pragma unroll
-    for (int t = 0; t < K; ++t) xv[t] = xp[c * L + t];
-#pragma unroll
-    for (int t = 0; t < K; ++t) {
-#pragma unroll
-      for (int o = 0; o < OPL; ++o) acc[o] = fmaf(wp[(c * K + t) * O + o], xv[t], acc[o]);
-    }
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = (_Float16)v[j];
+    hi[j] = h;
+    lo[j] = (_Float16)((v[j] - (float)h) * CV_SPLIT);
   }
-  float4* yp = reinterpret_cast<float4*>(y + (size_t)g * O + o0);
+}
+
+__global__ __launch_bounds__(64 * CV_WAVES) void k_conv1d_mfma(const float* __restrict__ x, const float* __restrict__ wt,
+                                                               const float* __restrict__ bias, float* __restrict__ y,
+                                                               int batch) {
+  __shared__ ConvLds L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the split weight fragments: lane l of (step s, column tile nt) holds B[k = 8 (l >> 4) + j][col l & 15], i.e.
+  // channel c = 4 s + (l >> 4), tap j (< 6, else 0), output o = 16 nt + (l & 15)
+  for (int e = tid; e < CV_STEPS * 2 * 64; e += 64 * CV_WAVES) {
+    const int s = e >> 7, nt = (e >> 6) & 1, l = e & 63;
+    const int c = 4 * s + (l >> 4), o = 16 * nt + (l & 15);
+    float v[8];
 #pragma unroll
-  for (int q = 0; q < OPL / 4; ++q) yp[q] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+    for (int j = 0; j < 8; ++j) v[j] = (c < CV_C && j < CV_K) ? wt[(c * CV_K + j) * CV_O + o] : 0.0f;
+    h8 hi, lo;
+    split8(v, hi, lo);
+    L.wf[s][nt][0][l] = hi;
+    L.wf[s][nt][1][l] = lo;
+  }
+  float (*X)[CV_LPAD] = L.x[wave];
+  for (int i = lane; i < CV_CPAD * CV_LPAD; i += 64) X[i / CV_LPAD][i % CV_LPAD] = 0.0f;  // pads stay zero
+  __syncthreads();
+
+  const int r = lane & 15, kg = lane >> 4;
+  const int rr = r < CV_LOUT ? r : CV_LOUT - 1;  // rows 14, 15 of the tile: a copy of row 13, never stored
+  const int stride = gridDim.x * CV_WAVES;
+  int b = blockIdx.x * CV_WAVES + wave;
+  float2 pre[CV_PER_LANE];
+  auto load = [&](int bs) {
+    const float2* src = reinterpret_cast<const float2*>(x + (size_t)bs * (CV_C * CV_L));
+#pragma unroll
+    for (int k = 0; k < CV_PER_LANE; ++k) {
+      const int i = lane + 64 * k;
+      pre[k] = i < CV_C * CV_L / 2 ? src[i] : make_float2(0.0f, 0.0f);
+    }
+  };
+  if (b < batch) load(b);
+  for (; b < batch; b += stride) {
+    // stage this sample (row c of 47 inputs -> X[c][0..46]); the wave's own LDS rows: in-order LDS, no barrier
+#pragma unroll
+    for (int k = 0; k < CV_PER_LANE; ++k) {
+      const int i = 2 * (lane + 64 * k);
+      if (i < CV_C * CV_L) {
+        X[i / CV_L][i % CV_L] = pre[k].x;
+        X[(i + 1) / CV_L][(i + 1) % CV_L] = pre[k].y;
+      }
+    }
+    if (b + stride < batch) load(b + stride);  // the next sample's loads fly during this one's products
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f4 acc[2][2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) acc[nt][0] = acc[nt][1] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < CV_STEPS; ++s) {
+      const float* row = &X[4 * s + kg][CV_S * rr];
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < CV_K; ++j) v[j] = row[j];
+      v[6] = v[7] = 0.0f;
+      h8 ah, al;
+      split8(v, ah, al);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const h8 bh = L.wf[s][nt][0][lane], bl = L.wf[s][nt][1][lane];
+        acc[nt][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[nt][0], 0, 0, 0);
+        acc[nt][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[nt][1], 0, 0, 0);
+        acc[nt][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[nt][1], 0, 0, 0);
+      }
+    }
+    // C/D: column lane & 15, rows 4 (lane >> 4) + i
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int o = 16 * nt + (lane & 15);
+      const float bo = bias[o];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int l = 4 * kg + i;
+        if (l < CV_LOUT) y[((size_t)b * CV_LOUT + l) * CV_O + o] = acc[nt][0][i] + acc[nt][1][i] * (1.0f / CV_SPLIT) + bo;
+      }
+    }
+    // the next staging overwrites X: every lane's reads of it precede those writes in the wave's LDS order
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 }  // namespace
@@ -56,15 +142,20 @@ int t1policy_conv1d_forward(const float* x, const float* wt, const float* bias, 
                             int length, int out_channels, int kernel, int stride, void* stream) {
   if (!x || !wt || !bias || !y || batch < 0) return -1;
   if (batch == 0) return 0;
-  if (!(channels == 66 && length == 47 && out_channels == 32 && kernel == 6 && stride == 3)) return 1;
-  constexpr int LOUT = (47 - 6) / 3 + 1;
-  const long long positions = (long long)batch * LOUT;
-  if (positions > 0x7fffffffLL) return -1;
-  const int block = 256;
-  const int grid = (int)((positions + block - 1) / block);
-  constexpr int OPL = 8;
-  hipLaunchKernelGGL((k_conv1d_direct<66, 47, 32, 6, 3, OPL>), dim3(grid, 32 / OPL), dim3(block), 0, (hipStream_t)stream, x, wt,
-                     bias, y, (int)positions);
+  if (!(channels == CV_C && length == CV_L && out_channels == CV_O && kernel == CV_K && stride == CV_S)) return 1;
+  if ((reinterpret_cast<uintptr_t>(x) & 7u) != 0) return -1;  // float2 sample loads
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
+  static int cu_count[64];  // per device, queried once
+  int cus = __atomic_load_n(&cu_count[dev], __ATOMIC_RELAXED);
+  if (cus <= 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return -2;
+    __atomic_store_n(&cu_count[dev], cus, __ATOMIC_RELAXED);
+  }
+  // one workgroup per CU (its LDS), never more workgroups than the samples need
+  const long long need = ((long long)batch + CV_WAVES - 1) / CV_WAVES;
+  const int grid = (int)(need < cus ? need : cus);
+  hipLaunchKernelGGL(k_conv1d_mfma, dim3(grid), dim3(64 * CV_WAVES), 0, (hipStream_t)stream, x, wt, bias, y, batch);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
