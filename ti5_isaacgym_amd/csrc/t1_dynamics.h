@@ -539,6 +539,57 @@ T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, con
   moments_flush(fric, A);
 }
 
+// body_contact_np in two halves, for a caller with independent work to run while the height loads are in flight:
+// contact_query (phase 1: transforms and terrain queries, one batch of NP <= T1_CONTACT_BATCH points) and
+// contact_apply (phase 2: the contact math), the same operations in the same order.
+template <int NP, typename R> struct ContactQuery {
+  V3<R> xs[NP];
+  R dz[NP], gx[NP], gy[NP];
+};
+template <bool HF, int NP, typename R>
+T1_HD void contact_query(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb, V3<R> base_abs,
+                         ContactQuery<NP, R>& Q) {
+  static_assert(NP <= T1_CONTACT_BATCH, "one batch");
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int c = c_begin + i;
+    Q.xs[i] = pb + mul(Rb, v3<R>(M.contact_point[c][0], M.contact_point[c][1], M.contact_point[c][2]));
+    V3<R> X = Q.xs[i] + base_abs;
+    Q.dz[i] = terrain_height<HF>(T, X.x, X.y, Q.gx[i], Q.gy[i]) - X.z;
+  }
+}
+template <bool HF, int NP, typename R>
+T1_HD void contact_apply(const DynModel& M, const ContactQuery<NP, R>& Q, const R Vb[6], R mu, R vtg, R dt, Sym6<R>& A,
+                         R g[6], R& amax) {
+  PointMoments<R> fric;
+  moments_zero(fric);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(T1_SCALAR_CONTACT)
+  if constexpr (std::is_same<R, float>::value && NP % 2 == 0) {
+    PairAcc pacc;
+    pair_acc_zero(pacc);
+#pragma unroll
+    for (int i = 0; i < NP; i += 2) {
+      const bool c0 = Q.dz[i] > R(0), c1 = Q.dz[i + 1] > R(0);
+      if (c0 || c1) {
+        const V3<R> n0 = terrain_normal<HF>(Q.gx[i], Q.gy[i]), n1 = terrain_normal<HF>(Q.gx[i + 1], Q.gy[i + 1]);
+        contact_pair(M, Q.xs[i], Q.xs[i + 1], n0, n1, Q.dz[i] * n0.z, Q.dz[i + 1] * n1.z, c0, c1, Vb, mu, vtg, dt, pacc,
+                     amax);
+      }
+    }
+    pair_acc_flush(pacc, A, g);
+  } else
+#endif
+  {
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+      if (Q.dz[i] > R(0)) {
+        const V3<R> n = terrain_normal<HF>(Q.gx[i], Q.gy[i]);
+        contact_point(M, Q.xs[i], n, Q.dz[i] * n.z, Vb, mu, vtg, dt, A, g, fric, V3<R>{R(0), R(0), R(0)}, &amax);
+      }
+  }
+  moments_flush(fric, A);
+}
+
 template <bool HF, typename R>
 T1_HD void body_contact_t(const DynModel& M, const Terrain& T, int c_begin, int c_end, const M3<R>& Rb, V3<R> pb,
                           V3<R> base_abs, const R Vb[6], R mu, R vtg, R dt, Sym6<R>& A, R g[6], R& amax) {
@@ -902,6 +953,27 @@ T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, R lowest, int
   } else {
     if (T.type == 0) body_contact_np<false, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, R(0), dt, A, g, amax);
     else body_contact_np<true, NP>(M, T, c_begin, Rb, pb, base_abs, Vb, mu, R(0), dt, A, g, amax);
+  }
+  vimp = restitution_episode(vimp, amax);
+}
+// body_contact_fixed for a body that is always evaluated (no height bound), with `between()` run after its terrain
+// queries are issued and before their heights are used (the helper's self-contact terms hide the load latency)
+template <int NP, typename R, typename Between>
+T1_HD void body_contact_query_apply(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb,
+                                    V3<R> base_abs, const R Vb[6], R mu, R e, R& vimp, R dt, Sym6<R>& A, R g[6],
+                                    Between&& between) {
+  ContactQuery<NP, R> Q;
+  if (T.type == 0) contact_query<false, NP>(M, T, c_begin, Rb, pb, base_abs, Q);
+  else contact_query<true, NP>(M, T, c_begin, Rb, pb, base_abs, Q);
+  between();
+  const R vtg = restitution_target(M, e, vimp);
+  R amax = R(-1);
+  if (t1_wave_any(vtg > R(0))) {
+    if (T.type == 0) contact_apply<false, NP>(M, Q, Vb, mu, vtg, dt, A, g, amax);
+    else contact_apply<true, NP>(M, Q, Vb, mu, vtg, dt, A, g, amax);
+  } else {
+    if (T.type == 0) contact_apply<false, NP>(M, Q, Vb, mu, R(0), dt, A, g, amax);
+    else contact_apply<true, NP>(M, Q, Vb, mu, R(0), dt, A, g, amax);
   }
   vimp = restitution_episode(vimp, amax);
 }

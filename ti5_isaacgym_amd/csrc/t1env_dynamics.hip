@@ -784,10 +784,13 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
 #pragma unroll
         for (int j = 0; j < 6; ++j) cs[i][j] = 0.0f;
       }
-      if (T1_SELF_CODE && M.self_collisions) self_terms_leg(M, leg, Ko, Kx, mu_self, dt, Cs, cs);
-      T1_PROF_MARK(21);
-      body_terms_at(M, T, Ko[1], lane, 1 + 6 * leg + K_FOOT, abs, mu, e, vi_ft, dt, Cs[1], cs[1], lds.ct[leg] + XCH,
-                    T1_NO_BOUND);
+      // the foot's terrain queries go out first; the self-contact terms run while its height loads are in flight
+      body_contact_query_apply<T1_POINTS_PER_BODY>(M, T, M.contact_start[1 + 6 * leg + K_FOOT], Ko[1].Rb, Ko[1].p, abs,
+                                                   Ko[1].V, mu, e, vi_ft, dt, Cs[1], cs[1], [&] {
+        if (T1_SELF_CODE && M.self_collisions) self_terms_leg(M, leg, Ko, Kx, mu_self, dt, Cs, cs);
+        T1_PROF_MARK(21);
+      });
+      lds_put_sym(lds.ct[leg] + XCH, lane, Cs[1], cs[1]);
       body_terms_at(M, T, Ko[0], lane, 1 + 6 * leg + K_SHANK, abs, mu, e, vi_sh, dt, Cs[0], cs[0], lds.ct[leg], bound_sh);
       T1_PROF_MARK(3);
       __syncthreads();  // S2: contact terms published

@@ -23,6 +23,8 @@ def main():
     p.add_argument("--num-envs", type=int, default=8192)
     p.add_argument("--bf16", action="store_true")
     p.add_argument("--rows", type=int, default=25)
+    p.add_argument("--eager", action="store_true", help="the eager minibatch step (DHPPO.graph_update off): the same "
+                   "kernels, each visible to the profiler")
     a = p.parse_args()
     dev = torch.device("cuda:0")
     env = make_t1_env(num_envs=a.num_envs, mesh_type="trimesh", seed=5, device=str(dev))
@@ -30,6 +32,7 @@ def main():
     r = DHOnPolicyRunner(env, class_to_dict(tc), None, device=str(dev))
     alg = r.alg
     alg.amp_dtype = torch.bfloat16 if a.bf16 else None
+    alg.graph_update = not a.eager
     alg.actor_critic.train()
     obs, priv = env.reset()
     critic = priv if priv is not None else obs
@@ -55,7 +58,7 @@ def main():
         alg.update()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-    print(f"update wall {dt * 1e3:.1f} ms ({'bf16' if a.bf16 else 'fp32'})")
+    print(f"update wall {dt * 1e3:.1f} ms ({'bf16' if a.bf16 else 'fp32'}, {'eager' if a.eager else 'graphed'})")
     ka = prof.key_averages()
     print(ka.table(sort_by="self_cpu_time_total", row_limit=a.rows, max_name_column_width=60))
     print(ka.table(sort_by="self_device_time_total", row_limit=a.rows, max_name_column_width=60))
