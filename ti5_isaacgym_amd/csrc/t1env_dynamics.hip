@@ -871,6 +871,13 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     sym_zero(Ab);
     leg_backward_nc(M, PL, q, qd, leg, dt, st, lb, Ab, g6);
     T1_PROF_MARK(2);
+    // the base block needs no contact term: built while the helpers finish theirs (the leg waits at S2)
+    Sym6<float> Ac;
+    float r[6];
+    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r[i] = -r[i];
+    T1_PROF_MARK(6);
     __syncthreads();  // S2
     T1_PROF_MARK(11);
     {
@@ -899,12 +906,6 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     eliminate_leg(lb, Ab, rb);
     lds_put_sym(lds.xch[leg], lane, Ab, rb);
     T1_PROF_MARK(4);
-    Sym6<float> Ac;
-    float r[6];
-    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) r[i] = -r[i];
-    T1_PROF_MARK(6);
     __syncthreads();  // S3
     T1_PROF_MARK(12);
 #pragma unroll
