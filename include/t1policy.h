@@ -9,6 +9,8 @@
 #ifndef T1POLICY_H
 #define T1POLICY_H
 
+#include <stdint.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -22,6 +24,18 @@ extern "C" {
  * -2 on a launch error.  Replaces (inference only, no autograd) nn.Conv1d.forward at actor_critic_dh.py:83-96. */
 int t1policy_conv1d_forward(const float* x, const float* wt, const float* bias, float* y, int batch, int channels,
                             int length, int out_channels, int kernel, int stride, void* stream);
+
+/* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
+ * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py
+ * _HistoryRows restates this in torch):
+ *   out[m] = seq[n, k : k + frames] flattened, with the frames of times < first[k, n] zeroed
+ *   (k = idx[m] / num_envs, n = idx[m] % num_envs, frame j of the window at time k - frames + 1 + j)
+ *   seq   (num_envs, frames + steps - 1, frame), elements of elem_bytes (2: bf16 / fp16, 4: fp32), contiguous
+ *   first (steps, num_envs) int64: the first valid time of each step's window; idx (rows) int64 in [0, steps*num_envs)
+ *   out   (rows, frames * frame), same element type
+ * Returns 0 on success, -1 on bad arguments, -2 on a launch error. */
+int t1policy_history_rows(const void* seq, const int64_t* first, const int64_t* idx, void* out, int rows, int num_envs,
+                          int steps, int frames, int frame, int elem_bytes, void* stream);
 
 #ifdef __cplusplus
 }

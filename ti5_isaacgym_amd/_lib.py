@@ -95,7 +95,7 @@ EXPORTS = ["t1env_create", "t1env_destroy", "t1env_init", "t1env_set_terrain", "
            "t1env_measure_heights", "t1env_critic_heights", "t1env_reset_idx", "t1env_set_substep_log"]
 
 # include/t1policy.h: the DH policy's HIP kernels, in the same library
-POLICY_EXPORTS = ["t1policy_conv1d_forward"]
+POLICY_EXPORTS = ["t1policy_conv1d_forward", "t1policy_history_rows"]
 
 _lib = None
 
@@ -130,6 +130,7 @@ def load():
         "t1env_reset_idx": ([vp, vp, P(StepArgs), vp], C.c_int),
         "t1env_critic_heights": ([vp, i32, i32, f32, vp, vp, vp, vp], C.c_int),
         "t1policy_conv1d_forward": ([vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
+        "t1policy_history_rows": ([vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -70,7 +70,8 @@ class DHPPO:
         # the device learning rate (a 0-d tensor Adam reads) on a HIP device; None on the host (the reference's floats)
         self._lr_t = torch.tensor(float(learning_rate), device=device) if cuda else None
         if cuda:
-            self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=self._lr_t, capturable=True, foreach=True)
+            # fused: one kernel per step (the capturable foreach Adam ran ~0.75 ms per step, r03x)
+            self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=self._lr_t, capturable=True, fused=True)
         else:
             self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=learning_rate)
         # created (and checkpointed) like the reference's; its separate step is disabled there as well

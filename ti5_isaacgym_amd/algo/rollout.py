@@ -195,6 +195,17 @@ class _HistoryRows:
         self.first.copy_(torch.cummax(reset_at, 0).values)
 
     def __getitem__(self, idx):
+        if self.seq.is_cuda:   # one HIP gather (include/t1policy.h t1policy_history_rows): the same rows, bit for bit
+            from .. import _lib
+            out = torch.empty(idx.numel(), self.frames * self.frame, dtype=self.seq.dtype, device=self.seq.device)
+            idx = idx.contiguous()
+            rc = _lib.load().t1policy_history_rows(self.seq.data_ptr(), self.first.data_ptr(), idx.data_ptr(),
+                                                   out.data_ptr(), idx.numel(), self.N, self.T, self.frames, self.frame,
+                                                   self.seq.element_size(),
+                                                   torch.cuda.current_stream(self.seq.device).cuda_stream)
+            if rc != 0:
+                raise RuntimeError(f"t1policy_history_rows failed (rc={rc})")
+            return out
         k, n = idx // self.N, idx % self.N
         pos = k.unsqueeze(1) + self.win.unsqueeze(0)                     # seq index = time + frames - 1
         rows = self.seq[n.unsqueeze(1), pos]                              # (M, frames, frame)

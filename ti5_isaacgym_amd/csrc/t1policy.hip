@@ -132,9 +132,49 @@ __global__ __launch_bounds__(64 * CV_WAVES) void k_conv1d_mfma(const float* __re
   }
 }
 
+// The PPO minibatch's actor observations rebuilt from the frame-history rollout storage (algo/rollout.py
+// _HistoryRows): row m is the window of frames k .. k + F - 1 of env n's sequence seq[n] ((F + T - 1) frames of `frame`
+// values, k = idx[m] / N, n = idx[m] % N), with the frames older than the env's latest reset at or before step k
+// (time < first[k, n], time = k - F + 1 + j for window frame j) zeroed -- a prefix of the window.  One wave per row;
+// 16-bit (bf16 / fp16 storage) or 32-bit elements copied as raw bits.
+template <typename E>
+__global__ __launch_bounds__(256) void k_history_rows(const E* __restrict__ seq, const int64_t* __restrict__ first,
+                                                      const int64_t* __restrict__ idx, E* __restrict__ out, int rows,
+                                                      int N, int T, int frames, int frame) {
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t g = idx[m];
+  const int k = (int)(g / N), n = (int)(g % N);
+  const int64_t f = first[(int64_t)k * N + n];
+  const int64_t t0 = (int64_t)k - frames + 1;  // time of window frame 0
+  const int64_t z = f - t0;
+  const int zero_frames = z <= 0 ? 0 : (z >= frames ? frames : (int)z);
+  const int len = frames * frame, zlen = zero_frames * frame;
+  const E* src = seq + ((int64_t)n * (frames + T - 1) + k) * frame;
+  E* dst = out + (int64_t)m * len;
+  for (int i = lane; i < len; i += 64) dst[i] = i < zlen ? E(0) : src[i];
+}
+
 }  // namespace
 
 extern "C" {
+
+int t1policy_history_rows(const void* seq, const int64_t* first, const int64_t* idx, void* out, int rows, int num_envs,
+                          int steps, int frames, int frame, int elem_bytes, void* stream) {
+  if (!seq || !first || !idx || !out || rows < 0 || num_envs <= 0 || steps <= 0 || frames <= 0 || frame <= 0) return -1;
+  if (rows == 0) return 0;
+  const dim3 grid((rows + 3) / 4), block(256);
+  if (elem_bytes == 2)
+    hipLaunchKernelGGL(k_history_rows<uint16_t>, grid, block, 0, (hipStream_t)stream, (const uint16_t*)seq, first, idx,
+                       (uint16_t*)out, rows, num_envs, steps, frames, frame);
+  else if (elem_bytes == 4)
+    hipLaunchKernelGGL(k_history_rows<uint32_t>, grid, block, 0, (hipStream_t)stream, (const uint32_t*)seq, first, idx,
+                       (uint32_t*)out, rows, num_envs, steps, frames, frame);
+  else
+    return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 // Returns 0 on success, 1 if the shape has no compiled instance (the caller keeps its GEMM path), -1 on bad
 // arguments, -2 on a launch error.
