@@ -25,16 +25,16 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int CV_C = 66, CV_L = 47, CV_O = 32, CV_K = 6, CV_S = 3, CV_LOUT = (CV_L - CV_K) / CV_S + 1;  // 14
 constexpr int CV_STEPS = 17;            // K-steps of 32: 4 channels each
-constexpr int CV_CPAD = 4 * CV_STEPS;   // 68 staged channel rows (66 + 2 zero rows)
-constexpr int CV_LPAD = 48;             // staged row length (47 + 1 zero)
-constexpr int CV_WAVES = 6;             // waves per workgroup (LDS: 69.6 KB of fragments + 6 x 13 KB of samples)
+constexpr int CV_CPAD = 4 * CV_STEPS;   // 68 staged channel rows (66 + 2 zero rows), 47 inputs each, unpadded: the
+                                        // sample's own layout, so staging is a straight copy
+constexpr int CV_WAVES = 6;             // waves per workgroup (LDS: 69.6 KB of fragments + 6 x 12.8 KB of samples)
 constexpr int CV_PER_LANE = (CV_C * CV_L / 2 + 63) / 64;  // float2 loads per lane per sample (1551 float2)
 constexpr float CV_SPLIT = 2048.0f;
 static_assert(CV_LOUT <= 16 && CV_O == 32, "one 16-row tile, two 16-column tiles");
 
 struct ConvLds {
   h8 wf[CV_STEPS][2][2][64];               // [step][column tile][hi, lo][lane]
-  float x[CV_WAVES][CV_CPAD][CV_LPAD];     // each wave's staged sample
+  uint32_t x[CV_WAVES][CV_CPAD * CV_L];   // each wave's staged sample, split: hi (low 16 bits) | lo (high 16 bits)
 };
 
 __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
@@ -44,6 +44,13 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
     hi[j] = h;
     lo[j] = (_Float16)((v[j] - (float)h) * CV_SPLIT);
   }
+}
+
+// one input split at staging (once per element, not once per use): fp16 hi | fp16 lo << 16
+__device__ __forceinline__ uint32_t split_word(float v) {
+  const _Float16 h = (_Float16)v;
+  const _Float16 l = (_Float16)((v - (float)h) * CV_SPLIT);
+  return (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
 }
 
 __global__ __launch_bounds__(64 * CV_WAVES) void k_conv1d_mfma(const float* __restrict__ x, const float* __restrict__ wt,
@@ -64,35 +71,32 @@ __global__ __launch_bounds__(64 * CV_WAVES) void k_conv1d_mfma(const float* __re
     L.wf[s][nt][0][l] = hi;
     L.wf[s][nt][1][l] = lo;
   }
-  float (*X)[CV_LPAD] = L.x[wave];
-  for (int i = lane; i < CV_CPAD * CV_LPAD; i += 64) X[i / CV_LPAD][i % CV_LPAD] = 0.0f;  // pads stay zero
+  uint32_t* X = L.x[wave];
+  for (int i = CV_C * CV_L + lane; i < CV_CPAD * CV_L; i += 64) X[i] = 0u;  // the 2 zero channels stay zero
   __syncthreads();
 
   const int r = lane & 15, kg = lane >> 4;
   const int rr = r < CV_LOUT ? r : CV_LOUT - 1;  // rows 14, 15 of the tile: a copy of row 13, never stored
   const int stride = gridDim.x * CV_WAVES;
   int b = blockIdx.x * CV_WAVES + wave;
-  float2 pre[CV_PER_LANE];
-  auto load = [&](int bs) {
+  // two samples in flight per wave: each buffer is refilled with the sample two strides ahead as soon as it is staged
+  float2 pa[CV_PER_LANE], pb[CV_PER_LANE];
+  auto load = [&](float2 (&dst)[CV_PER_LANE], int bs) {
     const float2* src = reinterpret_cast<const float2*>(x + (size_t)bs * (CV_C * CV_L));
 #pragma unroll
     for (int k = 0; k < CV_PER_LANE; ++k) {
       const int i = lane + 64 * k;
-      pre[k] = i < CV_C * CV_L / 2 ? src[i] : make_float2(0.0f, 0.0f);
+      dst[k] = i < CV_C * CV_L / 2 ? src[i] : make_float2(0.0f, 0.0f);
     }
   };
-  if (b < batch) load(b);
-  for (; b < batch; b += stride) {
-    // stage this sample (row c of 47 inputs -> X[c][0..46]); the wave's own LDS rows: in-order LDS, no barrier
+  auto process = [&](float2 (&cur)[CV_PER_LANE], int bc) {
+    // stage this sample (8-byte stores); the wave's own LDS rows: in-order LDS, no barrier
 #pragma unroll
     for (int k = 0; k < CV_PER_LANE; ++k) {
-      const int i = 2 * (lane + 64 * k);
-      if (i < CV_C * CV_L) {
-        X[i / CV_L][i % CV_L] = pre[k].x;
-        X[(i + 1) / CV_L][(i + 1) % CV_L] = pre[k].y;
-      }
+      const int i = lane + 64 * k;
+      if (i < CV_C * CV_L / 2) reinterpret_cast<uint2*>(X)[i] = make_uint2(split_word(cur[k].x), split_word(cur[k].y));
     }
-    if (b + stride < batch) load(b + stride);  // the next sample's loads fly during this one's products
+    if (bc + 2 * stride < batch) load(cur, bc + 2 * stride);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -101,13 +105,17 @@ __global__ __launch_bounds__(64 * CV_WAVES) void k_conv1d_mfma(const float* __re
     for (int nt = 0; nt < 2; ++nt) acc[nt][0] = acc[nt][1] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int s = 0; s < CV_STEPS; ++s) {
-      const float* row = &X[4 * s + kg][CV_S * rr];
-      float v[8];
+      const uint32_t* row = X + (4 * s + kg) * CV_L + CV_S * rr;
+      uint32_t w[CV_K];
 #pragma unroll
-      for (int j = 0; j < CV_K; ++j) v[j] = row[j];
-      v[6] = v[7] = 0.0f;
-      h8 ah, al;
-      split8(v, ah, al);
+      for (int j = 0; j < CV_K; ++j) w[j] = row[j];
+      // hi halves (low 16 bits) and lo halves (high 16 bits) of taps 0..5 packed pairwise; taps 6, 7 zero
+      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+      const u4 hv = {__builtin_amdgcn_perm(w[1], w[0], 0x05040100u), __builtin_amdgcn_perm(w[3], w[2], 0x05040100u),
+                     __builtin_amdgcn_perm(w[5], w[4], 0x05040100u), 0u};
+      const u4 lv = {__builtin_amdgcn_perm(w[1], w[0], 0x07060302u), __builtin_amdgcn_perm(w[3], w[2], 0x07060302u),
+                     __builtin_amdgcn_perm(w[5], w[4], 0x07060302u), 0u};
+      const h8 ah = __builtin_bit_cast(h8, hv), al = __builtin_bit_cast(h8, lv);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const h8 bh = L.wf[s][nt][0][lane], bl = L.wf[s][nt][1][lane];
@@ -124,11 +132,17 @@ __global__ __launch_bounds__(64 * CV_WAVES) void k_conv1d_mfma(const float* __re
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int l = 4 * kg + i;
-        if (l < CV_LOUT) y[((size_t)b * CV_LOUT + l) * CV_O + o] = acc[nt][0][i] + acc[nt][1][i] * (1.0f / CV_SPLIT) + bo;
+        if (l < CV_LOUT) y[((size_t)bc * CV_LOUT + l) * CV_O + o] = acc[nt][0][i] + acc[nt][1][i] * (1.0f / CV_SPLIT) + bo;
       }
     }
     // the next staging overwrites X: every lane's reads of it precede those writes in the wave's LDS order
     __builtin_amdgcn_wave_barrier();
+  };
+  if (b < batch) load(pa, b);
+  if (b + stride < batch) load(pb, b + stride);
+  for (; b < batch; b += 2 * stride) {
+    process(pa, b);
+    if (b + stride < batch) process(pb, b + stride);
   }
 }
 
