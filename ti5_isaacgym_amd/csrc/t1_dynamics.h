@@ -770,56 +770,79 @@ template <typename R> struct BodyKin {
   V3<R> p;
   R V[6];
 };
-// Self-contact terms of the shank (s = 0) and foot (s = 1) of leg `own` from the contact-body kinematics of that leg
-// (Ko) and of the other leg (Kx): accumulated (contact_point's convention) into C[s] / c[s].  mu: the robot's own
-// shapes' friction (the env's; PhysX's average of two equal values).  Self-contacts keep no restitution episode
-// (v_tgt = 0): a leg striking the other leg faster than the bounce threshold is not given a bounce.
-template <typename R>
-T1_HD void self_terms_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2], const BodyKin<R> (&Kx)[2], R mu, R dt,
-                          Sym6<R> (&C)[2], R (&c)[2][6]) {
-  CapPose<R> Po[2], Px[2];
+// One body's view for the self-contact terms: its capsule in world axes about O and its spatial velocity.
+template <typename R> struct SelfBody {
+  CapPose<R> cap;
+  R V[6];
+};
+template <typename R> T1_HD SelfBody<R> self_body(const DynModel& M, int leg, int s, const BodyKin<R>& K) {
+  SelfBody<R> B;
+  B.cap = cap_pose(M.self_cap[leg][s], K.Rb, K.p);
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    Po[s] = cap_pose(M.self_cap[own][s], Ko[s].Rb, Ko[s].p);
-    Px[s] = cap_pose(M.self_cap[1 - own][s], Kx[s].Rb, Kx[s].p);
-  }
+  for (int i = 0; i < 6; ++i) B.V[i] = K.V[i];
+  return B;
+}
+// Self-contact terms of the shank (s = 0) and foot (s = 1) of leg `own` (bodies O) against the other leg's (X):
+// accumulated (contact_point's convention) into C[s] / c[s].  mu: the robot's own shapes' friction (the env's; PhysX's
+// average of two equal values).  Self-contacts keep no restitution episode (v_tgt = 0): a leg striking the other leg
+// faster than the bounce threshold is not given a bounce.
+template <typename R>
+T1_HD void self_terms_bodies(const DynModel& M, int own, const SelfBody<R> (&O)[2], const SelfBody<R> (&X)[2], R mu, R dt,
+                             Sym6<R> (&C)[2], R (&c)[2][6]) {
   // the shank-foot pair within the leg: one query for both bodies (shank first)
   V3<R> xi, ni;
   R peni;
-  const bool intra = capsule_contact(Po[0], Po[1], true, xi, ni, peni);
+  const bool intra = capsule_contact(O[0].cap, O[1].cap, true, xi, ni, peni);
   // one instantiation per body (a plain loop this large is not unrolled, and its register arrays would go to scratch)
   auto body = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
     PointMoments<R> fric;
     moments_zero(fric);
-    self_pair_terms(M, Po[s], Ko[s].V, Px[0], Kx[0].V, own == 0, mu, dt, C[s], c[s], fric);
-    self_pair_terms(M, Po[s], Ko[s].V, Px[1], Kx[1].V, own == 0, mu, dt, C[s], c[s], fric);
+    self_pair_terms(M, O[s].cap, O[s].V, X[0].cap, X[0].V, own == 0, mu, dt, C[s], c[s], fric);
+    self_pair_terms(M, O[s].cap, O[s].V, X[1].cap, X[1].V, own == 0, mu, dt, C[s], c[s], fric);
     if (intra)
-      contact_point(M, xi, s == 0 ? ni : R(-1) * ni, peni, Ko[s].V, mu, R(0), dt, C[s], c[s], fric,
-                    point_velocity(Ko[1 - s].V, xi));
+      contact_point(M, xi, s == 0 ? ni : R(-1) * ni, peni, O[s].V, mu, R(0), dt, C[s], c[s], fric,
+                    point_velocity(O[1 - s].V, xi));
     moments_flush(fric, C[s]);
   };
   body(std::integral_constant<int, 0>{});
   body(std::integral_constant<int, 1>{});
 }
-// the net self-contact forces on the shank / foot of leg `own` (report)
+// the same from the contact-body kinematics of the two legs (Ko: leg `own`, Kx: the other)
 template <typename R>
-T1_HD void self_forces_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2], const BodyKin<R> (&Kx)[2], R mu,
-                           V3<R> (&F)[2]) {
-  CapPose<R> Po[2], Px[2];
+T1_HD void self_terms_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2], const BodyKin<R> (&Kx)[2], R mu, R dt,
+                          Sym6<R> (&C)[2], R (&c)[2][6]) {
+  SelfBody<R> O[2], X[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    Po[s] = cap_pose(M.self_cap[own][s], Ko[s].Rb, Ko[s].p);
-    Px[s] = cap_pose(M.self_cap[1 - own][s], Kx[s].Rb, Kx[s].p);
+    O[s] = self_body(M, own, s, Ko[s]);
+    X[s] = self_body(M, 1 - own, s, Kx[s]);
   }
+  self_terms_bodies(M, own, O, X, mu, dt, C, c);
+}
+// the net self-contact forces on the shank / foot of leg `own` (report)
+template <typename R>
+T1_HD void self_forces_bodies(const DynModel& M, int own, const SelfBody<R> (&O)[2], const SelfBody<R> (&X)[2], R mu,
+                              V3<R> (&F)[2]) {
   auto body = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
-    F[s] = self_pair_force(M, Po[s], Ko[s].V, Px[0], Kx[0].V, own == 0, mu) +
-           self_pair_force(M, Po[s], Ko[s].V, Px[1], Kx[1].V, own == 0, mu) +
-           self_pair_force(M, Po[s], Ko[s].V, Po[1 - s], Ko[1 - s].V, s == 0, mu);
+    F[s] = self_pair_force(M, O[s].cap, O[s].V, X[0].cap, X[0].V, own == 0, mu) +
+           self_pair_force(M, O[s].cap, O[s].V, X[1].cap, X[1].V, own == 0, mu) +
+           self_pair_force(M, O[s].cap, O[s].V, O[1 - s].cap, O[1 - s].V, s == 0, mu);
   };
   body(std::integral_constant<int, 0>{});
   body(std::integral_constant<int, 1>{});
+}
+template <typename R>
+T1_HD void self_forces_leg(const DynModel& M, int own, const BodyKin<R> (&Ko)[2], const BodyKin<R> (&Kx)[2], R mu,
+                           V3<R> (&F)[2]) {
+  SelfBody<R> O[2], X[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    O[s] = self_body(M, own, s, Ko[s]);
+    X[s] = self_body(M, 1 - own, s, Kx[s]);
+  }
+  self_forces_bodies(M, own, O, X, mu, F);
 }
 
 // ---------------------------------------------------------------------------------------------------

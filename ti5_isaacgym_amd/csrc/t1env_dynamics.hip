@@ -338,6 +338,7 @@ struct Dyn4Lds {
   float cap[2][CAP_N][DYN_ENVS];
   float epi[EPI_N][DYN_ENVS];
   float vib[2][DYN_ENVS];  // the base-box halves' end-of-step restitution episodes (helpers, for the report)
+  int xflag[2];            // helper h's self-collision bodies of the current (sub)step published (helper_signal)
 };
 static_assert(FR_N <= 2 * CT_N, "the fresh outputs fit the contact-term region");
 
@@ -385,11 +386,9 @@ static_assert(ST_N <= POSE_N, "the substep state fits the pose rows");
 #else
 #define T1_SELF_CODE 1
 #endif
-// a helper's kinematics of one published state: the base frame and the contact bodies of leg `leg` (own state P), and
-// with self-collision on (wave-uniform) those of the other leg too (its state Po: the same base rows)
-__device__ __forceinline__ void helper_kinematics(const DynModel& M, const float (*P)[DYN_ENVS],
-                                                  const float (*Po)[DYN_ENVS], int lane, int leg, BaseFrame<float>& F,
-                                                  BodyKin<float> (&Ko)[2], BodyKin<float> (&Kx)[2]) {
+// a helper's kinematics of one published state: the base frame and the contact bodies of leg `leg` (own state P)
+__device__ __forceinline__ void helper_kinematics(const DynModel& M, const float (*P)[DYN_ENVS], int lane, int leg,
+                                                  BaseFrame<float>& F, BodyKin<float> (&Ko)[2]) {
   BaseState<float> sb;
   float qh[NLEG], qdh[NLEG];
 #pragma unroll
@@ -400,11 +399,6 @@ __device__ __forceinline__ void helper_kinematics(const DynModel& M, const float
   for (int k = 0; k < NLEG; ++k) { qh[k] = P[ST_Q + k][lane]; qdh[k] = P[ST_QD + k][lane]; }
   base_frame(sb, F);
   leg_body_kinematics(M, F, qh, qdh, leg, Ko);
-  if (T1_SELF_CODE && M.self_collisions) {
-#pragma unroll
-    for (int k = 0; k < NLEG; ++k) { qh[k] = Po[ST_Q + k][lane]; qdh[k] = Po[ST_QD + k][lane]; }
-    leg_body_kinematics(M, F, qh, qdh, 1 - leg, Kx);
-  }
 }
 __device__ __forceinline__ void publish_state(float (*P)[DYN_ENVS], int lane, const BaseState<float>& sb,
                                               const float q[NLEG], const float qd[NLEG]) {
@@ -688,6 +682,54 @@ __device__ __forceinline__ void leg_report_rigid(const DynModel& M, const t1env_
   }
 }
 
+// Self-collision needs the other leg's shank / foot too: each helper publishes its own bodies' capsules and velocities
+// (rows SB_ROW.. of its leg's pose region, unused by the state) and the two helpers meet at an LDS flag -- a barrier of
+// the two helper waves only (the leg waves run their backward pass meanwhile), instead of each helper recomputing the
+// other leg's kinematics.  The flags count (sub)steps, so they never need resetting within a launch; a helper
+// overwrites its rows only after the next S1, after the other has read them (before S2).
+constexpr int SB_ROW = ST_N, SB_N = 12;  // per body: capsule ends p (3), q (3), spatial velocity (6)
+static_assert(SB_ROW + 2 * SB_N <= POSE_N, "the self-collision bodies fit the pose rows");
+__device__ __forceinline__ void publish_self_bodies(float (*P)[DYN_ENVS], int lane, const SelfBody<float> (&O)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    float (*D)[DYN_ENVS] = P + SB_ROW + s * SB_N;
+    D[0][lane] = O[s].cap.p.x; D[1][lane] = O[s].cap.p.y; D[2][lane] = O[s].cap.p.z;
+    D[3][lane] = O[s].cap.q.x; D[4][lane] = O[s].cap.q.y; D[5][lane] = O[s].cap.q.z;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) D[6 + i][lane] = O[s].V[i];
+  }
+}
+__device__ __forceinline__ void read_self_bodies(const DynModel& M, const float (*P)[DYN_ENVS], int lane, int leg,
+                                                 SelfBody<float> (&X)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const float (*D)[DYN_ENVS] = P + SB_ROW + s * SB_N;
+    X[s].cap.p = v3<float>(D[0][lane], D[1][lane], D[2][lane]);
+    X[s].cap.q = v3<float>(D[3][lane], D[4][lane], D[5][lane]);
+    X[s].cap.r = M.self_cap[leg][s].r;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) X[s].V[i] = D[6 + i][lane];
+  }
+}
+__device__ __forceinline__ void helper_signal(int* flag, int v, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's row stores before the flag
+  if (lane == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void helper_wait(const int* flag, int v) {
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// both helpers' self-collision bodies of (sub)step `tick` (1, 2, ...): O from this helper's kinematics, X the other's
+__device__ __forceinline__ void exchange_self_bodies(const DynModel& M, Dyn4Lds& lds, int lane, int leg, int tick,
+                                                     const BodyKin<float> (&Ko)[2], SelfBody<float> (&O)[2],
+                                                     SelfBody<float> (&X)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) O[s] = self_body(M, leg, s, Ko[s]);
+  publish_self_bodies(lds.pose[leg], lane, O);
+  helper_signal(&lds.xflag[leg], tick, lane);
+  helper_wait(&lds.xflag[1 - leg], tick);
+  read_self_bodies(M, lds.pose[1 - leg], lane, 1 - leg, X);
+}
 // the contact-force report from the poses the helper computes itself from the end-of-step state: terrain forces plus
 // the self-contact forces fself of the shank / foot
 // (vt: the restitution set points of the shank, foot and base half; the base box's whole report uses the larger of
@@ -757,9 +799,9 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     int cb, ce;
     base_contact_range(M, leg, cb, ce);
     const float (*P)[DYN_ENVS] = lds.pose[leg];
-    const float (*Po)[DYN_ENVS] = lds.pose[1 - leg];  // the other leg's published state (self-collision)
     // this helper's restitution episodes: its leg's shank, foot and base-box half (include/t1env.h contact_vimp)
     float* const vimp_row = B.contact_vimp + (size_t)n * NVIMP;
+    if (lane == 0) lds.xflag[leg] = 0;  // before the first S1; the other helper first reads it after that barrier
     float vi_sh = vimp_row[vimp_shank(leg)], vi_ft = vimp_row[vimp_foot(leg)], vi_b = vimp_row[vimp_base(leg)];
     T1_PROF_MARK(10);
     // the epilogue's inputs the step does not change, staged while the leg waves set up and run the first
@@ -770,8 +812,10 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
       __syncthreads();  // S1: the substep states published
       T1_PROF_MARK(8);
       BaseFrame<float> F;
-      BodyKin<float> Ko[2], Kx[2];
-      helper_kinematics(M, P, Po, lane, leg, F, Ko, Kx);
+      BodyKin<float> Ko[2];
+      helper_kinematics(M, P, lane, leg, F, Ko);
+      SelfBody<float> Os[2], Xs[2];
+      if (T1_SELF_CODE && M.self_collisions) exchange_self_bodies(M, lds, lane, leg, sub + 1, Ko, Os, Xs);
       T1_PROF_MARK(20);
       const V3<float> abs = F.abs;
       const int32_t bound_sh = terrain_bound_raw_any(T, Ko[0].p.x + abs.x, Ko[0].p.y + abs.y);
@@ -787,7 +831,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
       // the foot's terrain queries go out first; the self-contact terms run while its height loads are in flight
       body_contact_query_apply<T1_POINTS_PER_BODY>(M, T, M.contact_start[1 + 6 * leg + K_FOOT], Ko[1].Rb, Ko[1].p, abs,
                                                    Ko[1].V, mu, e, vi_ft, dt, Cs[1], cs[1], [&] {
-        if (T1_SELF_CODE && M.self_collisions) self_terms_leg(M, leg, Ko, Kx, mu_self, dt, Cs, cs);
+        if (T1_SELF_CODE && M.self_collisions) self_terms_bodies(M, leg, Os, Xs, mu_self, dt, Cs, cs);
         T1_PROF_MARK(21);
       });
       lds_put_sym(lds.ct[leg] + XCH, lane, Cs[1], cs[1]);
@@ -817,10 +861,14 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     float (*FR)[DYN_ENVS] = FUSED ? reinterpret_cast<float (*)[DYN_ENVS]>(&lds.ct[0][0][0]) : nullptr;
     {  // the contact-force report beside the leg wave's rigid-state report
       BaseFrame<float> F;
-      BodyKin<float> Ko[2], Kx[2];
-      helper_kinematics(M, P, Po, lane, leg, F, Ko, Kx);
+      BodyKin<float> Ko[2];
+      helper_kinematics(M, P, lane, leg, F, Ko);
       V3<float> fself[2] = {v3<float>(0.0f, 0.0f, 0.0f), v3<float>(0.0f, 0.0f, 0.0f)};
-      if (T1_SELF_CODE && M.self_collisions) self_forces_leg(M, leg, Ko, Kx, mu_self, fself);
+      if (T1_SELF_CODE && M.self_collisions) {
+        SelfBody<float> Os[2], Xs[2];
+        exchange_self_bodies(M, lds, lane, leg, C.decimation + 1, Ko, Os, Xs);
+        self_forces_bodies(M, leg, Os, Xs, mu_self, fself);
+      }
       const float vt[3] = {restitution_target(M, e, vi_sh), restitution_target(M, e, vi_ft),
                            restitution_target(M, e, vi_b)};
       const float vt_o = restitution_target(M, e, lds.vib[1 - leg][lane]);  // the other base half (leg 0 reports)
