@@ -339,6 +339,7 @@ struct Dyn4Lds {
   float epi[EPI_N][DYN_ENVS];
   float vib[2][DYN_ENVS];  // the base-box halves' end-of-step restitution episodes (helpers, for the report)
   int xflag[2];            // helper h's self-collision bodies of the current (sub)step published (helper_signal)
+  float vis[2][DYN_ENVS];  // the shanks' end-of-step restitution episodes (leg waves, for the helpers' report)
 };
 static_assert(FR_N <= 2 * CT_N, "the fresh outputs fit the contact-term region");
 
@@ -802,7 +803,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     // this helper's restitution episodes: its leg's shank, foot and base-box half (include/t1env.h contact_vimp)
     float* const vimp_row = B.contact_vimp + (size_t)n * NVIMP;
     if (lane == 0) lds.xflag[leg] = 0;  // before the first S1; the other helper first reads it after that barrier
-    float vi_sh = vimp_row[vimp_shank(leg)], vi_ft = vimp_row[vimp_foot(leg)], vi_b = vimp_row[vimp_base(leg)];
+    float vi_ft = vimp_row[vimp_foot(leg)], vi_b = vimp_row[vimp_base(leg)];
     T1_PROF_MARK(10);
     // the epilogue's inputs the step does not change, staged while the leg waves set up and run the first
     // forward pass (nothing writes them before the epilogue)
@@ -818,7 +819,6 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
       if (T1_SELF_CODE && M.self_collisions) exchange_self_bodies(M, lds, lane, leg, sub + 1, Ko, Os, Xs);
       T1_PROF_MARK(20);
       const V3<float> abs = F.abs;
-      const int32_t bound_sh = terrain_bound_raw_any(T, Ko[0].p.x + abs.x, Ko[0].p.y + abs.y);
       const int32_t bound_base = terrain_bound_raw_any(T, abs.x, abs.y);
       Sym6<float> Cs[2];
       float cs[2][6];
@@ -835,7 +835,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
         T1_PROF_MARK(21);
       });
       lds_put_sym(lds.ct[leg] + XCH, lane, Cs[1], cs[1]);
-      body_terms_at(M, T, Ko[0], lane, 1 + 6 * leg + K_SHANK, abs, mu, e, vi_sh, dt, Cs[0], cs[0], lds.ct[leg], bound_sh);
+      lds_put_sym(lds.ct[leg], lane, Cs[0], cs[0]);  // the shank's self terms (its terrain terms: the leg wave's)
       T1_PROF_MARK(3);
       __syncthreads();  // S2: contact terms published
       T1_PROF_MARK(11);
@@ -855,7 +855,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     }
     T1_PROF_MARK(7);
     lds.vib[leg][lane] = vi_b;
-    if (active) { vimp_row[vimp_shank(leg)] = vi_sh; vimp_row[vimp_foot(leg)] = vi_ft; vimp_row[vimp_base(leg)] = vi_b; }
+    if (active) { vimp_row[vimp_foot(leg)] = vi_ft; vimp_row[vimp_base(leg)] = vi_b; }
     __syncthreads();  // R1: the end-of-step states published
     T1_PROF_MARK(8);
     float (*FR)[DYN_ENVS] = FUSED ? reinterpret_cast<float (*)[DYN_ENVS]>(&lds.ct[0][0][0]) : nullptr;
@@ -869,7 +869,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
         exchange_self_bodies(M, lds, lane, leg, C.decimation + 1, Ko, Os, Xs);
         self_forces_bodies(M, leg, Os, Xs, mu_self, fself);
       }
-      const float vt[3] = {restitution_target(M, e, vi_sh), restitution_target(M, e, vi_ft),
+      const float vt[3] = {restitution_target(M, e, lds.vis[leg][lane]), restitution_target(M, e, vi_ft),
                            restitution_target(M, e, vi_b)};
       const float vt_o = restitution_target(M, e, lds.vib[1 - leg][lane]);  // the other base half (leg 0 reports)
       const float vt_base = vt_o > vt[2] ? vt_o : vt[2];
@@ -899,6 +899,10 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
 #pragma unroll
     for (int k = 0; k < NLEG; ++k)
       CAP[CAP_ACT + k][lane] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
+  // the shank's terrain contact is this wave's (its forward pass has the shank's pose; the helper, the critical path
+  // before S2, keeps the foot and the self-contacts): restitution episode, combined friction / restitution
+  float vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
+  const float e_g = ground_restitution(M, PB.restitution);
   T1_PROF_MARK(10);
   publish_state(P, lane, sb, q, qd);  // the helpers start each substep from the state (their own kinematics)
   for (int sub = 0; sub < C.decimation; ++sub) {
@@ -909,7 +913,19 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     base_frame(sb, F);
     LegPass<float> st;
     leg_forward_nc<T1_LEG_CONTACT_MASK>(M, PL, F, q, qd, leg, dt, st,
-                                        [&](auto, const M3<float>&, V3<float>, const float*) {});
+                                        [&](auto kc, const M3<float>& Rk, V3<float> pk, const float* V) {
+      if constexpr (decltype(kc)::value == K_SHANK) {
+        // the shank's terrain terms, stashed in this leg's base-block rows (free between S1 and S2) until the fold-in
+        const int b = 1 + 6 * leg + K_SHANK;
+        Sym6<float> Ct;
+        float ct6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        sym_zero(Ct);
+        const int32_t bnd = terrain_bound_raw_any(T, pk.x + F.abs.x, pk.y + F.abs.y);
+        body_contact_fixed<T1_POINTS_PER_BODY>(M, T, pk.z + F.abs.z - M.contact_radius[b], bnd, M.contact_start[b], Rk,
+                                               pk, F.abs, V, PB.friction, e_g, vi_sh, dt, Ct, ct6);
+        lds_put_sym(lds.xch[leg], lane, Ct, ct6);
+      }
+    });
     T1_PROF_MARK(1);
     pd_torques_staged(M, C, PD, lane, K, ctr, sub, L.lag, j0, q, qd, tau);
     T1_PROF_MARK(0);
@@ -931,7 +947,16 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     {
       Sym6<float> Csh, Cft;
       float csh[6], cft[6];
-      lds_get_sym(lds.ct[leg], lane, Csh, csh);
+      lds_get_sym(lds.ct[leg], lane, Csh, csh);  // the helper's self terms of the shank
+      {
+        Sym6<float> Ct;
+        float ct6[6];
+        lds_get_sym(lds.xch[leg], lane, Ct, ct6);  // plus this wave's terrain terms of it
+#pragma unroll
+        for (int i = 0; i < 21; ++i) Csh.a[i] += Ct.a[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) csh[i] += ct6[i];
+      }
       lds_get_sym(lds.ct[leg] + XCH, lane, Cft, cft);
       leg_apply_contacts<K_SHANK, K_FOOT>(Csh, csh, Cft, cft, tau, dt, st, lb, Ab, g6);
 #ifdef T1_WHATIF_FOLD2  // timing-only: the fold-in and elimination run twice (second result scaled by 0 and added)
@@ -1005,6 +1030,8 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     publish_state(P, lane, sb, q, qd);  // the helper read the previous one before S2; after the last substep: the
                                         // end-of-step state its contact-force report starts from
   }
+  lds.vis[leg][lane] = vi_sh;  // the shank's episode for the helper's contact-force report
+  if (active) B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
   __syncthreads();  // R1: the end-of-step state published (the helpers compute the contact forces meanwhile)
   T1_PROF_MARK(7);
   if (active) {
