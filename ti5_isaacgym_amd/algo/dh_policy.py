@@ -149,40 +149,6 @@ def conv1d_as_gemm(x, conv, channels_last=False):
     return y.view(B, Lout, conv.out_channels)
 
 
-def conv1d_blocked(x, conv, channels_last=False):
-    """nn.Conv1d with kernel = 2 * stride (both history convs: 6/3 and 4/2) without unfolding.  The input is cut into
-    non-overlapping blocks of `stride` positions (nb = Lout + 1 blocks); output position l sums block l through the
-    kernel's first half and block l + 1 through its second half, so ONE GEMM of the blocks against [W_first; W_second]
-    (2 O columns) and a shifted add replace the unfolded (B Lout) x (C k) matrix, which duplicates every input (the
-    update's unfold copy was 545 MB per minibatch, profiles/r03ak_ppo_update_profile_bf16_eager.txt).  Channels-last
-    blocks are views (no copy); channels-first blocks are one permuted copy of the used positions.  Returns
-    (B, Lout, O); same arithmetic as the convolution up to fp32 summation order."""
-    k, st = conv.kernel_size[0], conv.stride[0]
-    if k != 2 * st:
-        return conv1d_as_gemm(x, conv, channels_last)
-    if channels_last:
-        B, L, C = x.shape
-    else:
-        B, C, L = x.shape
-    Lout = (L - k) // st + 1
-    nb = Lout + 1
-    O = conv.out_channels
-    w = conv.weight.view(O, C, 2, st)                      # [o, c, half, tap in half]
-    if channels_last:   # block row = positions (tap-major), channels inner: a view of x
-        z = x[:, :nb * st, :].reshape(B * nb, st * C)
-        wcat = w.permute(2, 0, 3, 1).reshape(2 * O, st * C)
-    else:               # block row = channels (c-major), taps inner
-        z = x[..., :nb * st].reshape(B, C, nb, st).permute(0, 2, 1, 3).reshape(B * nb, C * st)
-        wcat = w.permute(2, 0, 1, 3).reshape(2 * O, C * st)
-    zero = torch.zeros(2 * O, device=x.device, dtype=conv.weight.dtype)
-    if torch.is_grad_enabled():   # split-K weight gradient (K = B * nb rows)
-        p = _LinearSplitK.apply(z, wcat, zero)
-    else:
-        p = torch.mm(z, wcat.t())
-    p = p.view(B, nb, 2 * O)
-    return p[:, :Lout, :O] + p[:, 1:, O:] + conv.bias
-
-
 class HistoryEncoder(nn.Sequential):
     """The reference's long-history CNN (actor_critic_dh.py:75-96): the same nn.Sequential layers and parameter
     names (so checkpoints load either way).  On the host the layers run as written (nn.Conv1d, bit-identical to the
@@ -200,7 +166,7 @@ class HistoryEncoder(nn.Sequential):
                 y = None
                 if not last and not torch.is_grad_enabled() and x.dtype == torch.float32 and m.weight.dtype == x.dtype:
                     y = conv1d_direct(x, m)   # inference (the rollout's act()): the HIP direct conv
-                x = y if y is not None else conv1d_blocked(x, m, channels_last=last)
+                x = y if y is not None else conv1d_as_gemm(x, m, channels_last=last)
                 last = True
             elif isinstance(m, nn.Flatten) and last:
                 x = x.transpose(1, 2).reshape(x.shape[0], -1)   # (B, O, Lout) order, as nn.Flatten of NCL
