@@ -25,6 +25,18 @@ extern "C" {
 int t1policy_conv1d_forward(const float* x, const float* wt, const float* bias, float* y, int batch, int channels,
                             int length, int out_channels, int kernel, int stride, void* stream);
 
+/* The same convolution with the weight prepared once per weight version (the rollout's act(): the weights change
+ * only at the PPO update).  pack_weights builds the kernel's split fp16 fragments of weight (out_channels, channels,
+ * kernel) -- the layout torch's nn.Conv1d holds -- into frag (frag_bytes() bytes, 16-byte aligned, caller-owned
+ * device memory); forward_packed then reads frag instead of a tap-major weight.  x and frag 16-byte aligned,
+ * batch * channels * length * 4 < 2^31.  Same results as t1policy_conv1d_forward up to fp32 summation order
+ * (both within 1e-5 * (1 + |y|) of an fp64 conv); same return codes. */
+int t1policy_conv1d_frag_bytes(void);
+int t1policy_conv1d_pack_weights(const float* weight, void* frag, int channels, int out_channels, int kernel,
+                                 void* stream);
+int t1policy_conv1d_forward_packed(const float* x, const void* frag, const float* bias, float* y, int batch,
+                                   int channels, int length, int out_channels, int kernel, int stride, void* stream);
+
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py
  * _HistoryRows restates this in torch):

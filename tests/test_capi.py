@@ -87,6 +87,9 @@ def test_policy_header_exports(lib):
         assert hasattr(lib, n), n
     # argument errors are reported without touching the GPU
     assert lib.t1policy_conv1d_forward(None, None, None, None, 1, 66, 47, 32, 6, 3, None) == -1
+    assert lib.t1policy_conv1d_forward_packed(None, None, None, None, 1, 66, 47, 32, 6, 3, None) == -1
+    assert lib.t1policy_conv1d_pack_weights(None, None, 66, 32, 6, None) == -1
+    assert lib.t1policy_conv1d_frag_bytes() == 17 * 2 * 2 * 64 * 16
 
 
 def test_env_refuses_external_torques():

@@ -95,7 +95,8 @@ EXPORTS = ["t1env_create", "t1env_destroy", "t1env_init", "t1env_set_terrain", "
            "t1env_measure_heights", "t1env_critic_heights", "t1env_reset_idx", "t1env_set_substep_log"]
 
 # include/t1policy.h: the DH policy's HIP kernels, in the same library
-POLICY_EXPORTS = ["t1policy_conv1d_forward", "t1policy_history_rows"]
+POLICY_EXPORTS = ["t1policy_conv1d_forward", "t1policy_history_rows", "t1policy_conv1d_frag_bytes",
+                  "t1policy_conv1d_pack_weights", "t1policy_conv1d_forward_packed"]
 
 _lib = None
 
@@ -131,6 +132,9 @@ def load():
         "t1env_critic_heights": ([vp, i32, i32, f32, vp, vp, vp, vp], C.c_int),
         "t1policy_conv1d_forward": ([vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
         "t1policy_history_rows": ([vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
+        "t1policy_conv1d_frag_bytes": ([], C.c_int),
+        "t1policy_conv1d_pack_weights": ([vp, vp, i32, i32, i32, vp], C.c_int),
+        "t1policy_conv1d_forward_packed": ([vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

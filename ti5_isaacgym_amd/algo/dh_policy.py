@@ -117,16 +117,56 @@ def conv1d_direct(x, conv):
     B, C, L = x.shape
     O = conv.out_channels
     lout = (L - k) // st + 1
-    wt = conv.weight.detach().permute(1, 2, 0).contiguous()   # tap-major: wt[c, t, o]
     bias = conv.bias.detach().contiguous()
     y = torch.empty(B, lout, O, device=x.device, dtype=torch.float32)
-    rc = lib.t1policy_conv1d_forward(x.data_ptr(), wt.data_ptr(), bias.data_ptr(), y.data_ptr(), B, C, L, O, k, st,
-                                     torch.cuda.current_stream(x.device).cuda_stream)
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    if x.data_ptr() % 16 == 0 and B * C * L * 4 < 2 ** 31:
+        frag = packed_conv_weights(conv, stream)
+        rc = 1 if frag is None else lib.t1policy_conv1d_forward_packed(
+            x.data_ptr(), frag.data_ptr(), bias.data_ptr(), y.data_ptr(), B, C, L, O, k, st, stream)
+    else:
+        wt = conv.weight.detach().permute(1, 2, 0).contiguous()   # tap-major: wt[c, t, o]
+        rc = lib.t1policy_conv1d_forward(x.data_ptr(), wt.data_ptr(), bias.data_ptr(), y.data_ptr(), B, C, L, O, k,
+                                         st, stream)
     if rc == 1:
         return None
     if rc != 0:
         raise RuntimeError(f"t1policy_conv1d_forward failed (rc={rc})")
     return y
+
+
+def packed_conv_weights(conv, stream=None):
+    """The conv's weights as the packed-fragment kernel's split fp16 fragments (t1policy_conv1d_pack_weights), kept on
+    the module and rebuilt only when the weight changed (its version counter: the optimizer's in-place step, a
+    load_state_dict).  A captured act() graph reads the buffer in place: refresh_packed_weights() before each replay
+    repacks after a PPO update.  None for a shape the library has no instance of."""
+    from .. import _lib
+    w = conv.weight
+    key = (w._version, w.data_ptr())
+    frag = getattr(conv, "_t1_frag", None)
+    if frag is not None and getattr(conv, "_t1_frag_key", None) == key:
+        return frag
+    lib = _lib.load()
+    if frag is None or frag.device != w.device:
+        frag = torch.empty(lib.t1policy_conv1d_frag_bytes(), device=w.device, dtype=torch.uint8)
+    if stream is None:
+        stream = torch.cuda.current_stream(w.device).cuda_stream
+    wc = w.detach().contiguous()
+    rc = lib.t1policy_conv1d_pack_weights(wc.data_ptr(), frag.data_ptr(), conv.in_channels, conv.out_channels,
+                                          conv.kernel_size[0], stream)
+    if rc == 1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"t1policy_conv1d_pack_weights failed (rc={rc})")
+    conv._t1_frag, conv._t1_frag_key = frag, key
+    return frag
+
+
+def refresh_packed_weights(module):
+    """Repack every Conv1d under `module` whose packed fragments are stale (before replaying a captured act())."""
+    for m in module.modules():
+        if isinstance(m, nn.Conv1d) and getattr(m, "_t1_frag", None) is not None:
+            packed_conv_weights(m)
 
 
 def conv1d_as_gemm(x, conv, channels_last=False):

@@ -26,7 +26,7 @@ import torch.optim as optim
 from torch.distributions import Normal
 
 from . import distributed as dist_util
-from .dh_policy import ActorCriticDH
+from .dh_policy import ActorCriticDH, refresh_packed_weights
 from .rollout import RolloutStorage
 
 
@@ -163,6 +163,7 @@ class DHPPO:
                 self.graph_act = False
                 return None
             entry = self._act_graphs[key] = (graph, outs)
+        refresh_packed_weights(self.actor_critic)  # the conv's packed weights after a PPO update (in place)
         entry[0].replay()
         return entry[1]
 

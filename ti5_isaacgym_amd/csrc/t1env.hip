@@ -429,6 +429,9 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
     e->dyn.shift_blocks = 0;
     if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))  // > 0: shift workgroups in the launch; -1: stand-alone shift
       if (atoi(sb) > 0 || atoi(sb) == -1) e->dyn.shift_blocks = atoi(sb);
+    e->dyn.shift_delay = T1_SHIFT_DELAY_DEFAULT;
+    if (const char* sd = getenv("T1ENV_SHIFT_DELAY"))  // tuning: delayed start of the in-launch shift (100 MHz ticks)
+      if (atoi(sd) >= 0) e->dyn.shift_delay = atoi(sd);
   }
   for (int b = 0; b < NB; ++b) e->max_contact_radius = fmaxf(e->max_contact_radius, dm.contact_radius[b]);
   *out = e;

@@ -130,7 +130,11 @@ __device__ __forceinline__ void zero_unit_resets(const ShiftArgs& S, int u, uint
 // A history-shift workgroup (j of nsw) of BS threads; `words` is LDS scratch of >= BS uint32.
 template <bool FUSED, int BS>
 __device__ __forceinline__ void shift_workgroup(const ShiftArgs& S, const FusedArgs& FA, int N, int j, int nsw,
-                                                uint32_t* words) {
+                                                uint32_t* words, int delay) {
+  if (delay > 0) {  // let the dynamics workgroups' prologue loads go first (wave-uniform; the 100 MHz real-time clock)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)delay) __builtin_amdgcn_s_sleep(32);
+  }
   if constexpr (!FUSED) {
     shift_history(S, (int64_t)j * BS + threadIdx.x, (int64_t)nsw * BS);
   } else {
@@ -771,11 +775,11 @@ template <bool HF, bool FUSED>
 __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* __restrict__ Mp, const t1env_config* __restrict__ Cp,
                                                    t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
                                                    t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA,
-                                                   SubLog LG) {
+                                                   SubLog LG, int shift_delay) {
   __shared__ Dyn4Lds lds;
   if ((int)blockIdx.x >= dyn_blocks) {
     shift_workgroup<FUSED, D4_BLOCK>(S, FA, Cp->num_envs, blockIdx.x - dyn_blocks, gridDim.x - dyn_blocks,
-                                     reinterpret_cast<uint32_t*>(&lds.xch[0][0][0]));
+                                     reinterpret_cast<uint32_t*>(&lds.xch[0][0][0]), shift_delay);
     return;
   }
   Terrain T = Tin;
@@ -1104,7 +1108,8 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
   const bool hf = T.type != 0;
   if (log && !fused) return (int)hipErrorInvalidValue;  // the substep log: fused steps only (the caller checks)
 #define T1_LAUNCH(HF, FU) \
-  hipLaunchKernelGGL((k_dyn4<HF, FU>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA, LG)
+  hipLaunchKernelGGL((k_dyn4<HF, FU>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA, LG, \
+                     cfg.shift_delay)
   if (fused) { if (hf) T1_LAUNCH(true, true); else T1_LAUNCH(false, true); }
   else { if (hf) T1_LAUNCH(true, false); else T1_LAUNCH(false, false); }
 #undef T1_LAUNCH

@@ -26,11 +26,15 @@ struct SubLog {
   float* torque;
 };
 
+// default delayed start of the in-launch history-shift workgroups (100 MHz ticks; DynLaunch::shift_delay)
+constexpr int T1_SHIFT_DELAY_DEFAULT = 0;
+
 // launch shape of the dynamics kernel
 struct DynLaunch {
   int waves;         // 4: k_dyn4 (leg waves + contact helper waves; the only kernel since round 3)
   int cus;           // compute units of the device (default history-shift grid)
   int shift_blocks;  // > 0: history-shift workgroups override (tuning)
+  int shift_delay;   // in-launch shift workgroups start this many 100 MHz ticks late (T1ENV_SHIFT_DELAY; 0 = at once)
 };
 int t1_dyn_waves_default();
 

@@ -18,6 +18,8 @@
 // each wave stages one sample (12.4 KB, coalesced) into its own LDS rows while the next sample's loads are in flight.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -146,6 +148,206 @@ __global__ __launch_bounds__(64 * CV_WAVES) void k_conv1d_mfma(const float* __re
   }
 }
 
+// ---- the packed-weight form (t1policy_conv1d_pack_weights + t1policy_conv1d_forward_packed).
+// The split weight fragments are built once per weight version by k_conv1d_pack (CV_FRAG_BYTES, [step][column tile]
+// [hi, lo][lane] h8, the layout of ConvLds::wf) and each wave of k_conv1d_regs holds all 68 of them in registers (272
+// VGPRs, most in AGPRs, which the MFMAs read directly): no fragment LDS traffic (69.6 KB per sample in k_conv1d_mfma)
+// and no per-workgroup fragment build.  One wave per SIMD; each wave takes a contiguous run of batch / waves samples
+// (8 at 8192 on 256 CUs: balanced, where k_conv1d_mfma's 6 waves per CU ran 5 or 6 samples each, two waves sharing
+// a SIMD), with the next two samples' loads in flight while it splits and multiplies the current one.
+constexpr int CV_FRAGS = CV_STEPS * 2 * 2;                       // 68 h8 per lane
+constexpr int CV_FRAG_BYTES = CV_FRAGS * 64 * 16;               // 69,632
+constexpr int CR_WAVES = 4;
+
+__global__ __launch_bounds__(256) void k_conv1d_pack(const float* __restrict__ w, h8* __restrict__ frag) {
+  // w: the Conv1d weight as torch holds it, (O, C, K) contiguous
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < CV_STEPS * 2 * 64; e += gridDim.x * blockDim.x) {
+    const int s = e >> 7, nt = (e >> 6) & 1, l = e & 63;
+    const int c = 4 * s + (l >> 4), o = 16 * nt + (l & 15);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (c < CV_C && j < CV_K) ? w[(o * CV_C + c) * CV_K + j] : 0.0f;
+    h8 hi, lo;
+    split8(v, hi, lo);
+    frag[((s * 2 + nt) * 2 + 0) * 64 + l] = hi;
+    frag[((s * 2 + nt) * 2 + 1) * 64 + l] = lo;
+  }
+}
+
+__global__ __launch_bounds__(64 * CR_WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_conv1d_regs(const float* __restrict__ x, const h8* __restrict__ frag, const float* __restrict__ bias,
+                   float* __restrict__ y, int batch) {
+  __shared__ uint32_t XS[CR_WAVES][CV_CPAD * CV_L];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = blockIdx.x * CR_WAVES + wave, nw = gridDim.x * CR_WAVES;
+  const int b0 = (int)((long long)g * batch / nw), b1 = (int)((long long)(g + 1) * batch / nw);
+  uint32_t* X = XS[wave];
+  for (int i = CV_C * CV_L + lane; i < CV_CPAD * CV_L; i += 64) X[i] = 0u;  // the 2 zero channels stay zero
+  // the sample loads: 8-byte loads (a sample is 12,408 B, 8-byte aligned), 25 per lane, nothing past the sample
+  float2 pa[CV_PER_LANE], pb[CV_PER_LANE];
+  // every load and store of the loop is unconditional (clamped indices), so the compiler's vmcnt bookkeeping stays
+  // exact and its waits for the current sample leave the next one's loads in flight
+  auto load = [&](float2 (&dst)[CV_PER_LANE], int bs) {
+    const float2* src = reinterpret_cast<const float2*>(x + (size_t)(bs < b1 ? bs : b1 - 1) * (CV_C * CV_L));
+#pragma unroll
+    for (int k = 0; k < CV_PER_LANE; ++k) {
+      const int i = lane + 64 * k;
+      dst[k] = src[i < CV_C * CV_L / 2 ? i : CV_C * CV_L / 2 - 1];
+    }
+  };
+  if (b0 < b1) load(pa, b0);
+  if (b0 + 1 < b1) load(pb, b0 + 1);
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  h8 bf[CV_STEPS][2][2];
+#pragma unroll
+  for (int s = 0; s < CV_STEPS; ++s)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) bf[s][nt][hl] = frag[((s * 2 + nt) * 2 + hl) * 64 + lane];
+  const int r = lane & 15, kg = lane >> 4;
+  const int rr = r < CV_LOUT ? r : CV_LOUT - 1;  // rows 14, 15 of the tile: a copy of row 13, never stored
+  float bo[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) bo[nt] = bias[16 * nt + (lane & 15)];
+  // the fragments retired before the loop (an empty asm use of each): otherwise the compiler's wait for them (the
+  // youngest loads at the loop entry) stays inside the loop as a vmcnt that also drains the next sample's loads
+#pragma unroll
+  for (int s = 0; s < CV_STEPS; ++s)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) asm volatile("" ::"v"(bf[s][nt][hl]));
+  asm volatile("" ::"v"(bo[0]), "v"(bo[1]));  // the bias too
+  auto process = [&](float2 (&cur)[CV_PER_LANE], int bc) {
+#pragma unroll
+    for (int k = 0; k < CV_PER_LANE; ++k) {
+      const int i = lane + 64 * k;
+      if (i < CV_C * CV_L / 2) reinterpret_cast<uint2*>(X)[i] = make_uint2(split_word(cur[k].x), split_word(cur[k].y));
+    }
+    load(cur, bc + 2);  // past the run: the run's last sample again (an L2 hit), not a branch
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f4 acc[2][2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) acc[nt][0] = acc[nt][1] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < CV_STEPS; ++s) {
+      const uint32_t* row = X + (4 * s + kg) * CV_L + CV_S * rr;
+      uint32_t w[CV_K];
+#pragma unroll
+      for (int j = 0; j < CV_K; ++j) w[j] = row[j];
+      const u4 hv = {__builtin_amdgcn_perm(w[1], w[0], 0x05040100u), __builtin_amdgcn_perm(w[3], w[2], 0x05040100u),
+                     __builtin_amdgcn_perm(w[5], w[4], 0x05040100u), 0u};
+      const u4 lv = {__builtin_amdgcn_perm(w[1], w[0], 0x07060302u), __builtin_amdgcn_perm(w[3], w[2], 0x07060302u),
+                     __builtin_amdgcn_perm(w[5], w[4], 0x07060302u), 0u};
+      const h8 ah = __builtin_bit_cast(h8, hv), al = __builtin_bit_cast(h8, lv);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        acc[nt][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf[s][nt][0], acc[nt][0], 0, 0, 0);
+        acc[nt][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf[s][nt][1], acc[nt][1], 0, 0, 0);
+        acc[nt][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf[s][nt][0], acc[nt][1], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int o = 16 * nt + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        // tile rows 14, 15 repeat row 13's inputs, so their results are row 13's bit for bit: stored there again
+        const int l = 4 * kg + i < CV_LOUT ? 4 * kg + i : CV_LOUT - 1;
+        y[((size_t)bc * CV_LOUT + l) * CV_O + o] = acc[nt][0][i] + acc[nt][1][i] * (1.0f / CV_SPLIT) + bo[nt];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next staging overwrites X after every lane's reads of it
+  };
+  for (int b = b0; b < b1; b += 2) {
+    process(pa, b);
+    if (b + 1 < b1) process(pb, b + 1);
+  }
+}
+
+// k_conv1d_pair: a workgroup is a pair of waves sharing each staged sample, wave w computing the 16 outputs of column
+// tile w: it holds only its tile's 34 fragments (136 VGPRs), so two waves fit a SIMD (<= 256 VGPRs) and latency hides
+// behind the other pair on it.  Each wave loads and splits half of every sample; the staged sample is double-buffered,
+// one barrier per sample.  4 pairs per CU, a contiguous run of batch / pairs samples each (8 at 8192 on 256 CUs).
+constexpr int CP_PAIRS_PER_CU = 4;
+constexpr int CP_HALF = (CV_C * CV_L / 2 + 1) / 2;                 // 776 float2 of a sample per wave
+constexpr int CP_PER_LANE = (CP_HALF + 63) / 64;                   // 13
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_conv1d_pair(const float* __restrict__ x, const h8* __restrict__ frag, const float* __restrict__ bias,
+                   float* __restrict__ y, int batch) {
+  __shared__ uint32_t XS[2][CV_CPAD * CV_L];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // column tile of this wave
+  const int b0 = (int)((long long)blockIdx.x * batch / gridDim.x), b1 = (int)((long long)(blockIdx.x + 1) * batch / gridDim.x);
+  for (int i = CV_C * CV_L + (int)threadIdx.x; i < CV_CPAD * CV_L; i += 128) { XS[0][i] = 0u; XS[1][i] = 0u; }
+  const int h0 = w * CP_HALF, h1 = w == 0 ? CP_HALF : CV_C * CV_L / 2;  // this wave's float2 range of a sample
+  float2 pa[CP_PER_LANE], pb[CP_PER_LANE];
+  // unconditional, clamped loads (exact vmcnt bookkeeping; past the run: the run's last sample again, an L2 hit)
+  auto load = [&](float2 (&dst)[CP_PER_LANE], int bs) {
+    const float2* src = reinterpret_cast<const float2*>(x + (size_t)(bs < b1 ? bs : b1 - 1) * (CV_C * CV_L));
+#pragma unroll
+    for (int k = 0; k < CP_PER_LANE; ++k) {
+      const int i = h0 + lane + 64 * k;
+      dst[k] = src[i < h1 ? i : h1 - 1];
+    }
+  };
+  if (b0 < b1) {
+    load(pa, b0);
+    load(pb, b0 + 1);
+  }
+  h8 bf[CV_STEPS][2];
+#pragma unroll
+  for (int s = 0; s < CV_STEPS; ++s)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) bf[s][hl] = frag[((s * 2 + w) * 2 + hl) * 64 + lane];
+  const float bo = bias[16 * w + (lane & 15)];
+  // the fragments and the bias retired before the loop (see k_conv1d_regs)
+#pragma unroll
+  for (int s = 0; s < CV_STEPS; ++s) asm volatile("" ::"v"(bf[s][0]), "v"(bf[s][1]));
+  asm volatile("" ::"v"(bo));
+  const int r = lane & 15, kg = lane >> 4;
+  const int rr = r < CV_LOUT ? r : CV_LOUT - 1;
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  auto process = [&](float2 (&cur)[CP_PER_LANE], int bc, uint32_t* X) {
+#pragma unroll
+    for (int k = 0; k < CP_PER_LANE; ++k) {
+      const int i = h0 + lane + 64 * k;
+      if (i < h1) reinterpret_cast<uint2*>(X)[i] = make_uint2(split_word(cur[k].x), split_word(cur[k].y));
+    }
+    load(cur, bc + 2);
+    __syncthreads();  // both halves staged (and, X being double-buffered, both waves done with the sample before last)
+    f4 acc0 = f4{0.0f, 0.0f, 0.0f, 0.0f}, acc1 = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < CV_STEPS; ++s) {
+      const uint32_t* row = X + (4 * s + kg) * CV_L + CV_S * rr;
+      uint32_t v[CV_K];
+#pragma unroll
+      for (int j = 0; j < CV_K; ++j) v[j] = row[j];
+      const u4 hv = {__builtin_amdgcn_perm(v[1], v[0], 0x05040100u), __builtin_amdgcn_perm(v[3], v[2], 0x05040100u),
+                     __builtin_amdgcn_perm(v[5], v[4], 0x05040100u), 0u};
+      const u4 lv = {__builtin_amdgcn_perm(v[1], v[0], 0x07060302u), __builtin_amdgcn_perm(v[3], v[2], 0x07060302u),
+                     __builtin_amdgcn_perm(v[5], v[4], 0x07060302u), 0u};
+      const h8 ah = __builtin_bit_cast(h8, hv), al = __builtin_bit_cast(h8, lv);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf[s][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf[s][1], acc1, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf[s][0], acc1, 0, 0, 0);
+    }
+    const int o = 16 * w + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int l = 4 * kg + i < CV_LOUT ? 4 * kg + i : CV_LOUT - 1;  // rows 14, 15 = row 13's result, bit for bit
+      y[((size_t)bc * CV_LOUT + l) * CV_O + o] = acc0[i] + acc1[i] * (1.0f / CV_SPLIT) + bo;
+    }
+  };
+  for (int b = b0; b < b1; b += 2) {
+    process(pa, b, XS[0]);
+    if (b + 1 < b1) process(pb, b + 1, XS[1]);
+  }
+}
+
 // The PPO minibatch's actor observations rebuilt from the frame-history rollout storage (algo/rollout.py
 // _HistoryRows): row m is the window of frames k .. k + F - 1 of env n's sequence seq[n] ((F + T - 1) frames of `frame`
 // values, k = idx[m] / N, n = idx[m] % N), with the frames older than the env's latest reset at or before step k
@@ -210,6 +412,50 @@ int t1policy_conv1d_forward(const float* x, const float* wt, const float* bias, 
   const long long need = ((long long)batch + CV_WAVES - 1) / CV_WAVES;
   const int grid = (int)(need < cus ? need : cus);
   hipLaunchKernelGGL(k_conv1d_mfma, dim3(grid), dim3(64 * CV_WAVES), 0, (hipStream_t)stream, x, wt, bias, y, batch);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_conv1d_frag_bytes(void) { return CV_FRAG_BYTES; }
+
+int t1policy_conv1d_pack_weights(const float* w, void* frag, int channels, int out_channels, int kernel,
+                                 void* stream) {
+  if (!w || !frag) return -1;
+  if (!(channels == CV_C && out_channels == CV_O && kernel == CV_K)) return 1;
+  if ((reinterpret_cast<uintptr_t>(frag) & 15u) != 0) return -1;
+  hipLaunchKernelGGL(k_conv1d_pack, dim3(CV_STEPS * 2 * 64 / 256 + 1), dim3(256), 0, (hipStream_t)stream, w,
+                     reinterpret_cast<h8*>(frag));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_conv1d_forward_packed(const float* x, const void* frag, const float* bias, float* y, int batch,
+                                   int channels, int length, int out_channels, int kernel, int stride, void* stream) {
+  if (!x || !frag || !bias || !y || batch < 0) return -1;
+  if (batch == 0) return 0;
+  if (!(channels == CV_C && length == CV_L && out_channels == CV_O && kernel == CV_K && stride == CV_S)) return 1;
+  if ((reinterpret_cast<uintptr_t>(x) & 15u) != 0 || (reinterpret_cast<uintptr_t>(frag) & 15u) != 0) return -1;
+  if ((long long)batch * (CV_C * CV_L * 4) > 0x7fffffffLL) return -1;  // 32-bit buffer offsets
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
+  static int cu_count[64];
+  int cus = __atomic_load_n(&cu_count[dev], __ATOMIC_RELAXED);
+  if (cus <= 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return -2;
+    __atomic_store_n(&cu_count[dev], cus, __ATOMIC_RELAXED);
+  }
+  // k_conv1d_pair (default): CP_PAIRS_PER_CU two-wave workgroups per CU; T1POLICY_CONV=regs: k_conv1d_regs, one
+  // 4-wave workgroup per CU (A/B).  No workgroup without a sample.
+  const char* kv = getenv("T1POLICY_CONV");
+  if (kv && kv[0] == 'r') {
+    const long long need = ((long long)batch + CR_WAVES - 1) / CR_WAVES;
+    const int grid = (int)(need < cus ? need : cus);
+    hipLaunchKernelGGL(k_conv1d_regs, dim3(grid), dim3(64 * CR_WAVES), 0, (hipStream_t)stream, x,
+                       reinterpret_cast<const h8*>(frag), bias, y, batch);
+  } else {
+    const long long slots = (long long)cus * CP_PAIRS_PER_CU;
+    const int grid = (int)(batch < slots ? batch : slots);
+    hipLaunchKernelGGL(k_conv1d_pair, dim3(grid), dim3(128), 0, (hipStream_t)stream, x,
+                       reinterpret_cast<const h8*>(frag), bias, y, batch);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
