@@ -567,14 +567,30 @@ __device__ __forceinline__ bool post_a_env(const DynModel& M, const t1env_config
   return post_a_core(M, C, B, A, n0, X, bq);
 }
 
+// the per-env inputs of compute_observations that reset_idx may rewrite (reset_env writes a resetting env's new values into it)
+struct ObsIn {
+  float cmd[4], dof[24], act[12], la[12], rv[6];
+  BaseQ bq;
+  int32_t gt[3];
+  int64_t el, pl;
+  float gstart;
+  int dl, il;
+};
+
 // =====================================================================================================
 // reset_idx for one env (t1_dh_stand_env.py:483-559 + legged_robot.py:604-651, 732-783, 1076-1120, 1138-1158)
 // =====================================================================================================
 // zero_reward_state = false: the caller's reward pass zeroes feet_air_time and the episode sums itself (the fused
 // epilogue, where that pass runs on another wave concurrently: post_a_core<POST_A_REWARDS>)
+// X != nullptr: the new state's observation inputs are also returned in X from registers (post_b_core), instead of
+// being read back from the rows just written -- the same values (stores and loads do not change them), one dependent
+// memory round trip less; X->cmd is left as it is (reset_idx does not touch the commands)
 __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B, const t1env_step_args& A,
-                          int n, uint32_t genv, uint32_t ctr, bool do_terrain, bool zero_reward_state = true) {
+                          int n, uint32_t genv, uint32_t ctr, bool do_terrain, bool zero_reward_state = true,
+                          ObsIn* X = nullptr) {
   const RngKey K = rng_key(C.seed, genv, ctr);
+  float org[3];
+  bool org_known = false;
   if (do_terrain && C.terrain_curriculum) {  // _update_terrain_curriculum
     const float* r = B.root_states + n * 13;
     const float* o = B.env_origins + n * 3;
@@ -587,31 +603,39 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
     lv = lv >= C.num_terrain_rows ? rnd : (lv < 0 ? 0 : lv);
     B.terrain_levels[n] = lv;
     const float* to = B.terrain_origins + ((size_t)lv * C.num_terrain_cols + B.terrain_types[n]) * 3;
-    B.env_origins[n * 3 + 0] = to[0];
-    B.env_origins[n * 3 + 1] = to[1];
-    B.env_origins[n * 3 + 2] = to[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      org[i] = to[i];
+      B.env_origins[n * 3 + i] = org[i];
+    }
+    org_known = true;
   }
+  if (!org_known)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) org[i] = B.env_origins[n * 3 + i];
   // the new episode starts in the air as far as restitution is concerned (no contact episode carried over)
 #pragma unroll
   for (int i = 0; i < NVIMP; ++i) B.contact_vimp[(size_t)n * NVIMP + i] = 0.0f;
   // _reset_dofs
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    B.dof_state[n * 24 + 2 * j] =
-        M.default_dof_pos[j] + rand_float(-C.reset_dof_range, C.reset_dof_range, K, SLOT_RESET_DOF + j);
+    const float dp = M.default_dof_pos[j] + rand_float(-C.reset_dof_range, C.reset_dof_range, K, SLOT_RESET_DOF + j);
+    B.dof_state[n * 24 + 2 * j] = dp;
     B.dof_state[n * 24 + 2 * j + 1] = 0.0f;
+    if (X) { X->dof[2 * j] = dp; X->dof[2 * j + 1] = 0.0f; }
   }
-  // _reset_root_states
-  float* r = B.root_states + n * 13;
+  // _reset_root_states (in registers, then stored)
+  float r[13];
 #pragma unroll
   for (int i = 0; i < 13; ++i) r[i] = M.base_init_state[i];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) r[i] += B.env_origins[n * 3 + i];
+  for (int i = 0; i < 3; ++i) r[i] += org[i];
   if (C.custom_origins) {
     const float p3 = C.reset_xy_range;
     r[0] += rand_float(-p3, p3, K, SLOT_RESET_ROOT_XY + 0);
     r[1] += rand_float(-p3, p3, K, SLOT_RESET_ROOT_XY + 1);
   }
+  strow(B.root_states + n * 13, r);
   // randomize_dof_props (torque_multi is redrawn every substep anyway; its reset draw has no effect)
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
@@ -634,8 +658,10 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   for (int i = 0; i < 16; ++i) B.imu_hist[(size_t)n * 16 + i] = 0.0f;
 #endif
   B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, K, SLOT_LAG_ACTION);
-  B.dof_lag_timestep[n] = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, K, SLOT_LAG_DOF);
-  B.imu_lag_timestep[n] = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, K, SLOT_LAG_IMU);
+  const int dl = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, K, SLOT_LAG_DOF);
+  const int il = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, K, SLOT_LAG_IMU);
+  B.dof_lag_timestep[n] = dl;
+  B.imu_lag_timestep[n] = il;
   // buffers
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
@@ -653,7 +679,8 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   B.episode_length_buf[n] = 0;
   B.phase_length_buf[n] = 0;
   B.reset_buf[n] = 1;
-  B.gait_start[n] = (float)rand_int(0, 2, K, SLOT_GAIT_START) * 0.5f;
+  const float gstart = (float)rand_int(0, 2, K, SLOT_GAIT_START) * 0.5f;
+  B.gait_start[n] = gstart;
   // generate_gait_time (t1:109-124)
   float g[3];
 #pragma unroll
@@ -669,8 +696,25 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   if (zero_reward_state)
 #pragma unroll
     for (int k = 0; k < T1_NREW; ++k) B.episode_sums[(size_t)k * C.num_envs + n] = 0.0f;
-  // base quantities of the reset env from the freshly written root state (t1:548-552)
-  base_quantities(B, n);
+  // base quantities of the reset env from the fresh root state (t1:548-552)
+  BaseQ bq;
+  base_quantities_r(r, bq);
+  store_base_quantities(B, n, bq);
+  if (X) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) { X->act[j] = 0.0f; X->la[j] = 0.0f; }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) X->rv[i] = r[7 + i];
+    X->bq = bq;
+    X->gt[0] = 0;
+    X->gt[1] = (int32_t)(0.0f + s0);
+    X->gt[2] = (int32_t)((0.0f + s0) + s1);
+    X->el = 0;
+    X->pl = 0;
+    X->gstart = gstart;
+    X->dl = dl;
+    X->il = il;
+  }
 }
 
 // the actor-frame noise of observation i (legged_robot.py compute_observations: (2 u - 1) * noise_vec * level, u keyed
@@ -683,15 +727,6 @@ __device__ __forceinline__ float obs_noise(const t1env_config& C, RngKey K, int 
 // =====================================================================================================
 // post-physics phase B: reset + observations (legged_robot.py:490-502, t1:368-481)
 // =====================================================================================================
-// the per-env inputs of compute_observations that reset_idx may rewrite (reloaded after a reset)
-struct ObsIn {
-  float cmd[4], dof[24], act[12], la[12], rv[6];
-  BaseQ bq;
-  int32_t gt[3];
-  int64_t el, pl;
-  float gstart;
-  int dl, il;
-};
 __device__ __forceinline__ void load_obs_in(const t1env_buffers& B, int n, ObsIn& X) {
   ldrow(X.cmd, B.commands + n * 4);
   ldrow(X.dof, B.dof_state + (size_t)n * 24);
@@ -745,13 +780,8 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
   const float (&et)[3] = E.et;
   const float (&cfz)[2] = E.cfz;
   const float fric = E.fric, mass = E.mass;
-  if (do_reset) {
-    reset_env(M, C, B, A, n, genv, ctr, true, zero_reward_state);
-    load_obs_in(B, n, X);
-  }
-  T1_PROF_MARK(20);
-  if (any_reset && resample_commands_r(C, A, X.el, X.gt, X.cmd, genv, ctr)) strow(B.commands + n * 4, X.cmd);
-  // lagged sensor samples (need the lag lengths loaded above)
+  // lagged sensor samples, loaded before the reset: a resetting env's rings are zeroed by its reset, so its samples
+  // are 0 whatever its new lag lengths (below); the others keep their lag lengths
   const float* ldp = B.dof_hist + ((size_t)n * 4 + ((A.counter - (uint32_t)(X.dl / 10)) & 3u)) * 24;
   const float* lip = B.imu_hist + ((size_t)n * 2 + ((A.counter - (uint32_t)(X.il / 10)) & 1u)) * 8;
   float ld[24], lraw[8], li[6];
@@ -767,6 +797,15 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
   ldrow(ld, ldp);
   ldrow(lraw, lip);
 #endif
+  if (do_reset) {
+    reset_env(M, C, B, A, n, genv, ctr, true, zero_reward_state, &X);
+#pragma unroll
+    for (int i = 0; i < 24; ++i) ld[i] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lraw[i] = 0.0f;
+  }
+  T1_PROF_MARK(20);
+  if (any_reset && resample_commands_r(C, A, X.el, X.gt, X.cmd, genv, ctr)) strow(B.commands + n * 4, X.cmd);
   imu_sample(lraw, li);
   // ---- compute_observations
   const float* cmd = X.cmd;
