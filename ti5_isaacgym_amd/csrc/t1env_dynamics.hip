@@ -442,65 +442,76 @@ __device__ __forceinline__ void stage_st(float (*dst)[DYN_ENVS], int nv, int t, 
     if (e < nv * L) dst[e % L][e / L] = v[i];
   }
 }
-__device__ __forceinline__ void stage_epilogue_inputs(const t1env_buffers& B, int N, int nb, int t,
-                                                      float (*E)[DYN_ENVS]) {
-  const int nv = N - nb < DYN_ENVS ? N - nb : DYN_ENVS;
+// the staged values of one helper thread between its loads and its LDS writes (epi_stage_load / epi_stage_store)
+constexpr int EPI_NES = (T1_NREW * DYN_ENVS + STAGE_NT - 1) / STAGE_NT;
+struct EpiStage {
   float la[stage_n<12>()], lla[stage_n<12>()], lrv[stage_n<6>()], ldv[stage_n<12>()], ref[stage_n<12>()];
   float cmd[stage_n<4>()], at[stage_n<2>()], fh[stage_n<2>()], lfz[stage_n<2>()], ef[stage_n<3>()];
   float et[stage_n<3>()], gt[stage_n<3>()], el[stage_n<2>()], pl[stage_n<2>()], gs[stage_n<1>()], lc[stage_n<2>()];
   float fr[stage_n<1>()], ms[stage_n<1>()], dl[stage_n<1>()], il[stage_n<1>()];
-  constexpr int NES = (T1_NREW * DYN_ENVS + STAGE_NT - 1) / STAGE_NT;
-  float es[NES];
-  stage_ld<12>(B.last_actions, nb, nv, t, la);
-  stage_ld<12>(B.last_last_actions, nb, nv, t, lla);
-  stage_ld<6>(B.last_root_vel, nb, nv, t, lrv);
-  stage_ld<12>(B.last_dof_vel, nb, nv, t, ldv);
-  stage_ld<12>(B.ref_dof_pos, nb, nv, t, ref);
-  stage_ld<4>(B.commands, nb, nv, t, cmd);
-  stage_ld<2>(B.feet_air_time, nb, nv, t, at);
-  stage_ld<2>(B.feet_height, nb, nv, t, fh);
-  stage_ld<2>(B.last_feet_z, nb, nv, t, lfz);
-  stage_ld<3>(B.ext_forces, nb, nv, t, ef);
-  stage_ld<3>(B.ext_torques, nb, nv, t, et);
-  stage_ld<3>(B.gait_time, nb, nv, t, gt);
-  stage_ld<2>(reinterpret_cast<const uint32_t*>(B.episode_length_buf), nb, nv, t, el);
-  stage_ld<2>(reinterpret_cast<const uint32_t*>(B.phase_length_buf), nb, nv, t, pl);
-  stage_ld<1>(B.gait_start, nb, nv, t, gs);
-  stage_ld<2>(B.last_contacts, nb, nv, t, lc);
-  stage_ld<1>(B.friction, nb, nv, t, fr);
-  stage_ld<1>(B.body_mass, nb, nv, t, ms);
-  stage_ld<1>(B.dof_lag_timestep, nb, nv, t, dl);
-  stage_ld<1>(B.imu_lag_timestep, nb, nv, t, il);
+  float es[EPI_NES];
+};
+__device__ __forceinline__ void epi_stage_load(const t1env_buffers& B, int N, int nb, int t, EpiStage& V) {
+  const int nv = N - nb < DYN_ENVS ? N - nb : DYN_ENVS;
+  stage_ld<12>(B.last_actions, nb, nv, t, V.la);
+  stage_ld<12>(B.last_last_actions, nb, nv, t, V.lla);
+  stage_ld<6>(B.last_root_vel, nb, nv, t, V.lrv);
+  stage_ld<12>(B.last_dof_vel, nb, nv, t, V.ldv);
+  stage_ld<12>(B.ref_dof_pos, nb, nv, t, V.ref);
+  stage_ld<4>(B.commands, nb, nv, t, V.cmd);
+  stage_ld<2>(B.feet_air_time, nb, nv, t, V.at);
+  stage_ld<2>(B.feet_height, nb, nv, t, V.fh);
+  stage_ld<2>(B.last_feet_z, nb, nv, t, V.lfz);
+  stage_ld<3>(B.ext_forces, nb, nv, t, V.ef);
+  stage_ld<3>(B.ext_torques, nb, nv, t, V.et);
+  stage_ld<3>(B.gait_time, nb, nv, t, V.gt);
+  stage_ld<2>(reinterpret_cast<const uint32_t*>(B.episode_length_buf), nb, nv, t, V.el);
+  stage_ld<2>(reinterpret_cast<const uint32_t*>(B.phase_length_buf), nb, nv, t, V.pl);
+  stage_ld<1>(B.gait_start, nb, nv, t, V.gs);
+  stage_ld<2>(B.last_contacts, nb, nv, t, V.lc);
+  stage_ld<1>(B.friction, nb, nv, t, V.fr);
+  stage_ld<1>(B.body_mass, nb, nv, t, V.ms);
+  stage_ld<1>(B.dof_lag_timestep, nb, nv, t, V.dl);
+  stage_ld<1>(B.imu_lag_timestep, nb, nv, t, V.il);
 #pragma unroll
-  for (int i = 0; i < NES; ++i) {  // episode_sums is [reward][env]: already row-contiguous
+  for (int i = 0; i < EPI_NES; ++i) {  // episode_sums is [reward][env]: already row-contiguous
     const int e = t + STAGE_NT * i;
-    es[i] = e < T1_NREW * nv ? B.episode_sums[(size_t)(e / nv) * N + nb + e % nv] : 0.0f;
+    V.es[i] = e < T1_NREW * nv ? B.episode_sums[(size_t)(e / nv) * N + nb + e % nv] : 0.0f;
   }
-  stage_st<12>(E + E_LA, nv, t, la);
-  stage_st<12>(E + E_LLA, nv, t, lla);
-  stage_st<6>(E + E_LRV, nv, t, lrv);
-  stage_st<12>(E + E_LDV, nv, t, ldv);
-  stage_st<12>(E + E_REF, nv, t, ref);
-  stage_st<4>(E + E_CMD, nv, t, cmd);
-  stage_st<2>(E + E_AT, nv, t, at);
-  stage_st<2>(E + E_FH, nv, t, fh);
-  stage_st<2>(E + E_LFZ, nv, t, lfz);
-  stage_st<3>(E + E_EF, nv, t, ef);
-  stage_st<3>(E + E_ET, nv, t, et);
-  stage_st<3>(E + E_GT, nv, t, gt);
-  stage_st<2>(E + E_EL, nv, t, el);
-  stage_st<2>(E + E_PL, nv, t, pl);
-  stage_st<1>(E + E_GS, nv, t, gs);
-  stage_st<2>(E + E_LC, nv, t, lc);
-  stage_st<1>(E + E_FRIC, nv, t, fr);
-  stage_st<1>(E + E_MASS, nv, t, ms);
-  stage_st<1>(E + E_DL, nv, t, dl);
-  stage_st<1>(E + E_IL, nv, t, il);
+}
+__device__ __forceinline__ void epi_stage_store(int N, int nb, int t, const EpiStage& V, float (*E)[DYN_ENVS]) {
+  const int nv = N - nb < DYN_ENVS ? N - nb : DYN_ENVS;
+  stage_st<12>(E + E_LA, nv, t, V.la);
+  stage_st<12>(E + E_LLA, nv, t, V.lla);
+  stage_st<6>(E + E_LRV, nv, t, V.lrv);
+  stage_st<12>(E + E_LDV, nv, t, V.ldv);
+  stage_st<12>(E + E_REF, nv, t, V.ref);
+  stage_st<4>(E + E_CMD, nv, t, V.cmd);
+  stage_st<2>(E + E_AT, nv, t, V.at);
+  stage_st<2>(E + E_FH, nv, t, V.fh);
+  stage_st<2>(E + E_LFZ, nv, t, V.lfz);
+  stage_st<3>(E + E_EF, nv, t, V.ef);
+  stage_st<3>(E + E_ET, nv, t, V.et);
+  stage_st<3>(E + E_GT, nv, t, V.gt);
+  stage_st<2>(E + E_EL, nv, t, V.el);
+  stage_st<2>(E + E_PL, nv, t, V.pl);
+  stage_st<1>(E + E_GS, nv, t, V.gs);
+  stage_st<2>(E + E_LC, nv, t, V.lc);
+  stage_st<1>(E + E_FRIC, nv, t, V.fr);
+  stage_st<1>(E + E_MASS, nv, t, V.ms);
+  stage_st<1>(E + E_DL, nv, t, V.dl);
+  stage_st<1>(E + E_IL, nv, t, V.il);
 #pragma unroll
-  for (int i = 0; i < NES; ++i) {
+  for (int i = 0; i < EPI_NES; ++i) {
     const int e = t + STAGE_NT * i;
-    if (e < T1_NREW * nv) E[E_ESUM + e / nv][e % nv] = es[i];
+    if (e < T1_NREW * nv) E[E_ESUM + e / nv][e % nv] = V.es[i];
   }
+}
+__device__ __forceinline__ void stage_epilogue_inputs(const t1env_buffers& B, int N, int nb, int t,
+                                                      float (*E)[DYN_ENVS]) {
+  EpiStage V;
+  epi_stage_load(B, N, nb, t, V);
+  epi_stage_store(N, nb, t, V, E);
 }
 
 // The fused step's post-physics for one k_dyn4 workgroup, run by the two leg waves: every input from LDS (fresh
@@ -811,7 +822,9 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     T1_PROF_MARK(10);
     // the epilogue's inputs the step does not change, staged while the leg waves set up and run the first
     // forward pass (nothing writes them before the epilogue)
+#ifndef T1_STAGE_LATE
     if constexpr (FUSED) stage_epilogue_inputs(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, lds.epi);
+#endif
     for (int sub = 0; sub < C.decimation; ++sub) {
       T1_PROF_MARK(7);
       __syncthreads();  // S1: the substep states published
@@ -854,6 +867,17 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
         lds_put_sym(lds.xch[2 + leg], lane, Cb, gw);
       }
       T1_PROF_MARK(5);
+#ifdef T1_STAGE_LATE  // A/B: the epilogue staging in the helpers' first S2..S1 idle window, not beside the legs' prologue
+      if constexpr (FUSED) {
+        if (sub == 0) {
+          EpiStage V;
+          epi_stage_load(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, V);
+          __syncthreads();  // S3
+          epi_stage_store(N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, V, lds.epi);
+          continue;
+        }
+      }
+#endif
       __syncthreads();  // S3: base system complete
       T1_PROF_MARK(12);
     }
@@ -1102,6 +1126,8 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
   int shift_blocks = cfg.shift_blocks > 0 ? cfg.shift_blocks : cfg.cus - dyn_blocks;
   if (shift_blocks < MIN_SHIFT_BLOCKS) shift_blocks = MIN_SHIFT_BLOCKS;
   if (shift_prelaunched) shift_blocks = 0;
+  // the shift's delayed start only where it has slack: as many shift workgroups as dynamics ones (N <= 8192 on 256 CUs)
+  const int shift_delay = shift_blocks >= dyn_blocks ? cfg.shift_delay : 0;
   const FusedArgs FA = fused ? *fused : FusedArgs{};
   const SubLog LG = log ? *log : SubLog{};
   const dim3 grid(dyn_blocks + shift_blocks);
@@ -1109,7 +1135,7 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
   if (log && !fused) return (int)hipErrorInvalidValue;  // the substep log: fused steps only (the caller checks)
 #define T1_LAUNCH(HF, FU) \
   hipLaunchKernelGGL((k_dyn4<HF, FU>), grid, dim3(D4_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, dyn_blocks, FA, LG, \
-                     cfg.shift_delay)
+                     shift_delay)
   if (fused) { if (hf) T1_LAUNCH(true, true); else T1_LAUNCH(false, true); }
   else { if (hf) T1_LAUNCH(true, false); else T1_LAUNCH(false, false); }
 #undef T1_LAUNCH

@@ -26,8 +26,11 @@ struct SubLog {
   float* torque;
 };
 
-// default delayed start of the in-launch history-shift workgroups (100 MHz ticks; DynLaunch::shift_delay)
-constexpr int T1_SHIFT_DELAY_DEFAULT = 0;
+// default delayed start of the in-launch history-shift workgroups (100 MHz ticks; DynLaunch::shift_delay): 30 us, so
+// the dynamics workgroups' prologue loads do not queue behind the shift's stream.  At 8192 trimesh envs 2,000-4,000
+// ticks measured -0.6..-0.8% per step against 0 (profiles/r03g_shift_grid.txt); applied only while the shift has at
+// least as many workgroups as the dynamics (its ~104 us then ends well before the ~160 us dynamics)
+constexpr int T1_SHIFT_DELAY_DEFAULT = 3000;
 
 // launch shape of the dynamics kernel
 struct DynLaunch {
