@@ -14,12 +14,17 @@ Same architecture, parameter names and initialisation as the reference, so its c
 856,972 parameters with the t1 config.  On MI355X the dense layers run as hipBLASLt GEMMs
 through PyTorch-ROCm; the per-step inference batch is every env on the rank.
 """
+import os
+
 import torch
 import torch.nn as nn
 from torch.distributions import Normal
 
 
 SPLITK_ROWS = 2048      # rows of the batch (K of the weight-gradient GEMM) per split-K slice
+# bf16 split-K partial products returned in fp32 by the GEMM itself (T1_WGRAD_OUT_F32=0: the bf16 partials widened
+# afterwards, the round-2 path; A/B)
+WGRAD_OUT_F32 = os.environ.get("T1_WGRAD_OUT_F32", "1") != "0"
 
 
 def wgrad_splitk(gy, x):
@@ -42,7 +47,13 @@ def wgrad_splitk(gy, x):
         # narrow it again): 28-57 us (profiles/r02bf_small_m_wgrad.txt)
         with torch.autocast(device_type="cuda", enabled=False):
             return wgrad_splitk(wide(gy), wide(x))
-    gw =wide(torch.bmm(gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1))).sum(0)
+    a, b = gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1)
+    if WGRAD_OUT_F32 and gy.is_cuda and gy.dtype in (torch.bfloat16, torch.float16) and b.dtype == gy.dtype:
+        # bf16 operands, fp32 partial products straight from the GEMM (aten::bmm.dtype): no bf16 rounding of the
+        # 2,048-row partial sums and no widening copy of them
+        gw = torch.bmm(a, b, out_dtype=torch.float32).sum(0)
+    else:
+        gw = wide(torch.bmm(a, b)).sum(0)
     if c < K:
         gw = gw + wide(gy[c:].t().mm(x[c:]))
     return gw
