@@ -822,9 +822,8 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
     T1_PROF_MARK(10);
     // the epilogue's inputs the step does not change, staged while the leg waves set up and run the first
     // forward pass (nothing writes them before the epilogue)
-#ifndef T1_STAGE_LATE
+    // (staging in the helpers' first S2..S1 idle window instead measured +5% per step: profiles/r03h_ab.txt)
     if constexpr (FUSED) stage_epilogue_inputs(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, lds.epi);
-#endif
     for (int sub = 0; sub < C.decimation; ++sub) {
       T1_PROF_MARK(7);
       __syncthreads();  // S1: the substep states published
@@ -867,17 +866,6 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
         lds_put_sym(lds.xch[2 + leg], lane, Cb, gw);
       }
       T1_PROF_MARK(5);
-#ifdef T1_STAGE_LATE  // A/B: the epilogue staging in the helpers' first S2..S1 idle window, not beside the legs' prologue
-      if constexpr (FUSED) {
-        if (sub == 0) {
-          EpiStage V;
-          epi_stage_load(B, N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, V);
-          __syncthreads();  // S3
-          epi_stage_store(N, blockIdx.x * DYN_ENVS, (int)threadIdx.x - 2 * DYN_ENVS, V, lds.epi);
-          continue;
-        }
-      }
-#endif
       __syncthreads();  // S3: base system complete
       T1_PROF_MARK(12);
     }
