@@ -48,10 +48,11 @@ def wgrad_splitk(gy, x):
         with torch.autocast(device_type="cuda", enabled=False):
             return wgrad_splitk(wide(gy), wide(x))
     a, b = gy[:c].view(S, SPLITK_ROWS, M).transpose(1, 2), x[:c].view(S, SPLITK_ROWS, -1)
-    if WGRAD_OUT_F32 and gy.is_cuda and gy.dtype in (torch.bfloat16, torch.float16) and b.dtype == gy.dtype:
+    if WGRAD_OUT_F32 and gy.is_cuda and gy.dtype in (torch.bfloat16, torch.float16):
         # bf16 operands, fp32 partial products straight from the GEMM (aten::bmm.dtype): no bf16 rounding of the
-        # 2,048-row partial sums and no widening copy of them
-        gw = torch.bmm(a, b, out_dtype=torch.float32).sum(0)
+        # 2,048-row partial sums and no widening copy of them.  An fp32 saved input is rounded to the gradient's dtype
+        # first, as autocast's bmm would (the once-per-update obs cast stays bit-identical to the per-minibatch one)
+        gw = torch.bmm(a, b if b.dtype == gy.dtype else b.to(gy.dtype), out_dtype=torch.float32).sum(0)
     else:
         gw = wide(torch.bmm(a, b)).sum(0)
     if c < K:
