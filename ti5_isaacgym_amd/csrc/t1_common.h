@@ -57,11 +57,9 @@ T1_HD RngKey rng_key(uint32_t seed, uint32_t env, uint32_t ctr) {
   return RngKey{mix32(h + ctr * 0x9E3779B1u)};
 }
 T1_HD uint32_t hash_k(RngKey k, uint32_t slot) { return mix32(k.h ^ (slot * 0x85EBCA77u)); }
-// the draws from a draw's hash (hash_k / hash4), so a hash computed elsewhere (the fused step's helper waves) gives the
-// same values bit for bit
-T1_HD float u01_h(uint32_t h) { return (float)(h >> 8) * (1.0f / 16777216.0f); }
-T1_HD float rand_float_h(float lo, float hi, uint32_t h) {
-  float u = u01_h(h);
+T1_HD float uniform01(RngKey k, uint32_t slot) { return (float)(hash_k(k, slot) >> 8) * (1.0f / 16777216.0f); }
+T1_HD float rand_float(float lo, float hi, RngKey k, uint32_t slot) {
+  float u = uniform01(k, slot);
 #if defined(__HIP_DEVICE_COMPILE__)
   // __fmul_rn / __fadd_rn alone are contracted into one v_fmac by the compiler (r03: ext-force draws U(-300, 600)
   // off by up to 5e-5 from the two-rounding value); the empty asm makes the rounded product opaque to that fusion
@@ -73,12 +71,10 @@ T1_HD float rand_float_h(float lo, float hi, uint32_t h) {
   return p + lo;
 #endif
 }
-T1_HD int32_t rand_int_h(int32_t lo, int32_t hi, uint32_t h) {
-  return lo + (int32_t)(((uint64_t)(h >> 8) * (uint64_t)(hi - lo)) >> 24);
+T1_HD int32_t rand_int(int32_t lo, int32_t hi, RngKey k, uint32_t slot) {
+  uint64_t h = hash_k(k, slot) >> 8;
+  return lo + (int32_t)((h * (uint64_t)(hi - lo)) >> 24);
 }
-T1_HD float uniform01(RngKey k, uint32_t slot) { return u01_h(hash_k(k, slot)); }
-T1_HD float rand_float(float lo, float hi, RngKey k, uint32_t slot) { return rand_float_h(lo, hi, hash_k(k, slot)); }
-T1_HD int32_t rand_int(int32_t lo, int32_t hi, RngKey k, uint32_t slot) { return rand_int_h(lo, hi, hash_k(k, slot)); }
 
 // reset_idx(env_ids) between steps keys its draws on (counter | T1_BETWEEN_STEP_SALT) (oracle/rng.py
 // BETWEEN_STEP_SALT): the in-step resets of the step that produced `counter` used the plain counter

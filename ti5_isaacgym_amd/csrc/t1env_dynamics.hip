@@ -344,9 +344,7 @@ struct Dyn4Lds {
   float vib[2][DYN_ENVS];  // the base-box halves' end-of-step restitution episodes (helpers, for the report)
   int xflag[2];            // helper h's self-collision bodies of the current (sub)step published (helper_signal)
   float vis[2][DYN_ENVS];  // the shanks' end-of-step restitution episodes (leg waves, for the helpers' report)
-  int preflag;             // helpers done with post_b's draw hashes (pose / xch rows after the epilogue barrier)
 };
-static_assert(PRE_ROWS0 <= 2 * POSE_N && PRE_ROWS - PRE_ROWS0 <= 4 * XCH, "post_b's draw hashes fit pose + xch");
 static_assert(FR_N <= 2 * CT_N, "the fresh outputs fit the contact-term region");
 
 __device__ __forceinline__ void lds_put_m3(float (*dst)[DYN_ENVS], int lane, const M3<float>& R) {
@@ -526,8 +524,7 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
                                                       const t1env_step_args& A, const ShiftArgs& S,
                                                       const FusedArgs& FA, int dyn_blocks, int lane,
                                                       const float (*E)[DYN_ENVS], const float (*FR)[DYN_ENVS],
-                                                      const float (*cap0)[DYN_ENVS], const float (*cap1)[DYN_ENVS],
-                                                      const uint32_t* pre0, const uint32_t* pre1, const int* preflag) {
+                                                      const float (*cap0)[DYN_ENVS], const float (*cap1)[DYN_ENVS]) {
   const int N = C.num_envs;
   const int n0 = blockIdx.x * DYN_ENVS + lane;
   const bool active = n0 < N;
@@ -617,19 +614,8 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
     Ex.cfz[0] = X.c0[2]; Ex.cfz[1] = X.c1[2];
     Ex.fric = E[E_FRIC][lane];
     Ex.mass = E[E_MASS][lane];
-    // post_b's draws: the hashes the helper waves computed after the epilogue barrier (both signal preflag)
-    DrawSrc H;
-    H.K = rng_key(C.seed, (uint32_t)(C.env_offset + n), A.counter + 1u);
-    H.r0 = pre0; H.r1 = pre1; H.lane = lane;
-#ifdef T1_NO_PRE_DRAWS  // A/B build: wave 1 hashes its draws itself
-    const DrawSrc* pre = nullptr;
-#else
-    while (__hip_atomic_load(preflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 2) __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const DrawSrc* pre = &H;
-#endif
 #ifndef T1_WHATIF_EPI_NO_POSTB  // timing-only what-if build: no reset / observations
-    post_b_core(M, C, B, A, n, do_reset, do_reset, O, Ex, /*zero_reward_state=*/false, pre);
+    post_b_core(M, C, B, A, n, do_reset, do_reset, O, Ex, /*zero_reward_state=*/false);
 #endif
   }
   T1_PROF_MARK(14);
@@ -906,22 +892,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
       helper_report_contacts_at(M, T, B, F, Ko, fself, n, leg, mu, vt, vt_base, lane, active, FR);
     }
     T1_PROF_MARK(11);
-    if constexpr (FUSED) {
-      __syncthreads();  // the epilogue barrier
-#ifndef T1_NO_PRE_DRAWS
-      // post_b's draw hashes (noise, reset_idx) for leg wave 1, which reaches them after its callback / termination
-      // prefix: rows leg, leg + 2, ... of pose (free once the report is done) and xch (free since the last S3)
-      const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), A.counter + 1u);
-      uint32_t* pre0 = reinterpret_cast<uint32_t*>(&lds.pose[0][0][0]);
-      uint32_t* pre1 = reinterpret_cast<uint32_t*>(&lds.xch[0][0][0]);
-      for (int r = leg; r < PRE_ROWS; r += 2) {
-        const uint32_t h = hash_k(K, pre_slot(r));
-        if (r < PRE_ROWS0) pre0[r * DYN_ENVS + lane] = h; else pre1[(r - PRE_ROWS0) * DYN_ENVS + lane] = h;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_fetch_add(&lds.preflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-    }
+    if constexpr (FUSED) __syncthreads();  // the epilogue barrier
     T1_PROF_END();
     return;
   }
@@ -949,7 +920,6 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
   float vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
   const float e_g = ground_restitution(M, PB.restitution);
   T1_PROF_MARK(10);
-  if (leg == 0 && lane == 0) lds.preflag = 0;  // before the first S1; the helpers increment it after the epilogue barrier
   publish_state(P, lane, sb, q, qd);  // the helpers start each substep from the state (their own kinematics)
   for (int sub = 0; sub < C.decimation; ++sub) {
     T1_PROF_MARK(7);
@@ -1115,14 +1085,10 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
   if constexpr (FUSED) {
     __syncthreads();  // all four waves: every output of the workgroup is in memory
     T1_PROF_MARK(12);
-    const uint32_t* pre0 = reinterpret_cast<const uint32_t*>(&lds.pose[0][0][0]);
-    const uint32_t* pre1 = reinterpret_cast<const uint32_t*>(&lds.xch[0][0][0]);
     if (leg == 0)
-      fused_epilogue_staged<POST_A_REWARDS>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, FR, lds.cap[0], lds.cap[1],
-                                            pre0, pre1, &lds.preflag);
+      fused_epilogue_staged<POST_A_REWARDS>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, FR, lds.cap[0], lds.cap[1]);
     else
-      fused_epilogue_staged<POST_A_STATE>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, FR, lds.cap[0], lds.cap[1],
-                                          pre0, pre1, &lds.preflag);
+      fused_epilogue_staged<POST_A_STATE>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, FR, lds.cap[0], lds.cap[1]);
   }
   T1_PROF_END();
 }

@@ -567,44 +567,6 @@ __device__ __forceinline__ bool post_a_env(const DynModel& M, const t1env_config
   return post_a_core(M, C, B, A, n0, X, bq);
 }
 
-// Post_b's draws (observation noise, reset_idx) for one env: computed here, or -- in the fused step -- the helper
-// waves' precomputed hashes (PRE_ROWS LDS rows of 64 envs, rows [0, PRE_ROWS0) at r0, the rest at r1).  The values
-// are the same bit for bit (rand_float_h / rand_int_h of the same hash).
-constexpr int PRE_ROWS = 141, PRE_ROWS0 = 108;
-__host__ __device__ constexpr int pre_row(uint32_t s) {
-  return (s >= SLOT_OBS_NOISE && s < SLOT_OBS_NOISE + 47) ? (int)(s - SLOT_OBS_NOISE)
-       : (s >= SLOT_RESET_DOF && s < SLOT_RESET_DOF + 12) ? 47 + (int)(s - SLOT_RESET_DOF)
-       : (s >= SLOT_RESET_ROOT_XY && s < SLOT_RESET_ROOT_XY + 2) ? 59 + (int)(s - SLOT_RESET_ROOT_XY)
-       : (s >= SLOT_DR_OFFSET && s < SLOT_DR_ARMATURE + 12 && (s - SLOT_DR_OFFSET) % 100 < 12)
-           ? 61 + 12 * (int)((s - SLOT_DR_OFFSET) / 100) + (int)((s - SLOT_DR_OFFSET) % 100)
-       : (s >= SLOT_LAG_ACTION && s <= SLOT_GAIT_START) ? 133 + (int)(s - SLOT_LAG_ACTION)
-       : (s >= SLOT_GAIT_TIME && s < SLOT_GAIT_TIME + 3) ? 137 + (int)(s - SLOT_GAIT_TIME)
-       : (s == SLOT_TERRAIN_LEVEL_RAND) ? 140 : -1;
-}
-__host__ __device__ constexpr uint32_t pre_slot(int r) {
-  return r < 47 ? SLOT_OBS_NOISE + r
-       : r < 59 ? SLOT_RESET_DOF + (r - 47)
-       : r < 61 ? SLOT_RESET_ROOT_XY + (r - 59)
-       : r < 133 ? SLOT_DR_OFFSET + 100 * ((r - 61) / 12) + (r - 61) % 12
-       : r < 137 ? SLOT_LAG_ACTION + (r - 133)
-       : r < 140 ? SLOT_GAIT_TIME + (r - 137)
-       : SLOT_TERRAIN_LEVEL_RAND;
-}
-static_assert(pre_row(pre_slot(0)) == 0 && pre_row(pre_slot(60)) == 60 && pre_row(pre_slot(61)) == 61 &&
-              pre_row(pre_slot(132)) == 132 && pre_row(pre_slot(136)) == 136 && pre_row(pre_slot(140)) == 140 &&
-              pre_row(SLOT_CMD_X) == -1 && pre_row(SLOT_DR_TORQUE) == -1, "pre_row inverts pre_slot");
-struct DrawSrc {
-  RngKey K;
-  const uint32_t* r0 = nullptr;  // nullptr: hash here
-  const uint32_t* r1 = nullptr;
-  int lane = 0;
-  __device__ __forceinline__ uint32_t operator()(uint32_t slot) const {
-    const int r = pre_row(slot);
-    if (r0 == nullptr || r < 0) return hash_k(K, slot);
-    return r < PRE_ROWS0 ? r0[r * 64 + lane] : r1[(r - PRE_ROWS0) * 64 + lane];
-  }
-};
-
 // the per-env inputs of compute_observations that reset_idx may rewrite (reset_env writes a resetting env's new values into it)
 struct ObsIn {
   float cmd[4], dof[24], act[12], la[12], rv[6];
@@ -625,9 +587,8 @@ struct ObsIn {
 // memory round trip less; X->cmd is left as it is (reset_idx does not touch the commands)
 __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B, const t1env_step_args& A,
                           int n, uint32_t genv, uint32_t ctr, bool do_terrain, bool zero_reward_state = true,
-                          ObsIn* X = nullptr, const DrawSrc* pre = nullptr) {
-  DrawSrc H;
-  if (pre) H = *pre; else H.K = rng_key(C.seed, genv, ctr);
+                          ObsIn* X = nullptr) {
+  const RngKey K = rng_key(C.seed, genv, ctr);
   float org[3];
   bool org_known = false;
   if (do_terrain && C.terrain_curriculum) {  // _update_terrain_curriculum
@@ -638,7 +599,7 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
     const float* cmd = B.commands + n * 4;
     const bool down = (dist < norm2(cmd[0], cmd[1]) * (C.episode_length_s * 0.5f)) && !up;
     int lv = B.terrain_levels[n] + (up ? 1 : 0) - (down ? 1 : 0);
-    const int rnd = rand_int_h(0, C.num_terrain_rows, H(SLOT_TERRAIN_LEVEL_RAND));
+    const int rnd = rand_int(0, C.num_terrain_rows, K, SLOT_TERRAIN_LEVEL_RAND);
     lv = lv >= C.num_terrain_rows ? rnd : (lv < 0 ? 0 : lv);
     B.terrain_levels[n] = lv;
     const float* to = B.terrain_origins + ((size_t)lv * C.num_terrain_cols + B.terrain_types[n]) * 3;
@@ -658,7 +619,7 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   // _reset_dofs
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    const float dp = M.default_dof_pos[j] + rand_float_h(-C.reset_dof_range, C.reset_dof_range, H(SLOT_RESET_DOF + j));
+    const float dp = M.default_dof_pos[j] + rand_float(-C.reset_dof_range, C.reset_dof_range, K, SLOT_RESET_DOF + j);
     B.dof_state[n * 24 + 2 * j] = dp;
     B.dof_state[n * 24 + 2 * j + 1] = 0.0f;
     if (X) { X->dof[2 * j] = dp; X->dof[2 * j + 1] = 0.0f; }
@@ -671,21 +632,21 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   for (int i = 0; i < 3; ++i) r[i] += org[i];
   if (C.custom_origins) {
     const float p3 = C.reset_xy_range;
-    r[0] += rand_float_h(-p3, p3, H(SLOT_RESET_ROOT_XY + 0));
-    r[1] += rand_float_h(-p3, p3, H(SLOT_RESET_ROOT_XY + 1));
+    r[0] += rand_float(-p3, p3, K, SLOT_RESET_ROOT_XY + 0);
+    r[1] += rand_float(-p3, p3, K, SLOT_RESET_ROOT_XY + 1);
   }
   strow(B.root_states + n * 13, r);
   // randomize_dof_props (torque_multi is redrawn every substep anyway; its reset draw has no effect)
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
     B.motor_offsets[n * 12 + j] =
-        rand_float_h(C.motor_offset_range[0], C.motor_offset_range[1], H(SLOT_DR_OFFSET + j));
-    B.kp[n * 12 + j] = rand_float_h(C.kp_mult_range[0], C.kp_mult_range[1], H(SLOT_DR_KP + j)) * M.p_gains[j];
-    B.kd[n * 12 + j] = rand_float_h(C.kd_mult_range[0], C.kd_mult_range[1], H(SLOT_DR_KD + j)) * M.d_gains[j];
-    B.coulomb[n * 12 + j] = rand_float_h(C.coulomb_range[0], C.coulomb_range[1], H(SLOT_DR_COULOMB + j));
-    B.viscous[n * 12 + j] = rand_float_h(C.viscous_range[0], C.viscous_range[1], H(SLOT_DR_VISCOUS + j));
+        rand_float(C.motor_offset_range[0], C.motor_offset_range[1], K, SLOT_DR_OFFSET + j);
+    B.kp[n * 12 + j] = rand_float(C.kp_mult_range[0], C.kp_mult_range[1], K, SLOT_DR_KP + j) * M.p_gains[j];
+    B.kd[n * 12 + j] = rand_float(C.kd_mult_range[0], C.kd_mult_range[1], K, SLOT_DR_KD + j) * M.d_gains[j];
+    B.coulomb[n * 12 + j] = rand_float(C.coulomb_range[0], C.coulomb_range[1], K, SLOT_DR_COULOMB + j);
+    B.viscous[n * 12 + j] = rand_float(C.viscous_range[0], C.viscous_range[1], K, SLOT_DR_VISCOUS + j);
     B.armature[n * 12 + j] =
-        rand_float_h(C.armature_range[j][0], C.armature_range[j][1], H(SLOT_DR_ARMATURE + j));
+        rand_float(C.armature_range[j][0], C.armature_range[j][1], K, SLOT_DR_ARMATURE + j);
   }
   // randomize_lag_props: zero the lag rings, redraw lag lengths
 #ifndef T1_WHATIF_NO_RING_ZERO  // timing-only what-if build
@@ -696,9 +657,9 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
 #pragma unroll
   for (int i = 0; i < 16; ++i) B.imu_hist[(size_t)n * 16 + i] = 0.0f;
 #endif
-  B.lag_timestep[n] = rand_int_h(C.lag_range[0], C.lag_range[1] + 1, H(SLOT_LAG_ACTION));
-  const int dl = rand_int_h(C.dof_lag_range[0], C.dof_lag_range[1] + 1, H(SLOT_LAG_DOF));
-  const int il = rand_int_h(C.imu_lag_range[0], C.imu_lag_range[1] + 1, H(SLOT_LAG_IMU));
+  B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, K, SLOT_LAG_ACTION);
+  const int dl = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, K, SLOT_LAG_DOF);
+  const int il = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, K, SLOT_LAG_IMU);
   B.dof_lag_timestep[n] = dl;
   B.imu_lag_timestep[n] = il;
   // buffers
@@ -718,13 +679,13 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   B.episode_length_buf[n] = 0;
   B.phase_length_buf[n] = 0;
   B.reset_buf[n] = 1;
-  const float gstart = (float)rand_int_h(0, 2, H(SLOT_GAIT_START)) * 0.5f;
+  const float gstart = (float)rand_int(0, 2, K, SLOT_GAIT_START) * 0.5f;
   B.gait_start[n] = gstart;
   // generate_gait_time (t1:109-124)
   float g[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
-    g[i] = rand_float_h(C.gait_time_range[i][0], C.gait_time_range[i][1], H(SLOT_GAIT_TIME + i));
+    g[i] = rand_float(C.gait_time_range[i][0], C.gait_time_range[i][1], K, SLOT_GAIT_TIME + i);
   const float s = (g[0] + g[1]) + g[2];
   const float f = C.max_episode_length / s;
   const float s0 = g[0] * f, s1 = g[1] * f;
@@ -758,8 +719,8 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
 
 // the actor-frame noise of observation i (legged_robot.py compute_observations: (2 u - 1) * noise_vec * level, u keyed
 // by the env's post-physics key)
-__device__ __forceinline__ float obs_noise(const t1env_config& C, const DrawSrc& H, int i) {
-  const float u = u01_h(H(SLOT_OBS_NOISE + i));
+__device__ __forceinline__ float obs_noise(const t1env_config& C, RngKey K, int i) {
+  const float u = uniform01(K, SLOT_OBS_NOISE + i);
   return ((2.0f * u - 1.0f) * C.noise_vec[i]) * C.noise_level;
 }
 
@@ -793,8 +754,7 @@ struct ObsExtra {
 };
 __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                             const t1env_step_args& A, int n, bool do_reset, bool any_reset, ObsIn& X,
-                                            const ObsExtra& E, bool zero_reward_state = true,
-                                            const DrawSrc* pre = nullptr);
+                                            const ObsExtra& E, bool zero_reward_state = true);
 __device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                            const t1env_step_args& A, int n, bool do_reset, bool any_reset) {
   ObsIn X;
@@ -812,11 +772,10 @@ __device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config
 // X: the inputs as they stand after post_a (reloaded here after a reset)
 __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                             const t1env_step_args& A, int n, bool do_reset, bool any_reset, ObsIn& X,
-                                            const ObsExtra& E, bool zero_reward_state, const DrawSrc* pre) {
+                                            const ObsExtra& E, bool zero_reward_state) {
   const uint32_t genv = (uint32_t)(C.env_offset + n);
   const uint32_t ctr = A.counter + 1u;
-  DrawSrc H;  // the draws keyed (seed, env, counter + 1): precomputed by the fused step's helpers, or hashed here
-  if (pre) H = *pre; else H.K = rng_key(C.seed, genv, ctr);
+  const RngKey K = rng_key(C.seed, genv, ctr);
   const float (&ef)[2] = E.ef;
   const float (&et)[3] = E.et;
   const float (&cfz)[2] = E.cfz;
@@ -839,7 +798,7 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
   ldrow(lraw, lip);
 #endif
   if (do_reset) {
-    reset_env(M, C, B, A, n, genv, ctr, true, zero_reward_state, &X, &H);
+    reset_env(M, C, B, A, n, genv, ctr, true, zero_reward_state, &X);
 #pragma unroll
     for (int i = 0; i < 24; ++i) ld[i] = 0.0f;
 #pragma unroll
@@ -945,7 +904,7 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
 #ifdef T1_WHATIF_NO_NOISE_DRAWS  // timing-only what-if build
       const float nz = 0.0f;
 #else
-      const float nz = obs_noise(C, H, i);
+      const float nz = obs_noise(C, K, i);
 #endif
       v[i] = clampf(v[i] + nz, -clipo, clipo);
     }
