@@ -81,9 +81,9 @@ def parse():
     p.add_argument("--cpu-envs", type=int, default=4096,
                    help="CPU-baseline sample size (BASELINE configs[1]'s 4096 envs; 256 understated the CPU by ~2x)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r03aj.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r03fa2.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
-    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r03aj_sq_counters.json"),
+    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r03fa2_sq_counters.json"),
                    help="SQ instruction counters of the fused kernel (tools/pmc_sq_summary.py): the VALU-issue roofline")
     return p.parse_args()
 

@@ -320,6 +320,9 @@ void k_conv1d_pair(const float* __restrict__ x, const h8* __restrict__ frag, con
     load(cur, bc + 2);
     __syncthreads();  // both halves staged (and, X being double-buffered, both waves done with the sample before last)
     f4 acc0 = f4{0.0f, 0.0f, 0.0f, 0.0f}, acc1 = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#ifdef T1_CONV_WHATIF_NO_MFMA  // timing-only what-if build: the staging, loads and stores without the K loop
+    acc0[0] = __uint_as_float(X[lane]);
+#else
 #pragma unroll
     for (int s = 0; s < CV_STEPS; ++s) {
       const uint32_t* row = X + (4 * s + kg) * CV_L + CV_S * rr;
@@ -335,6 +338,7 @@ void k_conv1d_pair(const float* __restrict__ x, const h8* __restrict__ frag, con
       acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf[s][1], acc1, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf[s][0], acc1, 0, 0, 0);
     }
+#endif
     const int o = 16 * w + (lane & 15);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
