@@ -14,8 +14,11 @@
 //
 // K order: 8 slots per channel (its 6 taps and 2 zeros), so a lane's A fragment (row = output position l, 8 slots of
 // one channel) is the 6 contiguous inputs x[c][3l .. 3l+5] and needs no transposition; a K-step of 32 covers 4
-// channels, 17 steps cover the 66 (2 zero channels).  Each workgroup builds the split weight fragments in LDS once;
-// each wave stages one sample (12.4 KB, coalesced) into its own LDS rows while the next sample's loads are in flight.
+// channels, 17 steps cover the 66 (2 zero channels).  k_conv1d_mfma (t1policy_conv1d_forward, tap-major weights):
+// each workgroup builds the split weight fragments in LDS once; each wave stages one sample (12.4 KB, coalesced)
+// into its own LDS rows while the next sample's loads are in flight.  The packed form (t1policy_conv1d_pack_weights +
+// t1policy_conv1d_forward_packed) takes fragments split once per weight version: k_conv1d_pair (default) and
+// k_conv1d_regs (A/B), below.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -352,88 +355,6 @@ void k_conv1d_pair(const float* __restrict__ x, const h8* __restrict__ frag, con
   }
 }
 
-// k_conv1d_grp: one 8-wave workgroup per CU, four wave pairs sharing the split fragments in LDS (69.6 KB, filled once
-// from the packed buffer) -- no fragment registers, so each wave keeps CG_NBUF half-samples of loads in flight while
-// it multiplies (the pair kernel's two buffers left the memory pipe idle during its K loop).  Pair p takes samples
-// B0 + p, B0 + p + 4, ... of the workgroup's contiguous run; every wave runs the same number of iterations (the
-// workgroup barriers), a multiple of CG_NBUF, and a pair past its last sample recomputes the run's last one (the same
-// values to the same addresses): no branch in the loop, so the compiler's wait counts stay exact.
-constexpr int CG_PAIRS = 4, CG_NBUF = 4;
-__global__ __launch_bounds__(64 * 2 * CG_PAIRS) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void k_conv1d_grp(const float* __restrict__ x, const h8* __restrict__ frag, const float* __restrict__ bias,
-                  float* __restrict__ y, int batch) {
-  __shared__ h8 WF[CV_STEPS][2][2][64];
-  __shared__ uint32_t XS[CG_PAIRS][CV_CPAD * CV_L];
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int p = wv >> 1, w = wv & 1;  // pair, column tile
-  const int B0 = (int)((long long)blockIdx.x * batch / gridDim.x), B1 = (int)((long long)(blockIdx.x + 1) * batch / gridDim.x);
-  const int T0 = (B1 - B0 + CG_PAIRS - 1) / CG_PAIRS;
-  const int T = (T0 + CG_NBUF - 1) / CG_NBUF * CG_NBUF;  // iterations, the same for every wave of the workgroup
-  const int h0 = w * CP_HALF, h1 = w == 0 ? CP_HALF : CV_C * CV_L / 2;
-  uint32_t* X = XS[p];
-  auto sample = [&](int t) { const int s = B0 + CG_PAIRS * t + p; return s < B1 ? s : B1 - 1; };
-  float2 buf[CG_NBUF][CP_PER_LANE];
-  auto load = [&](float2 (&dst)[CP_PER_LANE], int t) {
-    const float2* src = reinterpret_cast<const float2*>(x + (size_t)sample(t) * (CV_C * CV_L));
-#pragma unroll
-    for (int k = 0; k < CP_PER_LANE; ++k) {
-      const int i = h0 + lane + 64 * k;
-      dst[k] = src[i < h1 ? i : h1 - 1];
-    }
-  };
-#pragma unroll
-  for (int j = 0; j < CG_NBUF; ++j) load(buf[j], j);
-  for (int e = threadIdx.x; e < CV_STEPS * 2 * 2 * 64; e += 64 * 2 * CG_PAIRS) (&WF[0][0][0][0])[e] = frag[e];
-  for (int i = CV_C * CV_L + lane; i < CV_CPAD * CV_L; i += 64)
-    if (w == 0) X[i] = 0u;
-  const float bo = bias[16 * w + (lane & 15)];
-  asm volatile("" ::"v"(bo));
-  const int r = lane & 15, kg = lane >> 4;
-  const int rr = r < CV_LOUT ? r : CV_LOUT - 1;
-  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  auto step = [&](float2 (&cur)[CP_PER_LANE], int t) {
-    const int s = sample(t);
-    __syncthreads();  // the previous iteration's reads of X done (and, at t = 0, WF and the zero rows written)
-#pragma unroll
-    for (int k = 0; k < CP_PER_LANE; ++k) {
-      const int i = h0 + lane + 64 * k;
-      if (i < h1) reinterpret_cast<uint2*>(X)[i] = make_uint2(split_word(cur[k].x), split_word(cur[k].y));
-    }
-    load(cur, t + CG_NBUF);  // unconditional (clamped): exact wait counts
-    __syncthreads();  // both halves staged
-    {
-      f4 acc0 = f4{0.0f, 0.0f, 0.0f, 0.0f}, acc1 = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int st = 0; st < CV_STEPS; ++st) {
-        const uint32_t* row = X + (4 * st + kg) * CV_L + CV_S * rr;
-        uint32_t v[CV_K];
-#pragma unroll
-        for (int j = 0; j < CV_K; ++j) v[j] = row[j];
-        const u4 hv = {__builtin_amdgcn_perm(v[1], v[0], 0x05040100u), __builtin_amdgcn_perm(v[3], v[2], 0x05040100u),
-                       __builtin_amdgcn_perm(v[5], v[4], 0x05040100u), 0u};
-        const u4 lv = {__builtin_amdgcn_perm(v[1], v[0], 0x07060302u), __builtin_amdgcn_perm(v[3], v[2], 0x07060302u),
-                       __builtin_amdgcn_perm(v[5], v[4], 0x07060302u), 0u};
-        const h8 ah = __builtin_bit_cast(h8, hv), al = __builtin_bit_cast(h8, lv);
-        const h8 bh = WF[st][w][0][lane], bl = WF[st][w][1][lane];
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc1, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc1, 0, 0, 0);
-      }
-      const int o = 16 * w + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int l = 4 * kg + i < CV_LOUT ? 4 * kg + i : CV_LOUT - 1;  // rows 14, 15 = row 13's result
-        y[((size_t)s * CV_LOUT + l) * CV_O + o] = acc0[i] + acc1[i] * (1.0f / CV_SPLIT) + bo;
-      }
-    }
-  };
-  for (int t = 0; t < T; t += CG_NBUF) {
-#pragma unroll
-    for (int j = 0; j < CG_NBUF; ++j) step(buf[j], t + j);
-  }
-}
-
 // The PPO minibatch's actor observations rebuilt from the frame-history rollout storage (algo/rollout.py
 // _HistoryRows): row m is the window of frames k .. k + F - 1 of env n's sequence seq[n] ((F + T - 1) frames of `frame`
 // values, k = idx[m] / N, n = idx[m] % N), with the frames older than the env's latest reset at or before step k
@@ -531,12 +452,7 @@ int t1policy_conv1d_forward_packed(const float* x, const void* frag, const float
   // k_conv1d_pair (default): CP_PAIRS_PER_CU two-wave workgroups per CU; T1POLICY_CONV=regs: k_conv1d_regs, one
   // 4-wave workgroup per CU (A/B).  No workgroup without a sample.
   const char* kv = getenv("T1POLICY_CONV");
-  if (kv && kv[0] == 'g') {  // k_conv1d_grp: one 8-wave workgroup per CU
-    const long long need = ((long long)batch + CG_PAIRS - 1) / CG_PAIRS;
-    const int grid = (int)(need < cus ? need : cus);
-    hipLaunchKernelGGL(k_conv1d_grp, dim3(grid), dim3(64 * 2 * CG_PAIRS), 0, (hipStream_t)stream, x,
-                       reinterpret_cast<const h8*>(frag), bias, y, batch);
-  } else if (kv && kv[0] == 'r') {
+  if (kv && kv[0] == 'r') {
     const long long need = ((long long)batch + CR_WAVES - 1) / CR_WAVES;
     const int grid = (int)(need < cus ? need : cus);
     hipLaunchKernelGGL(k_conv1d_regs, dim3(grid), dim3(64 * CR_WAVES), 0, (hipStream_t)stream, x,

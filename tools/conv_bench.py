@@ -82,14 +82,8 @@ new()
 torch.cuda.synchronize()
 res["packed_regs_max_rel_err"] = ((y_new.double() - ref).abs() / (1 + ref.abs())).max().item()
 res["packed_regs"] = timed(new, a.iters)
-os.environ["T1POLICY_CONV"] = "grp"
-y_new.fill_(float("nan"))
-new()
-torch.cuda.synchronize()
-res["packed_grp_max_rel_err"] = ((y_new.double() - ref).abs() / (1 + ref.abs())).max().item()
-res["packed_grp"] = timed(new, a.iters)
 del os.environ["T1POLICY_CONV"]
-for k in ("old", "packed", "packed_regs", "packed_grp"):
+for k in ("old", "packed", "packed_regs"):
     res[k]["GBs"] = (res["bytes_in"] + res["bytes_out"]) / (res[k]["median_us"] * 1e-6) / 1e9
 print(json.dumps(res))
 if a.out:
