@@ -21,7 +21,8 @@ import torch.nn as nn
 from torch.distributions import Normal
 
 
-SPLITK_ROWS = 2048      # rows of the batch (K of the weight-gradient GEMM) per split-K slice
+# rows of the batch (K of the weight-gradient GEMM) per split-K slice (T1_SPLITK_ROWS: A/B)
+SPLITK_ROWS = int(os.environ.get("T1_SPLITK_ROWS", "2048"))
 # bf16 split-K partial products returned in fp32 by the GEMM itself (T1_WGRAD_OUT_F32=0: the bf16 partials widened
 # afterwards, the round-2 path; A/B)
 WGRAD_OUT_F32 = os.environ.get("T1_WGRAD_OUT_F32", "1") != "0"
