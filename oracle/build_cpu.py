@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 OUT = os.path.join(HERE, "_build", "libt1dyn_cpu.so")
 DEPS = [os.path.join(HERE, "dyn_cpu.cpp")] + [os.path.join(REPO, "ti5_isaacgym_amd", "csrc", f) for f in
-                                              ("t1_dynamics.h", "t1_common.h", "t1_model_conv.h")]
+                                              ("t1_dynamics.h", "t1_dyn5.h", "t1_common.h", "t1_model_conv.h")]
 
 
 def build(force=False):

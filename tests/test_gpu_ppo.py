@@ -219,3 +219,85 @@ def test_graphed_update_follows_optimizer_reload():
         for ls, w in runs[1:]:
             assert ls == runs[0][0], (first, [r[0] for r in runs])
             assert all(torch.equal(a, b) for a, b in zip(w, runs[0][1]))
+
+
+def _fill_storage(alg, N, T, dev, seed):
+    st = alg.storage
+    g = torch.Generator(device=dev).manual_seed(seed)
+    for t in (st.obs0, st.frames, st.privileged_observations, st.actions, st.values, st.returns, st.actions_log_prob,
+              st.mu, st.rewards):
+        t.normal_(generator=g)
+    st.sigma.uniform_(0.5, 1.5, generator=g)
+    st.step = T
+    alg.compute_returns(torch.randn(N, 219, device=dev, generator=g))
+
+
+def test_graphed_act_follows_graphed_updates():
+    """the graphed update's Adam steps are graph replays, which do not bump the weights' version
+    counter, so a conv-fragment cache keyed on it went stale from the second update on.  After three graphed updates
+    the graphed act() mean must equal the autograd path's (conv as an unfolded GEMM, no packed fragments)."""
+    from ti5_isaacgym_amd import task_registry
+    from ti5_isaacgym_amd.algo.dh_policy import ActorCriticDH
+    from ti5_isaacgym_amd.algo.dh_update import DHPPO
+    from ti5_isaacgym_amd.utils.helpers import class_to_dict
+    _, tc = task_registry.get_cfgs("t1_dh_stand")
+    cfg = class_to_dict(tc)
+    N, T, dev = 512, 24, torch.device("cuda:0")
+    torch.manual_seed(0)
+    ac = ActorCriticDH(235, 47, 219, 12, **cfg["policy"]).to(dev)
+    alg = DHPPO(ac, device=str(dev), **cfg["algorithm"])
+    assert alg.graph_update and alg.graph_act
+    alg.init_storage(N, T, [3102], [219], [12], history=(47, 66))
+    obs = torch.randn(N, 66 * 47, device=dev)
+    cobs = torch.randn(N, 219, device=dev)
+    for it in range(3):
+        with torch.inference_mode():
+            alg._graphed_act(obs, cobs)
+        _fill_storage(alg, N, T, dev, 20 + it)
+        ac.train()
+        alg.update()
+    assert alg._upd is not None  # the minibatch steps were replays
+    with torch.inference_mode():
+        m = alg._graphed_act(obs, cobs)[3].clone()
+    with torch.enable_grad():
+        ref = ac.actor(ac.actor_input(obs)).detach()
+    torch.testing.assert_close(m, ref, rtol=1e-5, atol=2e-5)
+
+
+def test_update_after_loading_plain_adam_state():
+    """a checkpoint's optimizer state written by a plain (non-capturable) torch Adam -- the
+    reference's, or an older build's -- replaces the param groups' flags on load; after_optimizer_load restores the
+    capturable fused Adam with the device learning rate, so the next update runs, and the loaded lr is the one used
+    unless the caller assigns another afterwards."""
+    from torch import optim
+    from ti5_isaacgym_amd import task_registry
+    from ti5_isaacgym_amd.algo.dh_policy import ActorCriticDH
+    from ti5_isaacgym_amd.algo.dh_update import DHPPO
+    from ti5_isaacgym_amd.utils.helpers import class_to_dict
+    _, tc = task_registry.get_cfgs("t1_dh_stand")
+    cfg = class_to_dict(tc)
+    N, T, dev = 256, 24, torch.device("cuda:0")
+    torch.manual_seed(0)
+    ac = ActorCriticDH(235, 47, 219, 12, **cfg["policy"]).to(dev)
+    plain = optim.Adam(ac.parameters(), lr=3e-4)
+    for p in ac.parameters():
+        p.grad = torch.zeros_like(p)
+    plain.step()
+    sd = plain.state_dict()
+    assert sd["param_groups"][0]["capturable"] is False
+    alg = DHPPO(ac, device=str(dev), **cfg["algorithm"])
+    alg.init_storage(N, T, [3102], [219], [12], history=(47, 66))
+    alg.optimizer.load_state_dict(sd)
+    alg.after_optimizer_load()
+    assert abs(alg.learning_rate - 3e-4) < 1e-10
+    _fill_storage(alg, N, T, dev, 5)
+    ac.train()
+    losses = alg.update()
+    assert all(map(lambda x: x == x, losses))
+    g = alg.optimizer.param_groups[0]
+    assert g["capturable"] and g["fused"] and g["lr"] is alg._lr_t
+    alg.learning_rate = 1e-4   # an assignment after the load wins
+    _fill_storage(alg, N, T, dev, 6)
+    alg.schedule = "fixed"
+    alg.update()
+    assert abs(alg.learning_rate - 1e-4) < 1e-10

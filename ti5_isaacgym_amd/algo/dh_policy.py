@@ -22,7 +22,18 @@ from torch.distributions import Normal
 
 
 # rows of the batch (K of the weight-gradient GEMM) per split-K slice (T1_SPLITK_ROWS: A/B)
-SPLITK_ROWS = int(os.environ.get("T1_SPLITK_ROWS", "2048"))
+def _splitk_rows(v):
+    """T1_SPLITK_ROWS, checked at import (a bad value would otherwise fail deep inside a backward pass)."""
+    try:
+        r = int(v)
+    except ValueError:
+        r = 0
+    if r <= 0:
+        raise ValueError(f"T1_SPLITK_ROWS must be a positive integer, got {v!r}")
+    return r
+
+
+SPLITK_ROWS = _splitk_rows(os.environ.get("T1_SPLITK_ROWS", "2048"))
 # bf16 split-K partial products returned in fp32 by the GEMM itself (T1_WGRAD_OUT_F32=0: the bf16 partials widened
 # afterwards, the round-2 path; A/B)
 WGRAD_OUT_F32 = os.environ.get("T1_WGRAD_OUT_F32", "1") != "0"
@@ -148,16 +159,17 @@ def conv1d_direct(x, conv):
     return y
 
 
-def packed_conv_weights(conv, stream=None):
+def packed_conv_weights(conv, stream=None, force=False):
     """The conv's weights as the packed-fragment kernel's split fp16 fragments (t1policy_conv1d_pack_weights), kept on
-    the module and rebuilt only when the weight changed (its version counter: the optimizer's in-place step, a
-    load_state_dict).  A captured act() graph reads the buffer in place: refresh_packed_weights() before each replay
-    repacks after a PPO update.  None for a shape the library has no instance of."""
+    the module and rebuilt when the weight changed.  An eager in-place change (a load_state_dict, an eager optimizer
+    step) moves the weight's version counter; a REPLAYED optimizer step (the graphed PPO update) does not -- a graph
+    replay bypasses the dispatcher -- so DHPPO.update() repacks with force=True after every update.  A
+    captured act() graph reads the buffer in place.  None for a shape the library has no instance of."""
     from .. import _lib
     w = conv.weight
     key = (w._version, w.data_ptr())
     frag = getattr(conv, "_t1_frag", None)
-    if frag is not None and getattr(conv, "_t1_frag_key", None) == key:
+    if not force and frag is not None and getattr(conv, "_t1_frag_key", None) == key:
         return frag
     lib = _lib.load()
     if frag is None or frag.device != w.device:
@@ -175,11 +187,12 @@ def packed_conv_weights(conv, stream=None):
     return frag
 
 
-def refresh_packed_weights(module):
-    """Repack every Conv1d under `module` whose packed fragments are stale (before replaying a captured act())."""
+def refresh_packed_weights(module, force=False):
+    """Repack every Conv1d under `module` whose packed fragments are stale (before replaying a captured act()), or
+    every packed one (force: after an update whose optimizer steps were graph replays)."""
     for m in module.modules():
         if isinstance(m, nn.Conv1d) and getattr(m, "_t1_frag", None) is not None:
-            packed_conv_weights(m)
+            packed_conv_weights(m, force=force)
 
 
 def conv1d_as_gemm(x, conv, channels_last=False):

@@ -109,6 +109,24 @@ class DHPPO:
         if self._lr_t is not None:
             self._lr_t.fill_(float(v))
 
+    def after_optimizer_load(self):
+        """After optimizer.load_state_dict (a checkpoint resume): load_state_dict replaces every param-group
+        hyperparameter with the saved one, so a state written by the reference (or by an older build) comes back with
+        capturable=False / fused=None, under which the device-tensor learning rate is rejected.  Restore the flags this
+        optimizer was built with, move the step counters to the parameters' device as fp32 (capturable Adam keeps them
+        there), and bind the lr tensor to the loaded value now, so a later `learning_rate = x` wins."""
+        if self._lr_t is None:
+            return
+        for g in self.optimizer.param_groups:
+            g["capturable"] = True
+            g["fused"] = True
+            g["foreach"] = None
+            for p in g["params"]:
+                st = self.optimizer.state.get(p)
+                if st and "step" in st:
+                    st["step"] = torch.as_tensor(st["step"], dtype=torch.float32, device=p.device).reshape(())
+        self._bind_lr()
+
     def _bind_lr(self):
         """Keep every param group's lr the device tensor (a loaded optimizer state or a caller may have put a float or
         another tensor there: its value is taken over)."""
@@ -266,6 +284,8 @@ class DHPPO:
                     self._minibatch_step(batch, amp, mse)
         finally:
             ac.validate_args = validate
+        if cuda:  # the optimizer steps were graph replays (no version bump): repack the conv's fragments now
+            refresh_packed_weights(ac, force=True)
         n = self.num_learning_epochs * self.num_mini_batches
         self.storage.clear()
         mv, ms, mse_ = (self._sums / n).tolist()

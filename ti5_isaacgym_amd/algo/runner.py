@@ -208,6 +208,7 @@ class DHOnPolicyRunner:
         if load_optimizer:
             self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
             self.alg.state_estimator_optimizer.load_state_dict(d["es_optimizer_state_dict"])
+            self.alg.after_optimizer_load()  # capturable / fused flags and the device lr after a foreign state
         self.current_learning_iteration = d["iter"]
         return d["infos"]
 

@@ -380,7 +380,8 @@ const char* t1env_last_error(void) { return g_err; }
 const char* t1env_version(void) { return "t1env-hip 0.1 (gfx950)"; }
 
 // one EP_PART_ROW-float row per k_dyn4 dynamics workgroup
-static size_t ep_part_bytes(int num_envs) { return sizeof(float) * EP_PART_ROW * (size_t)((num_envs + 63) / 64); }
+// one row per dynamics workgroup: k_dyn5 has 32 envs per workgroup (k_dyn4 64)
+static size_t ep_part_bytes(int num_envs) { return sizeof(float) * EP_PART_ROW * (size_t)((num_envs + 31) / 32); }
 
 int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_buffers* bufs, t1env** out) {
   if (!model || !cfg || !bufs || !out) return fail(T1ENV_E_ARG, "t1env_create: null argument");
@@ -426,6 +427,8 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
         hipSuccess) cus = 256;
     e->dyn.cus = cus;
     e->dyn.waves = t1_dyn_waves_default();
+    if (const char* dk = getenv("T1ENV_DYN_KERNEL"))  // A/B: 4 = k_dyn4, 5 = k_dyn5
+      if (atoi(dk) == 4 || atoi(dk) == 5) e->dyn.waves = atoi(dk);
     e->dyn.shift_blocks = 0;
     if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))  // > 0: shift workgroups in the launch; -1: stand-alone shift
       if (atoi(sb) > 0 || atoi(sb) == -1) e->dyn.shift_blocks = atoi(sb);

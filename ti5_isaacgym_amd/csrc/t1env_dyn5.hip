@@ -1,0 +1,955 @@
+// t1env_dyn5.hip -- k_dyn5, the env step's main launch with the dynamics on every CU at 8192 envs
+// (legged_robot.py:399-434 + Isaac Gym simulate(), and in the fused step post-physics, legged_robot.py:458-506).
+//
+// k_dyn4 (t1env_dynamics.hip) runs 64 envs per workgroup on four waves (two leg waves, two contact helpers): 4 lanes
+// per env, 128 workgroups at 8192 envs -- half the chip, one wave per SIMD, each wave one long dependent chain.
+// k_dyn5 gives every env 8 lanes: 32 envs per workgroup, both legs of an env in one wave (lanes 0-31 the left legs,
+// 32-63 the right legs of the same 32 envs, so every wave is full and the leg index is a per-lane value), and the
+// four waves are four roles of the substep (t1_dyn5.h): W0 core (chain, CRBA, fold-in, elimination, base solve,
+// integration), W1 bias (RNEA, PD torques, base block, base-box contacts), W2 terrain contacts of the shank and foot,
+// W3 self-contacts.  256 workgroups at 8192 envs: every CU.  Per substep
+//     W0: forward chain + CRBA backward pass       | W1 / W2 / W3: their terms from the published state
+//     S2 --------------------------------------------------------------------------------------------------
+//     W0: fold-in, elimination, base system of the | W1-W3: a slice of the workgroup's own history shift
+//         two halves (permlane32), solve, backsub,  |
+//         integration, publish the state           |
+//     S1 --------------------------------------------------------------------------------------------------
+// Two barriers per substep (k_dyn4: three); the two legs' base-block contributions meet by v_permlane32_swap.
+//
+// The robot model is copied to LDS once per launch: with the leg index per lane, model reads indexed by it are LDS
+// reads (two addresses per wave) instead of scalar loads.
+//
+// The history shift is no longer a set of separate workgroups: each workgroup shifts the 65/2 older frames of its
+// OWN 32 rows, a slice per substep on W1-W3 while W0 runs its post-S2 chain (those waves would wait for the next state
+// anyway).  The epilogue of the same workgroup then writes the newest frames and zeroes its reset rows itself: no
+// cross-workgroup handoff, no sc1 stores, no prelaunched shift at any N.
+#include <hip/hip_runtime.h>
+
+// -DT1_PHASE_PROF (tools/prof_dynamics_phases.py --kernel 5): lane 0 of every wave accumulates shader-clock deltas
+// between T1_PROF_MARK points into per-phase buckets; never part of the product build.
+#ifdef T1_PHASE_PROF
+constexpr int T1_NPROF5 = 24, T1_PROF_WAVES5 = 4;
+__device__ unsigned long long g_t1_prof5[T1_PROF_WAVES5][T1_NPROF5];
+__shared__ unsigned long long t1_prof_acc5[T1_PROF_WAVES5][T1_NPROF5 + 1];  // [wave][bucket], last = previous mark
+__device__ __forceinline__ unsigned long long t1_stamp5() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+__device__ __forceinline__ void t1_prof_mark5(int i) {
+  const int w = threadIdx.x / 64;
+  const unsigned long long now = t1_stamp5();
+  if ((threadIdx.x & 63) == 0) {
+    t1_prof_acc5[w][i] += now - t1_prof_acc5[w][T1_NPROF5];
+    t1_prof_acc5[w][T1_NPROF5] = now;
+  }
+}
+__device__ __forceinline__ void t1_prof_begin5() {
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    for (int i = 0; i < T1_NPROF5; ++i) t1_prof_acc5[w][i] = 0;
+    t1_prof_acc5[w][T1_NPROF5] = t1_stamp5();
+  }
+}
+__device__ __forceinline__ void t1_prof_end5() {
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < T1_NPROF5; ++i) atomicAdd(&g_t1_prof5[w][i], t1_prof_acc5[w][i]);
+}
+#define T1_PROF_MARK(i) t1_prof_mark5(i)
+#define T1_PROF_BEGIN() t1_prof_begin5()
+#define T1_PROF_END() t1_prof_end5()
+#else
+#define T1_PROF_BEGIN() ((void)0)
+#define T1_PROF_END() ((void)0)
+#endif
+
+#include "t1_dyn5.h"
+#include "t1env_device.h"
+#include "t1env_internal.h"
+#include "t1env_postphys.h"
+#include "t1env_fused.h"
+
+using namespace t1;
+
+constexpr int NE5 = 32;        // envs per workgroup
+constexpr int D5_BLOCK = 256;  // four waves
+constexpr int D5_SHIFT_T = 192;  // the shift's threads (W1-W3)
+#ifndef T1_D5_SHIFT_UNROLL
+#define T1_D5_SHIFT_UNROLL 8  // 16-B chunks per thread in flight in one shift batch
+#endif
+
+// float4 rows [row][lane]: one ds_write_b128 / ds_read_b128 per 4 values of a lane, conflict-free
+template <int K> struct Rows4 { float4 r[(K + 3) / 4][64]; };
+template <int K>
+__device__ __forceinline__ void put4(Rows4<K>& D, int lane, const float (&v)[K]) {
+#pragma unroll
+  for (int r = 0; r < (K + 3) / 4; ++r)
+    D.r[r][lane] = make_float4(v[4 * r], 4 * r + 1 < K ? v[4 * r + 1] : 0.0f, 4 * r + 2 < K ? v[4 * r + 2] : 0.0f,
+                               4 * r + 3 < K ? v[4 * r + 3] : 0.0f);
+}
+template <int K>
+__device__ __forceinline__ void get4(const Rows4<K>& D, int lane, float (&v)[K]) {
+#pragma unroll
+  for (int r = 0; r < (K + 3) / 4; ++r) {
+    const float4 x = D.r[r][lane];
+    v[4 * r] = x.x;
+    if (4 * r + 1 < K) v[4 * r + 1] = x.y;
+    if (4 * r + 2 < K) v[4 * r + 2] = x.z;
+    if (4 * r + 3 < K) v[4 * r + 3] = x.w;
+  }
+}
+
+// the value of the left-half lane and of the right-half lane of this lane's env, in every lane (v_permlane32_swap:
+// lanes 32-63 of the first operand trade with lanes 0-31 of the second, both copies of v)
+__device__ __forceinline__ void halves(float v, float& left, float& right) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  left = __uint_as_float(r[0]);
+  right = __uint_as_float(r[1]);
+}
+
+// The substep state W0 publishes (each half: the env's base state and its leg's joints)
+enum : int { Q_POS = 0, Q_QUAT = 3, Q_W = 7, Q_VO = 10, Q_Q = 13, Q_QD = 19, Q_N = 25 };
+// W1's terms: the torques, the bias / torque rhs, the leg's total bias, the base block with both base-box halves
+enum : int { B_TAU = 0, B_RG = 6, B_G = 12, B_AC = 18, B_R = 39, B_N = 45 };
+constexpr int CAP5_N = 2 * NLEG + 8;  // W0's sensor-lag capture: q, qd of the leg; the raw IMU sample (leg 0 lanes)
+
+struct Dyn5Lds {
+  DynModel model;
+  Rows4<Q_N> st;         // W0 -> all: substep state
+  Rows4<B_N> w1;         // W1 -> W0
+  Rows4<XCH> w2[2];      // W2 -> W0: terrain terms of the shank [0], foot [1]
+  Rows4<XCH> w3[2];      // W3 -> W0: self-contact terms of the shank, foot
+  PdStage<64> pd;        // W1: PD constants and action ring of each lane's leg
+  float cap[CAP5_N][64];
+  float act[12][NE5];    // the clipped actions (epilogue)
+  float epi[EPI_N][NE5];  // staged post-physics inputs (epilogue)
+  float fr[FR_N][NE5];   // this step's outputs (epilogue)
+  float vis[2][64];      // end-of-step restitution episodes of the shank / foot (W2 -> W3's report)
+  float vib[64];         // end-of-step episode of the base-box half (W1 -> W3's report)
+};
+
+__device__ __forceinline__ void state_pack(const BaseState<float>& sb, const float q[NLEG], const float qd[NLEG],
+                                           float (&v)[Q_N]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { v[Q_POS + i] = sb.pos[i]; v[Q_W + i] = sb.w[i]; v[Q_VO + i] = sb.vo[i]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[Q_QUAT + i] = sb.quat[i];
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) { v[Q_Q + k] = q[k]; v[Q_QD + k] = qd[k]; }
+}
+__device__ __forceinline__ void state_unpack(const float (&v)[Q_N], BaseState<float>& sb, float q[NLEG], float qd[NLEG]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { sb.pos[i] = v[Q_POS + i]; sb.w[i] = v[Q_W + i]; sb.vo[i] = v[Q_VO + i]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sb.quat[i] = v[Q_QUAT + i];
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) { q[k] = v[Q_Q + k]; qd[k] = v[Q_QD + k]; }
+}
+__device__ __forceinline__ void read_state(const Dyn5Lds& L, int lane, BaseState<float>& sb, float q[NLEG], float qd[NLEG]) {
+  float v[Q_N];
+  get4(L.st, lane, v);
+  state_unpack(v, sb, q, qd);
+}
+__device__ __forceinline__ void sym_pack(const Sym6<float>& A, const float g[6], float (&v)[XCH]) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) v[i] = A.a[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[21 + i] = g[i];
+}
+__device__ __forceinline__ void sym_unpack(const float (&v)[XCH], Sym6<float>& A, float g[6]) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) A.a[i] = v[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) g[i] = v[21 + i];
+}
+
+// ---- the workgroup's own history shift, a window of 16-B chunks per call: out[row, :F*(H-1)] = in[row, F:] for
+// the rows [r0, r1).  shift_rows_f32's addressing (32-bit row-local indices) over the chunk window [c_lo, c_hi) of the
+// range, plain stores (this workgroup zeroes its reset rows after, in program order behind the epilogue barrier).
+template <int F, int H, int U>
+__device__ __forceinline__ void shift_window_f32(const float* __restrict__ in, float* __restrict__ out, int64_t total,
+                                                 int64_t r0, int64_t r1, uint32_t c_lo, uint32_t c_hi, int t0, int stride) {
+  constexpr uint32_t ROW = F * H;
+  const float* __restrict__ in0 = in + r0 * ROW;
+  float* __restrict__ out0 = out + r0 * ROW;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);  // elements from in0 to the buffer end
+  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
+  const uint32_t nel = span < lim ? span : lim;
+  const uint32_t n4 = (nel + 3) / 4;
+  const uint32_t hi = c_hi < n4 ? c_hi : n4;
+  for (uint32_t base = c_lo + t0; base < hi; base += U * stride) {
+    float4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sa = ((base + u * stride) * 4 + F) & ~3u;
+      const uint32_t sc = sa + 8 <= lim ? sa : (lim - 8) & ~3u;  // tail: aligned in-bounds dummy
+      a[u] = *reinterpret_cast<const float4*>(in0 + sc);
+      b[u] = *reinterpret_cast<const float4*>(in0 + sc + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = base + u * stride;
+      if (c >= hi) break;
+      const uint32_t i = c * 4, sidx = i + F, sa = sidx & ~3u;
+      float4 x = a[u], y = b[u];
+      if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
+        float t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
+        x = make_float4(t[0], t[1], t[2], t[3]);
+        y = make_float4(t[4], t[5], t[6], t[7]);
+      }
+      const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+      const int rem = (int)(sidx - sa);
+      const uint32_t col0 = i - (i / ROW) * ROW;
+      if (col0 + 3 < ROW - F && i + 3 < lim) {  // 4 older-frame columns of one row
+        *reinterpret_cast<float4*>(out0 + i) = make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]);
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t e = i + k;
+        if (e >= lim) break;
+        if (e - (e / ROW) * ROW < ROW - F) out0[e] = src[rem + k];
+      }
+    }
+  }
+}
+// the fp16 histories (t1env_config.obs_half): shift_rows_f16's addressing over a chunk window of 8 halves
+template <int F, int H, int U>
+__device__ __forceinline__ void shift_window_f16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                 int64_t total, int64_t r0, int64_t r1, uint32_t c_lo, uint32_t c_hi,
+                                                 int t0, int stride) {
+  constexpr uint32_t ROW = F * H, REM = F % 8, M = REM / 2;
+  const uint16_t* __restrict__ in0 = in + r0 * ROW;
+  uint16_t* __restrict__ out0 = out + r0 * ROW;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
+  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
+  const uint32_t nel = span < lim ? span : lim;
+  const uint32_t n8 = (nel + 7) / 8;
+  const uint32_t hi = c_hi < n8 ? c_hi : n8;
+  for (uint32_t base = c_lo + t0; base < hi; base += U * stride) {
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sa = ((base + u * stride) * 8 + F) & ~7u;
+      const uint32_t sc = sa + 16 <= lim ? sa : (lim - 16) & ~7u;
+      a[u] = *reinterpret_cast<const u32x4*>(in0 + sc);
+      b[u] = *reinterpret_cast<const u32x4*>(in0 + sc + 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c8 = base + u * stride;
+      if (c8 >= hi) break;
+      const uint32_t i = c8 * 8, sa = (i + F) & ~7u;
+      uint32_t w[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
+      if (sa + 16 > lim) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t lo = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
+          const uint32_t hh = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
+          w[k] = lo | (hh << 16);
+        }
+      }
+      u32x4 o;
+      if constexpr (REM % 2 == 0) {
+        o = u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
+      } else {
+        o = u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], 2), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], 2),
+                  __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], 2), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], 2)};
+      }
+      const uint32_t col0 = i - (i / ROW) * ROW;
+      if (col0 + 7 < ROW - F && i + 7 < lim) {
+        *reinterpret_cast<u32x4*>(out0 + i) = o;
+        continue;
+      }
+      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t e = i + k;
+        if (e >= lim) break;
+        if (e - (e / ROW) * ROW < ROW - F) out0[e] = (uint16_t)(ow[k / 2] >> (16 * (k & 1)));
+      }
+    }
+  }
+}
+// slice `sl` of `nsl` of the workgroup's rows [r0, r1) of both histories, thread t0 of D5_SHIFT_T
+__device__ __forceinline__ void shift_slice(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int t0) {
+#ifdef T1_WHATIF_D5_NO_SHIFT  // timing-only what-if build: the history is not shifted
+  return;
+#endif
+  if (r1 <= r0) return;
+  const uint32_t rows = (uint32_t)(r1 - r0);
+  if (S.half) {
+    const uint32_t no = (rows * (T1_NOBS * T1_HIST) + 7) / 8, np = (rows * (T1_NPRIV * T1_CHIST) + 7) / 8;
+    shift_window_f16<T1_NOBS, T1_HIST, T1_D5_SHIFT_UNROLL>(reinterpret_cast<const uint16_t*>(S.obs_in),
+                                                           reinterpret_cast<uint16_t*>(S.obs_out), S.total_obs, r0, r1,
+                                                           no * sl / nsl, no * (sl + 1) / nsl, t0, D5_SHIFT_T);
+    shift_window_f16<T1_NPRIV, T1_CHIST, T1_D5_SHIFT_UNROLL>(reinterpret_cast<const uint16_t*>(S.priv_in),
+                                                             reinterpret_cast<uint16_t*>(S.priv_out), S.total_priv, r0,
+                                                             r1, np * sl / nsl, np * (sl + 1) / nsl, t0, D5_SHIFT_T);
+    return;
+  }
+  const uint32_t no = (rows * (T1_NOBS * T1_HIST) + 3) / 4, np = (rows * (T1_NPRIV * T1_CHIST) + 3) / 4;
+  shift_window_f32<T1_NOBS, T1_HIST, T1_D5_SHIFT_UNROLL>(S.obs_in, S.obs_out, S.total_obs, r0, r1, no * sl / nsl,
+                                                         no * (sl + 1) / nsl, t0, D5_SHIFT_T);
+  shift_window_f32<T1_NPRIV, T1_CHIST, T1_D5_SHIFT_UNROLL>(S.priv_in, S.priv_out, S.total_priv, r0, r1, np * sl / nsl,
+                                                           np * (sl + 1) / nsl, t0, D5_SHIFT_T);
+}
+
+// ---- the same shift with its loads issued before S2 (after the wave's role work, so its registers are free) and its
+// stores after S2: the load latency is spent in the S2 wait instead of on the critical post-S2 window.  One batch of
+// U chunks per thread and history per substep (32 rows x 3102 fp32 = 24,816 chunks over 10 substeps x 192 threads:
+// 13); chunks past the batch (never with 32-row workgroups and 10 substeps) go through the windowed loop.
+template <int U> struct ShiftPre {
+  u32x4 a[U], b[U];      // the two 16-B source chunks of each output chunk (fp32 or fp16 bits)
+  u32x4 pa, pb;          // the critic history's chunk (one per thread and substep)
+  uint32_t olo, ohi, plo, phi;  // this substep's chunk windows of the two histories
+};
+template <int F, int H>
+__device__ __forceinline__ uint32_t shift_nchunks(int64_t total, int64_t r0, int64_t r1, int per) {
+  const uint32_t ROW = F * H;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW), span = (uint32_t)((r1 - r0) * ROW);
+  return ((span < lim ? span : lim) + per - 1) / per;
+}
+// source chunk loads of output chunk c of the rows' range (16-B chunks of `per` elements, element size es)
+template <int F, int H>
+__device__ __forceinline__ void shift_src_ld(const uint8_t* in, int64_t total, int64_t r0, uint32_t c, int per, int es,
+                                             u32x4& a, u32x4& b) {
+  const uint32_t ROW = F * H;
+  const uint8_t* in0 = in + (size_t)(r0 * ROW) * es;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
+  const uint32_t sa = (c * per + F) & ~(uint32_t)(per - 1);
+  const uint32_t sc = sa + 2 * per <= lim ? sa : (lim - 2 * per) & ~(uint32_t)(per - 1);  // tail: in-bounds dummy
+  a = *reinterpret_cast<const u32x4*>(in0 + (size_t)sc * es);
+  b = *reinterpret_cast<const u32x4*>(in0 + (size_t)(sc + per) * es);
+}
+// the stores of output chunk c from its loaded source chunks (fp32: per = 4; fp16: per = 8)
+template <int F, int H, bool HALF>
+__device__ __forceinline__ void shift_chunk_st(const void* inv, void* outv, int64_t total, int64_t r0, uint32_t c,
+                                               u32x4 a, u32x4 b) {
+  constexpr uint32_t ROW = F * H;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
+  if constexpr (!HALF) {
+    const float* in0 = reinterpret_cast<const float*>(inv) + r0 * ROW;
+    float* out0 = reinterpret_cast<float*>(outv) + r0 * ROW;
+    const uint32_t i = c * 4, sidx = i + F, sa = sidx & ~3u;
+    float4 x = __builtin_bit_cast(float4, a), y = __builtin_bit_cast(float4, b);
+    if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
+      float t[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
+      x = make_float4(t[0], t[1], t[2], t[3]);
+      y = make_float4(t[4], t[5], t[6], t[7]);
+    }
+    const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    const int rem = (int)(sidx - sa);
+    const uint32_t col0 = i - (i / ROW) * ROW;
+    if (col0 + 3 < ROW - F && i + 3 < lim) {
+      *reinterpret_cast<float4*>(out0 + i) = make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]);
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t e = i + k;
+      if (e >= lim) break;
+      if (e - (e / ROW) * ROW < ROW - F) out0[e] = src[rem + k];
+    }
+  } else {
+    constexpr uint32_t REM = F % 8, MM = REM / 2;
+    const uint16_t* in0 = reinterpret_cast<const uint16_t*>(inv) + r0 * ROW;
+    uint16_t* out0 = reinterpret_cast<uint16_t*>(outv) + r0 * ROW;
+    const uint32_t i = c * 8, sa = (i + F) & ~7u;
+    uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if (sa + 16 > lim) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t lo = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
+        const uint32_t hh = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
+        w[k] = lo | (hh << 16);
+      }
+    }
+    u32x4 o;
+    if constexpr (REM % 2 == 0) {
+      o = u32x4{w[MM], w[MM + 1], w[MM + 2], w[MM + 3]};
+    } else {
+      o = u32x4{__builtin_amdgcn_alignbyte(w[MM + 1], w[MM], 2), __builtin_amdgcn_alignbyte(w[MM + 2], w[MM + 1], 2),
+                __builtin_amdgcn_alignbyte(w[MM + 3], w[MM + 2], 2), __builtin_amdgcn_alignbyte(w[MM + 4], w[MM + 3], 2)};
+    }
+    const uint32_t col0 = i - (i / ROW) * ROW;
+    if (col0 + 7 < ROW - F && i + 7 < lim) {
+      *reinterpret_cast<u32x4*>(out0 + i) = o;
+      return;
+    }
+    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t e = i + k;
+      if (e >= lim) break;
+      if (e - (e / ROW) * ROW < ROW - F) out0[e] = (uint16_t)(ow[k / 2] >> (16 * (k & 1)));
+    }
+  }
+}
+template <int U>
+__device__ __forceinline__ void shift_pre_issue(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int t0,
+                                                ShiftPre<U>& P) {
+  const int per = S.half ? 8 : 4, es = S.half ? 2 : 4;
+  const uint32_t no = r1 > r0 ? shift_nchunks<T1_NOBS, T1_HIST>(S.total_obs, r0, r1, per) : 0u;
+  const uint32_t np = r1 > r0 ? shift_nchunks<T1_NPRIV, T1_CHIST>(S.total_priv, r0, r1, per) : 0u;
+  P.olo = no * sl / nsl; P.ohi = no * (sl + 1) / nsl;
+  P.plo = np * sl / nsl; P.phi = np * (sl + 1) / nsl;
+#ifdef T1_WHATIF_D5_NO_SHIFT  // timing-only what-if build: the history is not shifted
+  P.ohi = P.olo; P.phi = P.plo;
+#endif
+  const uint8_t* oi = reinterpret_cast<const uint8_t*>(S.obs_in);
+  const uint8_t* pi = reinterpret_cast<const uint8_t*>(S.priv_in);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = P.olo + t0 + u * D5_SHIFT_T;
+    if (P.olo + u * D5_SHIFT_T < P.ohi)  // wave-uniform guard; lanes past the window load an in-bounds dummy
+      shift_src_ld<T1_NOBS, T1_HIST>(oi, S.total_obs, r0, c < P.ohi ? c : P.olo, per, es, P.a[u], P.b[u]);
+  }
+  if (P.plo < P.phi) {
+    const uint32_t c = P.plo + t0;
+    shift_src_ld<T1_NPRIV, T1_CHIST>(pi, S.total_priv, r0, c < P.phi ? c : P.plo, per, es, P.pa, P.pb);
+  }
+}
+template <bool HALF, int U>
+__device__ __forceinline__ void shift_pre_commit_t(const ShiftArgs& S, int64_t r0, int64_t r1, int t0, const ShiftPre<U>& P) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = P.olo + t0 + u * D5_SHIFT_T;
+    if (c < P.ohi) shift_chunk_st<T1_NOBS, T1_HIST, HALF>(S.obs_in, S.obs_out, S.total_obs, r0, c, P.a[u], P.b[u]);
+  }
+  if (P.plo + t0 < P.phi)
+    shift_chunk_st<T1_NPRIV, T1_CHIST, HALF>(S.priv_in, S.priv_out, S.total_priv, r0, P.plo + t0, P.pa, P.pb);
+  // chunks past the batch (a window larger than U x D5_SHIFT_T / D5_SHIFT_T): one at a time
+  const int per = HALF ? 8 : 4, es = HALF ? 2 : 4;
+  for (uint32_t c = P.olo + t0 + U * D5_SHIFT_T; c < P.ohi; c += D5_SHIFT_T) {
+    u32x4 a, b;
+    shift_src_ld<T1_NOBS, T1_HIST>(reinterpret_cast<const uint8_t*>(S.obs_in), S.total_obs, r0, c, per, es, a, b);
+    shift_chunk_st<T1_NOBS, T1_HIST, HALF>(S.obs_in, S.obs_out, S.total_obs, r0, c, a, b);
+  }
+  for (uint32_t c = P.plo + t0 + D5_SHIFT_T; c < P.phi; c += D5_SHIFT_T) {
+    u32x4 a, b;
+    shift_src_ld<T1_NPRIV, T1_CHIST>(reinterpret_cast<const uint8_t*>(S.priv_in), S.total_priv, r0, c, per, es, a, b);
+    shift_chunk_st<T1_NPRIV, T1_CHIST, HALF>(S.priv_in, S.priv_out, S.total_priv, r0, c, a, b);
+  }
+}
+template <int U>
+__device__ __forceinline__ void shift_pre_commit(const ShiftArgs& S, int64_t r0, int64_t r1, int t0, const ShiftPre<U>& P) {
+  if (S.half) shift_pre_commit_t<true>(S, r0, r1, t0, P);
+  else shift_pre_commit_t<false>(S, r0, r1, t0, P);
+}
+#ifndef T1_D5_PRE_U
+#define T1_D5_PRE_U 13
+#endif
+
+// ---------------------------------------------------------------------------------------------------
+// k_dyn5.  Lane l of every wave: env blockIdx.x * 32 + (l & 31), leg l >> 5.  Inactive lanes (past num_envs) shadow
+// the last env and store nothing.  The substep log (tests only, LG.root != nullptr) is a run-time switch of the one
+// product code object, like k_dyn4's.
+// ---------------------------------------------------------------------------------------------------
+template <bool HF, bool FUSED>
+__global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ Mg, const t1env_config* __restrict__ Cp,
+                                                   t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
+                                                   t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA,
+                                                   SubLog LG) {
+  __shared__ Dyn5Lds lds;
+  {  // the model to LDS
+    constexpr int NW = (int)(sizeof(DynModel) / 4);
+    static_assert(sizeof(DynModel) % 4 == 0, "the model copies as words");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(Mg);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&lds.model);
+    for (int i = threadIdx.x; i < NW; i += D5_BLOCK) dst[i] = src[i];
+  }
+  Terrain T = Tin;
+  T.type = HF ? 2 : 0;
+  const t1env_config& C = *Cp;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / 64);
+  const int lane = threadIdx.x & 63;
+  const int leg = lane >> 5;
+  const int e = lane & 31;
+  const int j0 = 6 * leg;
+  const int N = C.num_envs;
+  const int n0 = (int)blockIdx.x * NE5 + e;
+  const bool active = n0 < N;
+  const int n = active ? n0 : N - 1;
+  const float dt = C.sim_dt;
+  const uint32_t ctr = A.counter;
+  const int nsub = C.decimation;
+  const int64_t r0 = (int64_t)blockIdx.x * NE5, r1 = r0 + NE5 < N ? r0 + NE5 : N;
+  T1_PROF_BEGIN();
+  __syncthreads();  // the model in LDS
+  const DynModel& M = lds.model;
+
+  if (wave == 1) {
+    // ---------------- W1: bias, PD torques, base block, base-box contacts
+    BaseParams<float> PB;
+    LegParams<float> PL;
+    load_base_params(M, B, n, PB);
+    load_leg_params(M, B, n, j0, PL);
+    {  // actions = clip(actions) into the step's history slot (this wave owns the action ring), PD constants staged
+      PdStage<64>& P = lds.pd;
+      float a[NLEG];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) a[k] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
+      const int cs = (int)(ctr & 3u);
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) {
+        const int j = j0 + k;
+        P.kp[k][lane] = B.kp[n * 12 + j];
+        P.kd[k][lane] = B.kd[n * 12 + j];
+        P.off[k][lane] = B.motor_offsets[n * 12 + j];
+        P.visc[k][lane] = B.viscous[n * 12 + j];
+        P.coul[k][lane] = B.coulomb[n * 12 + j];
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k)
+          P.act[s][k][lane] = s == cs ? a[k] * C.action_scale : B.act_hist[((size_t)n * 4 + s) * 12 + j0 + k];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) lds.act[j0 + k][e] = a[k];
+      if (active) {
+        float* slot = B.act_hist + ((size_t)n * 4 + cs) * 12;
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) {
+          B.actions[n * 12 + j0 + k] = a[k];
+          slot[j0 + k] = a[k] * C.action_scale;
+        }
+      }
+    }
+    const int lag = B.lag_timestep[n];
+    const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
+    const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
+    const float mu = PB.friction, eg = ground_restitution(M, PB.restitution);
+    float vi_b = B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)];
+    int cb, ce;
+    base_contact_range(M, leg, cb, ce);
+    T1_PROF_MARK(0);
+    for (int sub = 0; sub < nsub; ++sub) {
+      __syncthreads();  // S1: the substep state published
+      T1_PROF_MARK(1);
+      BaseState<float> sb;
+      float q[NLEG], qd[NLEG], tau[NLEG];
+      read_state(lds, lane, sb, q, qd);
+      BaseFrame<float> F;
+      base_frame(sb, F);
+      const int32_t bound_b = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
+      pd_torques_staged(M, C, lds.pd, lane, K, ctr, sub, lag, j0, q, qd, tau);
+      T1_PROF_MARK(2);
+      float v[B_N];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) v[B_TAU + k] = tau[k];
+      {
+        float rg[NLEG], G[6];
+        leg_bias_rhs(M, PL, F, q, qd, tau, leg, dt, rg, G);
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) v[B_RG + k] = rg[k];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[B_G + i] = G[i];
+      }
+      T1_PROF_MARK(3);
+      {  // base block + the base-box halves (left first, the same sum in both halves)
+        Sym6<float> Ac, Cb;
+        float r[6], gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
+        sym_zero(Cb);
+        body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - M.contact_radius[0], bound_b, cb, F.R0,
+                                                   v3<float>(0, 0, 0), F.abs, F.V0, mu, eg, vi_b, dt, Cb, gw);
+#pragma unroll
+        for (int i = 0; i < 21; ++i) {
+          float l, rr;
+          halves(Cb.a[i], l, rr);
+          v[B_AC + i] = (Ac.a[i] + l) + rr;
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          float l, rr;
+          halves(gw[i], l, rr);
+          v[B_R + i] = (-r[i] - l) - rr;
+        }
+      }
+      T1_PROF_MARK(4);
+      put4(lds.w1, lane, v);
+      T1_PROF_MARK(5);
+#ifdef T1_D5_SHIFT_PRE
+      ShiftPre<T1_D5_PRE_U> sp;
+      shift_pre_issue(S, r0, r1, sub, nsub, (int)threadIdx.x - 64, sp);
+#endif
+      __syncthreads();  // S2: the terms published
+      T1_PROF_MARK(6);
+#ifdef T1_D5_SHIFT_PRE
+      shift_pre_commit(S, r0, r1, (int)threadIdx.x - 64, sp);
+#else
+      shift_slice(S, r0, r1, sub, nsub, (int)threadIdx.x - 64);
+#endif
+      T1_PROF_MARK(7);
+    }
+    lds.vib[lane] = vi_b;
+    if (active) B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)] = vi_b;
+    __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
+    __syncthreads();  // R1
+    T1_PROF_MARK(9);
+    if constexpr (FUSED) {
+      __syncthreads();  // the epilogue barrier
+      T1_PROF_MARK(11);
+      fused_epilogue_staged<POST_A_STATE, NE5, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
+                                                     lds.act + NLEG);
+    }
+    T1_PROF_END();
+    return;
+  }
+
+  if (wave >= 2) {
+    // ---------------- W2: terrain contacts of the shank and foot / W3: self-contacts
+    const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // robot shape vs ground (PhysX average)
+    const float mu_self = B.friction[n];                          // robot shape vs robot shape
+    const float eg = ground_restitution(M, B.restitution[n]);
+    float vi_sh = 0.0f, vi_ft = 0.0f;
+    if (wave == 2) {
+      vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
+      vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
+    }
+    // the epilogue's inputs the step does not change, staged while W0 sets up (nothing writes them before the epilogue)
+    if constexpr (FUSED) stage_epilogue_inputs<NE5, 128>(B, N, (int)r0, (int)threadIdx.x - 128, lds.epi);
+    const int bsh = 1 + 6 * leg + K_SHANK, bft = 1 + 6 * leg + K_FOOT;
+    T1_PROF_MARK(0);
+    for (int sub = 0; sub < nsub; ++sub) {
+      __syncthreads();  // S1
+      T1_PROF_MARK(1);
+      BaseState<float> sb;
+      float q[NLEG], qd[NLEG];
+      read_state(lds, lane, sb, q, qd);
+      BaseFrame<float> F;
+      base_frame(sb, F);
+      BodyKin<float> Ko[2];
+      leg_body_kinematics(M, F, q, qd, leg, Ko);
+      T1_PROF_MARK(2);
+      Sym6<float> Cs[2];
+      float cs[2][6];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        sym_zero(Cs[i]);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) cs[i][j] = 0.0f;
+      }
+      if (wave == 2) {
+        const int32_t bnd = terrain_bound_raw_any(T, Ko[0].p.x + F.abs.x, Ko[0].p.y + F.abs.y);
+        body_contact_fixed<T1_POINTS_PER_BODY>(M, T, Ko[0].p.z + F.abs.z - M.contact_radius[bsh], bnd,
+                                               M.contact_start[bsh], Ko[0].Rb, Ko[0].p, F.abs, Ko[0].V, mu, eg, vi_sh,
+                                               dt, Cs[0], cs[0]);
+        T1_PROF_MARK(3);
+        body_contact_query_apply<T1_POINTS_PER_BODY>(M, T, M.contact_start[bft], Ko[1].Rb, Ko[1].p, F.abs, Ko[1].V, mu,
+                                                     eg, vi_ft, dt, Cs[1], cs[1], [] {});
+        T1_PROF_MARK(4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          float v[XCH];
+          sym_pack(Cs[i], cs[i], v);
+          put4(lds.w2[i], lane, v);
+        }
+      } else {
+        if (M.self_collisions) {
+          SelfBody<float> O[2], X[2];
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            O[s] = self_body(M, leg, s, Ko[s]);
+            const float mine[12] = {O[s].cap.p.x, O[s].cap.p.y, O[s].cap.p.z, O[s].cap.q.x, O[s].cap.q.y,
+                                    O[s].cap.q.z, O[s].V[0],    O[s].V[1],    O[s].V[2],    O[s].V[3],
+                                    O[s].V[4],    O[s].V[5]};
+            float oth[12];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+              float l, r;
+              halves(mine[i], l, r);
+              oth[i] = leg ? l : r;
+            }
+            X[s].cap.p = v3<float>(oth[0], oth[1], oth[2]);
+            X[s].cap.q = v3<float>(oth[3], oth[4], oth[5]);
+            X[s].cap.r = M.self_cap[1 - leg][s].r;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) X[s].V[i] = oth[6 + i];
+          }
+          T1_PROF_MARK(3);
+          self_terms_bodies(M, leg, O, X, mu_self, dt, Cs, cs);
+          T1_PROF_MARK(4);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          float v[XCH];
+          sym_pack(Cs[i], cs[i], v);
+          put4(lds.w3[i], lane, v);
+        }
+      }
+      T1_PROF_MARK(5);
+#ifdef T1_D5_SHIFT_PRE
+      ShiftPre<T1_D5_PRE_U> sp;
+      shift_pre_issue(S, r0, r1, sub, nsub, (int)threadIdx.x - 64, sp);
+#endif
+      __syncthreads();  // S2
+      T1_PROF_MARK(6);
+#ifdef T1_D5_SHIFT_PRE
+      shift_pre_commit(S, r0, r1, (int)threadIdx.x - 64, sp);
+#else
+      shift_slice(S, r0, r1, sub, nsub, (int)threadIdx.x - 64);
+#endif
+      T1_PROF_MARK(7);
+    }
+    if (wave == 2) {
+      lds.vis[0][lane] = vi_sh;
+      lds.vis[1][lane] = vi_ft;
+      if (active) {
+        B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
+        B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)] = vi_ft;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
+    __syncthreads();  // R1: the end-of-step state and episodes published
+    T1_PROF_MARK(9);
+    if (wave == 3) {  // the contact-force report (terrain + self) from the end-of-step state
+      BaseState<float> sb;
+      float q[NLEG], qd[NLEG];
+      read_state(lds, lane, sb, q, qd);
+      BaseFrame<float> F;
+      base_frame(sb, F);
+      BodyKin<float> Ko[2];
+      leg_body_kinematics(M, F, q, qd, leg, Ko);
+      V3<float> fself[2] = {v3<float>(0.0f, 0.0f, 0.0f), v3<float>(0.0f, 0.0f, 0.0f)};
+      if (M.self_collisions) {
+        SelfBody<float> O[2], X[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          O[s] = self_body(M, leg, s, Ko[s]);
+          const float mine[12] = {O[s].cap.p.x, O[s].cap.p.y, O[s].cap.p.z, O[s].cap.q.x, O[s].cap.q.y, O[s].cap.q.z,
+                                  O[s].V[0],    O[s].V[1],    O[s].V[2],    O[s].V[3],    O[s].V[4],    O[s].V[5]};
+          float oth[12];
+#pragma unroll
+          for (int i = 0; i < 12; ++i) {
+            float l, r;
+            halves(mine[i], l, r);
+            oth[i] = leg ? l : r;
+          }
+          X[s].cap.p = v3<float>(oth[0], oth[1], oth[2]);
+          X[s].cap.q = v3<float>(oth[3], oth[4], oth[5]);
+          X[s].cap.r = M.self_cap[1 - leg][s].r;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) X[s].V[i] = oth[6 + i];
+        }
+        self_forces_bodies(M, leg, O, X, mu_self, fself);
+      }
+      const float vt[3] = {restitution_target(M, eg, lds.vis[0][lane]), restitution_target(M, eg, lds.vis[1][lane]),
+                           restitution_target(M, eg, lds.vib[lane])};
+      const float vt_o = restitution_target(M, eg, lds.vib[lane ^ 32]);  // the other base half (leg 0 reports)
+      const float vt_base = vt_o > vt[2] ? vt_o : vt[2];
+      helper_report_contacts_at<NE5>(M, T, B, F, Ko, fself, n, leg, mu, vt, vt_base, e, active,
+                                     FUSED ? lds.fr : nullptr);
+      T1_PROF_MARK(10);
+    }
+    if constexpr (FUSED) __syncthreads();  // the epilogue barrier
+    T1_PROF_MARK(11);
+    T1_PROF_END();
+    return;
+  }
+
+  // ---------------- W0: core
+  BaseParams<float> PB;
+  LegParams<float> PL;
+  BaseState<float> sb;
+  float q[NLEG], qd[NLEG];
+  load_base_params(M, B, n, PB);
+  load_leg_params(M, B, n, j0, PL);
+  load_base_state(M, PB, B.root_states + (size_t)n * 13, sb);
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
+    qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
+  }
+  int s_dof = 9 - B.dof_lag_timestep[n] % 10;
+#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
+  s_dof = s_dof > 0 ? s_dof - 1 : 0;
+#endif
+  const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
+  float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
+  float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
+  float tau[NLEG];
+  {
+    float v[Q_N];
+    state_pack(sb, q, qd, v);
+    put4(lds.st, lane, v);
+  }
+  T1_PROF_MARK(0);
+  for (int sub = 0; sub < nsub; ++sub) {
+    __syncthreads();  // S1: the substep state published
+    T1_PROF_MARK(1);
+    BaseFrame<float> F;
+    base_frame(sb, F);
+    LegFK<float> fk;
+    leg_fk_chain(M, F.R0, q, leg, fk);
+    T1_PROF_MARK(2);
+    float Sj[NLEG][6];
+    LegBlock<float> lb;
+    Sym6<float> Ab;
+    sym_zero(Ab);
+    leg_backward_crba(M, PL, q, qd, leg, dt, fk, Sj, lb, Ab);
+    T1_PROF_MARK(3);
+    __syncthreads();  // S2: W1-W3's terms published
+    T1_PROF_MARK(4);
+    float g6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    float w1v[B_N];
+    get4(lds.w1, lane, w1v);
+    {
+      float rg[NLEG], G[6];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { tau[k] = w1v[B_TAU + k]; rg[k] = w1v[B_RG + k]; }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) G[i] = w1v[B_G + i];
+      Sym6<float> Cb[2];
+      float cb[2][6];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // terrain + self terms of the shank [0] and foot [1]
+        float vt[XCH], vs[XCH];
+        get4(lds.w2[i], lane, vt);
+        get4(lds.w3[i], lane, vs);
+#pragma unroll
+        for (int k = 0; k < XCH; ++k) vt[k] += vs[k];
+        sym_unpack(vt, Cb[i], cb[i]);
+      }
+      leg_apply_terms<K_SHANK, K_FOOT>(Cb[0], cb[0], Cb[1], cb[1], rg, G, Sj, lb, Ab, g6);
+    }
+    T1_PROF_MARK(5);
+    float rb[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rb[i] = -g6[i];
+    eliminate_leg(lb, Ab, rb);
+    T1_PROF_MARK(6);
+    // the base system: W1's base block (with both base-box halves) + the left leg + the right leg, in every lane
+    Sym6<float> Ac;
+    float r[6];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) {
+      float l, rr;
+      halves(Ab.a[i], l, rr);
+      Ac.a[i] = (w1v[B_AC + i] + l) + rr;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      float l, rr;
+      halves(rb[i], l, rr);
+      r[i] = (w1v[B_R + i] + l) + rr;
+    }
+    solve_base(Ac, r);
+    float dq[NLEG];
+    backsub_leg(lb, r, dq);
+    integrate_base(sb, r, dt);
+    integrate_leg(M, leg, q, qd, dq, dt);
+    T1_PROF_MARK(7);
+    if (LG.root != nullptr) {  // wave-uniform (a kernel argument)
+      if (active) {
+        const size_t row = (size_t)sub * N + n;
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) {
+          LG.torque[row * 12 + j0 + k] = tau[k];
+          LG.dof[row * 24 + 2 * (j0 + k)] = q[k];
+          LG.dof[row * 24 + 2 * (j0 + k) + 1] = qd[k];
+        }
+        if (leg == 0) {
+          BaseFrame<float> FL;
+          base_frame(sb, FL);
+          float body[13];
+          root_row(M, PB, sb, FL, body);
+#pragma unroll
+          for (int i = 0; i < 13; ++i) LG.root[row * 13 + i] = body[i];
+        }
+      }
+    }
+    if (sub == s_dof) {
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { lds.cap[k][lane] = q[k]; lds.cap[NLEG + k][lane] = qd[k]; }
+    }
+    if (leg == 0 && sub == s_imu) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lds.cap[2 * NLEG + i][lane] = sb.quat[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) lds.cap[2 * NLEG + 4 + i][lane] = sb.w[i];
+    }
+    float v[Q_N];
+    state_pack(sb, q, qd, v);
+    put4(lds.st, lane, v);  // W1-W3 read the previous state before S2; after the last substep: the report's
+    T1_PROF_MARK(8);
+  }
+  if (active) {
+    if (s_dof < nsub) {  // the sensor-lag samples captured in the loop
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { dof_dst[j0 + k] = lds.cap[k][lane]; dof_dst[12 + j0 + k] = lds.cap[NLEG + k][lane]; }
+    }
+    if (leg == 0 && s_imu < nsub) {
+      const float quat[4] = {lds.cap[2 * NLEG][lane], lds.cap[2 * NLEG + 1][lane], lds.cap[2 * NLEG + 2][lane],
+                             lds.cap[2 * NLEG + 3][lane]};
+      const float w[3] = {lds.cap[2 * NLEG + 4][lane], lds.cap[2 * NLEG + 5][lane], lds.cap[2 * NLEG + 6][lane]};
+      capture_imu(quat, w, imu_dst);
+    }
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
+      B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
+      B.torques[n * 12 + j0 + k] = tau[k];
+    }
+  }
+  float (*FR)[NE5] = FUSED ? lds.fr : nullptr;
+  if constexpr (FUSED) {
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      lds.fr[F_DOF + 2 * (j0 + k)][e] = q[k];
+      lds.fr[F_DOF + 2 * (j0 + k) + 1][e] = qd[k];
+      lds.fr[F_TQ + j0 + k][e] = tau[k];
+    }
+  }
+  __syncthreads();  // R1: the end-of-step state published (W3 computes the contact forces meanwhile)
+  T1_PROF_MARK(9);
+  {
+    BaseFrame<float> F;
+    base_frame(sb, F);
+    leg_report_rigid<NE5>(M, B, PB, sb, F, q, qd, n, leg, active, e, FR);
+  }
+  T1_PROF_MARK(10);
+  if constexpr (FUSED) {
+    __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
+    T1_PROF_MARK(11);
+    fused_epilogue_staged<POST_A_REWARDS, NE5, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
+                                                     lds.act + NLEG);
+  }
+  T1_PROF_END();
+}
+
+#ifdef T1_PHASE_PROF
+// profiling build only: summed clock deltas per [wave][bucket] since the last reset
+extern "C" int t1env_debug_phase_cycles5(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_prof5), sizeof(g_t1_prof5));
+  if (e == hipSuccess && reset) {
+    static const unsigned long long zero[T1_PROF_WAVES5][T1_NPROF5] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_t1_prof5), zero, sizeof(zero));
+  }
+  return (int)e;
+}
+#endif
+
+int t1_launch_dyn5(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
+                   const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
+                   const FusedArgs* fused, hipStream_t s, const SubLog* log) {
+  const int blocks = (num_envs + NE5 - 1) / NE5;
+  const FusedArgs FA = fused ? *fused : FusedArgs{};
+  const SubLog LG = log ? *log : SubLog{};
+  const bool hf = T.type != 0;
+  if (log && !fused) return (int)hipErrorInvalidValue;  // the substep log: fused steps only (the caller checks)
+#define T1_LAUNCH5(HF, FU) \
+  hipLaunchKernelGGL((k_dyn5<HF, FU>), dim3(blocks), dim3(D5_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, blocks, FA, LG)
+  if (fused) { if (hf) T1_LAUNCH5(true, true); else T1_LAUNCH5(false, true); }
+  else { if (hf) T1_LAUNCH5(true, false); else T1_LAUNCH5(false, false); }
+#undef T1_LAUNCH5
+  return (int)hipGetLastError();
+}

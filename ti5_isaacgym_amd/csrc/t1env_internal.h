@@ -34,7 +34,8 @@ constexpr int T1_SHIFT_DELAY_DEFAULT = 3000;
 
 // launch shape of the dynamics kernel
 struct DynLaunch {
-  int waves;         // 4: k_dyn4 (leg waves + contact helper waves; the only kernel since round 3)
+  int waves;         // 5: k_dyn5 (t1env_dyn5.hip: 32 envs per workgroup, four roles, in-workgroup history shift; the
+                     //    default), 4: k_dyn4 (64 envs per workgroup, leg + contact helper waves; T1ENV_DYN_KERNEL=4)
   int cus;           // compute units of the device (default history-shift grid)
   int shift_blocks;  // > 0: history-shift workgroups override (tuning)
   int shift_delay;   // in-launch shift workgroups start this many 100 MHz ticks late (T1ENV_SHIFT_DELAY; 0 = at once)
@@ -52,3 +53,7 @@ int t1_launch_dynamics(const t1::DynModel* d_model, const t1env_config* d_cfg, c
 // per CU for k_dyn4: 148 KB of LDS) leave fewer than MIN_SHIFT_BLOCKS CUs idle, and shift workgroups of the
 // dynamics launch would each hold a whole CU's LDS for a small slice of the 26 KB/env stream.
 bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg);
+// k_dyn5 (t1env_dyn5.hip): the same contract as t1_launch_dynamics; each workgroup shifts its own history rows
+int t1_launch_dyn5(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const t1::Terrain& T,
+                   const float* actions, const t1env_step_args& A, int num_envs, const t1::ShiftArgs& S,
+                   const FusedArgs* fused, hipStream_t s, const SubLog* log);

@@ -38,6 +38,18 @@ HELPER_SUB = {16: "contacts: transforms + height queries (issue)", 17: "contacts
               21: "self-collision terms"}
 NB = len(BUCKETS)
 NW = 4
+# k_dyn5 (t1env_dyn5.hip): per-role mark meanings (ids 13-15 epilogue and 16-23 sub-marks as above)
+D5 = {
+    0: ["prologue", "S1 wait", "forward chain (poses)", "CRBA backward pass", "S2 wait", "LDS reads + fold-in",
+        "elimination", "base system + solve + backsub + integrate", "log / captures / publish", "stores + R1 wait",
+        "rigid report", "epilogue barrier"],
+    1: ["prologue (actions, PD stage)", "S1 wait", "state + PD torques", "RNEA bias + rhs", "base block + base box",
+        "publish", "S2 wait", "history shift slice", "-", "R1 wait", "-", "epilogue barrier"],
+    2: ["prologue + epilogue staging", "S1 wait", "state + kinematics", "shank terrain", "foot terrain", "publish",
+        "S2 wait", "history shift slice", "-", "R1 wait", "-", "epilogue barrier"],
+    3: ["prologue + epilogue staging", "S1 wait", "state + kinematics", "capsule exchange", "self-contact terms",
+        "publish", "S2 wait", "history shift slice", "-", "R1 wait", "contact-force report", "epilogue barrier"],
+}
 
 
 def main():
@@ -48,6 +60,7 @@ def main():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--split", action="store_true", help="time the split path (k_dynamics without epilogue)")
     p.add_argument("--no-self-collision", action="store_true", help="asset.self_collisions = 1 (A/B)")
+    p.add_argument("--kernel", type=int, default=5, choices=[4, 5], help="k_dyn5 (default) or k_dyn4")
     a = p.parse_args()
     sys.path.insert(0, REPO)
     if a.build:
@@ -55,6 +68,7 @@ def main():
         print(build.build(force=True, extra=["-DT1_PHASE_PROF"], out=PROF_LIB))
         return
     os.environ["T1ENV_LIB"] = PROF_LIB
+    os.environ["T1ENV_DYN_KERNEL"] = str(a.kernel)
     import torch
     from ti5_isaacgym_amd import make_t1_env
     def hook(cfg):
@@ -70,26 +84,33 @@ def main():
     for i in range(50):
         env.step(acts[i % 8])
     torch.cuda.synchronize()
-    assert lib.t1env_debug_phase_cycles(buf, 1) == 0
+    read = lib.t1env_debug_phase_cycles5 if a.kernel == 5 else lib.t1env_debug_phase_cycles
+    assert read(buf, 1) == 0
     env.set_timing(True)
     for i in range(a.steps):
         env.step(acts[i % 8])
     torch.cuda.synchronize()
     t = env.get_timing()
     env.set_timing(False)
-    assert lib.t1env_debug_phase_cycles(buf, 0) == 0
+    assert read(buf, 0) == 0
     kern_us = t["k_dynamics"]["ms"] / max(1, t["k_dynamics"]["launches"]) * 1e3
-    waves = (a.num_envs + 63) // 64
+    waves = (a.num_envs + 63) // 64 if a.kernel == 4 else (a.num_envs + 31) // 32
     print(f"k_dynamics {kern_us:.1f} us/launch (events), {a.mesh}, {a.num_envs} envs, {a.steps} steps, "
           f"{'split' if a.split else 'fused'}")
-    four = os.environ.get("T1ENV_DYN_WAVES", "4") != "2"
-    names = BUCKETS4 if four else BUCKETS
+    four = True
+    names = BUCKETS4
     roles = ["left leg", "right leg", "left contact helper", "right contact helper"]
-    for w in range(4 if four else 2):
+    if a.kernel == 5:
+        roles = ["W0 core", "W1 bias", "W2 terrain", "W3 self"]
+    for w in range(4):
         cyc = [buf[w * NB + i] / (waves * a.steps) for i in range(NB)]
         tot = sum(cyc)
         print(f"wave {w} ({roles[w]}): {tot:.0f} cycles/launch")
-        wn = [HELPER_SUB.get(i, nm) if (four and w >= 2) else nm for i, nm in enumerate(names)]
+        if a.kernel == 5:
+            wn = [D5[w][i] if i < len(D5[w]) else (HELPER_SUB.get(i, nm) if w >= 2 else nm)
+                  for i, nm in enumerate(names)]
+        else:
+            wn = [HELPER_SUB.get(i, nm) if (four and w >= 2) else nm for i, nm in enumerate(names)]
         for name, c in sorted(zip(wn, cyc), key=lambda x: -x[1]):
             if c > 0:
                 print(f"   {name:34s} {c:10.0f} cyc  {100 * c / tot:5.1f}%  ~{kern_us * c / tot:6.1f} us")
