@@ -5,9 +5,10 @@ num_envs_total = world N).  Every random draw is keyed by the global env id, ter
 (`terrain_types = floor(i / (N_total / 20))`, legged_robot.py:1490) and the one cross-env quantity of the step, the
 command-curriculum mean (legged_robot.py:1160-1169), is all-reduced (T1DHStandEnv._command_curriculum).
 tests/test_sharding.py checks those semantics on the CPU oracle; here the HIP kernels themselves run sharded: two
-`gloo` ranks on cuda:0, each with its own HIP env of N envs, and one unsharded 2N-env HIP env in the test process,
-all stepped with the same actions through terrain-curriculum resets and a command-curriculum step that only the
-global mean widens.  obs, priv, rew, reset, time-out, terrain levels, origins, commands, root / dof state and
+`gloo` ranks on cuda:0, each with its own HIP env of N envs, and one unsharded HIP env of all the ranks' envs in the test
+process, all stepped with the same actions through terrain-curriculum resets and a command-curriculum step that only
+the global mean widens.  Two layouts: 2 x 2048 envs, and config 4's own 8 x 8192 (global ids up to 65,535, terrain
+types spanning the eight shards).  obs, priv, rew, reset, time-out, terrain levels, origins, commands, root / dof state and
 episode lengths must be BIT-identical row for row, and all three must end with the same command ranges.
 """
 import os
@@ -19,7 +20,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-N_PER_RANK, WORLD, STEPS = 2048, 2, 5
+STEPS = 5
 KEYS = ("obs_buf", "privileged_obs_buf", "rew_buf", "reset_buf", "time_out_buf", "terrain_levels", "terrain_types",
         "env_origins", "commands", "root_states", "dof_state", "episode_length_buf", "randomized_p_gains")
 
@@ -30,8 +31,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _actions():
-    return np.random.default_rng(7).standard_normal((STEPS, N_PER_RANK * WORLD, 12)).astype(np.float32)
+def _actions(n_total):
+    return np.random.default_rng(7).standard_normal((STEPS, n_total, 12)).astype(np.float32)
 
 
 def _run(n, env_offset, n_total):
@@ -40,15 +41,16 @@ def _run(n, env_offset, n_total):
                       num_envs_total=n_total)
     env.reset()
     gid = torch.arange(n, device="cuda:0") + env_offset
-    # every 5th env times out on the command-curriculum step (counter 2400); rank 0's envs track well (1.35x the
-    # 0.8 threshold), rank 1's poorly (0.63x): only the mean over BOTH shards (1.06x) widens the command range
+    # every 5th env times out on the command-curriculum step (counter 2400); the first half of the global envs track
+    # well (1.35x the 0.8 threshold), the second half poorly (0.63x): only the mean over ALL shards (0.99x) widens the
+    # command range, the ranks' own means would disagree
     env.common_step_counter = 2400 - 3
     el = env.episode_length_buf.clone()
     el[gid % 5 == 0] = 2398
     env.episode_length_buf = el
-    good = torch.where(gid < N_PER_RANK, 1.35, 0.63)
+    good = torch.where(gid < n_total // 2, 1.35, 0.63)
     env.episode_sums["tracking_lin_vel"].copy_(2400 * good * env.reward_scales["tracking_lin_vel"])
-    acts = torch.from_numpy(_actions()[:, env_offset:env_offset + n]).to("cuda:0")
+    acts = torch.from_numpy(_actions(n_total)[:, env_offset:env_offset + n]).to("cuda:0")
     outs = []
     for t in range(STEPS):
         env.step(acts[t].contiguous())
@@ -59,23 +61,24 @@ def _run(n, env_offset, n_total):
     return outs
 
 
-def _rank(rank, port, out_dir):
+def _rank(rank, port, out_dir, n_per_rank, world):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        outs = _run(N_PER_RANK, rank * N_PER_RANK, N_PER_RANK * WORLD)
+        outs = _run(n_per_rank, rank * n_per_rank, n_per_rank * world)
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"),
                  **{f"{k}_{t}": v for t, d in enumerate(outs) for k, v in d.items()})
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_hip_envs_match_unsharded(tmp_path):
+@pytest.mark.parametrize("n_per_rank,world", [(2048, 2), (8192, 8)], ids=["2x2048", "config4_8x8192"])
+def test_sharded_hip_envs_match_unsharded(tmp_path, n_per_rank, world):
     import torch.multiprocessing as mp
-    mp.spawn(_rank, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
-    full = _run(N_PER_RANK * WORLD, 0, N_PER_RANK * WORLD)
-    shards = [np.load(tmp_path / f"rank{r}.npz") for r in range(WORLD)]
+    mp.spawn(_rank, args=(_free_port(), str(tmp_path), n_per_rank, world), nprocs=world, join=True)
+    full = _run(n_per_rank * world, 0, n_per_rank * world)
+    shards = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     widened = False
     for t in range(STEPS):
         for k in KEYS:
@@ -86,3 +89,6 @@ def test_sharded_hip_envs_match_unsharded(tmp_path):
         widened |= bool(full[t]["cmd_range"][1] > 0.5 + 1e-6)
     assert widened, "the command curriculum did not widen: the all-reduce path was not exercised"
     assert any(full[t]["reset_buf"].any() for t in range(STEPS))
+    # the terrain types of the global ids span every shard boundary (legged_robot.py:1490)
+    tt = full[0]["terrain_types"]
+    assert len(np.unique(tt)) == min(20, n_per_rank * world) and tt[-1] == 19

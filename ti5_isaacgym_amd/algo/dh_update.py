@@ -346,9 +346,13 @@ class DHPPO:
     def _losses(self, ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
                 old_sigma_b, hid_b, masks_b, mse):
         """The reference's minibatch losses (dh_ppo.py:130-178); the distribution terms in fp32 under autocast."""
-        # the reference calls ac.act() here for its distribution and drops the sample: the distribution alone (a
-        # sample's std >= 0 check is a host sync, which no graph capture allows; the losses do not use it)
+        # the reference calls ac.act() here for its distribution and drops the sample.  On the device the distribution
+        # alone (a sample's std >= 0 check is a host sync, which no graph capture allows; the losses do not use it); on
+        # the CPU the sample is drawn and dropped like the reference's, so the global RNG stream -- the next rollout's
+        # action samples -- stays the reference's (tests/test_runner_golden.py)
         ac.update_distribution(ac.actor_input(obs_b))
+        if not obs_b.is_cuda:
+            ac.distribution.sample()
         est_lin_vel = ac.state_estimator(obs_b[:, -self.num_short_obs:])
         ref_lin_vel = critic_b[:, self.lin_vel_idx:self.lin_vel_idx + 3].clone()
         logp_b = ac.get_actions_log_prob(actions_b)
