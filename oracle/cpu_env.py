@@ -6,6 +6,8 @@ plus the dynamics header compiled for the host with OpenMP (oracle/dyn_cpu.cpp),
 """
 import ctypes as C
 import os
+import threading
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -14,10 +16,13 @@ from .t1_oracle import T1Oracle
 
 
 class CpuT1Env:
-    def __init__(self, model, num_envs, seed=5, mesh_type="plane", terrain=None, fp64=False):
+    def __init__(self, model, num_envs, seed=5, mesh_type="plane", terrain=None, fp64=False, env_offset=0,
+                 reduce_fn=None, omp_threads=None):
         self.lib = C.CDLL(build_cpu.build())
         self.model = model
-        self.o = T1Oracle(num_envs, seed=seed, mesh_type=mesh_type, terrain=terrain)
+        self.omp_threads = omp_threads
+        self.o = T1Oracle(num_envs, seed=seed, mesh_type=mesh_type, terrain=terrain, env_offset=env_offset,
+                          reduce_fn=reduce_fn)
         self.fp64 = int(fp64)
         self.N = num_envs
         if terrain is not None and mesh_type in ("heightfield", "trimesh"):
@@ -42,6 +47,8 @@ class CpuT1Env:
                 f(o.restitution)]
         ext = f(o.applied_force[:, 0, :]) if o.force_pending else None
         rows, cols, hs, vs, border, mesh = self.tparams
+        if self.omp_threads:
+            self.lib.t1dyn_set_num_threads(int(self.omp_threads))   # this calling thread's OpenMP team size
         rc = self.lib.t1dyn_substeps(
             C.byref(self.model), self.N, self.fp64, root.ctypes.data_as(fp), dof.ctypes.data_as(fp),
             *[a.ctypes.data_as(fp) for a in args], self.vimp.ctypes.data_as(fp),
@@ -56,3 +63,47 @@ class CpuT1Env:
 
     def step(self, actions):
         return self.o.step(np.asarray(actions, np.float32), self._physics)
+
+
+class ShardedCpuT1Env:
+    """The CPU baseline on every host core: S shards of the env (global ids [s N/S, (s+1) N/S), like the multi-GPU
+    shards, so every draw and terrain type is the unsharded run's), each stepped by its own Python thread -- the numpy
+    post-physics releases the GIL in its array kernels -- with its physics on cores / S OpenMP threads.  The command
+    curriculum's global mean is reduced over the shards (the oracle's reduce_fn)."""
+
+    def __init__(self, model, num_envs, cores, shards=None, seed=5, mesh_type="plane", terrain=None):
+        S = max(1, min(shards or min(cores, 16), num_envs))
+        bounds = [num_envs * s // S for s in range(S + 1)]
+        self.bounds = bounds
+        self._bar = threading.Barrier(S)
+        self._acc = [0.0, 0]
+        self._lock = threading.Lock()
+        per = max(1, cores // S)
+        self.cores = per * S
+        t = None
+        if terrain is not None:
+            t = dict(terrain, num_envs_total=num_envs)
+        self.shards = [CpuT1Env(model, bounds[s + 1] - bounds[s], seed=seed, mesh_type=mesh_type, terrain=t,
+                                env_offset=bounds[s], reduce_fn=self._reduce if S > 1 else None, omp_threads=per)
+                       for s in range(S)]
+        self.pool = ThreadPoolExecutor(S)
+
+    def _reduce(self, s, c):
+        if self._bar.wait() == 0:
+            self._acc = [0.0, 0]
+        self._bar.wait()
+        with self._lock:
+            self._acc[0] += s
+            self._acc[1] += c
+        self._bar.wait()
+        return self._acc[0], self._acc[1]
+
+    def threads(self):
+        return self.cores
+
+    def reset(self):
+        list(self.pool.map(lambda e: e.reset(), self.shards))
+
+    def step(self, actions):
+        b = self.bounds
+        list(self.pool.map(lambda i: self.shards[i].step(actions[b[i]:b[i + 1]]), range(len(self.shards))))

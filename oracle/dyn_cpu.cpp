@@ -135,4 +135,7 @@ int t1dyn_accel(const t1env_model* model, const double* mass, const double* iner
 }
 
 int t1dyn_num_threads(void) { return omp_get_max_threads(); }
+// the OpenMP thread count of the calling thread's parallel regions (bench.py's CPU baseline sets it explicitly instead
+// of inheriting OMP_NUM_THREADS; each shard thread of oracle/cpu_env.py ShardedCpuT1Env sets its own share)
+void t1dyn_set_num_threads(int n) { if (n > 0) omp_set_num_threads(n); }
 }

@@ -116,3 +116,33 @@ def test_two_rank_shards_match_unsharded(tmp_path):
         widened |= ref["max_command_x"] > 0.5
     assert widened, "the run never reached the command-curriculum widening it is meant to exercise"
     assert any(full[t]["time_out"].any() for t in range(STEPS))
+
+
+def test_threaded_cpu_baseline_equals_unsharded():
+    """bench.py's CPU baseline (oracle/cpu_env.py ShardedCpuT1Env: env shards on threads, OpenMP physics per shard)
+    steps exactly like the one-shard CPU env: the same global ids, draws and terrain, row for row."""
+    import numpy as np
+    from oracle.cpu_env import CpuT1Env, ShardedCpuT1Env
+    from ti5_isaacgym_amd import task_registry
+    from ti5_isaacgym_amd.envs.t1_env import build_model
+    env_cfg, _ = task_registry.get_cfgs("t1_dh_stand")
+    m = build_model(env_cfg)[0]
+    n = 48
+    one = CpuT1Env(m, n, seed=5)
+    sh = ShardedCpuT1Env(m, n, cores=4, shards=3, seed=5)
+    one.reset()
+    sh.reset()
+    acts = np.random.default_rng(0).standard_normal((4, n, 12)).astype(np.float32)
+    for a in acts:
+        one.step(a)
+        sh.step(a)
+        for k in ("obs_buf", "priv_buf", "reset_buf"):
+            got = np.concatenate([getattr(e.o, k) for e in sh.shards], 0)
+            np.testing.assert_array_equal(got, getattr(one.o, k), err_msg=k)
+        # on a plane every shard lays out its own origin grid (the reference's per-process env spacing): compare the
+        # root state without its xy position
+        got = np.concatenate([e.o.root[:, 2:] for e in sh.shards], 0)
+        np.testing.assert_array_equal(got, one.o.root[:, 2:], err_msg="root")
+        # numpy's float32 reductions inside a few reward terms block by array size: the last ulp may differ
+        got = np.concatenate([e.o.rew_buf for e in sh.shards], 0)
+        np.testing.assert_allclose(got, one.o.rew_buf, rtol=2e-6, atol=1e-9)
