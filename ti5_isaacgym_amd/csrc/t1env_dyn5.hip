@@ -61,6 +61,12 @@ __device__ __forceinline__ void t1_prof_end5() {
 #define T1_PROF_MARK(i) t1_prof_mark5(i)
 #define T1_PROF_BEGIN() t1_prof_begin5()
 #define T1_PROF_END() t1_prof_end5()
+#elif defined(T1_ASM_MARKS)  // ISA analysis build (tools/isa_phases.py): the marks as assembly comments
+#define T1_ASM_STR2(x) #x
+#define T1_ASM_STR(x) T1_ASM_STR2(x)
+#define T1_PROF_MARK(i) asm volatile(";@@MARK " #i "@L" T1_ASM_STR(__LINE__))
+#define T1_PROF_BEGIN() asm volatile(";@@MARK begin")
+#define T1_PROF_END() asm volatile(";@@MARK end")
 #else
 #define T1_PROF_BEGIN() ((void)0)
 #define T1_PROF_END() ((void)0)
@@ -80,6 +86,9 @@ constexpr int D5_SHIFT_T = 192;  // the shift's threads (W1-W3)
 #ifndef T1_D5_SHIFT_UNROLL
 #define T1_D5_SHIFT_UNROLL 8  // 16-B chunks per thread in flight in one shift batch
 #endif
+
+constexpr int SH_ROUNDS = 16;  // LDS-DMA staging rounds per shift wave and substep (shift_glds below)
+struct ShiftRing { float4 blk[3][SH_ROUNDS][64]; };  // [shift wave][round][lane]
 
 // float4 rows [row][lane]: one ds_write_b128 / ds_read_b128 per 4 values of a lane, conflict-free
 template <int K> struct Rows4 { float4 r[(K + 3) / 4][64]; };
@@ -112,8 +121,8 @@ __device__ __forceinline__ void halves(float v, float& left, float& right) {
 
 // The substep state W0 publishes (each half: the env's base state and its leg's joints)
 enum : int { Q_POS = 0, Q_QUAT = 3, Q_W = 7, Q_VO = 10, Q_Q = 13, Q_QD = 19, Q_N = 25 };
-// W1's terms: the torques, the bias / torque rhs, the leg's total bias, the base block with both base-box halves
-enum : int { B_TAU = 0, B_RG = 6, B_G = 12, B_AC = 18, B_R = 39, B_N = 45 };
+// W1's terms: the bias part of each joint rhs (-S_k . sum_{j>=k} g_j), the leg's total bias, both base-box halves
+enum : int { B_RG = 0, B_G = 6, B_AC = 12, B_R = 33, B_N = 39 };
 constexpr int CAP5_N = 2 * NLEG + 8;  // W0's sensor-lag capture: q, qd of the leg; the raw IMU sample (leg 0 lanes)
 
 struct Dyn5Lds {
@@ -127,7 +136,12 @@ struct Dyn5Lds {
   float act[12][NE5];    // the clipped actions (epilogue)
   float epi[EPI_N][NE5];  // staged post-physics inputs (epilogue)
   float fr[FR_N][NE5];   // this step's outputs (epilogue)
-  float vis[2][64];      // end-of-step restitution episodes of the shank / foot (W2 -> W3's report)
+  float vis[2][64];      // end-of-step restitution episode of the shank [0] (W2 -> W3's report)
+  float vift[64];        // the foot's restitution episode (W0 updates it after S2 from amx; W2 / W3 read it)
+  float amx[2][64];      // the fastest approach among the foot points of W2 [0] / W3 [1] this substep
+#ifndef T1_D5_SHIFT_REGS
+  ShiftRing ring;        // the history shift's LDS-DMA staging (W1-W3)
+#endif
   float vib[64];         // end-of-step episode of the base-box half (W1 -> W3's report)
 };
 
@@ -448,6 +462,155 @@ __device__ __forceinline__ void shift_pre_commit(const ShiftArgs& S, int64_t r0,
 #define T1_D5_PRE_U 13
 #endif
 
+// ---- the in-workgroup shift staged through LDS by LDS-DMA (global_load_lds, no VGPR destination): the source blocks
+// of substep s's slice are loaded at the end of substep s-1's post-S2 window (in the prologue for s = 0) and land while
+// the waves run their substep-s role work; after S2 of substep s each wave forms its outputs from its own staged blocks
+// (ds_read) and stores them, then issues the loads of slice s + 1.  A wave-round loads 64 consecutive 16-B blocks of
+// the input (one per lane) and writes 63 output chunks (chunk c reads its source from the blocks c + F/per and
+// c + F/per + 1), so a wave reads only blocks it loaded itself and needs no barrier between DMA and use (its own
+// vmcnt); rounds go round-robin over the three shift waves.  32-row workgroups need at most 15 rounds per wave and
+// substep (fp32: 14 of the 66-frame history + 1 of the critic's).
+constexpr int SH_OUT = 63;                   // output chunks per round
+typedef __attribute__((address_space(3))) void* t1_lds_vp;
+typedef __attribute__((address_space(1))) void* t1_glb_vp;
+
+template <int F, int H, bool HALF> struct ShiftHist {
+  static constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4, ES = HALF ? 2 : 4, D = F / PER, REM = F % PER;
+};
+// output chunks of the workgroup's rows of one history (16-B chunks), and the elements from the rows' start to the
+// buffer end
+template <int F, int H, bool HALF>
+__device__ __forceinline__ void shift_extent(int64_t total, int64_t r0, int64_t r1, uint32_t& n_out, uint32_t& lim) {
+  using SH = ShiftHist<F, H, HALF>;
+  lim = (uint32_t)(total - r0 * (int64_t)SH::ROW);
+  const uint32_t span = (uint32_t)((r1 - r0) * SH::ROW);
+  n_out = ((span < lim ? span : lim) + SH::PER - 1) / SH::PER;
+}
+// issue the DMA of this wave's rounds of the slice [c_lo, c_hi) into ring rounds [slot0, ...); returns the rounds used
+template <int F, int H, bool HALF>
+__device__ __forceinline__ int shift_glds_issue(const void* in, int64_t total, int64_t r0, int64_t r1, uint32_t c_lo,
+                                               uint32_t c_hi, int w, int lane, ShiftRing& R, int slot0) {
+  using SH = ShiftHist<F, H, HALF>;
+  uint32_t n_out, lim;
+  shift_extent<F, H, HALF>(total, r0, r1, n_out, lim);
+  const uint32_t hi = c_hi < n_out ? c_hi : n_out;
+  if (hi <= c_lo || lim < 2 * SH::PER) return 0;
+  const int rounds = (int)((hi - c_lo + SH_OUT - 1) / SH_OUT);
+  const uint8_t* in0 = reinterpret_cast<const uint8_t*>(in) + (size_t)(r0 * SH::ROW) * SH::ES;
+  const uint32_t last = lim / SH::PER - 1;  // the last whole block in the buffer
+  int j = 0;
+  for (int k = w; k < rounds; k += 3, ++j) {
+    uint32_t b = c_lo + (uint32_t)k * SH_OUT + SH::D + (uint32_t)lane;
+    b = b < last ? b : last;  // past the buffer end: a valid dummy block (its outputs are not stored)
+    __builtin_amdgcn_global_load_lds((t1_glb_vp)(in0 + (size_t)b * 16), (t1_lds_vp)&R.blk[w][slot0 + j][0], 16, 0, 0);
+  }
+  return j;
+}
+// form and store this wave's outputs of the slice [c_lo, c_hi) from its staged rounds (their DMA complete)
+template <int F, int H, bool HALF>
+__device__ __forceinline__ int shift_glds_commit(const void* in, void* out, int64_t total, int64_t r0, int64_t r1,
+                                                uint32_t c_lo, uint32_t c_hi, int w, int lane, const ShiftRing& R,
+                                                int slot0) {
+  using SH = ShiftHist<F, H, HALF>;
+  uint32_t n_out, lim;
+  shift_extent<F, H, HALF>(total, r0, r1, n_out, lim);
+  const uint32_t hi = c_hi < n_out ? c_hi : n_out;
+  if (hi <= c_lo || lim < 2 * SH::PER) return 0;
+  const int rounds = (int)((hi - c_lo + SH_OUT - 1) / SH_OUT);
+  int j = 0;
+  for (int k = w; k < rounds; k += 3, ++j) {
+    const uint32_t c = c_lo + (uint32_t)k * SH_OUT + (uint32_t)lane;
+    const float4 xa = R.blk[w][slot0 + j][lane];
+    const float4 xb = R.blk[w][slot0 + j][lane < 63 ? lane + 1 : 63];
+    if (lane >= SH_OUT || c >= hi) continue;
+    const uint32_t i = c * SH::PER;  // first output element (rows-relative)
+    const bool tail = (c + SH::D + 1) * SH::PER + SH::PER > lim;  // a source block past the buffer end: elementwise
+    const uint32_t col0 = i - (i / SH::ROW) * SH::ROW;
+    if constexpr (!HALF) {
+      const float* in0 = reinterpret_cast<const float*>(in) + r0 * SH::ROW;
+      float* out0 = reinterpret_cast<float*>(out) + r0 * SH::ROW;
+      float src[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+      if (tail) {
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) {
+          const uint32_t e = (c + SH::D) * 4 + k2;
+          src[k2] = e < lim ? in0[e] : 0.0f;
+        }
+      }
+      if (col0 + 3 < SH::ROW - F && i + 3 < lim) {
+        *reinterpret_cast<float4*>(out0 + i) =
+            make_float4(src[SH::REM], src[SH::REM + 1], src[SH::REM + 2], src[SH::REM + 3]);
+        continue;
+      }
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {
+        const uint32_t e = i + k2;
+        if (e >= lim) break;
+        if (e - (e / SH::ROW) * SH::ROW < SH::ROW - F) out0[e] = src[SH::REM + k2];
+      }
+    } else {
+      constexpr uint32_t MM = SH::REM / 2;
+      const uint16_t* in0 = reinterpret_cast<const uint16_t*>(in) + r0 * SH::ROW;
+      uint16_t* out0 = reinterpret_cast<uint16_t*>(out) + r0 * SH::ROW;
+      const u32x4 a = __builtin_bit_cast(u32x4, xa), b = __builtin_bit_cast(u32x4, xb);
+      uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      if (tail) {
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) {
+          const uint32_t e = (c + SH::D) * 8 + 2 * k2;
+          const uint32_t lo = e < lim ? in0[e] : 0u, hh = e + 1 < lim ? in0[e + 1] : 0u;
+          wv[k2] = lo | (hh << 16);
+        }
+      }
+      u32x4 o;
+      if constexpr (SH::REM % 2 == 0) {
+        o = u32x4{wv[MM], wv[MM + 1], wv[MM + 2], wv[MM + 3]};
+      } else {
+        o = u32x4{__builtin_amdgcn_alignbyte(wv[MM + 1], wv[MM], 2), __builtin_amdgcn_alignbyte(wv[MM + 2], wv[MM + 1], 2),
+                  __builtin_amdgcn_alignbyte(wv[MM + 3], wv[MM + 2], 2), __builtin_amdgcn_alignbyte(wv[MM + 4], wv[MM + 3], 2)};
+      }
+      if (col0 + 7 < SH::ROW - F && i + 7 < lim) {
+        *reinterpret_cast<u32x4*>(out0 + i) = o;
+        continue;
+      }
+      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) {
+        const uint32_t e = i + k2;
+        if (e >= lim) break;
+        if (e - (e / SH::ROW) * SH::ROW < SH::ROW - F) out0[e] = (uint16_t)(ow[k2 / 2] >> (16 * (k2 & 1)));
+      }
+    }
+  }
+  return j;
+}
+// slice `sl` of `nsl` of both histories: issue its DMA / commit its outputs (shift wave w of 3)
+template <bool HALF>
+__device__ __forceinline__ void shift_glds_slice(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int w,
+                                                 int lane, ShiftRing& R, bool commit) {
+  if (r1 <= r0 || sl >= nsl) return;
+  uint32_t no, np, lim;
+  shift_extent<T1_NOBS, T1_HIST, HALF>(S.total_obs, r0, r1, no, lim);
+  shift_extent<T1_NPRIV, T1_CHIST, HALF>(S.total_priv, r0, r1, np, lim);
+  const uint32_t olo = no * sl / nsl, ohi = no * (sl + 1) / nsl, plo = np * sl / nsl, phi = np * (sl + 1) / nsl;
+  if (commit) {
+    const int used = shift_glds_commit<T1_NOBS, T1_HIST, HALF>(S.obs_in, S.obs_out, S.total_obs, r0, r1, olo, ohi, w,
+                                                               lane, R, 0);
+    shift_glds_commit<T1_NPRIV, T1_CHIST, HALF>(S.priv_in, S.priv_out, S.total_priv, r0, r1, plo, phi, w, lane, R, used);
+  } else {
+    const int used = shift_glds_issue<T1_NOBS, T1_HIST, HALF>(S.obs_in, S.total_obs, r0, r1, olo, ohi, w, lane, R, 0);
+    shift_glds_issue<T1_NPRIV, T1_CHIST, HALF>(S.priv_in, S.total_priv, r0, r1, plo, phi, w, lane, R, used);
+  }
+}
+__device__ __forceinline__ void shift_glds(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int w, int lane,
+                                           ShiftRing& R, bool commit) {
+#ifdef T1_WHATIF_D5_NO_SHIFT  // timing-only what-if build: the history is not shifted
+  return;
+#endif
+  if (S.half) shift_glds_slice<true>(S, r0, r1, sl, nsl, w, lane, R, commit);
+  else shift_glds_slice<false>(S, r0, r1, sl, nsl, w, lane, R, commit);
+}
+
 // ---------------------------------------------------------------------------------------------------
 // k_dyn5.  Lane l of every wave: env blockIdx.x * 32 + (l & 31), leg l >> 5.  Inactive lanes (past num_envs) shadow
 // the last env and store nothing.  The substep log (tests only, LG.root != nullptr) is a run-time switch of the one
@@ -487,77 +650,43 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
   const DynModel& M = lds.model;
 
   if (wave == 1) {
-    // ---------------- W1: bias, PD torques, base block, base-box contacts
+    // ---------------- W1: RNEA bias terms of the leg, both base-box halves
     BaseParams<float> PB;
     LegParams<float> PL;
     load_base_params(M, B, n, PB);
     load_leg_params(M, B, n, j0, PL);
-    {  // actions = clip(actions) into the step's history slot (this wave owns the action ring), PD constants staged
-      PdStage<64>& P = lds.pd;
-      float a[NLEG];
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) a[k] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
-      const int cs = (int)(ctr & 3u);
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) {
-        const int j = j0 + k;
-        P.kp[k][lane] = B.kp[n * 12 + j];
-        P.kd[k][lane] = B.kd[n * 12 + j];
-        P.off[k][lane] = B.motor_offsets[n * 12 + j];
-        P.visc[k][lane] = B.viscous[n * 12 + j];
-        P.coul[k][lane] = B.coulomb[n * 12 + j];
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int k = 0; k < NLEG; ++k)
-          P.act[s][k][lane] = s == cs ? a[k] * C.action_scale : B.act_hist[((size_t)n * 4 + s) * 12 + j0 + k];
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) lds.act[j0 + k][e] = a[k];
-      if (active) {
-        float* slot = B.act_hist + ((size_t)n * 4 + cs) * 12;
-#pragma unroll
-        for (int k = 0; k < NLEG; ++k) {
-          B.actions[n * 12 + j0 + k] = a[k];
-          slot[j0 + k] = a[k] * C.action_scale;
-        }
-      }
-    }
-    const int lag = B.lag_timestep[n];
-    const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
-    const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
     const float mu = PB.friction, eg = ground_restitution(M, PB.restitution);
     float vi_b = B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)];
     int cb, ce;
     base_contact_range(M, leg, cb, ce);
+    const float zero6[NLEG] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#if !defined(T1_D5_SHIFT_PRE) && !defined(T1_D5_SHIFT_REGS)
+    shift_glds(S, r0, r1, 0, nsub, 0, lane, lds.ring, false);  // the first slice's DMA
+#endif
     T1_PROF_MARK(0);
     for (int sub = 0; sub < nsub; ++sub) {
       __syncthreads();  // S1: the substep state published
       T1_PROF_MARK(1);
       BaseState<float> sb;
-      float q[NLEG], qd[NLEG], tau[NLEG];
+      float q[NLEG], qd[NLEG];
       read_state(lds, lane, sb, q, qd);
       BaseFrame<float> F;
       base_frame(sb, F);
       const int32_t bound_b = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
-      pd_torques_staged(M, C, lds.pd, lane, K, ctr, sub, lag, j0, q, qd, tau);
       T1_PROF_MARK(2);
       float v[B_N];
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) v[B_TAU + k] = tau[k];
       {
         float rg[NLEG], G[6];
-        leg_bias_rhs(M, PL, F, q, qd, tau, leg, dt, rg, G);
+        leg_bias_rhs(M, PL, F, q, qd, zero6, leg, dt, rg, G);  // -S_k . sum g (W0 adds dt tau_k)
 #pragma unroll
         for (int k = 0; k < NLEG; ++k) v[B_RG + k] = rg[k];
 #pragma unroll
         for (int i = 0; i < 6; ++i) v[B_G + i] = G[i];
       }
       T1_PROF_MARK(3);
-      {  // base block + the base-box halves (left first, the same sum in both halves)
-        Sym6<float> Ac, Cb;
-        float r[6], gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-        base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
+      {  // the base-box halves, summed left first (the same sum in both halves)
+        Sym6<float> Cb;
+        float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         sym_zero(Cb);
         body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - M.contact_radius[0], bound_b, cb, F.R0,
                                                    v3<float>(0, 0, 0), F.abs, F.V0, mu, eg, vi_b, dt, Cb, gw);
@@ -565,28 +694,33 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
         for (int i = 0; i < 21; ++i) {
           float l, rr;
           halves(Cb.a[i], l, rr);
-          v[B_AC + i] = (Ac.a[i] + l) + rr;
+          v[B_AC + i] = l + rr;
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
           float l, rr;
           halves(gw[i], l, rr);
-          v[B_R + i] = (-r[i] - l) - rr;
+          v[B_R + i] = -l - rr;
         }
       }
       T1_PROF_MARK(4);
       put4(lds.w1, lane, v);
       T1_PROF_MARK(5);
-#ifdef T1_D5_SHIFT_PRE
+#if defined(T1_D5_SHIFT_PRE)
       ShiftPre<T1_D5_PRE_U> sp;
       shift_pre_issue(S, r0, r1, sub, nsub, (int)threadIdx.x - 64, sp);
 #endif
       __syncthreads();  // S2: the terms published
       T1_PROF_MARK(6);
-#ifdef T1_D5_SHIFT_PRE
+#if defined(T1_D5_SHIFT_PRE)
       shift_pre_commit(S, r0, r1, (int)threadIdx.x - 64, sp);
-#else
+#elif defined(T1_D5_SHIFT_REGS)
       shift_slice(S, r0, r1, sub, nsub, (int)threadIdx.x - 64);
+#else
+      // this substep's staged slice (its DMA drained at the S2 barrier), then the next slice's DMA
+      shift_glds(S, r0, r1, sub, nsub, wave - 1, lane, lds.ring, true);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring reads done before the DMA rewrites it
+      shift_glds(S, r0, r1, sub + 1, nsub, wave - 1, lane, lds.ring, false);
 #endif
       T1_PROF_MARK(7);
     }
@@ -606,18 +740,18 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
   }
 
   if (wave >= 2) {
-    // ---------------- W2: terrain contacts of the shank and foot / W3: self-contacts
+    // ---------------- W2: shank terrain + foot points 0-3 / W3: self-contacts + foot points 4-7
     const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // robot shape vs ground (PhysX average)
     const float mu_self = B.friction[n];                          // robot shape vs robot shape
     const float eg = ground_restitution(M, B.restitution[n]);
-    float vi_sh = 0.0f, vi_ft = 0.0f;
-    if (wave == 2) {
-      vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
-      vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
-    }
+    float vi_sh = wave == 2 ? B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] : 0.0f;
     // the epilogue's inputs the step does not change, staged while W0 sets up (nothing writes them before the epilogue)
     if constexpr (FUSED) stage_epilogue_inputs<NE5, 128>(B, N, (int)r0, (int)threadIdx.x - 128, lds.epi);
     const int bsh = 1 + 6 * leg + K_SHANK, bft = 1 + 6 * leg + K_FOOT;
+    const int foot_c0 = M.contact_start[bft] + (wave == 2 ? 0 : T1_POINTS_PER_BODY / 2);
+#if !defined(T1_D5_SHIFT_PRE) && !defined(T1_D5_SHIFT_REGS)
+    shift_glds(S, r0, r1, 0, nsub, wave - 1, lane, lds.ring, false);  // the first slice's DMA
+#endif
     T1_PROF_MARK(0);
     for (int sub = 0; sub < nsub; ++sub) {
       __syncthreads();  // S1
@@ -629,6 +763,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
       base_frame(sb, F);
       BodyKin<float> Ko[2];
       leg_body_kinematics(M, F, q, qd, leg, Ko);
+      const float vtg_ft = restitution_target(M, eg, lds.vift[lane]);  // this substep's foot episode (W0 keeps it)
       T1_PROF_MARK(2);
       Sym6<float> Cs[2];
       float cs[2][6];
@@ -638,75 +773,76 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 6; ++j) cs[i][j] = 0.0f;
       }
+      // this wave's half of the foot's points: queries first, their heights used after the wave's other work
+      ContactQuery<T1_POINTS_PER_BODY / 2, float> Qf;
+      contact_query<HF, T1_POINTS_PER_BODY / 2>(M, T, foot_c0, Ko[1].Rb, Ko[1].p, F.abs, Qf);
       if (wave == 2) {
         const int32_t bnd = terrain_bound_raw_any(T, Ko[0].p.x + F.abs.x, Ko[0].p.y + F.abs.y);
         body_contact_fixed<T1_POINTS_PER_BODY>(M, T, Ko[0].p.z + F.abs.z - M.contact_radius[bsh], bnd,
                                                M.contact_start[bsh], Ko[0].Rb, Ko[0].p, F.abs, Ko[0].V, mu, eg, vi_sh,
                                                dt, Cs[0], cs[0]);
-        T1_PROF_MARK(3);
-        body_contact_query_apply<T1_POINTS_PER_BODY>(M, T, M.contact_start[bft], Ko[1].Rb, Ko[1].p, F.abs, Ko[1].V, mu,
-                                                     eg, vi_ft, dt, Cs[1], cs[1], [] {});
-        T1_PROF_MARK(4);
+      } else if (M.self_collisions) {
+        SelfBody<float> O[2], X[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          float v[XCH];
-          sym_pack(Cs[i], cs[i], v);
-          put4(lds.w2[i], lane, v);
-        }
-      } else {
-        if (M.self_collisions) {
-          SelfBody<float> O[2], X[2];
+        for (int s = 0; s < 2; ++s) {
+          O[s] = self_body(M, leg, s, Ko[s]);
+          const float mine[12] = {O[s].cap.p.x, O[s].cap.p.y, O[s].cap.p.z, O[s].cap.q.x, O[s].cap.q.y,
+                                  O[s].cap.q.z, O[s].V[0],    O[s].V[1],    O[s].V[2],    O[s].V[3],
+                                  O[s].V[4],    O[s].V[5]};
+          float oth[12];
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            O[s] = self_body(M, leg, s, Ko[s]);
-            const float mine[12] = {O[s].cap.p.x, O[s].cap.p.y, O[s].cap.p.z, O[s].cap.q.x, O[s].cap.q.y,
-                                    O[s].cap.q.z, O[s].V[0],    O[s].V[1],    O[s].V[2],    O[s].V[3],
-                                    O[s].V[4],    O[s].V[5]};
-            float oth[12];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) {
-              float l, r;
-              halves(mine[i], l, r);
-              oth[i] = leg ? l : r;
-            }
-            X[s].cap.p = v3<float>(oth[0], oth[1], oth[2]);
-            X[s].cap.q = v3<float>(oth[3], oth[4], oth[5]);
-            X[s].cap.r = M.self_cap[1 - leg][s].r;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) X[s].V[i] = oth[6 + i];
+          for (int i = 0; i < 12; ++i) {
+            float l, r;
+            halves(mine[i], l, r);
+            oth[i] = leg ? l : r;
           }
-          T1_PROF_MARK(3);
-          self_terms_bodies(M, leg, O, X, mu_self, dt, Cs, cs);
-          T1_PROF_MARK(4);
+          X[s].cap.p = v3<float>(oth[0], oth[1], oth[2]);
+          X[s].cap.q = v3<float>(oth[3], oth[4], oth[5]);
+          X[s].cap.r = M.self_cap[1 - leg][s].r;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) X[s].V[i] = oth[6 + i];
         }
+        self_terms_bodies(M, leg, O, X, mu_self, dt, Cs, cs);
+      }
+      T1_PROF_MARK(3);
+      float amax = -1.0f;
+      if (t1_wave_any(vtg_ft > 0.0f))
+        contact_apply<HF, T1_POINTS_PER_BODY / 2>(M, Qf, Ko[1].V, mu, vtg_ft, dt, Cs[1], cs[1], amax);
+      else
+        contact_apply<HF, T1_POINTS_PER_BODY / 2>(M, Qf, Ko[1].V, mu, 0.0f, dt, Cs[1], cs[1], amax);
+      T1_PROF_MARK(4);
+      {
+        Rows4<XCH>* dst = wave == 2 ? lds.w2 : lds.w3;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           float v[XCH];
           sym_pack(Cs[i], cs[i], v);
-          put4(lds.w3[i], lane, v);
+          put4(dst[i], lane, v);
         }
+        lds.amx[wave - 2][lane] = amax;
       }
       T1_PROF_MARK(5);
-#ifdef T1_D5_SHIFT_PRE
+#if defined(T1_D5_SHIFT_PRE)
       ShiftPre<T1_D5_PRE_U> sp;
       shift_pre_issue(S, r0, r1, sub, nsub, (int)threadIdx.x - 64, sp);
 #endif
       __syncthreads();  // S2
       T1_PROF_MARK(6);
-#ifdef T1_D5_SHIFT_PRE
+#if defined(T1_D5_SHIFT_PRE)
       shift_pre_commit(S, r0, r1, (int)threadIdx.x - 64, sp);
-#else
+#elif defined(T1_D5_SHIFT_REGS)
       shift_slice(S, r0, r1, sub, nsub, (int)threadIdx.x - 64);
+#else
+      // this substep's staged slice (its DMA drained at the S2 barrier), then the next slice's DMA
+      shift_glds(S, r0, r1, sub, nsub, wave - 1, lane, lds.ring, true);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring reads done before the DMA rewrites it
+      shift_glds(S, r0, r1, sub + 1, nsub, wave - 1, lane, lds.ring, false);
 #endif
       T1_PROF_MARK(7);
     }
     if (wave == 2) {
       lds.vis[0][lane] = vi_sh;
-      lds.vis[1][lane] = vi_ft;
-      if (active) {
-        B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
-        B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)] = vi_ft;
-      }
+      if (active) B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
     }
     __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
     __syncthreads();  // R1: the end-of-step state and episodes published
@@ -742,7 +878,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
         }
         self_forces_bodies(M, leg, O, X, mu_self, fself);
       }
-      const float vt[3] = {restitution_target(M, eg, lds.vis[0][lane]), restitution_target(M, eg, lds.vis[1][lane]),
+      const float vt[3] = {restitution_target(M, eg, lds.vis[0][lane]), restitution_target(M, eg, lds.vift[lane]),
                            restitution_target(M, eg, lds.vib[lane])};
       const float vt_o = restitution_target(M, eg, lds.vib[lane ^ 32]);  // the other base half (leg 0 reports)
       const float vt_base = vt_o > vt[2] ? vt_o : vt[2];
@@ -756,7 +892,8 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     return;
   }
 
-  // ---------------- W0: core
+  // ---------------- W0: core -- PD torques, base block, chain + CRBA; after S2 fold-in, elimination, base system,
+  // integration; owns the actions, the PD staging and the foot's restitution episode
   BaseParams<float> PB;
   LegParams<float> PL;
   BaseState<float> sb;
@@ -769,6 +906,42 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
     qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
   }
+  {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged
+    PdStage<64>& P = lds.pd;
+    float a[NLEG];
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) a[k] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
+    const int cs = (int)(ctr & 3u);
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      const int j = j0 + k;
+      P.kp[k][lane] = B.kp[n * 12 + j];
+      P.kd[k][lane] = B.kd[n * 12 + j];
+      P.off[k][lane] = B.motor_offsets[n * 12 + j];
+      P.visc[k][lane] = B.viscous[n * 12 + j];
+      P.coul[k][lane] = B.coulomb[n * 12 + j];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k)
+        P.act[s][k][lane] = s == cs ? a[k] * C.action_scale : B.act_hist[((size_t)n * 4 + s) * 12 + j0 + k];
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) lds.act[j0 + k][e] = a[k];
+    if (active) {
+      float* slot = B.act_hist + ((size_t)n * 4 + cs) * 12;
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) {
+        B.actions[n * 12 + j0 + k] = a[k];
+        slot[j0 + k] = a[k] * C.action_scale;
+      }
+    }
+  }
+  const int lag = B.lag_timestep[n];
+  const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
+  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
+  float vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
+  lds.vift[lane] = vi_ft;
   int s_dof = 9 - B.dof_lag_timestep[n] % 10;
 #ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
   s_dof = s_dof > 0 ? s_dof - 1 : 0;
@@ -788,6 +961,10 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     T1_PROF_MARK(1);
     BaseFrame<float> F;
     base_frame(sb, F);
+    pd_torques_staged(M, C, lds.pd, lane, K, ctr, sub, lag, j0, q, qd, tau);
+    Sym6<float> Ac;  // the base body's block (both halves compute it: the same values)
+    float r[6];
+    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
     LegFK<float> fk;
     leg_fk_chain(M, F.R0, q, leg, fk);
     T1_PROF_MARK(2);
@@ -802,16 +979,21 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     float g6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     float w1v[B_N];
     get4(lds.w1, lane, w1v);
+    {  // the foot's episode from the two halves of its points
+      const float am = fmaxf(lds.amx[0][lane], lds.amx[1][lane]);
+      vi_ft = restitution_episode(vi_ft, am);
+      lds.vift[lane] = vi_ft;  // W2 / W3 read it after the next S1
+    }
     {
       float rg[NLEG], G[6];
 #pragma unroll
-      for (int k = 0; k < NLEG; ++k) { tau[k] = w1v[B_TAU + k]; rg[k] = w1v[B_RG + k]; }
+      for (int k = 0; k < NLEG; ++k) rg[k] = dt * tau[k] + w1v[B_RG + k];
 #pragma unroll
       for (int i = 0; i < 6; ++i) G[i] = w1v[B_G + i];
       Sym6<float> Cb[2];
       float cb[2][6];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {  // terrain + self terms of the shank [0] and foot [1]
+      for (int i = 0; i < 2; ++i) {  // shank [0]: W2 terrain + W3 self; foot [1]: W2 half + W3 self and half
         float vt[XCH], vs[XCH];
         get4(lds.w2[i], lane, vt);
         get4(lds.w3[i], lane, vs);
@@ -827,20 +1009,18 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     for (int i = 0; i < 6; ++i) rb[i] = -g6[i];
     eliminate_leg(lb, Ab, rb);
     T1_PROF_MARK(6);
-    // the base system: W1's base block (with both base-box halves) + the left leg + the right leg, in every lane
-    Sym6<float> Ac;
-    float r[6];
+    // the base system: (base block + both base-box halves) + the left leg + the right leg, in every lane
 #pragma unroll
     for (int i = 0; i < 21; ++i) {
       float l, rr;
       halves(Ab.a[i], l, rr);
-      Ac.a[i] = (w1v[B_AC + i] + l) + rr;
+      Ac.a[i] = ((Ac.a[i] + w1v[B_AC + i]) + l) + rr;
     }
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       float l, rr;
       halves(rb[i], l, rr);
-      r[i] = (w1v[B_R + i] + l) + rr;
+      r[i] = ((-r[i] + w1v[B_R + i]) + l) + rr;
     }
     solve_base(Ac, r);
     float dq[NLEG];
@@ -883,6 +1063,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     T1_PROF_MARK(8);
   }
   if (active) {
+    B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)] = vi_ft;
     if (s_dof < nsub) {  // the sensor-lag samples captured in the loop
 #pragma unroll
       for (int k = 0; k < NLEG; ++k) { dof_dst[j0 + k] = lds.cap[k][lane]; dof_dst[12 + j0 + k] = lds.cap[NLEG + k][lane]; }

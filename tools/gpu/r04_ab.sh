@@ -12,7 +12,7 @@ for r in 1 2; do
   T1ENV_DYN_KERNEL=4 timeout -k 10 120 python bench.py --steps 300 --warmup 50 --no-cpu-baseline --time-every 0 \
     > $out/dyn4.$r.json 2> $out/dyn4.$r.err
   for v in "$@"; do
-    T1ENV_LIB=$PWD/ti5_isaacgym_amd/_lib/var/$v.so timeout -k 10 120 python bench.py --steps 300 --warmup 50 \
+    T1ENV_DYN_KERNEL=5 T1ENV_LIB=$PWD/ti5_isaacgym_amd/_lib/var/$v.so timeout -k 10 120 python bench.py --steps 300 --warmup 50 \
       --no-cpu-baseline --time-every 0 > $out/$v.$r.json 2> $out/$v.$r.err
   done
 done
