@@ -139,6 +139,8 @@ struct Dyn5Lds {
   float vis[2][64];      // end-of-step restitution episode of the shank [0] (W2 -> W3's report)
   float vift[64];        // the foot's restitution episode (W0 updates it after S2 from amx; W2 / W3 read it)
   float amx[2][64];      // the fastest approach among the foot points of W2 [0] / W3 [1] this substep
+  float rtf[2][3][64];   // the report: terrain forces on the shank [0] / foot [1] (W2)
+  float rsf[2][3][64];   // the report: self-contact forces on the shank / foot (W3)
 #ifndef T1_D5_SHIFT_REGS
   ShiftRing ring;        // the history shift's LDS-DMA staging (W1-W3)
 #endif
@@ -472,7 +474,19 @@ __device__ __forceinline__ void shift_pre_commit(const ShiftArgs& S, int64_t r0,
 // substep (fp32: 14 of the 66-frame history + 1 of the critic's).
 constexpr int SH_OUT = 63;                   // output chunks per round
 typedef __attribute__((address_space(3))) void* t1_lds_vp;
-typedef __attribute__((address_space(1))) void* t1_glb_vp;
+// One LDS-DMA of 16 B per lane into the wave-uniform LDS address lds_dst (+ lane x 16), by inline assembly: hipcc does
+// not count an asm load, so it adds no vmcnt(0) before the later LDS reads of other data (with the builtin it waited
+// for every outstanding store before each ring read, which serialised the shift on store acknowledgements); the ring is
+// instead retired by an explicit vmcnt(0) before the S2 barrier (shift_glds_retire).  M0 is saved and restored in the
+// statement (cdna_hip_programming.md, LDS-DMA recipe).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ void shift_glds_retire() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 template <int F, int H, bool HALF> struct ShiftHist {
   static constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4, ES = HALF ? 2 : 4, D = F / PER, REM = F % PER;
@@ -502,11 +516,74 @@ __device__ __forceinline__ int shift_glds_issue(const void* in, int64_t total, i
   for (int k = w; k < rounds; k += 3, ++j) {
     uint32_t b = c_lo + (uint32_t)k * SH_OUT + SH::D + (uint32_t)lane;
     b = b < last ? b : last;  // past the buffer end: a valid dummy block (its outputs are not stored)
-    __builtin_amdgcn_global_load_lds((t1_glb_vp)(in0 + (size_t)b * 16), (t1_lds_vp)&R.blk[w][slot0 + j][0], 16, 0, 0);
+    glds16(in0 + (size_t)b * 16, (uint32_t)(size_t)(t1_lds_vp)&R.blk[w][slot0 + j][0]);
   }
   return j;
 }
-// form and store this wave's outputs of the slice [c_lo, c_hi) from its staged rounds (their DMA complete)
+// one output chunk c (16 B) from the two staged source blocks xa, xb; TAIL: the second block may pass the buffer end
+// (the buffer's last rows), the source is then read from global memory element by element
+template <int F, int H, bool HALF, bool TAIL>
+__device__ __forceinline__ void shift_glds_out(const void* in, void* out, int64_t r0, uint32_t lim, uint32_t c, float4 xa,
+                                               float4 xb) {
+  using SH = ShiftHist<F, H, HALF>;
+  const uint32_t i = c * SH::PER;  // first output element (rows-relative)
+  const uint32_t col0 = i - (i / SH::ROW) * SH::ROW;
+  if constexpr (!HALF) {
+    const float* in0 = reinterpret_cast<const float*>(in) + r0 * SH::ROW;
+    float* out0 = reinterpret_cast<float*>(out) + r0 * SH::ROW;
+    float src[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) {
+        const uint32_t e = (c + SH::D) * 4 + k2;
+        src[k2] = e < lim ? in0[e] : 0.0f;
+      }
+    }
+    if (col0 + 3 < SH::ROW - F && i + 3 < lim) {
+      *reinterpret_cast<float4*>(out0 + i) = make_float4(src[SH::REM], src[SH::REM + 1], src[SH::REM + 2], src[SH::REM + 3]);
+      return;
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) {
+      const uint32_t e = i + k2;
+      if (e >= lim) break;
+      if (e - (e / SH::ROW) * SH::ROW < SH::ROW - F) out0[e] = src[SH::REM + k2];
+    }
+  } else {
+    constexpr uint32_t MM = SH::REM / 2;
+    const uint16_t* in0 = reinterpret_cast<const uint16_t*>(in) + r0 * SH::ROW;
+    uint16_t* out0 = reinterpret_cast<uint16_t*>(out) + r0 * SH::ROW;
+    const u32x4 a = __builtin_bit_cast(u32x4, xa), b = __builtin_bit_cast(u32x4, xb);
+    uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) {
+        const uint32_t e = (c + SH::D) * 8 + 2 * k2;
+        const uint32_t lo = e < lim ? in0[e] : 0u, hh = e + 1 < lim ? in0[e + 1] : 0u;
+        wv[k2] = lo | (hh << 16);
+      }
+    }
+    u32x4 o;
+    if constexpr (SH::REM % 2 == 0) {
+      o = u32x4{wv[MM], wv[MM + 1], wv[MM + 2], wv[MM + 3]};
+    } else {
+      o = u32x4{__builtin_amdgcn_alignbyte(wv[MM + 1], wv[MM], 2), __builtin_amdgcn_alignbyte(wv[MM + 2], wv[MM + 1], 2),
+                __builtin_amdgcn_alignbyte(wv[MM + 3], wv[MM + 2], 2), __builtin_amdgcn_alignbyte(wv[MM + 4], wv[MM + 3], 2)};
+    }
+    if (col0 + 7 < SH::ROW - F && i + 7 < lim) {
+      *reinterpret_cast<u32x4*>(out0 + i) = o;
+      return;
+    }
+    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      const uint32_t e = i + k2;
+      if (e >= lim) break;
+      if (e - (e / SH::ROW) * SH::ROW < SH::ROW - F) out0[e] = (uint16_t)(ow[k2 / 2] >> (16 * (k2 & 1)));
+    }
+  }
+}
+// form and store this wave's outputs of the slice [c_lo, c_hi) from its staged rounds (their DMA retired)
 template <int F, int H, bool HALF>
 __device__ __forceinline__ int shift_glds_commit(const void* in, void* out, int64_t total, int64_t r0, int64_t r1,
                                                 uint32_t c_lo, uint32_t c_hi, int w, int lane, const ShiftRing& R,
@@ -517,70 +594,18 @@ __device__ __forceinline__ int shift_glds_commit(const void* in, void* out, int6
   const uint32_t hi = c_hi < n_out ? c_hi : n_out;
   if (hi <= c_lo || lim < 2 * SH::PER) return 0;
   const int rounds = (int)((hi - c_lo + SH_OUT - 1) / SH_OUT);
+  // chunks whose second source block would pass the buffer end (the buffer's last rows) take the TAIL form
+  const uint32_t c_tail = lim / SH::PER >= SH::D + 2 ? lim / SH::PER - SH::D - 1 : 0u;
+  const bool any_tail = hi > c_tail;  // wave-uniform
   int j = 0;
   for (int k = w; k < rounds; k += 3, ++j) {
     const uint32_t c = c_lo + (uint32_t)k * SH_OUT + (uint32_t)lane;
     const float4 xa = R.blk[w][slot0 + j][lane];
     const float4 xb = R.blk[w][slot0 + j][lane < 63 ? lane + 1 : 63];
     if (lane >= SH_OUT || c >= hi) continue;
-    const uint32_t i = c * SH::PER;  // first output element (rows-relative)
-    const bool tail = (c + SH::D + 1) * SH::PER + SH::PER > lim;  // a source block past the buffer end: elementwise
-    const uint32_t col0 = i - (i / SH::ROW) * SH::ROW;
-    if constexpr (!HALF) {
-      const float* in0 = reinterpret_cast<const float*>(in) + r0 * SH::ROW;
-      float* out0 = reinterpret_cast<float*>(out) + r0 * SH::ROW;
-      float src[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-      if (tail) {
-#pragma unroll
-        for (int k2 = 0; k2 < 8; ++k2) {
-          const uint32_t e = (c + SH::D) * 4 + k2;
-          src[k2] = e < lim ? in0[e] : 0.0f;
-        }
-      }
-      if (col0 + 3 < SH::ROW - F && i + 3 < lim) {
-        *reinterpret_cast<float4*>(out0 + i) =
-            make_float4(src[SH::REM], src[SH::REM + 1], src[SH::REM + 2], src[SH::REM + 3]);
-        continue;
-      }
-#pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) {
-        const uint32_t e = i + k2;
-        if (e >= lim) break;
-        if (e - (e / SH::ROW) * SH::ROW < SH::ROW - F) out0[e] = src[SH::REM + k2];
-      }
-    } else {
-      constexpr uint32_t MM = SH::REM / 2;
-      const uint16_t* in0 = reinterpret_cast<const uint16_t*>(in) + r0 * SH::ROW;
-      uint16_t* out0 = reinterpret_cast<uint16_t*>(out) + r0 * SH::ROW;
-      const u32x4 a = __builtin_bit_cast(u32x4, xa), b = __builtin_bit_cast(u32x4, xb);
-      uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      if (tail) {
-#pragma unroll
-        for (int k2 = 0; k2 < 8; ++k2) {
-          const uint32_t e = (c + SH::D) * 8 + 2 * k2;
-          const uint32_t lo = e < lim ? in0[e] : 0u, hh = e + 1 < lim ? in0[e + 1] : 0u;
-          wv[k2] = lo | (hh << 16);
-        }
-      }
-      u32x4 o;
-      if constexpr (SH::REM % 2 == 0) {
-        o = u32x4{wv[MM], wv[MM + 1], wv[MM + 2], wv[MM + 3]};
-      } else {
-        o = u32x4{__builtin_amdgcn_alignbyte(wv[MM + 1], wv[MM], 2), __builtin_amdgcn_alignbyte(wv[MM + 2], wv[MM + 1], 2),
-                  __builtin_amdgcn_alignbyte(wv[MM + 3], wv[MM + 2], 2), __builtin_amdgcn_alignbyte(wv[MM + 4], wv[MM + 3], 2)};
-      }
-      if (col0 + 7 < SH::ROW - F && i + 7 < lim) {
-        *reinterpret_cast<u32x4*>(out0 + i) = o;
-        continue;
-      }
-      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-      for (int k2 = 0; k2 < 8; ++k2) {
-        const uint32_t e = i + k2;
-        if (e >= lim) break;
-        if (e - (e / SH::ROW) * SH::ROW < SH::ROW - F) out0[e] = (uint16_t)(ow[k2 / 2] >> (16 * (k2 & 1)));
-      }
-    }
+    if (!any_tail) shift_glds_out<F, H, HALF, false>(in, out, r0, lim, c, xa, xb);
+    else if (c < c_tail) shift_glds_out<F, H, HALF, false>(in, out, r0, lim, c, xa, xb);
+    else shift_glds_out<F, H, HALF, true>(in, out, r0, lim, c, xa, xb);
   }
   return j;
 }
@@ -705,6 +730,9 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
       }
       T1_PROF_MARK(4);
       put4(lds.w1, lane, v);
+#if !defined(T1_D5_SHIFT_PRE) && !defined(T1_D5_SHIFT_REGS)
+      shift_glds_retire();  // this substep's staged slice landed (issued a substep ago) before S2
+#endif
       T1_PROF_MARK(5);
 #if defined(T1_D5_SHIFT_PRE)
       ShiftPre<T1_D5_PRE_U> sp;
@@ -717,7 +745,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
 #elif defined(T1_D5_SHIFT_REGS)
       shift_slice(S, r0, r1, sub, nsub, (int)threadIdx.x - 64);
 #else
-      // this substep's staged slice (its DMA drained at the S2 barrier), then the next slice's DMA
+      // this substep's staged slice (its DMA retired before S2), then the next slice's DMA
       shift_glds(S, r0, r1, sub, nsub, wave - 1, lane, lds.ring, true);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring reads done before the DMA rewrites it
       shift_glds(S, r0, r1, sub + 1, nsub, wave - 1, lane, lds.ring, false);
@@ -727,8 +755,29 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     lds.vib[lane] = vi_b;
     if (active) B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)] = vi_b;
     __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
-    __syncthreads();  // R1
+    __syncthreads();  // R1: the end-of-step state and episodes published
     T1_PROF_MARK(9);
+    {  // the report's base-box force (leg-0 lanes: the whole box, the larger restitution set point of its halves)
+      V3<float> fb = v3<float>(0.0f, 0.0f, 0.0f);
+      if (leg == 0) {
+        BaseState<float> sb;
+        float q[NLEG], qd[NLEG];
+        read_state(lds, lane, sb, q, qd);
+        BaseFrame<float> F;
+        base_frame(sb, F);
+        const float vt0 = restitution_target(M, eg, lds.vib[lane]), vt1 = restitution_target(M, eg, lds.vib[lane ^ 32]);
+        fb = body_contact_force(M, T, 0, F.R0, v3<float>(0, 0, 0), F.abs, F.V0, mu, vt0 > vt1 ? vt0 : vt1);
+      }
+      T1_PROF_MARK(10);
+      __syncthreads();  // RB: the report's parts in LDS
+      if (leg == 0) {
+        if (active) {
+          float* cf = B.contact_forces + (size_t)n * 39;
+          cf[0] = fb.x; cf[1] = fb.y; cf[2] = fb.z;
+        }
+        if constexpr (FUSED) { lds.fr[F_CFB][e] = fb.x; lds.fr[F_CFB + 1][e] = fb.y; lds.fr[F_CFB + 2][e] = fb.z; }
+      }
+    }
     if constexpr (FUSED) {
       __syncthreads();  // the epilogue barrier
       T1_PROF_MARK(11);
@@ -821,6 +870,9 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
         }
         lds.amx[wave - 2][lane] = amax;
       }
+#if !defined(T1_D5_SHIFT_PRE) && !defined(T1_D5_SHIFT_REGS)
+      shift_glds_retire();  // this substep's staged slice landed (issued a substep ago) before S2
+#endif
       T1_PROF_MARK(5);
 #if defined(T1_D5_SHIFT_PRE)
       ShiftPre<T1_D5_PRE_U> sp;
@@ -833,7 +885,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
 #elif defined(T1_D5_SHIFT_REGS)
       shift_slice(S, r0, r1, sub, nsub, (int)threadIdx.x - 64);
 #else
-      // this substep's staged slice (its DMA drained at the S2 barrier), then the next slice's DMA
+      // this substep's staged slice (its DMA retired before S2), then the next slice's DMA
       shift_glds(S, r0, r1, sub, nsub, wave - 1, lane, lds.ring, true);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring reads done before the DMA rewrites it
       shift_glds(S, r0, r1, sub + 1, nsub, wave - 1, lane, lds.ring, false);
@@ -847,7 +899,8 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
     __syncthreads();  // R1: the end-of-step state and episodes published
     T1_PROF_MARK(9);
-    if (wave == 3) {  // the contact-force report (terrain + self) from the end-of-step state
+    {  // the contact-force report from the end-of-step state: W2 the terrain forces of its leg's shank and foot, W3
+       // their self-contact forces; W2 sums them after RB (the base box: W1)
       BaseState<float> sb;
       float q[NLEG], qd[NLEG];
       read_state(lds, lane, sb, q, qd);
@@ -855,36 +908,59 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
       base_frame(sb, F);
       BodyKin<float> Ko[2];
       leg_body_kinematics(M, F, q, qd, leg, Ko);
-      V3<float> fself[2] = {v3<float>(0.0f, 0.0f, 0.0f), v3<float>(0.0f, 0.0f, 0.0f)};
-      if (M.self_collisions) {
-        SelfBody<float> O[2], X[2];
+      if (wave == 2) {
+        const float vt[2] = {restitution_target(M, eg, lds.vis[0][lane]), restitution_target(M, eg, lds.vift[lane])};
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          O[s] = self_body(M, leg, s, Ko[s]);
-          const float mine[12] = {O[s].cap.p.x, O[s].cap.p.y, O[s].cap.p.z, O[s].cap.q.x, O[s].cap.q.y, O[s].cap.q.z,
-                                  O[s].V[0],    O[s].V[1],    O[s].V[2],    O[s].V[3],    O[s].V[4],    O[s].V[5]};
-          float oth[12];
-#pragma unroll
-          for (int i = 0; i < 12; ++i) {
-            float l, r;
-            halves(mine[i], l, r);
-            oth[i] = leg ? l : r;
-          }
-          X[s].cap.p = v3<float>(oth[0], oth[1], oth[2]);
-          X[s].cap.q = v3<float>(oth[3], oth[4], oth[5]);
-          X[s].cap.r = M.self_cap[1 - leg][s].r;
-#pragma unroll
-          for (int i = 0; i < 6; ++i) X[s].V[i] = oth[6 + i];
+        for (int sb2 = 0; sb2 < 2; ++sb2) {
+          const int b = 1 + 6 * leg + (sb2 == 0 ? K_SHANK : K_FOOT);
+          const V3<float> f = body_contact_force(M, T, b, Ko[sb2].Rb, Ko[sb2].p, F.abs, Ko[sb2].V, mu, vt[sb2]);
+          lds.rtf[sb2][0][lane] = f.x; lds.rtf[sb2][1][lane] = f.y; lds.rtf[sb2][2][lane] = f.z;
         }
-        self_forces_bodies(M, leg, O, X, mu_self, fself);
+      } else {
+        V3<float> fself[2] = {v3<float>(0.0f, 0.0f, 0.0f), v3<float>(0.0f, 0.0f, 0.0f)};
+        if (M.self_collisions) {
+          SelfBody<float> O[2], X[2];
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            O[s] = self_body(M, leg, s, Ko[s]);
+            const float mine[12] = {O[s].cap.p.x, O[s].cap.p.y, O[s].cap.p.z, O[s].cap.q.x, O[s].cap.q.y, O[s].cap.q.z,
+                                    O[s].V[0],    O[s].V[1],    O[s].V[2],    O[s].V[3],    O[s].V[4],    O[s].V[5]};
+            float oth[12];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+              float l, r;
+              halves(mine[i], l, r);
+              oth[i] = leg ? l : r;
+            }
+            X[s].cap.p = v3<float>(oth[0], oth[1], oth[2]);
+            X[s].cap.q = v3<float>(oth[3], oth[4], oth[5]);
+            X[s].cap.r = M.self_cap[1 - leg][s].r;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) X[s].V[i] = oth[6 + i];
+          }
+          self_forces_bodies(M, leg, O, X, mu_self, fself);
+        }
+#pragma unroll
+        for (int sb2 = 0; sb2 < 2; ++sb2) {
+          lds.rsf[sb2][0][lane] = fself[sb2].x; lds.rsf[sb2][1][lane] = fself[sb2].y; lds.rsf[sb2][2][lane] = fself[sb2].z;
+        }
       }
-      const float vt[3] = {restitution_target(M, eg, lds.vis[0][lane]), restitution_target(M, eg, lds.vift[lane]),
-                           restitution_target(M, eg, lds.vib[lane])};
-      const float vt_o = restitution_target(M, eg, lds.vib[lane ^ 32]);  // the other base half (leg 0 reports)
-      const float vt_base = vt_o > vt[2] ? vt_o : vt[2];
-      helper_report_contacts_at<NE5>(M, T, B, F, Ko, fself, n, leg, mu, vt, vt_base, e, active,
-                                     FUSED ? lds.fr : nullptr);
       T1_PROF_MARK(10);
+      __syncthreads();  // RB: the report's parts in LDS
+      if (wave == 2) {
+        float* cf = B.contact_forces + (size_t)n * 39;
+#pragma unroll
+        for (int sb2 = 0; sb2 < 2; ++sb2) {
+          const int b = 1 + 6 * leg + (sb2 == 0 ? K_SHANK : K_FOOT);
+          const float f[3] = {lds.rtf[sb2][0][lane] + lds.rsf[sb2][0][lane], lds.rtf[sb2][1][lane] + lds.rsf[sb2][1][lane],
+                              lds.rtf[sb2][2][lane] + lds.rsf[sb2][2][lane]};
+          if (active) { cf[b * 3 + 0] = f[0]; cf[b * 3 + 1] = f[1]; cf[b * 3 + 2] = f[2]; }
+          if (FUSED && sb2 == 1) {
+            const int r = leg == 0 ? F_C0 : F_C1;
+            lds.fr[r][e] = f[0]; lds.fr[r + 1][e] = f[1]; lds.fr[r + 2][e] = f[2];
+          }
+        }
+      }
     }
     if constexpr (FUSED) __syncthreads();  // the epilogue barrier
     T1_PROF_MARK(11);
@@ -1098,6 +1174,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     leg_report_rigid<NE5>(M, B, PB, sb, F, q, qd, n, leg, active, e, FR);
   }
   T1_PROF_MARK(10);
+  __syncthreads();  // RB: the contact-force report's parts in LDS (W1-W3 store it)
   if constexpr (FUSED) {
     __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
     T1_PROF_MARK(11);
