@@ -659,7 +659,11 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
   const t1env_config& C = *Cp;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / 64);
   const int lane = threadIdx.x & 63;
+#ifdef T1_WHATIF_D5_SCALAR_MODEL  // timing-only what-if: every lane runs the left leg's model through scalar loads
+  const int leg = 0;
+#else
   const int leg = lane >> 5;
+#endif
   const int e = lane & 31;
   const int j0 = 6 * leg;
   const int N = C.num_envs;
@@ -672,7 +676,11 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
   const int64_t r0 = (int64_t)blockIdx.x * NE5, r1 = r0 + NE5 < N ? r0 + NE5 : N;
   T1_PROF_BEGIN();
   __syncthreads();  // the model in LDS
+#ifdef T1_WHATIF_D5_SCALAR_MODEL
+  const DynModel& M = *Mg;
+#else
   const DynModel& M = lds.model;
+#endif
 
   if (wave == 1) {
     // ---------------- W1: RNEA bias terms of the leg, both base-box halves
