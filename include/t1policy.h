@@ -37,6 +37,31 @@ int t1policy_conv1d_pack_weights(const float* weight, void* frag, int channels, 
 int t1policy_conv1d_forward_packed(const float* x, const void* frag, const float* bias, float* y, int batch,
                                    int channels, int length, int out_channels, int kernel, int stride, void* stream);
 
+/* The rest of the rollout's act() after the first conv, one fused kernel (t1policy_heads.hip): the history tail
+ * (conv2 + ReLU, flatten, 96 -> 128 ELU -> 64), the state estimator (235 -> 256 -> 128 -> 64 -> 3, ELU), the actor
+ * ([short | estimate | code] 302 -> 512 -> 256 -> 128 -> 12, ELU), the critic (219 -> 768 -> 256 -> 128 -> 1, ELU),
+ * and the Normal sample of DHPPO._act_body.  Replaces ActorCriticDH.act / evaluate / get_actions_log_prob
+ * (actor_critic_dh.py:45-111,163-188; the torch restatement ti5_isaacgym_amd/algo/dh_policy.py) for inference.
+ *
+ *   params  host array of 31 device pointers, fp32, contiguous: (weight, bias) of the 15 layers in the order
+ *           conv2, history fc1, fc2, estimator 1..4, actor 1..4, critic 1..4, then the 12 action stds
+ *   dims    host array of 30 ints, (out, in) per layer (conv2: 16, 32 * 4): checked against the compiled shapes
+ *   frag    heads_frag_bytes() bytes of device memory (16-byte aligned) that heads_pack fills from params (split
+ *           fp16 fragments) and heads_forward reads; pack again after any weight change
+ *   y1      the first conv's output (batch, 14, 32) channels-last (t1policy_conv1d_forward_packed), before its ReLU
+ *   obs     (batch, obs_cols) actor observations, the short history = the last 235 columns
+ *   critic_obs (batch, 219); eps (batch, 12) standard-normal draws
+ *   out     mean, actions = mean + std eps, sigma (batch, 12); logp (batch) = sum of the Normal log-densities of
+ *           actions; value (batch)
+ * fp32 results within ~1e-6 relative of an fp64 forward (split fp16 matrix cores, fp32 accumulation).  Returns 0,
+ * 1 for shapes without a compiled instance, -1 on bad arguments, -2 on a launch error. */
+int t1policy_heads_frag_bytes(void);
+int t1policy_heads_pack(const uint64_t* params, const int* dims, void* frag, void* stream);
+int t1policy_heads_forward(const uint64_t* params, const int* dims, const void* frag, const float* y1,
+                           const float* obs, int obs_cols, const float* critic_obs, int critic_cols, const float* eps,
+                           float* mean, float* actions, float* sigma, float* logp, float* value, int batch,
+                           void* stream);
+
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py
  * _HistoryRows restates this in torch):

@@ -49,7 +49,9 @@ def test_graphed_act_matches_eager():
     n = 1024
     obs = torch.randn(n, 66 * 47, device="cuda:0")
     cobs = torch.randn(n, 219, device="cuda:0")
-    tol = dict(rtol=1e-6, atol=1e-6)  # the same kernels; a library may still pick another GEMM solution
+    # the graphed act() runs the fused HIP heads (split-fp16 matrix cores, fp32-class: tests/test_gpu_policy_heads.py)
+    # against torch's fp32 layers here; FUSED_ACT=0 would run the same torch kernels
+    tol = dict(rtol=1e-5, atol=1e-5)
     with torch.inference_mode():
         a1, v1, lp1, m1, s1 = [t.clone() for t in alg._graphed_act(obs, cobs)]
         a2 = alg._graphed_act(obs, cobs)[0].clone()
@@ -58,7 +60,7 @@ def test_graphed_act_matches_eager():
         torch.testing.assert_close(s1, (mean * 0.0 + ac.std).expand_as(s1), **tol)
         torch.testing.assert_close(v1, ac.critic(cobs), **tol)
         lp = Normal(m1, s1, validate_args=False).log_prob(a1).sum(-1)
-        torch.testing.assert_close(lp1, lp, **tol)
+        torch.testing.assert_close(lp1, lp, rtol=1e-6, atol=1e-5)
         assert not torch.equal(a1, a2)
     with torch.no_grad():
         for p in ac.parameters():   # in-place update (what the optimizer step does)

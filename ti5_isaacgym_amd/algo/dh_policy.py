@@ -195,6 +195,76 @@ def refresh_packed_weights(module, force=False):
             packed_conv_weights(m, force=force)
 
 
+def _heads_layers(ac):
+    """The fused heads kernel's 15 layers in its parameter order (include/t1policy.h t1policy_heads_*): the history
+    encoder's second conv and its two Linears, the state estimator's four, the actor's four, the critic's four.  None
+    when the model is not built from those parts (ELU activations, ReLU after the convs, alpha 1)."""
+    lin = lambda seq: [m for m in seq if isinstance(m, nn.Linear)]   # noqa: E731
+    acts = [m for seq in (ac.actor, ac.critic, ac.state_estimator) for m in seq if not isinstance(m, nn.Linear)]
+    if not all(isinstance(m, nn.ELU) and m.alpha == 1.0 for m in acts):
+        return None
+    lh = list(ac.long_history)
+    convs = [m for m in lh if isinstance(m, nn.Conv1d)]
+    if len(convs) != 2 or any(not isinstance(m, (nn.Conv1d, nn.ReLU, nn.Flatten, nn.Linear, nn.ELU)) for m in lh):
+        return None
+    layers = [convs[1], *lin(lh), *lin(ac.state_estimator), *lin(ac.actor), *lin(ac.critic)]
+    return layers if len(layers) == 15 else None
+
+
+def heads_forward(ac, obs, critic_obs, eps):
+    """The rollout's act() after the first conv as the fused HIP kernel (t1policy_heads_forward): returns mean,
+    actions = mean + std eps, sigma (B, 12), log-prob (B,) and value (B, 1) -- DHPPO._act_body's outputs -- or None
+    when the model or inputs have no compiled instance (the caller keeps the torch path).  The weights are packed
+    into the kernel's split fp16 fragments on every call (3.6 MB, inside a captured act() graph too), so they always
+    follow the parameters."""
+    from .. import _lib
+    import ctypes as C
+    layers = _heads_layers(ac)
+    if (layers is None or not obs.is_cuda or obs.dtype != torch.float32 or critic_obs.dtype != torch.float32
+            or obs.dim() != 2 or critic_obs.dim() != 2 or eps.shape != (obs.shape[0], ac.std.numel())):
+        return None
+    lib = _lib.load()
+    dims, ptrs = [], []
+    for m in layers:
+        w = m.weight
+        if w.dtype != torch.float32 or not w.is_contiguous() or not m.bias.is_contiguous():
+            return None
+        dims += [w.shape[0], w[0].numel()]
+        ptrs += [w.data_ptr(), m.bias.data_ptr()]
+    ptrs.append(ac.std.data_ptr())
+    dims_c = (C.c_int * 30)(*dims)
+    ptrs_c = (C.c_uint64 * 31)(*ptrs)
+    dev = obs.device
+    frag = getattr(ac, "_t1_heads_frag", None)
+    if frag is None or frag.device != dev:
+        frag = ac._t1_heads_frag = torch.empty(lib.t1policy_heads_frag_bytes(), device=dev, dtype=torch.uint8)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    obs = obs.contiguous()
+    B = obs.shape[0]
+    y1 = conv1d_direct(obs.view(B, ac.in_channels, ac.num_proprio_obs), ac.long_history[0])
+    if y1 is None:
+        return None
+    rc = lib.t1policy_heads_pack(ptrs_c, dims_c, frag.data_ptr(), stream)
+    if rc == 1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"t1policy_heads_pack failed (rc={rc})")
+    critic_obs, eps = critic_obs.contiguous(), eps.contiguous()
+    na = ac.std.numel()
+    mean = torch.empty(B, na, device=dev)
+    actions, sigma = torch.empty_like(mean), torch.empty_like(mean)
+    logp = torch.empty(B, device=dev)
+    value = torch.empty(B, 1, device=dev)
+    rc = lib.t1policy_heads_forward(ptrs_c, dims_c, frag.data_ptr(), y1.data_ptr(), obs.data_ptr(), obs.shape[1],
+                                    critic_obs.data_ptr(), critic_obs.shape[1], eps.data_ptr(), mean.data_ptr(),
+                                    actions.data_ptr(), sigma.data_ptr(), logp.data_ptr(), value.data_ptr(), B, stream)
+    if rc == 1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"t1policy_heads_forward failed (rc={rc})")
+    return mean, actions, sigma, logp, value
+
+
 def conv1d_as_gemm(x, conv, channels_last=False):
     """nn.Conv1d (no padding / dilation / groups) as one GEMM over unfolded windows.  x: (B, C, L), or (B, L, C) with
     channels_last; returns (B, Lout, O) (channels last).  The windows x[b, :, s*l : s*l + k] become rows of a

@@ -18,6 +18,7 @@ replay the graph; eager and graphed steps run the same kernels (bit-identical, t
 """
 import contextlib
 import math
+import os
 import warnings
 
 import torch
@@ -26,8 +27,11 @@ import torch.optim as optim
 from torch.distributions import Normal
 
 from . import distributed as dist_util
-from .dh_policy import ActorCriticDH, refresh_packed_weights
+from .dh_policy import ActorCriticDH, heads_forward, refresh_packed_weights
 from .rollout import RolloutStorage
+
+# the rollout's act() through the fused HIP heads (t1policy_heads_forward; T1_FUSED_ACT=0: the torch layers, A/B)
+FUSED_ACT = os.environ.get("T1_FUSED_ACT", "1") != "0"
 
 
 _GRAPH_RNG_ANCHOR = {}
@@ -154,6 +158,14 @@ class DHPPO:
         torch.normal's std >= 0 test (the sample is drawn as mean + std * N(0, 1), the same distribution)."""
         ac = self.actor_critic
         obs, critic_obs = obs.float(), critic_obs.float()   # fp16 env histories (state_dtype="fp16"): no-op for fp32
+        if obs.is_cuda and FUSED_ACT:
+            # the fused HIP heads (t1policy_heads_forward): the same draw (randn of the mean's shape), one kernel for
+            # every layer after the first conv plus the sample and its log-prob
+            eps = torch.randn(obs.shape[0], ac.std.numel(), device=obs.device)
+            out = heads_forward(ac, obs, critic_obs, eps)
+            if out is not None:
+                mean, actions, sigma, logp, value = out
+                return actions, value, logp, mean, sigma
         mean = ac.actor(ac.actor_input(obs))
         std = mean * 0.0 + ac.std
         dist = Normal(mean, std, validate_args=False)

@@ -1,0 +1,447 @@
+// The DH policy's rollout forward after the first history conv, fused into one kernel (include/t1policy.h,
+// t1policy_heads_*): every dense layer of actor_critic_dh.py:8-188 the rollout's act() runs --
+//
+//   long history tail  conv2 (32 -> 16, k4 s2) + ReLU, flatten (16 x 6), 96 -> 128 ELU -> 64      (actor_critic_dh.py:83-96)
+//   state estimator    short history (235) -> 256 ELU -> 128 ELU -> 64 ELU -> 3                  (:98-111)
+//   actor              [short | estimate | code] (302) -> 512 ELU -> 256 ELU -> 128 ELU -> 12    (:45-58, :163-170)
+//   critic             privileged (219) -> 768 ELU -> 256 ELU -> 128 ELU -> 1                   (:60-73, :185-188)
+//
+// plus the Normal sample, its log-prob and the broadcast sigma (DHPPO._act_body), from the first conv's output
+// (t1policy_conv1d_forward_packed), the actor and critic observations and a standard-normal draw.
+//
+// A workgroup owns 32 envs and one role (actor chain or critic); every layer is a chain of
+// v_mfma_f32_32x32x16_f16 with the WEIGHTS as the A operand (32 output features x 16 inputs) and the ACTIVATIONS as
+// the B operand (16 inputs x 32 envs), so a layer's 32 x 32 result has the env on the lane and the features in the
+// 16 accumulator registers -- exactly the B fragments of the next layer's two k-steps (permuted k order, cdna guide
+// "An accumulator tile as the next MFMA's operand"): an output tile goes to LDS as two 1-KB fragments per precision
+// half with one ds_write_b128 each, and the next layer reads them back with one ds_read_b128 each, no transposes.
+// The weight fragments are packed once per act() (k_heads_pack) in that permuted k order.
+//
+// fp32 accuracy from the fp16 matrix cores, as the first conv (t1policy.hip): v = hi + lo / 2^11 with hi = fp16(v),
+// lo = fp16((v - hi) 2^11), y = sum hi.hi + 2^-11 sum (hi.lo + lo.hi) in two fp32 accumulators; the dropped lo.lo
+// and the residual rounding are ~2^-22 of each product.
+//
+// Bounds: per 32-env tile the actor chain is 976 step-tiles and the critic 792 (one step-tile = a
+// 32 x 16 weight fragment pair = 3 MFMAs, 2 KB of fragments): 3.6 MB of fragments streamed from L2 per tile pair and
+// 1.4 M MFMA-cycles per tile pair -- at the XCD L2's ~70 GB/s/CU of shared rows the fragment stream, not the matrix
+// cores, sets the time.  Actor workgroups run on XCDs 0-3 and critic workgroups on XCDs 4-7 (blockIdx mod 8 = XCD),
+// so each XCD's 4 MB L2 holds only its role's fragments (1.9 or 1.6 MB).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr float PH_SPLIT = 2048.0f;
+constexpr int PH_M = 32;      // envs per workgroup (one MFMA column tile)
+constexpr int PH_WAVES = 4;
+constexpr int PH_OBS_SHORT = 235, PH_CRITIC = 219, PH_Y1 = 14 * 32;
+constexpr int PH_NLAYER = 15;
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2 };
+
+// An input segment of a layer's k axis: `steps` k-steps starting at step `s0` map to input columns col0 .. col0 +
+// len - 1, in natural order (staged from global memory: element j of lane half h of step s = column 16 (s - s0) +
+// 8 h + j) or in the permuted order of an accumulator tile (column 16 (s - s0) + 8 (j >> 2) + 4 h + (j & 3)).
+struct Seg {
+  int s0, steps, col0, len, perm;
+};
+struct Layer {
+  int n, k, ks, act;  // outputs, inputs (the weight's row length), k-steps, activation
+  Seg seg[3];
+  int nseg;
+};
+// layer order = parameter order of t1policy_heads_* (include/t1policy.h)
+constexpr Layer PH_L[PH_NLAYER] = {
+    // long-history tail: conv2 as a 448 -> 96 Toeplitz layer over the channels-last conv1 output (flatten order
+    // o * 6 + l of nn.Flatten on (16, 6)), then the two Linears
+    {96, 128, 28, ACT_RELU, {{0, 28, 0, PH_Y1, 0}}, 1},
+    {128, 96, 6, ACT_ELU, {{0, 6, 0, 96, 1}}, 1},
+    {64, 128, 8, ACT_NONE, {{0, 8, 0, 128, 1}}, 1},
+    // state estimator
+    {256, PH_OBS_SHORT, 15, ACT_ELU, {{0, 15, 0, PH_OBS_SHORT, 0}}, 1},
+    {128, 256, 16, ACT_ELU, {{0, 16, 0, 256, 1}}, 1},
+    {64, 128, 8, ACT_ELU, {{0, 8, 0, 128, 1}}, 1},
+    {3, 64, 4, ACT_NONE, {{0, 4, 0, 64, 1}}, 1},
+    // actor: [short (natural) | estimate (permuted, rows 0..2 of one half-tile) | code (permuted)]
+    {512, 302, 20, ACT_ELU, {{0, 15, 0, PH_OBS_SHORT, 0}, {15, 1, 235, 3, 1}, {16, 4, 238, 64, 1}}, 3},
+    {256, 512, 32, ACT_ELU, {{0, 32, 0, 512, 1}}, 1},
+    {128, 256, 16, ACT_ELU, {{0, 16, 0, 256, 1}}, 1},
+    {12, 128, 8, ACT_NONE, {{0, 8, 0, 128, 1}}, 1},
+    // critic
+    {768, PH_CRITIC, 14, ACT_ELU, {{0, 14, 0, PH_CRITIC, 0}}, 1},
+    {256, 768, 48, ACT_ELU, {{0, 48, 0, 768, 1}}, 1},
+    {128, 256, 16, ACT_ELU, {{0, 16, 0, 256, 1}}, 1},
+    {1, 128, 8, ACT_NONE, {{0, 8, 0, 128, 1}}, 1},
+};
+constexpr int ph_nt(int l) { return (PH_L[l].n + 31) / 32; }
+constexpr int ph_off(int l) {  // first step-tile of layer l in the fragment buffer
+  int o = 0;
+  for (int i = 0; i < l; ++i) o += ph_nt(i) * PH_L[i].ks;
+  return o;
+}
+constexpr int PH_UNITS = ph_off(PH_NLAYER);          // 1,768 step-tiles
+constexpr int PH_FRAG_BYTES = PH_UNITS * 2 * 64 * 16;  // hi + lo, 64 lanes x 16 B: 3,620,864
+
+struct PhParams {
+  const float* w[PH_NLAYER];
+  const float* b[PH_NLAYER];
+  const float* std;
+};
+
+// the weight element feeding output o from input column col of layer L (conv2 as its Toeplitz matrix)
+template <int L>
+__device__ __forceinline__ float ph_weight(const PhParams& P, int o, int col) {
+  if constexpr (L == 0) {
+    const int oc = o / 6, lp = o % 6, p = col >> 5, c = col & 31, t = p - 2 * lp;
+    return (t >= 0 && t < 4) ? P.w[0][(oc * 32 + c) * 4 + t] : 0.0f;
+  } else {
+    return P.w[L][o * PH_L[L].k + col];
+  }
+}
+
+template <int L>
+__device__ __forceinline__ int ph_col(int s, int h, int j) {
+  constexpr Layer Y = PH_L[L];
+#pragma unroll
+  for (int g = 0; g < Y.nseg; ++g) {
+    const Seg q = Y.seg[g];
+    if (s >= q.s0 && s < q.s0 + q.steps) {
+      const int r = 16 * (s - q.s0) + (q.perm ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j);
+      return r < q.len ? q.col0 + r : -1;
+    }
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 x = (_Float16)v[j];
+    hi[j] = x;
+    lo[j] = (_Float16)((v[j] - (float)x) * PH_SPLIT);
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void ph_pack_unit(const PhParams& P, h8* __restrict__ frag, int u, int lane) {
+  constexpr Layer Y = PH_L[L];
+  const int nt = u / Y.ks, s = u % Y.ks;
+  const int o = 32 * nt + (lane & 31), h = lane >> 5;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = ph_col<L>(s, h, j);
+    v[j] = (o < Y.n && col >= 0) ? ph_weight<L>(P, o, col) : 0.0f;
+  }
+  h8 hi, lo;
+  split8(v, hi, lo);
+  const int unit = ph_off(L) + u;
+  frag[(unit * 2 + 0) * 64 + lane] = hi;
+  frag[(unit * 2 + 1) * 64 + lane] = lo;
+}
+
+template <int L>
+__device__ __forceinline__ bool ph_pack_dispatch(const PhParams& P, h8* frag, int unit, int lane) {
+  if constexpr (L == PH_NLAYER) {
+    return false;
+  } else {
+    if (unit < ph_off(L + 1)) {
+      ph_pack_unit<L>(P, frag, unit - ph_off(L), lane);
+      return true;
+    }
+    return ph_pack_dispatch<L + 1>(P, frag, unit, lane);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_heads_pack(PhParams P, h8* __restrict__ frag) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < PH_UNITS * 64; e += gridDim.x * blockDim.x)
+    ph_pack_dispatch<0>(P, frag, e >> 6, e & 63);
+}
+
+// ---- the forward kernel
+typedef h8 Frag[2][64];  // one k-step of B fragments in LDS: [hi, lo][lane]
+
+struct ActorLds {
+  Frag x[20];  // actor input: short history (steps 0..14), estimate (15), history code (16..19)
+  Frag p[32];  // 512-wide activations (and the staged conv1 output, 28 steps)
+  Frag q[16];  // 256-wide activations
+};
+struct CriticLds {
+  Frag p[48];  // 768-wide activations
+  Frag q[16];  // the staged privileged observations (14 steps), then 256-wide activations
+};
+union PhLds {
+  ActorLds a;
+  CriticLds c;
+};
+
+__device__ __forceinline__ float ph_act(float v, int act) {
+  if (act == ACT_RELU) return v > 0.0f ? v : 0.0f;
+  if (act == ACT_ELU) return v > 0.0f ? v : expm1f(v);
+  return v;
+}
+
+// stage `steps` k-steps of natural-order B fragments from rows of global memory: element j of lane (r, h) of step s
+// = src[env r][col0 + 16 s + 8 h + j] (0 past len or past the batch), split into hi / lo.  Steps round-robin over the
+// waves.
+template <bool RELU>
+__device__ __forceinline__ void ph_stage(Frag* dst, int steps, const float* __restrict__ src, long long stride,
+                                         int col0, int len, int env, bool live, int wave, int lane) {
+  const int h = lane >> 5;
+  const float* row = src + (long long)env * stride + col0;
+  for (int s = wave; s < steps; s += PH_WAVES) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 16 * s + 8 * h + j;
+      float x = (live && c < len) ? row[c] : 0.0f;
+      v[j] = RELU ? (x > 0.0f ? x : 0.0f) : x;
+    }
+    h8 hi, lo;
+    split8(v, hi, lo);
+    dst[s][0][lane] = hi;
+    dst[s][1][lane] = lo;
+  }
+}
+
+enum { OUT_LDS = 0, OUT_LDS_HALF = 1, OUT_MEAN = 2, OUT_VALUE = 3 };
+
+struct PhOut {  // the global outputs (OUT_MEAN / OUT_VALUE layers)
+  const float* eps;
+  const float* std;
+  float* mean;
+  float* actions;
+  float* sigma;
+  float* logp;
+  float* value;
+  int env;
+  bool live;
+};
+
+// one dense layer for this wave's output tiles nt = wave + 4 i: B fragments from `in` (LDS), A fragments streamed
+// from the packed buffer, result + bias through the activation into `out` (LDS, k-steps out0 + 2 nt + {0, 1}) or the
+// global outputs.  Waves past the layer's tile count recompute the last tile and store nothing.
+template <int L, int OUT>
+__device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhParams& P, const Frag* in, Frag* out,
+                                         int out0, const PhOut& G, int wave, int lane) {
+  constexpr Layer Y = PH_L[L];
+  constexpr int NT = ph_nt(L), KS = Y.ks, T = (NT + PH_WAVES - 1) / PH_WAVES, OFF = ph_off(L);
+  // fragment loads run D k-steps ahead of their MFMAs (~8 x 96 cycles of MFMAs in flight over an L2 hit), through a
+  // ring of D + 1 register slots; the B fragments one step ahead
+  constexpr int D0 = T >= 4 ? 2 : (T >= 2 ? 4 : 8);
+  constexpr int D = D0 < KS ? D0 : KS - 1;
+  constexpr int R = D + 1;
+  const int h = lane >> 5;
+  f16v acc0[T], acc1[T];
+#pragma unroll
+  for (int i = 0; i < T; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc0[i][r] = acc1[i][r] = 0.0f;
+  const h8* wl = frag + lane;
+  int ntc[T];
+#pragma unroll
+  for (int i = 0; i < T; ++i) ntc[i] = (wave + PH_WAVES * i) < NT ? wave + PH_WAVES * i : NT - 1;
+  h8 wr[R][T][2];
+  auto load = [&](int slot, int s) {
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      const h8* w = wl + (size_t)((OFF + ntc[i] * KS + s) * 2) * 64;
+      wr[slot][i][0] = w[0];
+      wr[slot][i][1] = w[64];
+    }
+  };
+#pragma clang loop unroll(full)
+  for (int s = 0; s < D; ++s) load(s, s);
+  h8 bq[2][2];
+  bq[0][0] = in[0][0][lane];
+  bq[0][1] = in[0][1][lane];
+#pragma clang loop unroll(full)
+  for (int s = 0; s < KS; ++s) {
+    if (s + D < KS) load((s + D) % R, s + D);
+    if (s + 1 < KS) {
+      bq[(s + 1) & 1][0] = in[s + 1][0][lane];
+      bq[(s + 1) & 1][1] = in[s + 1][1][lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const h8 bh = bq[s & 1][0], bl = bq[s & 1][1];
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      const h8 ah = wr[s % R][i][0], al = wr[s % R][i][1];
+      acc0[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc0[i], 0, 0, 0);
+      acc1[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc1[i], 0, 0, 0);
+      acc1[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc1[i], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 0; i < T; ++i) {
+    const int nt = wave + PH_WAVES * i;
+    if (nt >= NT) break;  // wave-uniform
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * nt + (r & 3) + 8 * (r >> 2) + 4 * h;  // C/D row of register r
+      const float b = row < Y.n ? P.b[L][row] : 0.0f;
+      v[r] = ph_act(acc0[i][r] + acc1[i][r] * (1.0f / PH_SPLIT) + b, Y.act);
+    }
+    if constexpr (OUT == OUT_LDS || OUT == OUT_LDS_HALF) {
+#pragma unroll
+      for (int s = 0; s < (OUT == OUT_LDS ? 2 : 1); ++s) {
+        float u[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[j] = v[8 * s + j];
+        h8 hi, lo;
+        split8(u, hi, lo);
+        out[out0 + 2 * nt + s][0][lane] = hi;
+        out[out0 + 2 * nt + s][1][lane] = lo;
+      }
+    } else if constexpr (OUT == OUT_MEAN) {
+      // the Normal sample a = mean + sigma eps and its log-prob, summed over the 12 actions (DHPPO._act_body;
+      // torch.distributions.Normal.log_prob): rows 0-3, 8-11 on lane half 0, rows 4-7 on half 1
+      float lp = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < Y.n && G.live) {
+          const float sd = G.std[row];
+          const size_t ix = (size_t)G.env * Y.n + row;
+          const float a = v[r] + sd * G.eps[ix];
+          const float d = a - v[r];
+          lp += -(d * d) / (2.0f * (sd * sd)) - logf(sd) - 0.91893853320467274178f;  // log(sqrt(2 pi))
+          G.mean[ix] = v[r];
+          G.actions[ix] = a;
+          G.sigma[ix] = sd;
+        }
+      }
+      lp += __shfl_xor(lp, 32);
+      if (h == 0 && G.live) G.logp[G.env] = lp;
+    } else {
+      if (h == 0 && G.live) G.value[G.env] = v[0];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_heads(PhParams P, const h8* __restrict__ frag, const float* __restrict__ y1, const float* __restrict__ obs,
+             int obs_cols, const float* __restrict__ cobs, int cobs_cols, PhOut G, int batch, int xcd_split) {
+  __shared__ PhLds S;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // role and tile: blockIdx mod 8 is the XCD; actor tiles on XCDs 0-3, critic tiles on 4-7 (xcd_split), else
+  // alternating
+  const int bid = blockIdx.x;
+  const bool critic = xcd_split ? (bid & 4) != 0 : (bid & 1) != 0;
+  const int tile = xcd_split ? (bid >> 3) * 4 + (bid & 3) : bid >> 1;
+  const int env0 = tile * PH_M;
+  if (env0 >= batch) return;
+  const int env = env0 + (lane & 31);
+  const bool live = env < batch;
+  const int envc = live ? env : batch - 1;
+  G.env = envc;
+  G.live = live;
+  if (!critic) {
+    ActorLds& A = S.a;
+    ph_stage<true>(A.p, 28, y1, PH_Y1, 0, PH_Y1, envc, live, wave, lane);                       // relu(conv1)
+    ph_stage<false>(A.x, 15, obs, obs_cols, obs_cols - PH_OBS_SHORT, PH_OBS_SHORT, envc, live, wave, lane);
+    __syncthreads();
+    ph_layer<0, OUT_LDS>(frag, P, A.p, A.q, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<1, OUT_LDS>(frag, P, A.q, A.p, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<2, OUT_LDS>(frag, P, A.p, A.x, 16, G, wave, lane);  // history code -> actor input steps 16..19
+    ph_layer<3, OUT_LDS>(frag, P, A.x, A.q, 0, G, wave, lane);   // reads steps 0..14 only: no barrier needed
+    __syncthreads();
+    ph_layer<4, OUT_LDS>(frag, P, A.q, A.p, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<5, OUT_LDS>(frag, P, A.p, A.q, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<6, OUT_LDS_HALF>(frag, P, A.q, A.x, 15, G, wave, lane);  // estimate -> actor input step 15
+    __syncthreads();
+    ph_layer<7, OUT_LDS>(frag, P, A.x, A.p, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<8, OUT_LDS>(frag, P, A.p, A.q, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<9, OUT_LDS>(frag, P, A.q, A.p, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<10, OUT_MEAN>(frag, P, A.p, nullptr, 0, G, wave, lane);
+  } else {
+    CriticLds& C = S.c;
+    ph_stage<false>(C.q, 14, cobs, cobs_cols, 0, PH_CRITIC, envc, live, wave, lane);
+    __syncthreads();
+    ph_layer<11, OUT_LDS>(frag, P, C.q, C.p, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<12, OUT_LDS>(frag, P, C.p, C.q, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<13, OUT_LDS>(frag, P, C.q, C.p, 0, G, wave, lane);
+    __syncthreads();
+    ph_layer<14, OUT_VALUE>(frag, P, C.p, nullptr, 0, G, wave, lane);
+  }
+}
+
+bool ph_params(const uint64_t* params, PhParams& P) {
+  for (int l = 0; l < PH_NLAYER; ++l) {
+    P.w[l] = reinterpret_cast<const float*>(params[2 * l]);
+    P.b[l] = reinterpret_cast<const float*>(params[2 * l + 1]);
+    if (!P.w[l] || !P.b[l]) return false;
+  }
+  P.std = reinterpret_cast<const float*>(params[2 * PH_NLAYER]);
+  return P.std != nullptr;
+}
+
+// the parameter shapes the kernels are compiled for: (out, in) per layer, conv2 as (16, 32 * 4)
+bool ph_dims_match(const int* dims) {
+  static const int want[PH_NLAYER][2] = {{16, 128}, {128, 96}, {64, 128}, {256, 235}, {128, 256}, {64, 128}, {3, 64},
+                                         {512, 302}, {256, 512}, {128, 256}, {12, 128}, {768, 219}, {256, 768},
+                                         {128, 256}, {1, 128}};
+  for (int l = 0; l < PH_NLAYER; ++l)
+    if (dims[2 * l] != want[l][0] || dims[2 * l + 1] != want[l][1]) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int t1policy_heads_frag_bytes(void) { return PH_FRAG_BYTES; }
+
+int t1policy_heads_pack(const uint64_t* params, const int* dims, void* frag, void* stream) {
+  if (!params || !dims || !frag) return -1;
+  if (!ph_dims_match(dims)) return 1;
+  if ((reinterpret_cast<uintptr_t>(frag) & 15u) != 0) return -1;
+  PhParams P;
+  if (!ph_params(params, P)) return -1;
+  hipLaunchKernelGGL(k_heads_pack, dim3((PH_UNITS * 64 + 255) / 256), dim3(256), 0, (hipStream_t)stream, P,
+                     reinterpret_cast<h8*>(frag));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_heads_forward(const uint64_t* params, const int* dims, const void* frag, const float* y1,
+                           const float* obs, int obs_cols, const float* critic_obs, int critic_cols, const float* eps,
+                           float* mean, float* actions, float* sigma, float* logp, float* value, int batch,
+                           void* stream) {
+  if (!params || !dims || !frag || !y1 || !obs || !critic_obs || !eps || !mean || !actions || !sigma || !logp ||
+      !value || batch < 0)
+    return -1;
+  if (!ph_dims_match(dims)) return 1;
+  if (obs_cols < PH_OBS_SHORT || critic_cols != PH_CRITIC) return 1;
+  if (batch == 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(frag) & 15u) != 0) return -1;
+  PhParams P;
+  if (!ph_params(params, P)) return -1;
+  PhOut G{eps, P.std, mean, actions, sigma, logp, value, 0, false};
+  const int tiles = (batch + PH_M - 1) / PH_M;
+  const char* xv = getenv("T1POLICY_HEADS_XCD");
+  const int xcd_split = !(xv && xv[0] == '0');
+  const int grid = xcd_split ? 8 * ((tiles + 3) / 4) : 2 * tiles;
+  hipLaunchKernelGGL(k_heads, dim3(grid), dim3(64 * PH_WAVES), 0, (hipStream_t)stream, P,
+                     reinterpret_cast<const h8*>(frag), y1, obs, obs_cols, critic_obs, critic_cols, G, batch,
+                     xcd_split);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"
