@@ -303,3 +303,33 @@ def test_update_after_loading_plain_adam_state():
     alg.schedule = "fixed"
     alg.update()
     assert abs(alg.learning_rate - 1e-4) < 1e-10
+
+
+def test_device_lr_schedule_matches_python_floats():
+    """the adaptive schedule on the device steps the learning rate in fp64 like the reference's Python
+    float (dh_ppo.py:120-135), so 40 down / up steps land on exactly the reference's value; Adam reads its fp32 copy."""
+    from ti5_isaacgym_amd import task_registry
+    from ti5_isaacgym_amd.algo.dh_policy import ActorCriticDH
+    from ti5_isaacgym_amd.algo.dh_update import DHPPO
+    from ti5_isaacgym_amd.utils.helpers import class_to_dict
+    _, tc = task_registry.get_cfgs("t1_dh_stand")
+    cfg = class_to_dict(tc)
+    dev = torch.device("cuda:0")
+    ac = ActorCriticDH(235, 47, 219, 12, **cfg["policy"]).to(dev)
+    alg = DHPPO(ac, device=str(dev), **cfg["algorithm"])
+    ref = alg.learning_rate
+    mu = torch.zeros(8, 12, device=dev)
+    sig = torch.ones(8, 12, device=dev)
+    g = torch.Generator().manual_seed(3)
+    for _ in range(40):
+        big = bool(torch.rand(1, generator=g) < 0.5)
+        old_mu = mu + (0.5 if big else 1e-4)   # KL far above 2 x desired, or far below half of it
+        kl = float(torch.sum((torch.square(old_mu - mu)) / 2.0, -1).mean())
+        if kl > alg.desired_kl * 2.0:
+            ref = max(1e-5, ref / 1.5)
+        elif 0.0 < kl < alg.desired_kl / 2.0:
+            ref = min(1e-2, ref * 1.5)
+        alg._adapt_lr(mu, sig, old_mu, sig)
+        assert alg.learning_rate == ref
+    assert float(alg._lr_t) == torch.tensor(ref, dtype=torch.float32).item()
+    assert alg.optimizer.param_groups[0]["lr"] is alg._lr_t

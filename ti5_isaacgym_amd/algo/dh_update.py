@@ -71,8 +71,11 @@ class DHPPO:
         self.actor_critic.to(self.device)
         self.storage = None
         cuda = torch.device(device).type == "cuda"
-        # the device learning rate (a 0-d tensor Adam reads) on a HIP device; None on the host (the reference's floats)
+        # the device learning rate (a 0-d tensor Adam reads) on a HIP device; None on the host (the reference's floats).
+        # The adaptive schedule runs on _lr64, an fp64 device copy (the reference's Python float: lr / 1.5 and lr * 1.5
+        # round as it does), and _lr_t, the fp32 value Adam reads, is refreshed from it
         self._lr_t = torch.tensor(float(learning_rate), device=device) if cuda else None
+        self._lr64 = torch.tensor(float(learning_rate), dtype=torch.float64, device=device) if cuda else None
         if cuda:
             # fused: one kernel per step (the capturable foreach Adam ran ~0.75 ms per step, r03x)
             self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=self._lr_t, capturable=True, fused=True)
@@ -105,12 +108,13 @@ class DHPPO:
     @property
     def learning_rate(self):
         """The current learning rate (the adaptive schedule's; on a HIP device read from the device)."""
-        return float(self._lr_t) if self._lr_t is not None else self._lr
+        return float(self._lr64) if self._lr64 is not None else self._lr
 
     @learning_rate.setter
     def learning_rate(self, v):
         self._lr = float(v)
         if self._lr_t is not None:
+            self._lr64.fill_(float(v))
             self._lr_t.fill_(float(v))
 
     def after_optimizer_load(self):
@@ -136,6 +140,7 @@ class DHPPO:
         another tensor there: its value is taken over)."""
         for g in self.optimizer.param_groups:
             if g["lr"] is not self._lr_t:
+                self._lr64.fill_(float(g["lr"]))
                 self._lr_t.fill_(float(g["lr"]))
                 g["lr"] = self._lr_t
 
@@ -236,12 +241,14 @@ class DHPPO:
             kl_mean = dist_util.all_reduce_mean_(torch.mean(kl).reshape(1))[0]
             if self._lr_t is not None:
                 # the same decision on the device (no host sync; capturable): lr / 1.5 floored at 1e-5 above twice the
-                # target KL, lr * 1.5 capped at 1e-2 below half of it (a KL of exactly 0 keeps lr)
-                lr = self._lr_t
+                # target KL, lr * 1.5 capped at 1e-2 below half of it (a KL of exactly 0 keeps lr); the KL compared in
+                # fp32 as the reference's tensor comparisons, the lr stepped in fp64 as its Python float
+                lr = self._lr64
                 down = torch.clamp(lr / 1.5, min=1e-5)
                 up = torch.clamp(lr * 1.5, max=1e-2)
                 low = (kl_mean > 0.0) & (kl_mean < self.desired_kl / 2.0)
                 lr.copy_(torch.where(kl_mean > self.desired_kl * 2.0, down, torch.where(low, up, lr)))
+                self._lr_t.copy_(lr)
                 return
             kl_mean = float(kl_mean)
         if kl_mean > self.desired_kl * 2.0:
