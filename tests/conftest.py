@@ -25,3 +25,25 @@ def pytest_sessionfinish(session, exitstatus):
            for k, v in sorted(mod.WORST.items())}
     with open(path, "w") as f:
         json.dump({"rtol": mod.RTOL, "atol": mod.ATOL, "fields": rep}, f, indent=1)
+
+
+# the step's dynamics kernels (T1ENV_DYN_KERNEL / T1ENV_D5_SHIFT, read when an env is created): k_dyn5 with its
+# in-workgroup history shift (the default), k_dyn5 beside the concurrent k_shift5 launch, and k_dyn4
+DYN_KERNELS = {"dyn5": {"T1ENV_DYN_KERNEL": "5", "T1ENV_D5_SHIFT": "0"},
+               "dyn5_concshift": {"T1ENV_DYN_KERNEL": "5", "T1ENV_D5_SHIFT": "1"},
+               "dyn4": {"T1ENV_DYN_KERNEL": "4"}}
+
+
+@pytest.fixture(params=sorted(DYN_KERNELS))
+def dyn_kernel(request, monkeypatch):
+    for k, v in DYN_KERNELS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+@pytest.fixture(params=["dyn5", "dyn4"])
+def dyn_solver(request, monkeypatch):
+    """The two dynamics kernels (the shift mode does not touch the solver)."""
+    for k, v in DYN_KERNELS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param

@@ -90,8 +90,8 @@ def test_policy_header_exports(lib):
     assert lib.t1policy_conv1d_forward_packed(None, None, None, None, 1, 66, 47, 32, 6, 3, None) == -1
     assert lib.t1policy_conv1d_pack_weights(None, None, 66, 32, 6, None) == -1
     assert lib.t1policy_conv1d_frag_bytes() == 17 * 2 * 2 * 64 * 16
-    # fused heads: 1,768 step-tiles (32 outputs x 16 inputs) of hi + lo fragments
-    assert lib.t1policy_heads_frag_bytes() == 1768 * 2 * 64 * 16
+    # fused heads: 1,768 step-tiles (32 outputs x 16 inputs) of hi + lo fragments, 90 output tiles of bias
+    assert lib.t1policy_heads_frag_bytes() == 1768 * 2 * 64 * 16 + 90 * 4 * 64 * 16   # + the bias fragments
     assert lib.t1policy_heads_pack(None, None, None, None) == -1
     dims = (ctypes.c_int * 30)(*([1] * 30))
     ptrs = (ctypes.c_uint64 * 31)(*([1] * 31))

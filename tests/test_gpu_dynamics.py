@@ -41,13 +41,8 @@ def _state(root, dof):
             "q": dof[..., 0], "qd": dof[..., 1]}
 
 
-@pytest.fixture(params=["4"], ids=["dyn4"])
-def dyn_waves(request):
-    return request.param   # k_dyn4 is the only dynamics kernel since round 3 (the 2-wave k_dynamics was retired)
-
-
 @pytest.mark.parametrize("mesh", ["plane", "trimesh"])
-def test_dynamics_one_step_matches_fp64_host(mesh, dyn_waves):
+def test_dynamics_one_step_matches_fp64_host(mesh, dyn_solver):
     from ti5_isaacgym_amd import make_t1_env
     env = make_t1_env(num_envs=N, mesh_type=mesh, seed=5, device="cuda:0",
                       cfg_hook=_terrain_hook if mesh != "plane" else None)

@@ -27,7 +27,7 @@ def _skew(w):
     return np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
 
 
-def test_one_substep_in_contact_matches_independent_formulation():
+def test_one_substep_in_contact_matches_independent_formulation(dyn_solver):
     from test_dynamics_contact import _place_on_ground, scenario
     from ti5_isaacgym_amd import make_t1_env
     from ti5_isaacgym_amd.envs.t1_env import SOLVER

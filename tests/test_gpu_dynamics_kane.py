@@ -35,7 +35,7 @@ def _skew(w):
 
 
 @pytest.mark.parametrize("ext_force", [False, True], ids=["no_force", "base_ext_force"])
-def test_one_substep_matches_kane_equations(ext_force):
+def test_one_substep_matches_kane_equations(ext_force, dyn_solver):
     from ti5_isaacgym_amd import make_t1_env
     from ti5_isaacgym_amd.utils.urdf import load_model
 

@@ -43,11 +43,6 @@ def _env(n, mesh, fused):
     return env
 
 
-@pytest.fixture(params=["4"], ids=["dyn4"])
-def dyn_waves(request):
-    return request.param   # k_dyn4 is the only dynamics kernel since round 3 (the 2-wave k_dynamics was retired)
-
-
 # 16384 envs: k_dyn4 fills every CU, so the history shift runs as its own launch ahead of the fused kernel and
 # the epilogue zeroes the reset rows directly (t1_shift_prelaunch)
 # 1 env: one workgroup with 63 shadow lanes; 65 envs: a second workgroup holding one live env; 13001: the
@@ -56,7 +51,7 @@ def dyn_waves(request):
                                     (65, "trimesh"), (13001, "plane")],
                          ids=["8192_trimesh", "ragged777_plane", "16384_plane_prelaunched_shift", "single_env",
                               "65_trimesh", "ragged13001_prelaunched_shift"])
-def test_fused_step_equals_split_sequence(n, mesh, dyn_waves):
+def test_fused_step_equals_split_sequence(n, mesh, dyn_kernel):
     fused, split = _env(n, mesh, True), _env(n, mesh, False)
     g = torch.Generator(device="cuda:0").manual_seed(1)
     resets = 0

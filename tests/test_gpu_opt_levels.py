@@ -27,7 +27,7 @@ def test_dynamics_o3_build_matches_fp64_host():
     assert os.path.exists(lib), f"-O3 guard build missing: {lib} (run __graft_entry__.build())"
     env = dict(os.environ, T1ENV_LIB=lib)
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
-           "tests/test_gpu_dynamics.py", "tests/test_gpu_product_parity.py", "-k", "dyn4 or config2"]
+           "tests/test_gpu_dynamics.py", "tests/test_gpu_product_parity.py", "-k", "test_dynamics_one_step or config2"]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
     print(r.stdout[-2000:])
     assert r.returncode == 0, f"-O3 dynamics build fails the dynamics checks:\n{r.stdout[-4000:]}\n{r.stderr[-2000:]}"

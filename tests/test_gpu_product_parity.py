@@ -121,7 +121,7 @@ def compare(env, o, rp, step):
     (777, "trimesh", True, 5, None), (4096, "trimesh", False, 5, 397), (8192, "trimesh", False, 10, 96397)],
     ids=["config2_4096_plane", "config3_8192_trimesh", "config5_32768_hf_push", "ragged777_trimesh_push",
          "extforce_window_400", "extforce_window_96400_applied"])
-def test_product_kernel_matches_oracle(n, mesh, push, steps, counter0):
+def test_product_kernel_matches_oracle(n, mesh, push, steps, counter0, dyn_solver):
     from ti5_isaacgym_amd import make_t1_env
     env = make_t1_env(num_envs=n, mesh_type=mesh, seed=3, device="cuda:0", cfg_hook=_push_hook if push else None)
     o = oracle_for(env, push)

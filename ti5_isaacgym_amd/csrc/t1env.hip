@@ -22,6 +22,7 @@
 #include "t1env_device.h"
 #include "t1env_internal.h"
 #include "t1env_postphys.h"
+#include "t1env_fused.h"
 
 using namespace t1;
 
@@ -72,6 +73,8 @@ struct t1env {
   float max_contact_radius;
   SubLog log;             // t1env_set_substep_log (tests): fused steps write it
   int log_on;
+  hipStream_t side;       // k_dyn5's concurrent history shift (k_shift5), forked from / joined to the step's stream
+  hipEvent_t ev_fork, ev_join;
 };
 
 // k_physics_injected: the same decimation loop with the physics states supplied by the caller (golden
@@ -175,6 +178,58 @@ __global__ __launch_bounds__(BLOCK) void k_post_b(const DynModel* __restrict__ M
 // shift_history as k_dynamics' tail workgroups, as its own launch on the caller's stream
 __global__ __launch_bounds__(256) void k_shift(ShiftArgs S) {
   shift_history(S, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+}
+
+// chunks per lane in flight in the concurrent shift launch (k_shift5): 93 VGPRs at 4 (8 spills), so one of its waves fits beside
+// a k_dyn5 wave on every SIMD
+#ifndef T1_D5_SHIFT_UNROLL
+#define T1_D5_SHIFT_UNROLL 4
+#endif
+// ---------------------------------------------------------------------------------------------------
+// k_shift5 (compiled here at -O3; the dynamics unit's -O1 spilled its 64-bit addresses): the history shift as a launch of its own, on a second stream beside k_dyn5 (DynLaunch::d5_shift = 1).
+// One 256-thread workgroup per CU with no LDS but its handoff words and <= 96 VGPRs per wave, so it fits next to
+// the k_dyn5 workgroup on every CU (k_dyn5 holds ~405 of a SIMD's 512 registers and 98 KB of LDS without the
+// in-workgroup shift's staging ring) whichever launch the dispatcher places first: the shift's loads and stores
+// issue in the dynamics waves' latency gaps instead of on their instruction stream and their vmcnt.  Each
+// workgroup shifts a contiguous run of SHIFT_UNIT-row units; FUSED: then hands each unit off (unit_handoff, the
+// k_dyn4 protocol, t1env_fused.h) -- whichever of the shift and k_dyn5's epilogue finishes a unit last zeroes its
+// reset rows.  Not FUSED (the split step): k_post_b zeroes them after the caller's join.
+// ---------------------------------------------------------------------------------------------------
+template <bool FUSED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8)))
+void k_shift5(ShiftArgs S, FusedArgs FA, int N) {
+  __shared__ uint32_t words[256];
+  const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
+  const int nsw = gridDim.x, j = blockIdx.x;
+  const int per = (units + nsw - 1) / nsw;
+  const int u0 = j * per < units ? j * per : units, u1 = u0 + per < units ? u0 + per : units;
+  const int mine = u1 - u0;
+  if (mine > 0) {
+    const int64_t r0 = (int64_t)u0 * SHIFT_UNIT, r1 = (int64_t)u1 * SHIFT_UNIT < N ? (int64_t)u1 * SHIFT_UNIT : N;
+    shift_rows_range_sc1<T1_D5_SHIFT_UNROLL>(S, r0, r1, threadIdx.x, 256);
+  }
+  if constexpr (FUSED) {
+    // every lane's sc1 stores complete (visible at agent scope) before any handoff
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int k0 = 0; k0 < mine; k0 += 256) {
+      const int k = k0 + (int)threadIdx.x;
+      if (k < mine) words[threadIdx.x] = unit_handoff(FA.unit_state + u0 + k, FA.epoch, HANDOFF_SHIFT);
+      __syncthreads();
+      const int cnt = mine - k0 < 256 ? mine - k0 : 256;
+      for (int i = 0; i < cnt; ++i)
+        if (handoff_complete(words[i])) zero_unit_resets(S, u0 + k0 + i, words[i], threadIdx.x, 256);
+      __syncthreads();
+    }
+  }
+}
+
+int t1_launch_shift5(const ShiftArgs& S, const FusedArgs* fused, int num_envs, int cus, hipStream_t s) {
+  const int units = (num_envs + SHIFT_UNIT - 1) / SHIFT_UNIT;
+  const int grid = units < cus ? units : cus;
+  if (fused) hipLaunchKernelGGL(k_shift5<true>, dim3(grid), dim3(256), 0, s, S, *fused, num_envs);
+  else hipLaunchKernelGGL(k_shift5<false>, dim3(grid), dim3(256), 0, s, S, FusedArgs{}, num_envs);
+  return (int)hipGetLastError();
 }
 
 // extras finalisation for t1env_reset_all (one wave)
@@ -433,10 +488,16 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
     if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))  // > 0: shift workgroups in the launch; -1: stand-alone shift
       if (atoi(sb) > 0 || atoi(sb) == -1) e->dyn.shift_blocks = atoi(sb);
     e->dyn.shift_delay = T1_SHIFT_DELAY_DEFAULT;
+    e->dyn.d5_shift = 0;
+    if (const char* ds = getenv("T1ENV_D5_SHIFT"))  // A/B: 1 = the shift as a concurrent launch (k_shift5)
+      if (atoi(ds) == 0 || atoi(ds) == 1) e->dyn.d5_shift = atoi(ds);
     if (const char* sd = getenv("T1ENV_SHIFT_DELAY"))  // tuning: delayed start of the in-launch shift (100 MHz ticks)
       if (atoi(sd) >= 0) e->dyn.shift_delay = atoi(sd);
   }
   for (int b = 0; b < NB; ++b) e->max_contact_radius = fmaxf(e->max_contact_radius, dm.contact_radius[b]);
+  HIP_TRY(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
   *out = e;
   return 0;
 }
@@ -449,6 +510,9 @@ int t1env_destroy(t1env* e) {
   (void)hipFree(e->d_unit_state);
   (void)hipFree(e->d_ep_part);
   if (e->d_hmax) (void)hipFree(e->d_hmax);
+  if (e->side) (void)hipStreamDestroy(e->side);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   for (int i = 0; i < e->n_events; ++i) {
     (void)hipEventDestroy(e->ev_start[i]);
     (void)hipEventDestroy(e->ev_stop[i]);
@@ -506,6 +570,21 @@ static int launch_shift(t1env* e, const t1env_step_args* a, hipStream_t s) {
   return 0;
 }
 
+// k_dyn5 with the concurrent shift (DynLaunch::d5_shift): the side stream starts after everything enqueued on s so far
+// (fork), runs k_shift5 beside the dynamics launch, and s waits for it before anything after the step (join)
+static bool concurrent_shift(const t1env* e) { return e->dyn.waves == 5 && e->dyn.d5_shift == 1; }
+static int shift_fork(t1env* e, hipStream_t s) {
+  HIP_TRY(hipEventRecord(e->ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+  return 0;
+}
+static int shift_join(t1env* e, const t1env_step_args* a, const FusedArgs* fa, hipStream_t s) {
+  HIP_TRY((hipError_t)t1_launch_shift5(shift_args(e, a), fa, e->cfg.num_envs, e->dyn.cus, e->side));
+  HIP_TRY(hipEventRecord(e->ev_join, e->side));
+  HIP_TRY(hipStreamWaitEvent(s, e->ev_join, 0));
+  return 0;
+}
+
 static int launch_physics(t1env* e, const float* actions, const t1env_step_args* a, const t1env_injected* inj,
                           hipStream_t s) {
   if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
@@ -516,6 +595,9 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
   const bool pre = !inj && t1_shift_prelaunch(N, e->dyn);
   if (pre)
     if (int rc = launch_shift(e, a, s)) return rc;
+  const bool conc = !inj && concurrent_shift(e);
+  if (conc)
+    if (int rc = shift_fork(e, s)) return rc;
   int t = t_begin(e, 0, s);
   if (inj)
     hipLaunchKernelGGL(k_physics_injected, dim3(grid(N, BLOCK)), dim3(BLOCK), 0, s, e->d_model, e->d_cfg, e->buf,
@@ -525,6 +607,8 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
                                            shift_args(e, a), e->dyn, nullptr, s, pre));
   t_end(e, t, s);
   HIP_TRY(hipGetLastError());
+  if (conc)
+    if (int rc = shift_join(e, a, nullptr, s)) return rc;
   if (inj) {
     if (int rc = launch_shift(e, a, s)) return rc;
   }
@@ -577,11 +661,16 @@ static int launch_fused(t1env* e, const float* actions, const t1env_step_args* a
   const bool pre = t1_shift_prelaunch(e->cfg.num_envs, e->dyn);
   if (pre)
     if (int rc = launch_shift(e, a, s)) return rc;
+  const bool conc = concurrent_shift(e);
+  if (conc)
+    if (int rc = shift_fork(e, s)) return rc;
   const int t = t_begin(e, 0, s);
   const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch, pre ? 1 : 0, e->d_ep_part};
   HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, e->cfg.num_envs,
                                          shift_args(e, a), e->dyn, &FA, s, pre, e->log_on ? &e->log : nullptr));
   t_end(e, t, s);
+  if (conc)
+    if (int rc = shift_join(e, a, &FA, s)) return rc;
   t_end(e, e->step_timer, s);
   e->step_timer = -1;
   e->shift_pending = 0;

@@ -285,7 +285,8 @@ __device__ __forceinline__ void shift_rows_f32(const float* __restrict__ in, flo
         y = make_float4(t[4], t[5], t[6], t[7]);
       }
       const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-      const int rem = (int)(sidx - sa);
+      // sidx - sa = (4 c + F) mod 4: a compile-time offset (a run-time one indexes src through scratch at -O1)
+      constexpr int rem = (int)(F & 3u);
       const uint32_t col0 = i - (i / ROW) * ROW;
       if (col0 + 3 < ROW - F && i + 3 < lim) {  // 4 older-frame columns of one row
         store4<SC1>(out0 + i, make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]));

@@ -82,10 +82,6 @@ using namespace t1;
 
 constexpr int NE5 = 32;        // envs per workgroup
 constexpr int D5_BLOCK = 256;  // four waves
-constexpr int D5_SHIFT_T = 192;  // the shift's threads (W1-W3)
-#ifndef T1_D5_SHIFT_UNROLL
-#define T1_D5_SHIFT_UNROLL 8  // 16-B chunks per thread in flight in one shift batch
-#endif
 
 constexpr int SH_ROUNDS = 16;  // LDS-DMA staging rounds per shift wave and substep (shift_glds below)
 struct ShiftRing { float4 blk[3][SH_ROUNDS][64]; };  // [shift wave][round][lane]
@@ -125,7 +121,7 @@ enum : int { Q_POS = 0, Q_QUAT = 3, Q_W = 7, Q_VO = 10, Q_Q = 13, Q_QD = 19, Q_N
 enum : int { B_RG = 0, B_G = 6, B_AC = 12, B_R = 33, B_N = 39 };
 constexpr int CAP5_N = 2 * NLEG + 8;  // W0's sensor-lag capture: q, qd of the leg; the raw IMU sample (leg 0 lanes)
 
-struct Dyn5Lds {
+struct Dyn5Lds {  // without the in-workgroup shift's staging (the concurrent shift launch, Dyn5LdsSh below)
   DynModel model;
   Rows4<Q_N> st;         // W0 -> all: substep state
   Rows4<B_N> w1;         // W1 -> W0
@@ -141,11 +137,13 @@ struct Dyn5Lds {
   float amx[2][64];      // the fastest approach among the foot points of W2 [0] / W3 [1] this substep
   float rtf[2][3][64];   // the report: terrain forces on the shank [0] / foot [1] (W2)
   float rsf[2][3][64];   // the report: self-contact forces on the shank / foot (W3)
-#ifndef T1_D5_SHIFT_REGS
-  ShiftRing ring;        // the history shift's LDS-DMA staging (W1-W3)
-#endif
   float vib[64];         // end-of-step episode of the base-box half (W1 -> W3's report)
 };
+struct Dyn5LdsSh : Dyn5Lds {
+  ShiftRing ring;        // the in-workgroup history shift's LDS-DMA staging (W1-W3)
+};
+template <bool SH> struct Dyn5LdsT { typedef Dyn5Lds type; };
+template <> struct Dyn5LdsT<true> { typedef Dyn5LdsSh type; };
 
 __device__ __forceinline__ void state_pack(const BaseState<float>& sb, const float q[NLEG], const float qd[NLEG],
                                            float (&v)[Q_N]) {
@@ -181,288 +179,6 @@ __device__ __forceinline__ void sym_unpack(const float (&v)[XCH], Sym6<float>& A
 #pragma unroll
   for (int i = 0; i < 6; ++i) g[i] = v[21 + i];
 }
-
-// ---- the workgroup's own history shift, a window of 16-B chunks per call: out[row, :F*(H-1)] = in[row, F:] for
-// the rows [r0, r1).  shift_rows_f32's addressing (32-bit row-local indices) over the chunk window [c_lo, c_hi) of the
-// range, plain stores (this workgroup zeroes its reset rows after, in program order behind the epilogue barrier).
-template <int F, int H, int U>
-__device__ __forceinline__ void shift_window_f32(const float* __restrict__ in, float* __restrict__ out, int64_t total,
-                                                 int64_t r0, int64_t r1, uint32_t c_lo, uint32_t c_hi, int t0, int stride) {
-  constexpr uint32_t ROW = F * H;
-  const float* __restrict__ in0 = in + r0 * ROW;
-  float* __restrict__ out0 = out + r0 * ROW;
-  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);  // elements from in0 to the buffer end
-  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
-  const uint32_t nel = span < lim ? span : lim;
-  const uint32_t n4 = (nel + 3) / 4;
-  const uint32_t hi = c_hi < n4 ? c_hi : n4;
-  for (uint32_t base = c_lo + t0; base < hi; base += U * stride) {
-    float4 a[U], b[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t sa = ((base + u * stride) * 4 + F) & ~3u;
-      const uint32_t sc = sa + 8 <= lim ? sa : (lim - 8) & ~3u;  // tail: aligned in-bounds dummy
-      a[u] = *reinterpret_cast<const float4*>(in0 + sc);
-      b[u] = *reinterpret_cast<const float4*>(in0 + sc + 4);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t c = base + u * stride;
-      if (c >= hi) break;
-      const uint32_t i = c * 4, sidx = i + F, sa = sidx & ~3u;
-      float4 x = a[u], y = b[u];
-      if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
-        float t[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
-        x = make_float4(t[0], t[1], t[2], t[3]);
-        y = make_float4(t[4], t[5], t[6], t[7]);
-      }
-      const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-      const int rem = (int)(sidx - sa);
-      const uint32_t col0 = i - (i / ROW) * ROW;
-      if (col0 + 3 < ROW - F && i + 3 < lim) {  // 4 older-frame columns of one row
-        *reinterpret_cast<float4*>(out0 + i) = make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]);
-        continue;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t e = i + k;
-        if (e >= lim) break;
-        if (e - (e / ROW) * ROW < ROW - F) out0[e] = src[rem + k];
-      }
-    }
-  }
-}
-// the fp16 histories (t1env_config.obs_half): shift_rows_f16's addressing over a chunk window of 8 halves
-template <int F, int H, int U>
-__device__ __forceinline__ void shift_window_f16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
-                                                 int64_t total, int64_t r0, int64_t r1, uint32_t c_lo, uint32_t c_hi,
-                                                 int t0, int stride) {
-  constexpr uint32_t ROW = F * H, REM = F % 8, M = REM / 2;
-  const uint16_t* __restrict__ in0 = in + r0 * ROW;
-  uint16_t* __restrict__ out0 = out + r0 * ROW;
-  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
-  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
-  const uint32_t nel = span < lim ? span : lim;
-  const uint32_t n8 = (nel + 7) / 8;
-  const uint32_t hi = c_hi < n8 ? c_hi : n8;
-  for (uint32_t base = c_lo + t0; base < hi; base += U * stride) {
-    u32x4 a[U], b[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t sa = ((base + u * stride) * 8 + F) & ~7u;
-      const uint32_t sc = sa + 16 <= lim ? sa : (lim - 16) & ~7u;
-      a[u] = *reinterpret_cast<const u32x4*>(in0 + sc);
-      b[u] = *reinterpret_cast<const u32x4*>(in0 + sc + 8);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t c8 = base + u * stride;
-      if (c8 >= hi) break;
-      const uint32_t i = c8 * 8, sa = (i + F) & ~7u;
-      uint32_t w[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
-      if (sa + 16 > lim) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t lo = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
-          const uint32_t hh = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
-          w[k] = lo | (hh << 16);
-        }
-      }
-      u32x4 o;
-      if constexpr (REM % 2 == 0) {
-        o = u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
-      } else {
-        o = u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], 2), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], 2),
-                  __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], 2), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], 2)};
-      }
-      const uint32_t col0 = i - (i / ROW) * ROW;
-      if (col0 + 7 < ROW - F && i + 7 < lim) {
-        *reinterpret_cast<u32x4*>(out0 + i) = o;
-        continue;
-      }
-      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t e = i + k;
-        if (e >= lim) break;
-        if (e - (e / ROW) * ROW < ROW - F) out0[e] = (uint16_t)(ow[k / 2] >> (16 * (k & 1)));
-      }
-    }
-  }
-}
-// slice `sl` of `nsl` of the workgroup's rows [r0, r1) of both histories, thread t0 of D5_SHIFT_T
-__device__ __forceinline__ void shift_slice(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int t0) {
-#ifdef T1_WHATIF_D5_NO_SHIFT  // timing-only what-if build: the history is not shifted
-  return;
-#endif
-  if (r1 <= r0) return;
-  const uint32_t rows = (uint32_t)(r1 - r0);
-  if (S.half) {
-    const uint32_t no = (rows * (T1_NOBS * T1_HIST) + 7) / 8, np = (rows * (T1_NPRIV * T1_CHIST) + 7) / 8;
-    shift_window_f16<T1_NOBS, T1_HIST, T1_D5_SHIFT_UNROLL>(reinterpret_cast<const uint16_t*>(S.obs_in),
-                                                           reinterpret_cast<uint16_t*>(S.obs_out), S.total_obs, r0, r1,
-                                                           no * sl / nsl, no * (sl + 1) / nsl, t0, D5_SHIFT_T);
-    shift_window_f16<T1_NPRIV, T1_CHIST, T1_D5_SHIFT_UNROLL>(reinterpret_cast<const uint16_t*>(S.priv_in),
-                                                             reinterpret_cast<uint16_t*>(S.priv_out), S.total_priv, r0,
-                                                             r1, np * sl / nsl, np * (sl + 1) / nsl, t0, D5_SHIFT_T);
-    return;
-  }
-  const uint32_t no = (rows * (T1_NOBS * T1_HIST) + 3) / 4, np = (rows * (T1_NPRIV * T1_CHIST) + 3) / 4;
-  shift_window_f32<T1_NOBS, T1_HIST, T1_D5_SHIFT_UNROLL>(S.obs_in, S.obs_out, S.total_obs, r0, r1, no * sl / nsl,
-                                                         no * (sl + 1) / nsl, t0, D5_SHIFT_T);
-  shift_window_f32<T1_NPRIV, T1_CHIST, T1_D5_SHIFT_UNROLL>(S.priv_in, S.priv_out, S.total_priv, r0, r1, np * sl / nsl,
-                                                           np * (sl + 1) / nsl, t0, D5_SHIFT_T);
-}
-
-// ---- the same shift with its loads issued before S2 (after the wave's role work, so its registers are free) and its
-// stores after S2: the load latency is spent in the S2 wait instead of on the critical post-S2 window.  One batch of
-// U chunks per thread and history per substep (32 rows x 3102 fp32 = 24,816 chunks over 10 substeps x 192 threads:
-// 13); chunks past the batch (never with 32-row workgroups and 10 substeps) go through the windowed loop.
-template <int U> struct ShiftPre {
-  u32x4 a[U], b[U];      // the two 16-B source chunks of each output chunk (fp32 or fp16 bits)
-  u32x4 pa, pb;          // the critic history's chunk (one per thread and substep)
-  uint32_t olo, ohi, plo, phi;  // this substep's chunk windows of the two histories
-};
-template <int F, int H>
-__device__ __forceinline__ uint32_t shift_nchunks(int64_t total, int64_t r0, int64_t r1, int per) {
-  const uint32_t ROW = F * H;
-  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW), span = (uint32_t)((r1 - r0) * ROW);
-  return ((span < lim ? span : lim) + per - 1) / per;
-}
-// source chunk loads of output chunk c of the rows' range (16-B chunks of `per` elements, element size es)
-template <int F, int H>
-__device__ __forceinline__ void shift_src_ld(const uint8_t* in, int64_t total, int64_t r0, uint32_t c, int per, int es,
-                                             u32x4& a, u32x4& b) {
-  const uint32_t ROW = F * H;
-  const uint8_t* in0 = in + (size_t)(r0 * ROW) * es;
-  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
-  const uint32_t sa = (c * per + F) & ~(uint32_t)(per - 1);
-  const uint32_t sc = sa + 2 * per <= lim ? sa : (lim - 2 * per) & ~(uint32_t)(per - 1);  // tail: in-bounds dummy
-  a = *reinterpret_cast<const u32x4*>(in0 + (size_t)sc * es);
-  b = *reinterpret_cast<const u32x4*>(in0 + (size_t)(sc + per) * es);
-}
-// the stores of output chunk c from its loaded source chunks (fp32: per = 4; fp16: per = 8)
-template <int F, int H, bool HALF>
-__device__ __forceinline__ void shift_chunk_st(const void* inv, void* outv, int64_t total, int64_t r0, uint32_t c,
-                                               u32x4 a, u32x4 b) {
-  constexpr uint32_t ROW = F * H;
-  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
-  if constexpr (!HALF) {
-    const float* in0 = reinterpret_cast<const float*>(inv) + r0 * ROW;
-    float* out0 = reinterpret_cast<float*>(outv) + r0 * ROW;
-    const uint32_t i = c * 4, sidx = i + F, sa = sidx & ~3u;
-    float4 x = __builtin_bit_cast(float4, a), y = __builtin_bit_cast(float4, b);
-    if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
-      float t[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
-      x = make_float4(t[0], t[1], t[2], t[3]);
-      y = make_float4(t[4], t[5], t[6], t[7]);
-    }
-    const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-    const int rem = (int)(sidx - sa);
-    const uint32_t col0 = i - (i / ROW) * ROW;
-    if (col0 + 3 < ROW - F && i + 3 < lim) {
-      *reinterpret_cast<float4*>(out0 + i) = make_float4(src[rem], src[rem + 1], src[rem + 2], src[rem + 3]);
-      return;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t e = i + k;
-      if (e >= lim) break;
-      if (e - (e / ROW) * ROW < ROW - F) out0[e] = src[rem + k];
-    }
-  } else {
-    constexpr uint32_t REM = F % 8, MM = REM / 2;
-    const uint16_t* in0 = reinterpret_cast<const uint16_t*>(inv) + r0 * ROW;
-    uint16_t* out0 = reinterpret_cast<uint16_t*>(outv) + r0 * ROW;
-    const uint32_t i = c * 8, sa = (i + F) & ~7u;
-    uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    if (sa + 16 > lim) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t lo = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
-        const uint32_t hh = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
-        w[k] = lo | (hh << 16);
-      }
-    }
-    u32x4 o;
-    if constexpr (REM % 2 == 0) {
-      o = u32x4{w[MM], w[MM + 1], w[MM + 2], w[MM + 3]};
-    } else {
-      o = u32x4{__builtin_amdgcn_alignbyte(w[MM + 1], w[MM], 2), __builtin_amdgcn_alignbyte(w[MM + 2], w[MM + 1], 2),
-                __builtin_amdgcn_alignbyte(w[MM + 3], w[MM + 2], 2), __builtin_amdgcn_alignbyte(w[MM + 4], w[MM + 3], 2)};
-    }
-    const uint32_t col0 = i - (i / ROW) * ROW;
-    if (col0 + 7 < ROW - F && i + 7 < lim) {
-      *reinterpret_cast<u32x4*>(out0 + i) = o;
-      return;
-    }
-    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t e = i + k;
-      if (e >= lim) break;
-      if (e - (e / ROW) * ROW < ROW - F) out0[e] = (uint16_t)(ow[k / 2] >> (16 * (k & 1)));
-    }
-  }
-}
-template <int U>
-__device__ __forceinline__ void shift_pre_issue(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int t0,
-                                                ShiftPre<U>& P) {
-  const int per = S.half ? 8 : 4, es = S.half ? 2 : 4;
-  const uint32_t no = r1 > r0 ? shift_nchunks<T1_NOBS, T1_HIST>(S.total_obs, r0, r1, per) : 0u;
-  const uint32_t np = r1 > r0 ? shift_nchunks<T1_NPRIV, T1_CHIST>(S.total_priv, r0, r1, per) : 0u;
-  P.olo = no * sl / nsl; P.ohi = no * (sl + 1) / nsl;
-  P.plo = np * sl / nsl; P.phi = np * (sl + 1) / nsl;
-#ifdef T1_WHATIF_D5_NO_SHIFT  // timing-only what-if build: the history is not shifted
-  P.ohi = P.olo; P.phi = P.plo;
-#endif
-  const uint8_t* oi = reinterpret_cast<const uint8_t*>(S.obs_in);
-  const uint8_t* pi = reinterpret_cast<const uint8_t*>(S.priv_in);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint32_t c = P.olo + t0 + u * D5_SHIFT_T;
-    if (P.olo + u * D5_SHIFT_T < P.ohi)  // wave-uniform guard; lanes past the window load an in-bounds dummy
-      shift_src_ld<T1_NOBS, T1_HIST>(oi, S.total_obs, r0, c < P.ohi ? c : P.olo, per, es, P.a[u], P.b[u]);
-  }
-  if (P.plo < P.phi) {
-    const uint32_t c = P.plo + t0;
-    shift_src_ld<T1_NPRIV, T1_CHIST>(pi, S.total_priv, r0, c < P.phi ? c : P.plo, per, es, P.pa, P.pb);
-  }
-}
-template <bool HALF, int U>
-__device__ __forceinline__ void shift_pre_commit_t(const ShiftArgs& S, int64_t r0, int64_t r1, int t0, const ShiftPre<U>& P) {
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint32_t c = P.olo + t0 + u * D5_SHIFT_T;
-    if (c < P.ohi) shift_chunk_st<T1_NOBS, T1_HIST, HALF>(S.obs_in, S.obs_out, S.total_obs, r0, c, P.a[u], P.b[u]);
-  }
-  if (P.plo + t0 < P.phi)
-    shift_chunk_st<T1_NPRIV, T1_CHIST, HALF>(S.priv_in, S.priv_out, S.total_priv, r0, P.plo + t0, P.pa, P.pb);
-  // chunks past the batch (a window larger than U x D5_SHIFT_T / D5_SHIFT_T): one at a time
-  const int per = HALF ? 8 : 4, es = HALF ? 2 : 4;
-  for (uint32_t c = P.olo + t0 + U * D5_SHIFT_T; c < P.ohi; c += D5_SHIFT_T) {
-    u32x4 a, b;
-    shift_src_ld<T1_NOBS, T1_HIST>(reinterpret_cast<const uint8_t*>(S.obs_in), S.total_obs, r0, c, per, es, a, b);
-    shift_chunk_st<T1_NOBS, T1_HIST, HALF>(S.obs_in, S.obs_out, S.total_obs, r0, c, a, b);
-  }
-  for (uint32_t c = P.plo + t0 + D5_SHIFT_T; c < P.phi; c += D5_SHIFT_T) {
-    u32x4 a, b;
-    shift_src_ld<T1_NPRIV, T1_CHIST>(reinterpret_cast<const uint8_t*>(S.priv_in), S.total_priv, r0, c, per, es, a, b);
-    shift_chunk_st<T1_NPRIV, T1_CHIST, HALF>(S.priv_in, S.priv_out, S.total_priv, r0, c, a, b);
-  }
-}
-template <int U>
-__device__ __forceinline__ void shift_pre_commit(const ShiftArgs& S, int64_t r0, int64_t r1, int t0, const ShiftPre<U>& P) {
-  if (S.half) shift_pre_commit_t<true>(S, r0, r1, t0, P);
-  else shift_pre_commit_t<false>(S, r0, r1, t0, P);
-}
-#ifndef T1_D5_PRE_U
-#define T1_D5_PRE_U 13
-#endif
 
 // ---- the in-workgroup shift staged through LDS by LDS-DMA (global_load_lds, no VGPR destination): the source blocks
 // of substep s's slice are loaded at the end of substep s-1's post-S2 window (in the prologue for s = 0) and land while
@@ -641,12 +357,12 @@ __device__ __forceinline__ void shift_glds(const ShiftArgs& S, int64_t r0, int64
 // the last env and store nothing.  The substep log (tests only, LG.root != nullptr) is a run-time switch of the one
 // product code object, like k_dyn4's.
 // ---------------------------------------------------------------------------------------------------
-template <bool HF, bool FUSED>
+template <bool HF, bool FUSED, bool SH>
 __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ Mg, const t1env_config* __restrict__ Cp,
                                                    t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
                                                    t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA,
                                                    SubLog LG) {
-  __shared__ Dyn5Lds lds;
+  __shared__ typename Dyn5LdsT<SH>::type lds;
   {  // the model to LDS
     constexpr int NW = (int)(sizeof(DynModel) / 4);
     static_assert(sizeof(DynModel) % 4 == 0, "the model copies as words");
@@ -693,9 +409,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     int cb, ce;
     base_contact_range(M, leg, cb, ce);
     const float zero6[NLEG] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-#if !defined(T1_D5_SHIFT_PRE) && !defined(T1_D5_SHIFT_REGS)
-    shift_glds(S, r0, r1, 0, nsub, 0, lane, lds.ring, false);  // the first slice's DMA
-#endif
+    if constexpr (SH) shift_glds(S, r0, r1, 0, nsub, 0, lane, lds.ring, false);  // the first slice's DMA
     T1_PROF_MARK(0);
     for (int sub = 0; sub < nsub; ++sub) {
       __syncthreads();  // S1: the substep state published
@@ -738,31 +452,21 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
       }
       T1_PROF_MARK(4);
       put4(lds.w1, lane, v);
-#if !defined(T1_D5_SHIFT_PRE) && !defined(T1_D5_SHIFT_REGS)
-      shift_glds_retire();  // this substep's staged slice landed (issued a substep ago) before S2
-#endif
+      if constexpr (SH) shift_glds_retire();  // this substep's staged slice landed (issued a substep ago) before S2
       T1_PROF_MARK(5);
-#if defined(T1_D5_SHIFT_PRE)
-      ShiftPre<T1_D5_PRE_U> sp;
-      shift_pre_issue(S, r0, r1, sub, nsub, (int)threadIdx.x - 64, sp);
-#endif
       __syncthreads();  // S2: the terms published
       T1_PROF_MARK(6);
-#if defined(T1_D5_SHIFT_PRE)
-      shift_pre_commit(S, r0, r1, (int)threadIdx.x - 64, sp);
-#elif defined(T1_D5_SHIFT_REGS)
-      shift_slice(S, r0, r1, sub, nsub, (int)threadIdx.x - 64);
-#else
-      // this substep's staged slice (its DMA retired before S2), then the next slice's DMA
-      shift_glds(S, r0, r1, sub, nsub, wave - 1, lane, lds.ring, true);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring reads done before the DMA rewrites it
-      shift_glds(S, r0, r1, sub + 1, nsub, wave - 1, lane, lds.ring, false);
-#endif
+      if constexpr (SH) {
+        // this substep's staged slice (its DMA retired before S2), then the next slice's DMA
+        shift_glds(S, r0, r1, sub, nsub, wave - 1, lane, lds.ring, true);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring reads done before the DMA rewrites it
+        shift_glds(S, r0, r1, sub + 1, nsub, wave - 1, lane, lds.ring, false);
+      }
       T1_PROF_MARK(7);
     }
     lds.vib[lane] = vi_b;
     if (active) B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)] = vi_b;
-    __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
+    if constexpr (SH) __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
     __syncthreads();  // R1: the end-of-step state and episodes published
     T1_PROF_MARK(9);
     {  // the report's base-box force (leg-0 lanes: the whole box, the larger restitution set point of its halves)
@@ -789,7 +493,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     if constexpr (FUSED) {
       __syncthreads();  // the epilogue barrier
       T1_PROF_MARK(11);
-      fused_epilogue_staged<POST_A_STATE, NE5, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
+      fused_epilogue_staged<POST_A_STATE, NE5, SH>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
                                                      lds.act + NLEG);
     }
     T1_PROF_END();
@@ -806,9 +510,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     if constexpr (FUSED) stage_epilogue_inputs<NE5, 128>(B, N, (int)r0, (int)threadIdx.x - 128, lds.epi);
     const int bsh = 1 + 6 * leg + K_SHANK, bft = 1 + 6 * leg + K_FOOT;
     const int foot_c0 = M.contact_start[bft] + (wave == 2 ? 0 : T1_POINTS_PER_BODY / 2);
-#if !defined(T1_D5_SHIFT_PRE) && !defined(T1_D5_SHIFT_REGS)
-    shift_glds(S, r0, r1, 0, nsub, wave - 1, lane, lds.ring, false);  // the first slice's DMA
-#endif
+    if constexpr (SH) shift_glds(S, r0, r1, 0, nsub, wave - 1, lane, lds.ring, false);  // the first slice's DMA
     T1_PROF_MARK(0);
     for (int sub = 0; sub < nsub; ++sub) {
       __syncthreads();  // S1
@@ -878,33 +580,23 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
         }
         lds.amx[wave - 2][lane] = amax;
       }
-#if !defined(T1_D5_SHIFT_PRE) && !defined(T1_D5_SHIFT_REGS)
-      shift_glds_retire();  // this substep's staged slice landed (issued a substep ago) before S2
-#endif
+      if constexpr (SH) shift_glds_retire();  // this substep's staged slice landed (issued a substep ago) before S2
       T1_PROF_MARK(5);
-#if defined(T1_D5_SHIFT_PRE)
-      ShiftPre<T1_D5_PRE_U> sp;
-      shift_pre_issue(S, r0, r1, sub, nsub, (int)threadIdx.x - 64, sp);
-#endif
       __syncthreads();  // S2
       T1_PROF_MARK(6);
-#if defined(T1_D5_SHIFT_PRE)
-      shift_pre_commit(S, r0, r1, (int)threadIdx.x - 64, sp);
-#elif defined(T1_D5_SHIFT_REGS)
-      shift_slice(S, r0, r1, sub, nsub, (int)threadIdx.x - 64);
-#else
-      // this substep's staged slice (its DMA retired before S2), then the next slice's DMA
-      shift_glds(S, r0, r1, sub, nsub, wave - 1, lane, lds.ring, true);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring reads done before the DMA rewrites it
-      shift_glds(S, r0, r1, sub + 1, nsub, wave - 1, lane, lds.ring, false);
-#endif
+      if constexpr (SH) {
+        // this substep's staged slice (its DMA retired before S2), then the next slice's DMA
+        shift_glds(S, r0, r1, sub, nsub, wave - 1, lane, lds.ring, true);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring reads done before the DMA rewrites it
+        shift_glds(S, r0, r1, sub + 1, nsub, wave - 1, lane, lds.ring, false);
+      }
       T1_PROF_MARK(7);
     }
     if (wave == 2) {
       lds.vis[0][lane] = vi_sh;
       if (active) B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
     }
-    __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
+    if constexpr (SH) __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
     __syncthreads();  // R1: the end-of-step state and episodes published
     T1_PROF_MARK(9);
     {  // the contact-force report from the end-of-step state: W2 the terrain forces of its leg's shank and foot, W3
@@ -1186,7 +878,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
   if constexpr (FUSED) {
     __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
     T1_PROF_MARK(11);
-    fused_epilogue_staged<POST_A_REWARDS, NE5, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
+    fused_epilogue_staged<POST_A_REWARDS, NE5, SH>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
                                                      lds.act + NLEG);
   }
   T1_PROF_END();
@@ -1206,16 +898,22 @@ extern "C" int t1env_debug_phase_cycles5(unsigned long long* out, int reset) {
 
 int t1_launch_dyn5(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
                    const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
-                   const FusedArgs* fused, hipStream_t s, const SubLog* log) {
+                   const FusedArgs* fused, hipStream_t s, const SubLog* log, bool inwg_shift) {
   const int blocks = (num_envs + NE5 - 1) / NE5;
   const FusedArgs FA = fused ? *fused : FusedArgs{};
   const SubLog LG = log ? *log : SubLog{};
   const bool hf = T.type != 0;
   if (log && !fused) return (int)hipErrorInvalidValue;  // the substep log: fused steps only (the caller checks)
-#define T1_LAUNCH5(HF, FU) \
-  hipLaunchKernelGGL((k_dyn5<HF, FU>), dim3(blocks), dim3(D5_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, blocks, FA, LG)
-  if (fused) { if (hf) T1_LAUNCH5(true, true); else T1_LAUNCH5(false, true); }
-  else { if (hf) T1_LAUNCH5(true, false); else T1_LAUNCH5(false, false); }
+#define T1_LAUNCH5(HF, FU, SH) \
+  hipLaunchKernelGGL((k_dyn5<HF, FU, SH>), dim3(blocks), dim3(D5_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, blocks, FA, LG)
+  if (inwg_shift) {
+    if (fused) { if (hf) T1_LAUNCH5(true, true, true); else T1_LAUNCH5(false, true, true); }
+    else { if (hf) T1_LAUNCH5(true, false, true); else T1_LAUNCH5(false, false, true); }
+  } else {
+    if (fused) { if (hf) T1_LAUNCH5(true, true, false); else T1_LAUNCH5(false, true, false); }
+    else { if (hf) T1_LAUNCH5(true, false, false); else T1_LAUNCH5(false, false, false); }
+  }
 #undef T1_LAUNCH5
   return (int)hipGetLastError();
 }
+

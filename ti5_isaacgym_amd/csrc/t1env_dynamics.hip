@@ -614,7 +614,7 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
   T1_PROF_END();
 }
 
-int t1_dyn_waves_default() { return 4; }  // k_dyn5 opt-in (T1ENV_DYN_KERNEL=5) until validated on the GPU
+int t1_dyn_waves_default() { return 5; }  // k_dyn5 (T1ENV_DYN_KERNEL=4: k_dyn4, A/B)
 
 constexpr int MIN_SHIFT_BLOCKS = 64;
 bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg) {
@@ -629,7 +629,8 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
                        const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
                        const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s, bool shift_prelaunched,
                        const SubLog* log) {
-  if (cfg.waves == 5) return t1_launch_dyn5(d_model, d_cfg, B, T, actions, A, num_envs, S, fused, s, log);
+  if (cfg.waves == 5)  // the shift in the workgroup (d5_shift 0) or the caller's concurrent k_shift5 launch (1)
+    return t1_launch_dyn5(d_model, d_cfg, B, T, actions, A, num_envs, S, fused, s, log, cfg.d5_shift == 0);
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
   // history-shift workgroups: the workgroup slots the dynamics leave free (a k_dyn4 wave holds a whole SIMD's
   // registers: one workgroup per CU), at least MIN_SHIFT_BLOCKS; none when the caller ran the shift as its own

@@ -39,6 +39,8 @@ struct DynLaunch {
   int cus;           // compute units of the device (default history-shift grid)
   int shift_blocks;  // > 0: history-shift workgroups override (tuning)
   int shift_delay;   // in-launch shift workgroups start this many 100 MHz ticks late (T1ENV_SHIFT_DELAY; 0 = at once)
+  int d5_shift;      // k_dyn5's history shift: 0 = in the workgroup through LDS-DMA (default), 1 = a concurrent launch
+                     // on a second stream (k_shift5; T1ENV_D5_SHIFT=1, A/B: the same step time, r04e)
 };
 int t1_dyn_waves_default();
 
@@ -56,4 +58,7 @@ bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg);
 // k_dyn5 (t1env_dyn5.hip): the same contract as t1_launch_dynamics; each workgroup shifts its own history rows
 int t1_launch_dyn5(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const t1::Terrain& T,
                    const float* actions, const t1env_step_args& A, int num_envs, const t1::ShiftArgs& S,
-                   const FusedArgs* fused, hipStream_t s, const SubLog* log);
+                   const FusedArgs* fused, hipStream_t s, const SubLog* log, bool inwg_shift);
+// k_dyn5's history shift as its own launch (k_shift5), for a second stream beside k_dyn5 (d5_shift = 1); fused: the
+// unit handoff with the fused epilogue, else plain (k_post_b zeroes the reset rows)
+int t1_launch_shift5(const t1::ShiftArgs& S, const FusedArgs* fused, int num_envs, int cus, hipStream_t s);

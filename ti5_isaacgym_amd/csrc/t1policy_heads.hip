@@ -85,7 +85,16 @@ constexpr int ph_off(int l) {  // first step-tile of layer l in the fragment buf
   return o;
 }
 constexpr int PH_UNITS = ph_off(PH_NLAYER);          // 1,768 step-tiles
-constexpr int PH_FRAG_BYTES = PH_UNITS * 2 * 64 * 16;  // hi + lo, 64 lanes x 16 B: 3,620,864
+constexpr int ph_toff(int l) {  // first output tile of layer l (bias fragments)
+  int o = 0;
+  for (int i = 0; i < l; ++i) o += ph_nt(i);
+  return o;
+}
+constexpr int PH_TILES = ph_toff(PH_NLAYER);          // 90 output tiles
+// the weight fragments (hi + lo, 64 lanes x 16 B per step-tile), then each output tile's bias in the C/D layout
+// (4 x float4 per lane: [tile][quad][lane], register r of lane l = bias of row (r & 3) + 8 (r >> 2) + 4 (l >> 5))
+constexpr int PH_WFRAG_BYTES = PH_UNITS * 2 * 64 * 16;  // 3,620,864
+constexpr int PH_FRAG_BYTES = PH_WFRAG_BYTES + PH_TILES * 4 * 64 * 16;  // + 368,640
 
 struct PhParams {
   const float* w[PH_NLAYER];
@@ -158,9 +167,36 @@ __device__ __forceinline__ bool ph_pack_dispatch(const PhParams& P, h8* frag, in
   }
 }
 
+template <int L>
+__device__ __forceinline__ bool ph_pack_bias(const PhParams& P, float4* __restrict__ bf, int tile, int lane) {
+  if constexpr (L == PH_NLAYER) {
+    return false;
+  } else {
+    if (tile < ph_toff(L + 1)) {
+      const int nt = tile - ph_toff(L), h = lane >> 5;
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * nt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        // conv2 (L = 0): one bias per output channel, row = channel * 6 + position (the flatten order)
+        v[r] = row < PH_L[L].n ? P.b[L][L == 0 ? row / 6 : row] : 0.0f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bf[(tile * 4 + q) * 64 + lane] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      return true;
+    }
+    return ph_pack_bias<L + 1>(P, bf, tile, lane);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_heads_pack(PhParams P, h8* __restrict__ frag) {
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < PH_UNITS * 64; e += gridDim.x * blockDim.x)
-    ph_pack_dispatch<0>(P, frag, e >> 6, e & 63);
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < (PH_UNITS + PH_TILES) * 64; e += gridDim.x * blockDim.x) {
+    if (e < PH_UNITS * 64)
+      ph_pack_dispatch<0>(P, frag, e >> 6, e & 63);
+    else
+      ph_pack_bias<0>(P, reinterpret_cast<float4*>(reinterpret_cast<char*>(frag) + PH_WFRAG_BYTES),
+                      (e >> 6) - PH_UNITS, e & 63);
+  }
 }
 
 // ---- the forward kernel
@@ -182,7 +218,11 @@ union PhLds {
 
 __device__ __forceinline__ float ph_act(float v, int act) {
   if (act == ACT_RELU) return v > 0.0f ? v : 0.0f;
+#ifdef T1_HEADS_WHATIF_NOELU  // timing-only what-if build: ELU as ReLU
+  if (act == ACT_ELU) return v > 0.0f ? v : 0.0f;
+#else
   if (act == ACT_ELU) return v > 0.0f ? v : expm1f(v);
+#endif
   return v;
 }
 
@@ -226,43 +266,72 @@ struct PhOut {  // the global outputs (OUT_MEAN / OUT_VALUE layers)
 // one dense layer for this wave's output tiles nt = wave + 4 i: B fragments from `in` (LDS), A fragments streamed
 // from the packed buffer, result + bias through the activation into `out` (LDS, k-steps out0 + 2 nt + {0, 1}) or the
 // global outputs.  Waves past the layer's tile count recompute the last tile and store nothing.
-template <int L, int OUT>
+// the weight-fragment register ring of layer L: its loads run D k-steps ahead of their MFMAs through D + 1 slots
+// (about 16 x 96 MFMA cycles of cover over an L2 hit under load); its first D steps are issued during the previous
+// layer (ph_prologue), so no layer starts on an empty pipeline
+template <int L> struct PhRing {
+  static constexpr int NT = ph_nt(L), KS = PH_L[L].ks, T = (NT + PH_WAVES - 1) / PH_WAVES;
+  static constexpr int D0 = T >= 4 ? 4 : (T >= 2 ? 8 : 16);
+  static constexpr int D = D0 < KS ? D0 : KS - 1;
+  static constexpr int R = D + 1;
+  h8 w[R][T][2];
+};
+template <int L>
+__device__ __forceinline__ void ph_load(const h8* __restrict__ frag, PhRing<L>& rg, int slot, int s, int wave,
+                                        int lane) {
+  typedef PhRing<L> G;
+  constexpr int OFF = ph_off(L);
+#pragma unroll
+  for (int i = 0; i < G::T; ++i) {
+    const int nt = (wave + PH_WAVES * i) < G::NT ? wave + PH_WAVES * i : G::NT - 1;
+#ifdef T1_HEADS_WHATIF_NOLOAD  // timing-only what-if build: every fragment load hits the same 2 KB (L1)
+    const h8* w = frag + lane + (size_t)(((OFF + nt * G::KS + s) & 0) * 2) * 64;
+#else
+    const h8* w = frag + lane + (size_t)((OFF + nt * G::KS + s) * 2) * 64;
+#endif
+    rg.w[slot][i][0] = w[0];
+    rg.w[slot][i][1] = w[64];
+  }
+}
+template <int L>
+__device__ __forceinline__ void ph_prologue(const h8* __restrict__ frag, PhRing<L>& rg, int wave, int lane) {
+#pragma clang loop unroll(full)
+  for (int s = 0; s < PhRing<L>::D; ++s) ph_load<L>(frag, rg, s, s, wave, lane);
+}
+
+// one dense layer for this wave's output tiles nt = wave + 4 i: B fragments from `in` (LDS), A fragments through
+// the ring rg (prologue already issued), result + bias through the activation into `out` (LDS, k-steps
+// out0 + 2 nt + {0, 1}) or the global outputs.  LN >= 0: layer LN's prologue is issued into *nx before this layer's
+// epilogue.  Waves past the layer's tile count recompute the last tile and store nothing.
+template <int L, int OUT, int LN>
 __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhParams& P, const Frag* in, Frag* out,
-                                         int out0, const PhOut& G, int wave, int lane) {
+                                         int out0, const PhOut& G, int wave, int lane, PhRing<L>& rg,
+                                         PhRing<(LN < 0 ? L : LN)>* nx) {
   constexpr Layer Y = PH_L[L];
-  constexpr int NT = ph_nt(L), KS = Y.ks, T = (NT + PH_WAVES - 1) / PH_WAVES, OFF = ph_off(L);
-  // fragment loads run D k-steps ahead of their MFMAs (~8 x 96 cycles of MFMAs in flight over an L2 hit), through a
-  // ring of D + 1 register slots; the B fragments one step ahead
-  constexpr int D0 = T >= 4 ? 2 : (T >= 2 ? 4 : 8);
-  constexpr int D = D0 < KS ? D0 : KS - 1;
-  constexpr int R = D + 1;
+  typedef PhRing<L> RG;
+  constexpr int NT = RG::NT, KS = RG::KS, T = RG::T, D = RG::D, R = RG::R;
   const int h = lane >> 5;
   f16v acc0[T], acc1[T];
 #pragma unroll
   for (int i = 0; i < T; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc0[i][r] = acc1[i][r] = 0.0f;
-  const h8* wl = frag + lane;
-  int ntc[T];
-#pragma unroll
-  for (int i = 0; i < T; ++i) ntc[i] = (wave + PH_WAVES * i) < NT ? wave + PH_WAVES * i : NT - 1;
-  h8 wr[R][T][2];
-  auto load = [&](int slot, int s) {
-#pragma unroll
-    for (int i = 0; i < T; ++i) {
-      const h8* w = wl + (size_t)((OFF + ntc[i] * KS + s) * 2) * 64;
-      wr[slot][i][0] = w[0];
-      wr[slot][i][1] = w[64];
-    }
-  };
-#pragma clang loop unroll(full)
-  for (int s = 0; s < D; ++s) load(s, s);
+  float4 bias[T][4];
   h8 bq[2][2];
   bq[0][0] = in[0][0][lane];
   bq[0][1] = in[0][1][lane];
 #pragma clang loop unroll(full)
   for (int s = 0; s < KS; ++s) {
-    if (s + D < KS) load((s + D) % R, s + D);
+    if (s + D < KS) ph_load<L>(frag, rg, (s + D) % R, s + D, wave, lane);
+    if (s == KS - 1 - D) {  // the bias fragments behind the layer's last weight loads (no drain at the epilogue)
+      const float4* bf = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(frag) + PH_WFRAG_BYTES);
+#pragma unroll
+      for (int i = 0; i < T; ++i) {
+        const int nt = (wave + PH_WAVES * i) < NT ? wave + PH_WAVES * i : NT - 1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bias[i][q] = bf[((ph_toff(L) + nt) * 4 + q) * 64 + lane];
+      }
+    }
     if (s + 1 < KS) {
       bq[(s + 1) & 1][0] = in[s + 1][0][lane];
       bq[(s + 1) & 1][1] = in[s + 1][1][lane];
@@ -271,13 +340,18 @@ __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhPa
     const h8 bh = bq[s & 1][0], bl = bq[s & 1][1];
 #pragma unroll
     for (int i = 0; i < T; ++i) {
-      const h8 ah = wr[s % R][i][0], al = wr[s % R][i][1];
+      const h8 ah = rg.w[s % R][i][0], al = rg.w[s % R][i][1];
+#ifdef T1_HEADS_WHATIF_NOMFMA  // timing-only what-if build: one MFMA per step-tile instead of three
+      acc0[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah + al, bh + bl, acc0[i], 0, 0, 0);
+#else
       acc0[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc0[i], 0, 0, 0);
       acc1[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc1[i], 0, 0, 0);
       acc1[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc1[i], 0, 0, 0);
+#endif
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if constexpr (LN >= 0) ph_prologue<LN>(frag, *nx, wave, lane);  // the next layer's first fragments in flight
 #pragma unroll
   for (int i = 0; i < T; ++i) {
     const int nt = wave + PH_WAVES * i;
@@ -285,8 +359,8 @@ __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhPa
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = 32 * nt + (r & 3) + 8 * (r >> 2) + 4 * h;  // C/D row of register r
-      const float b = row < Y.n ? P.b[L][row] : 0.0f;
+      const float4 b4 = bias[i][r >> 2];
+      const float b = (r & 3) == 0 ? b4.x : (r & 3) == 1 ? b4.y : (r & 3) == 2 ? b4.z : b4.w;
       v[r] = ph_act(acc0[i][r] + acc1[i][r] * (1.0f / PH_SPLIT) + b, Y.act);
     }
     if constexpr (OUT == OUT_LDS || OUT == OUT_LDS_HALF) {
@@ -348,38 +422,55 @@ void k_heads(PhParams P, const h8* __restrict__ frag, const float* __restrict__ 
     ActorLds& A = S.a;
     ph_stage<true>(A.p, 28, y1, PH_Y1, 0, PH_Y1, envc, live, wave, lane);                       // relu(conv1)
     ph_stage<false>(A.x, 15, obs, obs_cols, obs_cols - PH_OBS_SHORT, PH_OBS_SHORT, envc, live, wave, lane);
+    PhRing<0> g0;
+    ph_prologue<0>(frag, g0, wave, lane);  // the first layer's fragments load across the barrier
     __syncthreads();
-    ph_layer<0, OUT_LDS>(frag, P, A.p, A.q, 0, G, wave, lane);
+    PhRing<1> g1;
+    ph_layer<0, OUT_LDS, 1>(frag, P, A.p, A.q, 0, G, wave, lane, g0, &g1);
     __syncthreads();
-    ph_layer<1, OUT_LDS>(frag, P, A.q, A.p, 0, G, wave, lane);
+    PhRing<2> g2;
+    ph_layer<1, OUT_LDS, 2>(frag, P, A.q, A.p, 0, G, wave, lane, g1, &g2);
     __syncthreads();
-    ph_layer<2, OUT_LDS>(frag, P, A.p, A.x, 16, G, wave, lane);  // history code -> actor input steps 16..19
-    ph_layer<3, OUT_LDS>(frag, P, A.x, A.q, 0, G, wave, lane);   // reads steps 0..14 only: no barrier needed
+    PhRing<3> g3;
+    ph_layer<2, OUT_LDS, 3>(frag, P, A.p, A.x, 16, G, wave, lane, g2, &g3);  // history code -> actor input 16..19
+    PhRing<4> g4;
+    ph_layer<3, OUT_LDS, 4>(frag, P, A.x, A.q, 0, G, wave, lane, g3, &g4);  // reads steps 0..14 only: no barrier
     __syncthreads();
-    ph_layer<4, OUT_LDS>(frag, P, A.q, A.p, 0, G, wave, lane);
+    PhRing<5> g5;
+    ph_layer<4, OUT_LDS, 5>(frag, P, A.q, A.p, 0, G, wave, lane, g4, &g5);
     __syncthreads();
-    ph_layer<5, OUT_LDS>(frag, P, A.p, A.q, 0, G, wave, lane);
+    PhRing<6> g6;
+    ph_layer<5, OUT_LDS, 6>(frag, P, A.p, A.q, 0, G, wave, lane, g5, &g6);
     __syncthreads();
-    ph_layer<6, OUT_LDS_HALF>(frag, P, A.q, A.x, 15, G, wave, lane);  // estimate -> actor input step 15
+    PhRing<7> g7;
+    ph_layer<6, OUT_LDS_HALF, 7>(frag, P, A.q, A.x, 15, G, wave, lane, g6, &g7);  // estimate -> actor input 15
     __syncthreads();
-    ph_layer<7, OUT_LDS>(frag, P, A.x, A.p, 0, G, wave, lane);
+    PhRing<8> g8;
+    ph_layer<7, OUT_LDS, 8>(frag, P, A.x, A.p, 0, G, wave, lane, g7, &g8);
     __syncthreads();
-    ph_layer<8, OUT_LDS>(frag, P, A.p, A.q, 0, G, wave, lane);
+    PhRing<9> g9;
+    ph_layer<8, OUT_LDS, 9>(frag, P, A.p, A.q, 0, G, wave, lane, g8, &g9);
     __syncthreads();
-    ph_layer<9, OUT_LDS>(frag, P, A.q, A.p, 0, G, wave, lane);
+    PhRing<10> g10;
+    ph_layer<9, OUT_LDS, 10>(frag, P, A.q, A.p, 0, G, wave, lane, g9, &g10);
     __syncthreads();
-    ph_layer<10, OUT_MEAN>(frag, P, A.p, nullptr, 0, G, wave, lane);
+    ph_layer<10, OUT_MEAN, -1>(frag, P, A.p, nullptr, 0, G, wave, lane, g10, nullptr);
   } else {
     CriticLds& C = S.c;
     ph_stage<false>(C.q, 14, cobs, cobs_cols, 0, PH_CRITIC, envc, live, wave, lane);
+    PhRing<11> g11;
+    ph_prologue<11>(frag, g11, wave, lane);
     __syncthreads();
-    ph_layer<11, OUT_LDS>(frag, P, C.q, C.p, 0, G, wave, lane);
+    PhRing<12> g12;
+    ph_layer<11, OUT_LDS, 12>(frag, P, C.q, C.p, 0, G, wave, lane, g11, &g12);
     __syncthreads();
-    ph_layer<12, OUT_LDS>(frag, P, C.p, C.q, 0, G, wave, lane);
+    PhRing<13> g13;
+    ph_layer<12, OUT_LDS, 13>(frag, P, C.p, C.q, 0, G, wave, lane, g12, &g13);
     __syncthreads();
-    ph_layer<13, OUT_LDS>(frag, P, C.q, C.p, 0, G, wave, lane);
+    PhRing<14> g14;
+    ph_layer<13, OUT_LDS, 14>(frag, P, C.q, C.p, 0, G, wave, lane, g13, &g14);
     __syncthreads();
-    ph_layer<14, OUT_VALUE>(frag, P, C.p, nullptr, 0, G, wave, lane);
+    ph_layer<14, OUT_VALUE, -1>(frag, P, C.p, nullptr, 0, G, wave, lane, g14, nullptr);
   }
 }
 
@@ -415,7 +506,7 @@ int t1policy_heads_pack(const uint64_t* params, const int* dims, void* frag, voi
   if ((reinterpret_cast<uintptr_t>(frag) & 15u) != 0) return -1;
   PhParams P;
   if (!ph_params(params, P)) return -1;
-  hipLaunchKernelGGL(k_heads_pack, dim3((PH_UNITS * 64 + 255) / 256), dim3(256), 0, (hipStream_t)stream, P,
+  hipLaunchKernelGGL(k_heads_pack, dim3(((PH_UNITS + PH_TILES) * 64 + 255) / 256), dim3(256), 0, (hipStream_t)stream, P,
                      reinterpret_cast<h8*>(frag));
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -5,7 +5,7 @@ set -e
 tag=${1:-r04}
 kexpr=${2:-}
 out=gpurun_out/$tag
-export T1ENV_DYN_KERNEL=${KERNEL:-5}
+# (the dynamics kernel: the default, k_dyn5; the tests parametrize both)
 mkdir -p $out
 if [ -n "$kexpr" ]; then
   T1_PARITY_REPORT=$out/parity_report.json timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 200 \

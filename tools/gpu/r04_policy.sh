@@ -15,3 +15,4 @@ T1POLICY_HEADS_XCD=0 timeout -k 10 200 python tools/act_bench.py > $out/act_fuse
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o act -- python tools/act_bench.py --iters 100 > $out/prof.log 2>&1
 tail -3 $out/tests.log
 cat $out/act_fused.json $out/act_torch.json $out/act_fused_noxcd.json
+timeout -k 10 400 python tools/ppo_update_profile.py --bf16 --eager --rows 30 > $out/upd_prof_bf16_eager.txt 2>&1

@@ -62,10 +62,12 @@ def main():
     ka = prof.key_averages()
     print(ka.table(sort_by="self_cpu_time_total", row_limit=a.rows, max_name_column_width=60))
     print(ka.table(sort_by="self_device_time_total", row_limit=a.rows, max_name_column_width=60))
-    for e in prof.key_averages(group_by_input_shape=True):
-        if e.key in ("aten::bmm", "aten::mm", "aten::addmm"):
-            print(f"{e.key:12s} calls {e.count:4d} self cpu {e.self_cpu_time_total / max(e.count, 1):9.1f} us/call  "
-                  f"device {e.self_device_time_total / max(e.count, 1):8.1f} us/call  {e.input_shapes}")
+    rows = [e for e in prof.key_averages(group_by_input_shape=True) if e.key.startswith("aten::")
+            and e.self_device_time_total > 0]
+    rows.sort(key=lambda e: -e.self_device_time_total)
+    for e in rows[:60]:   # the device time by op and input shapes: where the casts, sums and GEMMs come from
+        print(f"{e.key:22s} calls {e.count:4d} device {e.self_device_time_total / 1e3:8.3f} ms total "
+              f"{e.self_device_time_total / max(e.count, 1):8.1f} us/call  {e.input_shapes}")
 
 
 if __name__ == "__main__":
