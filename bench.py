@@ -16,7 +16,7 @@ roofline: SURVEY.md §8(d): achieved = env_steps_per_s x B_alg (30,678 algorithm
 the 8 TB/s HBM3E peak; `traffic` = PMC-measured HBM bytes per step (profiles/traffic_*.json, tools/
 pmc_traffic.py).  Per-kernel durations are measured live with HIP events around each launch on every
 --time-every'th timed step (event records cost host time, so not on every step), with each kernel's own
-algorithmic bytes; the dominant kernel is k_dyn4, the whole fused step (latency-bound at one wave per SIMD).
+algorithmic bytes; the dominant kernel is k_dyn5, the whole fused step (latency-bound at one wave per SIMD).
 cpu_baseline: the build's CPU restatement (numpy oracle post-physics + OpenMP dynamics), rank 0, N = 1 only.
 """
 import argparse
@@ -35,12 +35,12 @@ B_ALG = 30678          # algorithmic bytes per env-step (fp32,
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SHADER_GHZ = 2.4       # MI355X peak engine clock
 LONE_WAVE_VALU_PER_CYCLE = 0.25  # one VALU instruction per 4 cycles for a wave alone on its SIMD (MI355X_MICROARCH.md,
-                                 # 'vector-instruction ISSUE cost'); k_dyn4 runs one wave per SIMD (363+ VGPRs)
+                                 # 'vector-instruction ISSUE cost'); k_dyn5 runs one wave per SIMD (405 registers)
 # timer slots of include/t1env.h: slot "k_dynamics" brackets the dynamics launch, which on a normal step is the
-# whole fused step (k_dyn4: dynamics + post-physics epilogue + history-shift workgroups, t1env_dynamics.hip);
+# whole fused step (k_dyn5: dynamics + in-workgroup history shift + post-physics epilogue, t1env_dyn5.hip);
 # k_post_a / k_post_b only launch on the split (command-curriculum, 1 in 2400) steps
 KERNELS = ["k_dynamics", "k_post_a", "k_post_b"]
-FUSED_KERNEL = "k_dynamics" if os.environ.get("T1ENV_DYN_WAVES") == "2" else "k_dyn4"
+FUSED_KERNEL = "k_dyn4" if os.environ.get("T1ENV_DYN_KERNEL") == "4" else "k_dyn5"
 # per-kernel algorithmic bytes per env (reads + writes it must do) for the split sequence
 SHIFT_BYTES = 2 * 4 * ((3102 - 47) + (219 - 73))
 KERNEL_BYTES = {

@@ -76,6 +76,7 @@ class DHPPO:
         # round as it does), and _lr_t, the fp32 value Adam reads, is refreshed from it
         self._lr_t = torch.tensor(float(learning_rate), device=device) if cuda else None
         self._lr64 = torch.tensor(float(learning_rate), dtype=torch.float64, device=device) if cuda else None
+        self._c15 = torch.tensor(1.5, dtype=torch.float64, device=device) if cuda else None
         if cuda:
             # fused: one kernel per step (the capturable foreach Adam ran ~0.75 ms per step, r03x)
             self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=self._lr_t, capturable=True, fused=True)
@@ -244,7 +245,9 @@ class DHPPO:
                 # target KL, lr * 1.5 capped at 1e-2 below half of it (a KL of exactly 0 keeps lr); the KL compared in
                 # fp32 as the reference's tensor comparisons, the lr stepped in fp64 as its Python float
                 lr = self._lr64
-                down = torch.clamp(lr / 1.5, min=1e-5)
+                # a tensor divisor: torch divides by a host scalar as a multiply by its reciprocal (one more rounding
+                # than the reference's Python lr / 1.5)
+                down = torch.clamp(lr / self._c15, min=1e-5)
                 up = torch.clamp(lr * 1.5, max=1e-2)
                 low = (kl_mean > 0.0) & (kl_mean < self.desired_kl / 2.0)
                 lr.copy_(torch.where(kl_mean > self.desired_kl * 2.0, down, torch.where(low, up, lr)))

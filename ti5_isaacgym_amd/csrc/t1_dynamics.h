@@ -979,6 +979,22 @@ T1_HD void body_contact_fixed(const DynModel& M, const Terrain& T, R lowest, int
   }
   vimp = restitution_episode(vimp, amax);
 }
+// body_contact_fixed with the terrain queries already issued (contact_query, possibly before the bound was known:
+// a speculative query costs the loads of a body that turns out to be out of reach, and saves the round trip the
+// bound test put between the bound's load and the heights' loads); the same operations in the same order
+template <bool HF, int NP, typename R>
+T1_HD void body_contact_fixed_q(const DynModel& M, const ContactQuery<NP, R>& Q, R lowest, int32_t bound_raw,
+                                const Terrain& T, const R Vb[6], R mu, R e, R& vimp, R dt, Sym6<R>& A, R g[6]) {
+  if (lowest > bound_height<R>(T, bound_raw)) {
+    vimp = R(0);  // cannot touch the terrain: no contact episode
+    return;
+  }
+  const R vtg = restitution_target(M, e, vimp);
+  R amax = R(-1);
+  if (t1_wave_any(vtg > R(0))) contact_apply<HF, NP>(M, Q, Vb, mu, vtg, dt, A, g, amax);
+  else contact_apply<HF, NP>(M, Q, Vb, mu, R(0), dt, A, g, amax);
+  vimp = restitution_episode(vimp, amax);
+}
 // body_contact_fixed for a body that is always evaluated (no height bound), with `between()` run after its terrain
 // queries are issued and before their heights are used (the helper's self-contact terms hide the load latency)
 template <int NP, typename R, typename Between>

@@ -1,5 +1,6 @@
-# round-4 A/B over environment settings of the product library: each argument is NAME=ENV (ENV: space-separated
-# VAR=value pairs, quoted), two interleaved rounds of bench.py, then optionally the k_dyn5 phase profile.
+# round-4 A/B over environment settings of the product library: each argument is NAME=ENV[|BENCH ARGS] (ENV:
+# space-separated VAR=value pairs, quoted), two interleaved rounds of bench.py, then optionally the k_dyn5 phase
+# profile.
 #   bash tools/gpu/r04_ab2.sh <tag> <phases 0|1> 'conc=T1ENV_DYN_KERNEL=5' 'inwg=T1ENV_DYN_KERNEL=5 T1ENV_D5_SHIFT=0' ...
 set -e
 tag=$1; shift
@@ -8,8 +9,9 @@ out=gpurun_out/$tag
 mkdir -p $out
 for r in 1 2; do
   for v in "$@"; do
-    name=${v%%=*}; envs=${v#*=}
-    env $envs timeout -k 10 120 python bench.py --steps 300 --warmup 50 --no-cpu-baseline --time-every 0 \
+    name=${v%%=*}; rest=${v#*=}
+    envs=${rest%%|*}; args=; [ "$rest" != "$envs" ] && args=${rest#*|}
+    env $envs timeout -k 10 120 python bench.py --steps 300 --warmup 50 --no-cpu-baseline --time-every 0 $args \
       > $out/$name.$r.json 2> $out/$name.$r.err
   done
 done

@@ -4,9 +4,10 @@
         --envs 8192 -o profiles/<tag>_sq_counters.json
 
 Per counter: the value summed over the kernel's per-SE instances of one dispatch, averaged over the dispatches
-of k_dyn4.  Derived ("Roofline"):
-  * valu_insts_per_dyn_wave: SQ_INSTS_VALU over the 4 ceil(N / 64) dynamics waves (the shift waves issue a few
-    hundred VALU each, so this slightly overstates a dynamics wave);
+of --kernel (k_dyn5, the default step kernel; k_dyn4).  Derived ("Roofline"):
+  * valu_insts_per_dyn_wave: SQ_INSTS_VALU over the dynamics waves: k_dyn5 4 ceil(N / 32) (four role waves per 32
+    envs, each also shifting history rows), k_dyn4 4 ceil(N / 64) (the shift waves issue a few hundred VALU each, so
+    this slightly overstates a dynamics wave);
   * kernel_cycles = SQ_BUSY_CYCLES / 32 shader engines (SQ_BUSY_CYCLES is summed over the SEs) and the effective
     shader clock = kernel_cycles / the traced mean duration of the same dispatches;
   * dyn_wave_issue_frac = 4 valu_insts_per_dyn_wave / kernel_cycles: a dynamics wave's VALU issue over the launch,
@@ -22,7 +23,7 @@ import json
 import sqlite3
 from collections import defaultdict
 
-KERNEL = "k_dyn4"
+KERNEL = "k_dyn5"
 NUM_SE = 32   # MI355X shader engines (MI355X_MICROARCH.md)
 
 
@@ -50,8 +51,11 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("dbs", nargs="+")
     p.add_argument("--envs", type=int, default=8192)
+    p.add_argument("--kernel", default="k_dyn5", choices=["k_dyn5", "k_dyn4"])
     p.add_argument("-o", "--out")
     a = p.parse_args()
+    global KERNEL
+    KERNEL = a.kernel
     vals, n, durs = {}, {}, []
     for db in a.dbs:
         v, k = collect(db)
@@ -61,7 +65,7 @@ def main():
             durs += durations_ns(db)
         except sqlite3.Error:
             pass
-    dyn_waves = 4 * ((a.envs + 63) // 64)
+    dyn_waves = 4 * ((a.envs + 31) // 32) if a.kernel == "k_dyn5" else 4 * ((a.envs + 63) // 64)
     d = {}
     if "SQ_INSTS_VALU" in vals:
         d["valu_insts_per_dyn_wave"] = vals["SQ_INSTS_VALU"] / dyn_waves
@@ -79,7 +83,7 @@ def main():
         d["valu_active_frac_all_waves"] = vals["SQ_ACTIVE_INST_VALU"] / vals["SQ_WAVE_CYCLES"]
     if "SQ_WAIT_ANY" in vals and "SQ_WAVE_CYCLES" in vals:
         d["wait_any_frac"] = vals["SQ_WAIT_ANY"] / vals["SQ_WAVE_CYCLES"]
-    out = {"kernel": KERNEL, "envs": a.envs, "dispatches": n, "counters": vals, "derived": d,
+    out = {"kernel": a.kernel, "envs": a.envs, "dispatches": n, "counters": vals, "derived": d,
            "sources": a.dbs}
     print(json.dumps(out, indent=1))
     if a.out:
