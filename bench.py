@@ -90,6 +90,32 @@ def parse():
     return p.parse_args()
 
 
+def effective_cores():
+    """The cores this process can use: its CPU affinity, capped by the cgroup CPU quota.  On the GPU box the affinity
+    lists every core of the host (256) while the job's cgroup grants a share of them (cpu.max, e.g. 16): 256 threads
+    on a 16-core quota ran the CPU baseline 3.5x slower than 16 (r04fa)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    quota = None
+    try:  # cgroup v2
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except Exception:
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except Exception:
+            quota = None
+    if quota is not None:
+        n = min(n, max(1, int(quota + 0.5)))
+    return n
+
+
 def cpu_baseline(env, args):
     """Bounded sample of the same workload on the host cores (the build's CPU restatement)."""
     from oracle.cpu_env import ShardedCpuT1Env
@@ -99,11 +125,8 @@ def cpu_baseline(env, args):
         terrain = {"terrain_origins": env._terrain.env_origins, "height_samples": env._terrain.heightsamples,
                    "horizontal_scale": tc.horizontal_scale, "vertical_scale": tc.vertical_scale,
                    "border_size": tc.border_size, "num_envs_total": args.cpu_envs}
-    try:
-        aff = len(os.sched_getaffinity(0))
-    except Exception:
-        aff = os.cpu_count()
-    # every core in this process's affinity (not the inherited OMP_NUM_THREADS): shards of the env on
+    aff = effective_cores()
+    # every core this process may run on (not the inherited OMP_NUM_THREADS): shards of the env on
     # Python threads (the numpy post-physics releases the GIL in its array kernels), each with cores / shards OpenMP
     # threads for its physics
     cpu = ShardedCpuT1Env(env._model, args.cpu_envs, cores=aff, shards=min(aff, args.cpu_shards), seed=5,
@@ -125,7 +148,7 @@ def cpu_baseline(env, args):
             "sample": f"{args.cpu_envs} envs x {n} steps ({dt:.1f} s), same cfg/terrain as the GPU run; "
                       f"{len(cpu.shards)} env shards on Python threads (numpy oracle PD + post-physics) with "
                       f"{cpu.threads() // len(cpu.shards)} OpenMP threads each for the fp32 dynamics: {cpu.threads()} "
-                      f"threads on the {aff} cores of this process's affinity, {model}"}
+                      f"threads on the {aff} cores this process may use (affinity capped by the cgroup CPU quota), {model}"}
 
 
 def main():
