@@ -40,7 +40,13 @@ LONE_WAVE_VALU_PER_CYCLE = 0.25  # one VALU instruction per 4 cycles for a wave 
 # whole fused step (k_dyn5: dynamics + in-workgroup history shift + post-physics epilogue, t1env_dyn5.hip);
 # k_post_a / k_post_b only launch on the split (command-curriculum, 1 in 2400) steps
 KERNELS = ["k_dynamics", "k_post_a", "k_post_b"]
-FUSED_KERNEL = "k_dyn4" if os.environ.get("T1ENV_DYN_KERNEL") == "4" else "k_dyn5"
+def fused_kernel(num_envs, cus=256):
+    """The step kernel t1env picks (t1_dyn_waves_default): k_dyn5 up to 32 envs per CU, k_dyn4 above; the
+    T1ENV_DYN_KERNEL override wins."""
+    k = os.environ.get("T1ENV_DYN_KERNEL")
+    if k in ("4", "5"):
+        return "k_dyn" + k
+    return "k_dyn5" if (num_envs + 31) // 32 <= cus else "k_dyn4"
 # per-kernel algorithmic bytes per env (reads + writes it must do; DESIGN.md §3) for the split sequence
 SHIFT_BYTES = 2 * 4 * ((3102 - 47) + (219 - 73))
 KERNEL_BYTES = {
@@ -83,9 +89,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--cpu-shards", type=int, default=32,
                    help="CPU baseline: env shards stepped on Python threads (at most the affinity's core count)")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r03fa2.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r04fa.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
-    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r03fa2_sq_counters.json"),
+    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r04fa_sq_counters.json"),
                    help="SQ instruction counters of the fused kernel (tools/pmc_sq_summary.py): the VALU-issue roofline")
     return p.parse_args()
 
@@ -214,6 +220,8 @@ def main():
     # at large N the history shift runs as its own launch ahead of the fused kernel (t1_shift_prelaunch)
     pre_shift = kt["k_shift"]["launches"] > 0
     per_kernel = {}
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count if torch.cuda.is_available() else 256
+    FUSED_KERNEL = fused_kernel(N, cus)
     for k in KERNELS + (["k_shift"] if pre_shift else []):
         ms = kt[k]["ms"] / max(1, kt[k]["launches"])
         if k == "k_shift":

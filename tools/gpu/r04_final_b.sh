@@ -12,3 +12,4 @@ timeout -k 10 200 $B --num-envs 16384 --mesh trimesh --no-cpu-baseline > $out/n1
 timeout -k 10 200 $B --num-envs 32768 --mesh heightfield --push --no-cpu-baseline > $out/cfg5_32768_hf_push_fp32.json 2> $out/cfg5a.err
 timeout -k 10 200 $B --num-envs 32768 --mesh heightfield --push --state-dtype fp16 --no-cpu-baseline > $out/cfg5_32768_hf_push_fp16.json 2> $out/cfg5b.err
 echo done
+timeout -k 10 300 python bench.py > gpurun_out/$1/bench_default.json 2> gpurun_out/$1/bench_default.err
