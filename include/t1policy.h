@@ -62,6 +62,27 @@ int t1policy_heads_forward(const uint64_t* params, const int* dims, const void* 
                            float* mean, float* actions, float* sigma, float* logp, float* value, int batch,
                            void* stream);
 
+/* The same first conv in the PPO update under the opt-in bf16 update (t1policy_train.hip), forward and weight
+ * gradient on bf16 inputs without the unfolded copy (the autograd path dh_policy.conv1d_as_gemm unfolds 545 MB per
+ * minibatch).  Shapes as t1policy_conv1d_forward (only 66/47/32/6/3 compiled; 1 otherwise).
+ *   pack_bf16      weight (out_channels, channels, kernel) fp32 -> frag (frag_bytes(), 16-byte aligned): bf16 (round
+ *                  to nearest even, as torch's .to(torch.bfloat16)) fragments
+ *   forward_bf16   x (batch, channels, length) bf16 -> y (batch, Lout, out_channels) bf16 = bf16(fp32 sum of the bf16
+ *                  products + bf16(bias)), autocast's addmm arithmetic; x 4-byte aligned
+ *   wgrad_bf16     grad_weight (out_channels, channels, kernel) fp32 = sum_{b,l} gy[b,l,o] x[b,c,stride l + t],
+ *                  grad_bias (out_channels) fp32 = sum gy, from gy (batch, Lout, out_channels) bf16; workspace of
+ *                  workspace_bytes() device bytes; the per-workgroup partials are summed in a fixed order
+ *                  (deterministic)
+ * Replaces the training-time nn.Conv1d forward / weight gradient at actor_critic_dh.py:83-96. */
+int t1policy_conv1_bf16_frag_bytes(void);
+int t1policy_conv1_bf16_workspace_bytes(void);
+int t1policy_conv1_pack_bf16(const float* weight, void* frag, int channels, int out_channels, int kernel, void* stream);
+int t1policy_conv1_forward_bf16(const void* x, const void* frag, const float* bias, void* y, int batch, int channels,
+                                int length, int out_channels, int kernel, int stride, void* stream);
+int t1policy_conv1_wgrad_bf16(const void* x, const void* gy, void* workspace, float* grad_weight, float* grad_bias,
+                              int batch, int channels, int length, int out_channels, int kernel, int stride,
+                              void* stream);
+
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py
  * _HistoryRows restates this in torch):

@@ -1,0 +1,68 @@
+"""The update's first history conv under the bf16 update as HIP kernels (t1policy_conv1_*_bf16,
+ti5_isaacgym_amd/csrc/t1policy_train.hip) against fp64 torch on the same bf16 operands -- needs the MI355X.
+
+forward: y = bf16(sum of the bf16 products + bf16(bias)) -- autocast's addmm arithmetic -- within one bf16 rounding of
+the fp64 value; weight / bias gradients: fp32 sums over every (sample, position) within 1e-3 relative of fp64, the
+same bits on a second run (the partials are summed in a fixed order, which the graphed == eager update relies on)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _conv():
+    torch.manual_seed(0)
+    return torch.nn.Conv1d(66, 32, kernel_size=6, stride=3).to(DEV)
+
+
+def _ref_forward(x, conv):
+    w = conv.weight.detach().to(torch.bfloat16).double()
+    b = conv.bias.detach().to(torch.bfloat16).double()
+    return torch.nn.functional.conv1d(x.double(), w, b, stride=3).transpose(1, 2)  # (B, 14, 32)
+
+
+@pytest.mark.parametrize("n", [1, 777, 8192])
+def test_conv1_bf16_forward_matches_fp64(n):
+    from ti5_isaacgym_amd.algo.dh_policy import conv1d_train_bf16
+    conv = _conv()
+    g = torch.Generator(device=DEV).manual_seed(n)
+    x = (torch.randn(n, 66, 47, device=DEV, generator=g) * 2.0).to(torch.bfloat16)
+    with torch.no_grad():
+        y = conv1d_train_bf16(x, conv)
+    assert y is not None and y.dtype == torch.bfloat16 and y.shape == (n, 14, 32)
+    ref = _ref_forward(x, conv)
+    # one bf16 rounding (2^-8 relative) of the fp32-accumulated value, plus the fp32 summation order
+    err = (y.double() - ref).abs()
+    assert (err <= ref.abs() * 2.0 ** -8 + 1e-4).all(), float((err - ref.abs() * 2.0 ** -8).max())
+
+
+@pytest.mark.parametrize("n", [777, 49152])
+def test_conv1_bf16_weight_gradient_matches_fp64(n):
+    from ti5_isaacgym_amd.algo.dh_policy import conv1d_train_bf16
+    conv = _conv()
+    g = torch.Generator(device=DEV).manual_seed(n + 1)
+    x = (torch.randn(n, 66, 47, device=DEV, generator=g) * 2.0).to(torch.bfloat16)
+    gy = torch.randn(n, 14, 32, device=DEV, generator=g).to(torch.bfloat16)
+    y = conv1d_train_bf16(x, conv)
+    y.backward(gy)
+    gw, gb = conv.weight.grad.clone(), conv.bias.grad.clone()
+    # fp64 reference on the same bf16 operands: gW[o, c, t] = sum_{b,l} gy[b,l,o] x[b,c,3l+t]
+    win = x.double().unfold(2, 6, 3)                       # (B, 66, 14, 6)
+    ref_w = torch.einsum("blo,bclt->oct", gy.double(), win)
+    ref_b = gy.double().sum((0, 1))
+    torch.testing.assert_close(gw.double(), ref_w, rtol=1e-3, atol=1e-3 * ref_w.abs().max().item() * 1e-2)
+    torch.testing.assert_close(gb.double(), ref_b, rtol=1e-3, atol=1e-2)
+    # deterministic: a second backward gives the same bits
+    conv.weight.grad = None
+    conv.bias.grad = None
+    conv1d_train_bf16(x, conv).backward(gy)
+    assert torch.equal(conv.weight.grad, gw) and torch.equal(conv.bias.grad, gb)
+
+
+def test_conv1_bf16_refuses_other_shapes():
+    from ti5_isaacgym_amd.algo.dh_policy import conv1d_train_bf16
+    conv = torch.nn.Conv1d(66, 16, kernel_size=6, stride=3).to(DEV)
+    x = torch.randn(4, 66, 47, device=DEV).to(torch.bfloat16)
+    assert conv1d_train_bf16(x, conv) is None
+    assert conv1d_train_bf16(x.float(), _conv()) is None

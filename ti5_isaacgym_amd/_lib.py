@@ -97,7 +97,9 @@ EXPORTS = ["t1env_create", "t1env_destroy", "t1env_init", "t1env_set_terrain", "
 # include/t1policy.h: the DH policy's HIP kernels, in the same library
 POLICY_EXPORTS = ["t1policy_conv1d_forward", "t1policy_history_rows", "t1policy_conv1d_frag_bytes",
                   "t1policy_conv1d_pack_weights", "t1policy_conv1d_forward_packed", "t1policy_heads_frag_bytes",
-                  "t1policy_heads_pack", "t1policy_heads_forward"]
+                  "t1policy_heads_pack", "t1policy_heads_forward", "t1policy_conv1_bf16_frag_bytes",
+                  "t1policy_conv1_bf16_workspace_bytes", "t1policy_conv1_pack_bf16", "t1policy_conv1_forward_bf16",
+                  "t1policy_conv1_wgrad_bf16"]
 
 _lib = None
 
@@ -139,6 +141,11 @@ def load():
         "t1policy_heads_frag_bytes": ([], C.c_int),
         "t1policy_heads_pack": ([vp, vp, vp, vp], C.c_int),
         "t1policy_heads_forward": ([vp, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, i32, vp], C.c_int),
+        "t1policy_conv1_bf16_frag_bytes": ([], C.c_int),
+        "t1policy_conv1_bf16_workspace_bytes": ([], C.c_int),
+        "t1policy_conv1_pack_bf16": ([vp, vp, i32, i32, i32, vp], C.c_int),
+        "t1policy_conv1_forward_bf16": ([vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
+        "t1policy_conv1_wgrad_bf16": ([vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -195,6 +195,78 @@ def refresh_packed_weights(module, force=False):
             packed_conv_weights(m, force=force)
 
 
+# the update's first history conv as HIP kernels under the bf16 update (T1_CONV1_TRAIN=0: unfold + GEMM, A/B)
+CONV1_TRAIN = os.environ.get("T1_CONV1_TRAIN", "1") != "0"
+
+
+def _conv1_train_call(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc})")
+
+
+class _HistoryConvBf16(torch.autograd.Function):
+    """The history encoder's first Conv1d in the PPO update on bf16 inputs (the opt-in bf16 update): the HIP forward
+    (t1policy_conv1_forward_bf16, channels-last (B, Lout, O) bf16, autocast's addmm arithmetic) and weight gradient
+    (t1policy_conv1_wgrad_bf16: fp32 sums in a fixed order), no unfolded copy of the input.  The input is the
+    observation history, which needs no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from .. import _lib
+        lib = _lib.load()
+        B, C, L = x.shape
+        O, _, K = weight.shape
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        frag = torch.empty(lib.t1policy_conv1_bf16_frag_bytes(), device=x.device, dtype=torch.uint8)
+        _conv1_train_call(lib.t1policy_conv1_pack_bf16(weight.detach().contiguous().data_ptr(), frag.data_ptr(), C, O, K,
+                                                       stream), "t1policy_conv1_pack_bf16")
+        lout = (L - K) // 3 + 1
+        y = torch.empty(B, lout, O, device=x.device, dtype=torch.bfloat16)
+        _conv1_train_call(lib.t1policy_conv1_forward_bf16(x.data_ptr(), frag.data_ptr(),
+                                                          bias.detach().contiguous().data_ptr(), y.data_ptr(), B, C, L,
+                                                          O, K, 3, stream), "t1policy_conv1_forward_bf16")
+        ctx.save_for_backward(x)
+        ctx.shape = (C, L, O, K)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _lib
+        lib = _lib.load()
+        x, = ctx.saved_tensors
+        C, L, O, K = ctx.shape
+        gy = gy.to(torch.bfloat16).contiguous()
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        ws = torch.empty(lib.t1policy_conv1_bf16_workspace_bytes(), device=x.device, dtype=torch.uint8)
+        gw = torch.empty(O, C, K, device=x.device, dtype=torch.float32)
+        gb = torch.empty(O, device=x.device, dtype=torch.float32)
+        _conv1_train_call(lib.t1policy_conv1_wgrad_bf16(x.data_ptr(), gy.data_ptr(), ws.data_ptr(), gw.data_ptr(),
+                                                        gb.data_ptr(), x.shape[0], C, L, O, K, 3, stream),
+                          "t1policy_conv1_wgrad_bf16")
+        return None, gw, gb
+
+
+def _bf16_operands(x):
+    """x reaches the conv's GEMM as bf16: already bf16 (the cast-once observations), or fp32 under a bf16 autocast."""
+    if x.dtype == torch.bfloat16:
+        return True
+    return (x.dtype == torch.float32 and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
+def conv1d_train_bf16(x, conv):
+    """The first history conv of the update on a bf16 (B, 66, 47) input as the HIP kernels (channels-last (B, 14, 32)
+    bf16 out), or None when the conv or the input is not that shape (the caller keeps unfold + GEMM)."""
+    if (conv.in_channels, conv.out_channels, conv.kernel_size[0], conv.stride[0]) != (66, 32, 6, 3) or \
+            x.dim() != 3 or x.shape[1:] != (66, 47) or x.dtype != torch.bfloat16 or conv.padding != (0,) or \
+            conv.dilation != (1,) or conv.groups != 1 or conv.bias is None:
+        return None
+    x = x.contiguous()
+    if x.data_ptr() % 4 != 0:
+        return None
+    return _HistoryConvBf16.apply(x, conv.weight, conv.bias)
+
+
 def _heads_layers(ac):
     """The fused heads kernel's 15 layers in its parameter order (include/t1policy.h t1policy_heads_*): the history
     encoder's second conv and its two Linears, the state estimator's four, the actor's four, the critic's four.  None
@@ -302,6 +374,9 @@ class HistoryEncoder(nn.Sequential):
                 y = None
                 if not last and not torch.is_grad_enabled() and x.dtype == torch.float32 and m.weight.dtype == x.dtype:
                     y = conv1d_direct(x, m)   # inference (the rollout's act()): the HIP direct conv
+                elif not last and torch.is_grad_enabled() and CONV1_TRAIN and _bf16_operands(x):
+                    # the bf16 update: the HIP forward + weight gradient on the bf16 operands autocast would make
+                    y = conv1d_train_bf16(x.to(torch.bfloat16), m)
                 x = y if y is not None else conv1d_as_gemm(x, m, channels_last=last)
                 last = True
             elif isinstance(m, nn.Flatten) and last:

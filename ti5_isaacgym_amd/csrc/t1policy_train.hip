@@ -1,0 +1,309 @@
+// The DH policy's first history conv in the PPO update under the opt-in bf16 update (include/t1policy.h,
+// t1policy_conv1_*_bf16): forward and weight gradient on the matrix cores, straight from the (B, 66, 47) bf16
+// observation history -- no unfolded (B x 14, 396) copy.
+//
+// The reference's layer (actor_critic_dh.py:83-96): nn.Conv1d(66 -> 32, kernel 6, stride 3) over the 47 features of
+// the 66 frames.  The build's autograd path ran it as unfold + GEMM (dh_policy.conv1d_as_gemm): at the update's
+// 49,152-sample minibatch a 545 MB unfold copy (310 us), a 688k x 396 GEMM (121 us) and a split-K weight-gradient
+// bmm + sum (199 + 32 us) per minibatch (profiles/r04p2_ppo_update_profile_bf16_eager.txt).  Here:
+//
+//   k_conv1_fwd_bf16    y[b, l, o] = bf16(bias[o] + sum_{c,t} w[o, c, t] x[b, c, 3 l + t]): per sample a (14 x 396) .
+//                       (396 x 32) product on v_mfma_f32_16x16x32_bf16 -- the inference conv's K order (8 slots per
+//                       channel: its 6 taps and 2 zeros, so a lane's A fragment is 6 contiguous inputs), the bf16
+//                       weight fragments in registers, each wave streaming a contiguous run of samples through its own
+//                       LDS rows.  As autocast's addmm: bf16 operands, fp32 accumulation, bias added as bf16 then one
+//                       rounding of the sum to bf16.
+//   k_conv1_wgrad_bf16  gW[o, c, t] = sum_{b, l} gy[b, l, o] x[b, c, 3 l + t], gb[o] = sum gy: per sample ONE k-step of
+//                       v_mfma_f32_32x32x16_bf16 (k = the 14 output positions + 2 zero rows) for each of the 13 32-column
+//                       tiles of the 396 (c, t) columns; a workgroup accumulates a run of samples in registers and
+//                       stores one fp32 partial; k_conv1_wgrad_reduce sums the partials in a fixed order
+//                       (deterministic, so eager and graph-replayed updates stay bit-identical).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int TC_C = 66, TC_L = 47, TC_O = 32, TC_K = 6, TC_S = 3, TC_LOUT = 14;
+constexpr int TC_STEPS = 17;                     // forward K-steps of 32: 4 channels each (66 + 2 zero channels)
+constexpr int TC_CPAD = 4 * TC_STEPS;            // 68 staged channel rows
+constexpr int TC_SAMPLE = TC_C * TC_L;           // 3,102 bf16 per sample
+constexpr int TC_FRAG_BYTES = TC_STEPS * 2 * 64 * 16;  // [step][column tile][lane] bf8: 34,816
+constexpr int TC_COLS = TC_C * TC_K;             // 396 weight-gradient columns (c, t)
+constexpr int TC_CT = (TC_COLS + 31) / 32;       // 13 column tiles of 32
+constexpr int TC_PART = TC_O * TC_CT * 32 + TC_O;  // partial floats per workgroup: 32 x 416 + 32 bias
+constexpr int TC_WG_BLOCKS = 512;                // weight-gradient workgroups (partials)
+
+__device__ __forceinline__ uint16_t bf16_bits(float v) {  // round to nearest even, as torch's .to(torch.bfloat16)
+  const uint32_t u = __float_as_uint(v);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));  // inf / nan
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_float(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
+
+// ---- forward weight fragments: lane l of (step s, column tile nt) holds B[k = 8 (l >> 4) + j][n = l & 15] =
+// bf16(w[o = 16 nt + (l & 15)][c = 4 s + (l >> 4)][t = j]) for j < 6, else 0 (the layout of t1policy.hip's fragments)
+__global__ __launch_bounds__(256) void k_conv1_pack_bf16(const float* __restrict__ w, uint16_t* __restrict__ frag) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= TC_STEPS * 2 * 64) return;
+  const int s = e >> 7, nt = (e >> 6) & 1, l = e & 63;
+  const int c = 4 * s + (l >> 4), o = 16 * nt + (l & 15);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    frag[(size_t)e * 8 + j] = (c < TC_C && j < TC_K) ? bf16_bits(w[(o * TC_C + c) * TC_K + j]) : (uint16_t)0;
+}
+
+// One wave per SIMD, four waves per workgroup, each wave a contiguous run of samples staged in its own LDS rows
+// (the next sample's loads in flight while the current one multiplies).
+constexpr int TF_WAVES = 4;
+constexpr int TF_PER_LANE = (TC_SAMPLE / 2 + 63) / 64;  // 25 32-bit words per lane (1,551 per sample)
+__global__ __launch_bounds__(64 * TF_WAVES) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void k_conv1_fwd_bf16(const uint16_t* __restrict__ x, const bf8* __restrict__ frag, const float* __restrict__ bias,
+                      uint16_t* __restrict__ y, int batch) {
+  __shared__ uint32_t XS[TF_WAVES][TC_CPAD * TC_L / 2 + 1];  // bf16 pairs; channels 66, 67 stay zero
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = blockIdx.x * TF_WAVES + wave, nw = gridDim.x * TF_WAVES;
+  const int b0 = (int)((long long)g * batch / nw), b1 = (int)((long long)(g + 1) * batch / nw);
+  uint32_t* X = XS[wave];
+  for (int i = TC_SAMPLE / 2 + lane; i < TC_CPAD * TC_L / 2 + 1; i += 64) X[i] = 0u;
+  bf8 bfr[TC_STEPS][2];
+#pragma unroll
+  for (int s = 0; s < TC_STEPS; ++s)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) bfr[s][nt] = frag[(s * 2 + nt) * 64 + lane];
+  float bo[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) bo[nt] = bf16_float(bf16_bits(bias[16 * nt + (lane & 15)]));
+  const uint32_t* xw = reinterpret_cast<const uint32_t*>(x);  // a sample is 6,204 B: 4-byte aligned
+  uint32_t pa[TF_PER_LANE];
+  auto load = [&](int bs) {
+    const uint32_t* src = xw + (size_t)(bs < b1 ? bs : b1 - 1) * (TC_SAMPLE / 2);
+#pragma unroll
+    for (int k = 0; k < TF_PER_LANE; ++k) {
+      const int i = lane + 64 * k;
+      pa[k] = src[i < TC_SAMPLE / 2 ? i : TC_SAMPLE / 2 - 1];
+    }
+  };
+  if (b0 < b1) load(b0);
+  const int r = lane & 15, kg = lane >> 4;
+  const int rr = r < TC_LOUT ? r : TC_LOUT - 1;  // rows 14, 15: row 13's inputs, never stored
+  const uint16_t* Xh = reinterpret_cast<const uint16_t*>(X);
+  for (int b = b0; b < b1; ++b) {
+#pragma unroll
+    for (int k = 0; k < TF_PER_LANE; ++k) {
+      const int i = lane + 64 * k;
+      if (i < TC_SAMPLE / 2) X[i] = pa[k];
+    }
+    load(b + 1);  // past the run: the run's last sample again (an L2 hit)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f4 acc[2] = {f4{0.0f, 0.0f, 0.0f, 0.0f}, f4{0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+    for (int s = 0; s < TC_STEPS; ++s) {
+      const uint16_t* row = Xh + (4 * s + kg) * TC_L + TC_S * rr;
+      typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+      u16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = j < TC_K ? row[j] : (uint16_t)0;
+      const bf8 a = __builtin_bit_cast(bf8, v);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[s][nt], acc[nt], 0, 0, 0);
+    }
+    // C/D: column lane & 15, rows 4 (lane >> 4) + i
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int o = 16 * nt + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int l = 4 * kg + i;
+        if (l < TC_LOUT) y[((size_t)b * TC_LOUT + l) * TC_O + o] = bf16_bits(acc[nt][i] + bo[nt]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next staging overwrites X after every lane's reads of it
+  }
+}
+
+// ---- weight gradient.  Workgroup g of TC_WG_BLOCKS: samples [b0, b1), staged one at a time into LDS (x: 3,102 bf16;
+// gy: 14 x 32 bf16), the next sample's loads in flight.  Wave w owns column tiles w, w + 4, w + 8, w + 12 (< 13):
+// A (32 x 16) = gy^T of the sample (rows o, k = output position l, rows 14, 15 zero), B (16 x 32) = the sample's
+// unfolded inputs x[c, 3 l + t] for the tile's 32 (c, t) columns.
+constexpr int TW_X = TC_SAMPLE / 2;       // 1,551 words
+constexpr int TW_G = TC_LOUT * TC_O / 2;  // 224 words
+constexpr int TW_LX = (TW_X + 255) / 256, TW_LG = (TW_G + 255) / 256;  // words per thread: 7, 1
+__global__ __launch_bounds__(256) void k_conv1_wgrad_bf16(const uint16_t* __restrict__ x,
+                                                          const uint16_t* __restrict__ gy, float* __restrict__ part,
+                                                          int batch) {
+  __shared__ uint32_t XS[2][TW_X + 1];
+  __shared__ uint32_t GS[2][TW_G];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, h = lane >> 5, n = lane & 31;
+  const int b0 = (int)((long long)blockIdx.x * batch / gridDim.x), b1 = (int)((long long)(blockIdx.x + 1) * batch / gridDim.x);
+  const uint32_t* xw = reinterpret_cast<const uint32_t*>(x);
+  const uint32_t* gw = reinterpret_cast<const uint32_t*>(gy);
+  uint32_t px[TW_LX], pg[TW_LG];
+  auto load = [&](int bs) {
+    const int bc = bs < b1 ? bs : b1 - 1;
+    const uint32_t* sx = xw + (size_t)bc * TW_X;
+    const uint32_t* sg = gw + (size_t)bc * TW_G;
+#pragma unroll
+    for (int k = 0; k < TW_LX; ++k) {
+      const int i = t + 256 * k;
+      px[k] = sx[i < TW_X ? i : TW_X - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < TW_LG; ++k) {
+      const int i = t + 256 * k;
+      pg[k] = sg[i < TW_G ? i : TW_G - 1];
+    }
+  };
+  // the tiles' (c, t) columns: col = 32 tile + n, c = col / 6, t = col % 6 (0 past the 396)
+  constexpr int TPW = (TC_CT + 3) / 4;  // 4 tiles per wave at most
+  int xoff[TPW];
+  bool xcol[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int col = 32 * (wave + 4 * i) + n;
+    xcol[i] = (wave + 4 * i) < TC_CT && col < TC_COLS;
+    const int cc = xcol[i] ? col / TC_K : 0, tt = xcol[i] ? col % TC_K : 0;
+    xoff[i] = cc * TC_L + tt;  // x[c, 3 l + t] = X[xoff + 3 l]
+  }
+  f16v acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[i][q] = 0.0f;
+  float gbs = 0.0f;  // sum of this lane's gy values (o = n, positions 8 h .. 8 h + 7)
+  if (b0 < b1) load(b0);
+  int buf = 0;
+  for (int b = b0; b < b1; ++b, buf ^= 1) {
+#pragma unroll
+    for (int k = 0; k < TW_LX; ++k) {
+      const int i = t + 256 * k;
+      if (i < TW_X) XS[buf][i] = px[k];
+    }
+#pragma unroll
+    for (int k = 0; k < TW_LG; ++k) {
+      const int i = t + 256 * k;
+      if (i < TW_G) GS[buf][i] = pg[k];
+    }
+    load(b + 1);
+    __syncthreads();  // staged (double-buffered: the sample before last's readers are done)
+    const uint16_t* Xh = reinterpret_cast<const uint16_t*>(XS[buf]);
+    const uint16_t* Gh = reinterpret_cast<const uint16_t*>(GS[buf]);
+    typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+    // A: lane (o = n, h) holds gy[b, l = 8 h + j, o], zero for l >= 14
+    u16x8 av;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int l = 8 * h + j;
+      av[j] = l < TC_LOUT ? Gh[l * TC_O + n] : (uint16_t)0;
+      gbs += bf16_float(av[j]);
+    }
+    const bf8 a = __builtin_bit_cast(bf8, av);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      if (wave + 4 * i >= TC_CT) break;  // wave-uniform
+      // B: lane (column n, h) holds x[c, 3 (8 h + j) + t], zero for positions >= 14 and past the 396 columns
+      u16x8 bv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int l = 8 * h + j;
+        bv[j] = (l < TC_LOUT && xcol[i]) ? Xh[xoff[i] + TC_S * l] : (uint16_t)0;
+      }
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(bf8, bv), acc[i], 0, 0, 0);
+    }
+  }
+  // the partial: [o][tile * 32 + n] (C/D: column n, row o = (q & 3) + 8 (q >> 2) + 4 h), then the 32 bias sums
+  float* P = part + (size_t)blockIdx.x * TC_PART;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    if (wave + 4 * i >= TC_CT) break;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int o = (q & 3) + 8 * (q >> 2) + 4 * h;
+      P[(size_t)o * (TC_CT * 32) + 32 * (wave + 4 * i) + n] = acc[i][q];
+    }
+  }
+  if (wave == 0) {
+    gbs += __shfl_xor(gbs, 32);  // the two position halves of column o = n
+    if (h == 0) P[TC_O * TC_CT * 32 + n] = gbs;
+  }
+}
+
+// gW[o, c, t] (the (32, 66, 6) fp32 weight layout) and gb[o]: the partials summed in workgroup order
+__global__ __launch_bounds__(256) void k_conv1_wgrad_reduce(const float* __restrict__ part, int parts,
+                                                            float* __restrict__ gw, float* __restrict__ gb) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= TC_O * TC_COLS + TC_O) return;
+  int src;
+  if (e < TC_O * TC_COLS) {
+    const int o = e / TC_COLS, col = e % TC_COLS;
+    src = o * (TC_CT * 32) + col;
+  } else {
+    src = TC_O * TC_CT * 32 + (e - TC_O * TC_COLS);
+  }
+  float s = 0.0f;
+  for (int g = 0; g < parts; ++g) s += part[(size_t)g * TC_PART + src];
+  if (e < TC_O * TC_COLS) gw[e] = s;
+  else gb[e - TC_O * TC_COLS] = s;
+}
+
+bool tc_shape(int channels, int length, int out_channels, int kernel, int stride) {
+  return channels == TC_C && length == TC_L && out_channels == TC_O && kernel == TC_K && stride == TC_S;
+}
+
+}  // namespace
+
+extern "C" {
+
+int t1policy_conv1_bf16_frag_bytes(void) { return TC_FRAG_BYTES; }
+
+int t1policy_conv1_bf16_workspace_bytes(void) { return TC_WG_BLOCKS * TC_PART * 4; }
+
+int t1policy_conv1_pack_bf16(const float* weight, void* frag, int channels, int out_channels, int kernel,
+                             void* stream) {
+  if (!weight || !frag) return -1;
+  if (!tc_shape(channels, TC_L, out_channels, kernel, TC_S)) return 1;
+  if ((reinterpret_cast<uintptr_t>(frag) & 15u) != 0) return -1;
+  hipLaunchKernelGGL(k_conv1_pack_bf16, dim3((TC_STEPS * 2 * 64 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     weight, reinterpret_cast<uint16_t*>(frag));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_conv1_forward_bf16(const void* x, const void* frag, const float* bias, void* y, int batch, int channels,
+                                int length, int out_channels, int kernel, int stride, void* stream) {
+  if (!x || !frag || !bias || !y || batch < 0) return -1;
+  if (!tc_shape(channels, length, out_channels, kernel, stride)) return 1;
+  if (batch == 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 3u) != 0 || (reinterpret_cast<uintptr_t>(frag) & 15u) != 0) return -1;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+      hipSuccess || cus <= 0) return -2;
+  const long long need = ((long long)batch + TF_WAVES - 1) / TF_WAVES;
+  const int grid = (int)(need < 2LL * cus ? need : 2LL * cus);
+  hipLaunchKernelGGL(k_conv1_fwd_bf16, dim3(grid), dim3(64 * TF_WAVES), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const bf8*>(frag), bias,
+                     reinterpret_cast<uint16_t*>(y), batch);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_conv1_wgrad_bf16(const void* x, const void* gy, void* workspace, float* grad_weight, float* grad_bias,
+                              int batch, int channels, int length, int out_channels, int kernel, int stride,
+                              void* stream) {
+  if (!x || !gy || !workspace || !grad_weight || !grad_bias || batch <= 0) return -1;
+  if (!tc_shape(channels, length, out_channels, kernel, stride)) return 1;
+  if ((reinterpret_cast<uintptr_t>(x) & 3u) != 0 || (reinterpret_cast<uintptr_t>(gy) & 3u) != 0) return -1;
+  const int parts = batch < TC_WG_BLOCKS ? batch : TC_WG_BLOCKS;
+  float* part = reinterpret_cast<float*>(workspace);
+  hipLaunchKernelGGL(k_conv1_wgrad_bf16, dim3(parts), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(gy), part, batch);
+  hipLaunchKernelGGL(k_conv1_wgrad_reduce, dim3((TC_O * TC_COLS + TC_O + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, part, parts, grad_weight, grad_bias);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"
