@@ -83,6 +83,13 @@ int t1policy_conv1_wgrad_bf16(const void* x, const void* gy, void* workspace, fl
                               int batch, int channels, int length, int out_channels, int kernel, int stride,
                               void* stream);
 
+/* Column sums of a (rows, cols) row-major gradient, bf16 (elem_bytes 2) or fp32 (4): out[c] = sum_r g[r, c] in fp32,
+ * in a fixed order (workspace of colsum_workspace_bytes(rows, cols) device bytes): the PPO update's Linear bias
+ * gradients (gy.sum(0) in dh_policy._LinearSplitK; torch's dim-0 sum ran 8-32 us per call at 49,152 rows).
+ * Returns 0, -1 on bad arguments, -2 on a launch error. */
+int t1policy_colsum_workspace_bytes(int rows, int cols);
+int t1policy_colsum(const void* g, int elem_bytes, int rows, int cols, void* workspace, float* out, void* stream);
+
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py
  * _HistoryRows restates this in torch):

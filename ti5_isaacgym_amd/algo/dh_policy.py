@@ -72,6 +72,29 @@ def wgrad_splitk(gy, x):
     return gw
 
 
+# the Linear bias gradients as the HIP column sum (opt-in, T1_BIAS_COLSUM=1): measured slower than torch's dim-0 sum
+# in the graphed update (bf16 update 39.8 vs 38.1 ms per iteration, profiles/r04q3_*), so torch's stays the default
+BIAS_COLSUM = os.environ.get("T1_BIAS_COLSUM", "0") == "1"
+
+
+def bias_grad(gy):
+    """gy.sum(0) of a (K, M) gradient: on the device the HIP column sum (t1policy_colsum: fp32 accumulation in a fixed
+    order, an fp32 result for the fp32 bias), on the host torch's."""
+    if not (gy.is_cuda and BIAS_COLSUM and gy.dim() == 2 and gy.dtype in (torch.bfloat16, torch.float32)):
+        return gy.sum(0)
+    from .. import _lib
+    lib = _lib.load()
+    gy = gy.contiguous()
+    K, M = gy.shape
+    ws = torch.empty(lib.t1policy_colsum_workspace_bytes(K, M), device=gy.device, dtype=torch.uint8)
+    out = torch.empty(M, device=gy.device, dtype=torch.float32)
+    rc = lib.t1policy_colsum(gy.data_ptr(), gy.element_size(), K, M, ws.data_ptr(), out.data_ptr(),
+                             torch.cuda.current_stream(gy.device).cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"t1policy_colsum failed (rc={rc})")
+    return out
+
+
 class _LinearSplitK(torch.autograd.Function):
     # custom_fwd / custom_bwd: under torch.autocast (the opt-in bf16 update) the GEMMs run in the autocast dtype in
     # both passes; autograd casts the returned gradients to the fp32 parameters' dtype
@@ -88,7 +111,7 @@ class _LinearSplitK(torch.autograd.Function):
         gy = gy.contiguous()
         gx = gy.mm(w) if ctx.needs_input_grad[0] else None
         gw = wgrad_splitk(gy, x) if ctx.needs_input_grad[1] else None
-        gb = gy.sum(0) if ctx.needs_input_grad[2] else None
+        gb = bias_grad(gy) if ctx.needs_input_grad[2] else None
         return gx, gw, gb
 
 

@@ -252,6 +252,48 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_reduce(const float* __restr
   else gb[e - TC_O * TC_COLS] = s;
 }
 
+// ---- column sums of a (rows, cols) gradient (the Linear bias gradients gy.sum(0) of the PPO update: 49,152 rows),
+// fp32 accumulation in a fixed order: stage 1, block (column group of 64, chunk of CS_ROWS rows) -> partial; stage 2,
+// the chunks summed in order
+constexpr int CS_ROWS = 256;  // rows per stage-1 block: 49,152 rows -> 192 chunks (768 blocks at 256 columns)
+template <typename T> __device__ __forceinline__ float cs_load(const T* p);
+template <> __device__ __forceinline__ float cs_load<uint16_t>(const uint16_t* p) { return bf16_float(*p); }
+template <> __device__ __forceinline__ float cs_load<float>(const float* p) { return *p; }
+template <typename T>
+__global__ __launch_bounds__(256) void k_colsum_part(const T* __restrict__ g, int rows, int cols, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * CS_ROWS, r1 = r0 + CS_ROWS < rows ? r0 + CS_ROWS : rows;
+  // rows rg, rg + 4, ... of the chunk: 8 independent loads and partial sums in flight, combined in a fixed order
+  float s8[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  if (c < cols) {
+    for (int r = r0 + rg; r < r1; r += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rr = r + 4 * u;
+        s8[u] += rr < r1 ? cs_load<T>(g + (size_t)rr * cols + c) : 0.0f;
+      }
+    }
+  }
+  const float s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < cols)
+    part[(size_t)blockIdx.y * cols + c] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+__global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ part, int chunks, int cols,
+                                                      float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  int k = 0;
+  for (; k + 4 <= chunks; k += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s4[u] += part[(size_t)(k + u) * cols + c];
+  for (; k < chunks; ++k) s4[0] += part[(size_t)k * cols + c];
+  out[c] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+}
+
 bool tc_shape(int channels, int length, int out_channels, int kernel, int stride) {
   return channels == TC_C && length == TC_L && out_channels == TC_O && kernel == TC_K && stride == TC_S;
 }
@@ -303,6 +345,29 @@ int t1policy_conv1_wgrad_bf16(const void* x, const void* gy, void* workspace, fl
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(gy), part, batch);
   hipLaunchKernelGGL(k_conv1_wgrad_reduce, dim3((TC_O * TC_COLS + TC_O + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, part, parts, grad_weight, grad_bias);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_colsum_workspace_bytes(int rows, int cols) {
+  if (rows <= 0 || cols <= 0) return -1;
+  return ((rows + CS_ROWS - 1) / CS_ROWS) * cols * 4;
+}
+
+int t1policy_colsum(const void* g, int elem_bytes, int rows, int cols, void* workspace, float* out, void* stream) {
+  if (!g || !workspace || !out || rows <= 0 || cols <= 0) return -1;
+  const int chunks = (rows + CS_ROWS - 1) / CS_ROWS;
+  const dim3 grid((cols + 63) / 64, chunks);
+  float* part = reinterpret_cast<float*>(workspace);
+  if (elem_bytes == 2)
+    hipLaunchKernelGGL(k_colsum_part<uint16_t>, grid, dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint16_t*>(g), rows, cols, part);
+  else if (elem_bytes == 4)
+    hipLaunchKernelGGL(k_colsum_part<float>, grid, dim3(256), 0, (hipStream_t)stream, reinterpret_cast<const float*>(g),
+                       rows, cols, part);
+  else
+    return -1;
+  hipLaunchKernelGGL(k_colsum_final, dim3((cols + 255) / 256), dim3(256), 0, (hipStream_t)stream, part, chunks, cols,
+                     out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
