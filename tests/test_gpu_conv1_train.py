@@ -70,12 +70,12 @@ def test_conv1_bf16_refuses_other_shapes():
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("rows,cols", [(49152, 256), (49152, 3), (777, 768)])
-def test_bias_colsum_matches_fp64(rows, cols, dtype):
+def test_bias_colsum_matches_fp64(rows, cols, dtype, monkeypatch):
     """The update's Linear bias gradients (dh_policy.bias_grad, t1policy_colsum): fp32 sums in a fixed order, within
     fp32 summation error of an fp64 sum, the same bits on a second call."""
     from ti5_isaacgym_amd.algo import dh_policy
     from ti5_isaacgym_amd.algo.dh_policy import bias_grad
-    dh_policy.BIAS_COLSUM = True   # the opt-in kernel (torch's sum is the default)
+    monkeypatch.setattr(dh_policy, "BIAS_COLSUM", True)   # the opt-in kernel (torch's sum is the default)
     g = torch.Generator(device=DEV).manual_seed(rows + cols)
     gy = torch.randn(rows, cols, device=DEV, generator=g).to(dtype)
     out = bias_grad(gy)
@@ -83,4 +83,3 @@ def test_bias_colsum_matches_fp64(rows, cols, dtype):
     ref = gy.double().sum(0)
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-3)
     assert torch.equal(bias_grad(gy), out)
-    dh_policy.BIAS_COLSUM = False
