@@ -23,6 +23,9 @@
 // OWN 32 rows, a slice per substep on W1-W3 while W0 runs its post-S2 chain (those waves would wait for the next state
 // anyway).  The epilogue of the same workgroup then writes the newest frames and zeroes its reset rows itself: no
 // cross-workgroup handoff, no sc1 stores, no prelaunched shift at any N.
+//
+// The fused epilogue (post-physics of the workgroup's 32 envs, t1env_fused.h) runs on all four waves: W0 the rewards
+// and the reset rows, W1 the state stores and reset_idx, W2 the privileged frame and last_* rows, W3 the actor frame.
 #include <hip/hip_runtime.h>
 
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py --kernel 5): lane 0 of every wave accumulates shader-clock deltas
@@ -672,8 +675,15 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
         }
       }
     }
-    if constexpr (FUSED) __syncthreads();  // the epilogue barrier
-    T1_PROF_MARK(11);
+    if constexpr (FUSED) {
+      __syncthreads();  // the epilogue barrier
+      T1_PROF_MARK(11);
+      if (wave == 2)
+        fused_epilogue_obs<POST_OBS_PRIV, NE5>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
+      else
+        fused_epilogue_obs<POST_OBS_ACTOR, NE5>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
+      T1_PROF_MARK(15);
+    }
     T1_PROF_END();
     return;
   }

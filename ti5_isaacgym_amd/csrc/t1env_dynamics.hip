@@ -411,7 +411,15 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
       helper_report_contacts_at<DYN_ENVS>(M, T, B, F, Ko, fself, n, leg, mu, vt, vt_base, lane, active, FR);
     }
     T1_PROF_MARK(11);
-    if constexpr (FUSED) __syncthreads();  // the epilogue barrier
+    if constexpr (FUSED) {
+      __syncthreads();  // the epilogue barrier
+      if (leg == 0)
+        fused_epilogue_obs<POST_OBS_PRIV, DYN_ENVS>(M, C, B, A, lane, lds.epi, FR, lds.cap[0] + CAP_ACT,
+                                                    lds.cap[1] + CAP_ACT);
+      else
+        fused_epilogue_obs<POST_OBS_ACTOR, DYN_ENVS>(M, C, B, A, lane, lds.epi, FR, lds.cap[0] + CAP_ACT,
+                                                     lds.cap[1] + CAP_ACT);
+    }
     T1_PROF_END();
     return;
   }

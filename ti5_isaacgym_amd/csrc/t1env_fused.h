@@ -290,12 +290,13 @@ __device__ __forceinline__ void stage_epilogue_inputs(const t1env_buffers& B, in
   epi_stage_store<NE, NT>(N, nb, t, V, E);
 }
 
-// The fused step's post-physics for the NE envs of one workgroup, run by two waves (lane = env; lanes >= NE shadow
-// an env of the workgroup and store nothing): every input from LDS (fresh outputs FR, staged state E, the clipped
-// actions in ACT0 (joints 0-5) / ACT1 (joints 6-11)).  Both waves run post_a's callback + termination prefix; PART =
-// POST_A_REWARDS then the 24 rewards, their stores and extras sums and the reset rows, POST_A_STATE the state
-// stores, post_b (reset_idx, observations, newest history frame) and the terrain-level sum.  After one barrier the
-// rewards wave signals completion (the extras finaliser).
+// The fused step's post-physics for the NE envs of one workgroup, run by four waves after the epilogue barrier (lane =
+// env; lanes >= NE shadow an env of the workgroup and store nothing), every input from LDS (fresh outputs FR, staged
+// state E, the clipped actions in ACT0 (joints 0-5) / ACT1 (joints 6-11)).  This function is the two post_a waves:
+// both run post_a's callback + termination prefix; PART = POST_A_REWARDS then the 24 rewards, their stores and extras
+// sums and the reset rows, POST_A_STATE the state stores, reset_idx of the resetting envs (their new state, commands
+// redrawn) and the terrain-level sum.  The observations are the other two waves' (fused_epilogue_obs).  After one
+// barrier the rewards wave signals completion (the extras finaliser).
 template <int PART, int NE, bool INWG>
 __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                                       const t1env_step_args& A, const ShiftArgs& S,
@@ -367,34 +368,16 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
     T1_PROF_MARK(15);
     return;
   }
-  if (active) {
-    ObsIn O;
+  if (active && do_reset) {  // reset_idx (post_b's first half): the new state; the observation waves take its inputs
+    const uint32_t genv = (uint32_t)(C.env_offset + n);
+    const uint32_t ctr = A.counter + 1u;
+    const float pos_cmd[4] = {X.root[0], X.root[1], X.cmd[0], X.cmd[1]};
+    reset_env(M, C, B, A, n, genv, ctr, true, /*zero_reward_state=*/false, /*obs_elsewhere=*/true, pos_cmd);
+    ObsIn O;  // the new gait times (the reset's draws again), then the commands redrawn at the new episode's start
 #pragma unroll
     for (int i = 0; i < 4; ++i) O.cmd[i] = X.cmd[i];
-#pragma unroll
-    for (int i = 0; i < 24; ++i) O.dof[i] = X.dof[i];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) { O.act[i] = X.a[i]; O.la[i] = X.la[i]; }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) O.rv[i] = X.root[7 + i];
-    O.bq = bq;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) O.gt[i] = X.gt[i];
-    O.el = X.el;
-    O.pl = X.pl;
-    O.gstart = X.gstart;
-    O.dl = __float_as_int(E[E_DL][e]);
-    O.il = __float_as_int(E[E_IL][e]);
-    ObsExtra Ex;
-    Ex.ef[0] = X.ef[0]; Ex.ef[1] = X.ef[1];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) Ex.et[i] = X.et[i];
-    Ex.cfz[0] = X.c0[2]; Ex.cfz[1] = X.c1[2];
-    Ex.fric = E[E_FRIC][e];
-    Ex.mass = E[E_MASS][e];
-#ifndef T1_WHATIF_EPI_NO_POSTB  // timing-only what-if build: no reset / observations
-    post_b_core(M, C, B, A, n, do_reset, do_reset, O, Ex, /*zero_reward_state=*/false);
-#endif
+    reset_obs_inputs(M, C, rng_key(C.seed, genv, ctr), O, /*dof=*/false);
+    if (resample_commands_r(C, A, O.el, O.gt, O.cmd, genv, ctr)) strow(B.commands + n * 4, O.cmd);
   }
   T1_PROF_MARK(14);
   // the terrain-level sum reads the levels reset_idx may just have changed
@@ -402,6 +385,95 @@ __device__ __forceinline__ void fused_epilogue_staged(const DynModel& M, const t
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();  // E2
   T1_PROF_MARK(15);
+}
+
+// The fused step's observation writers (the helper waves after the epilogue barrier): PART = POST_OBS_PRIV the
+// privileged frame, ref_dof_pos and the last_* rows, POST_OBS_ACTOR the actor frame (post_b's compute_observations,
+// legged_robot.py:490-502, t1:368-481).  Each wave runs the part of post_a's callback + termination prefix it needs on
+// the same LDS inputs (deterministic: the values the state wave computes) and takes a resetting env's new inputs from
+// its reset draws (reset_obs_inputs), so neither waits for the state wave's stores; none of their rows is written by
+// another wave.  No wave-wide operations: lanes without an env leave at once.
+template <int PART, int NE>
+__device__ __forceinline__ void fused_epilogue_obs(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                                   const t1env_step_args& A, int lane, const float (*E)[NE],
+                                                   const float (*FR)[NE], const float (*ACT0)[NE],
+                                                   const float (*ACT1)[NE]) {
+  static_assert(PART == POST_OBS_PRIV || PART == POST_OBS_ACTOR, "an observation part");
+  constexpr bool PRIV = PART == POST_OBS_PRIV;
+  const int e = lane % NE;
+  const int n = (int)blockIdx.x * NE + lane;
+  if (lane >= NE || n >= C.num_envs) return;
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  const uint32_t ctr = A.counter + 1u;
+  const RngKey K = rng_key(C.seed, genv, ctr);
+  float ld[24], lraw[8];
+  if constexpr (!PRIV)  // issued first: the lagged samples are the actor wave's only memory reads
+    load_lagged(B, A, n, __float_as_int(E[E_DL][e]), __float_as_int(E[E_IL][e]), ld, lraw);
+  ObsIn O;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) O.cmd[i] = E[E_CMD + i][e];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) O.gt[i] = __float_as_int(E[E_GT + i][e]);
+  const int64_t el = (int64_t)(((uint64_t)(uint32_t)__float_as_int(E[E_EL + 1][e]) << 32) |
+                               (uint32_t)__float_as_int(E[E_EL][e])) + 1;
+  const int64_t pl = (int64_t)(((uint64_t)(uint32_t)__float_as_int(E[E_PL + 1][e]) << 32) |
+                               (uint32_t)__float_as_int(E[E_PL][e])) + 1;
+  O.gstart = E[E_GS][e];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) O.dof[i] = FR[F_DOF + i][e];
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) { O.act[k] = ACT0[k][e]; O.act[NLEG + k] = ACT1[k][e]; }
+  ObsExtra Ex;
+  if constexpr (PRIV) {  // post_a's prefix: base quantities of the step's root state, then the callback
+    float root[13], ef[3], et[3], af[3];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) root[i] = FR[F_ROOT + i][e];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { ef[i] = E[E_EF + i][e]; et[i] = E[E_ET + i][e]; }
+#pragma unroll
+    for (int i = 0; i < 12; ++i) O.la[i] = E[E_LA + i][e];
+    base_quantities_r(root, O.bq);
+    bool ext_store;
+    post_callback(C, A, genv, ctr, K, el, O.gt, O.cmd, root, ef, et, af, ext_store);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) O.rv[i] = root[7 + i];
+    Ex.ef[0] = ef[0]; Ex.ef[1] = ef[1];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Ex.et[i] = et[i];
+    Ex.cfz[0] = FR[F_C0 + 2][e]; Ex.cfz[1] = FR[F_C1 + 2][e];
+    Ex.fric = E[E_FRIC][e];
+    Ex.mass = E[E_MASS][e];
+  } else {
+    resample_commands_r(C, A, el, O.gt, O.cmd, genv, ctr);  // the only part of the callback the actor frame reads
+  }
+  // check_termination (legged_robot.py:509-517), as post_a_core
+  const bool term = norm3(FR[F_CFB][e], FR[F_CFB + 1][e], FR[F_CFB + 2][e]) > 1.0f;
+  const bool tout = (float)el > C.max_episode_length;
+  const bool do_reset = term || tout;
+  O.el = el;
+  O.pl = is_stand(C, O.cmd) ? 0 : pl;  // post_a's _get_phase zeroing (the state wave stores it)
+  if (do_reset) {
+    reset_obs_inputs(M, C, K, O, /*dof=*/PRIV);
+    resample_commands_r(C, A, O.el, O.gt, O.cmd, genv, ctr);
+    if constexpr (!PRIV) {
+#pragma unroll
+      for (int i = 0; i < 24; ++i) ld[i] = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lraw[i] = 0.0f;
+    }
+  }
+  const bool stand = is_stand(C, O.cmd);
+  if (stand) O.pl = 0;
+  ObsPhase P;
+  obs_phase(M, C, O, stand, P);
+  if constexpr (PRIV) {
+    store_priv_frame(M, C, B, A, n, O, Ex, P);
+    store_obs_last(B, n, O, P.ref);
+  } else {
+    float li[6];
+    imu_sample(lraw, li);
+    store_actor_frame(M, C, B, A, n, K, O, ld, li, P);
+  }
 }
 
 // the Gym root-state row (pos, quat xyzw, COM linear velocity, angular velocity; world) of the internal base state

@@ -227,6 +227,42 @@ __device__ __forceinline__ void load_post_a_in(const t1env_buffers& B, size_t N,
   X.gstart = B.gait_start[n];
 }
 
+// ---- _post_physics_step_callback (t1_dh_stand_env.py:179-215) on an env's registers: the commands redrawn at gait
+// slots (el: the incremented episode step), pushes into root's velocities, the external force and torque; af = the
+// force applied this step, ext_store = whether ef / et changed.  Returns whether the commands changed.
+__device__ __forceinline__ bool post_callback(const t1env_config& C, const t1env_step_args& A, uint32_t genv,
+                                              uint32_t ctr, RngKey K, int64_t el, const int32_t gt[3], float cmd[4],
+                                              float root[13], float ef[3], float et[3], float af[3], bool& ext_store) {
+  const bool cmd_dirty = resample_commands_r(C, A, el, gt, cmd, genv, ctr);
+  if (A.push_call) {  // _push_robots (t1:217-231): drawn every call (is_first_push reset is commented out)
+    root[7] = rand_float(-C.push_vel_xy, C.push_vel_xy, K, SLOT_PUSH_VEL + 0);
+    root[8] = rand_float(-C.push_vel_xy, C.push_vel_xy, K, SLOT_PUSH_VEL + 1);
+    root[10] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 0);
+    root[11] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 1);
+    root[12] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 2);
+  }
+  af[0] = af[1] = af[2] = 0.0f;
+  ext_store = true;
+  if (A.ext_force_call) {  // _add_ext_force (t1:233-247)
+    if (A.ext_force_first) {
+      ef[0] = rand_float(-C.ext_force_max[0] / 2, C.ext_force_max[0], K, SLOT_EXT_FORCE + 0);
+      ef[1] = rand_float(-C.ext_force_max[1], C.ext_force_max[1], K, SLOT_EXT_FORCE + 1);
+      ef[2] = rand_float(-C.ext_force_max[2], C.ext_force_max[2], K, SLOT_EXT_FORCE + 2);
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        et[k] = rand_float(-C.ext_torque_max, C.ext_torque_max, K, SLOT_EXT_TORQUE + k);
+    } else {
+      const float st = is_stand(C, cmd) ? 1.0f : 0.0f;
+      af[0] = ef[0] * st; af[1] = ef[1] * st; af[2] = ef[2] * st;
+      ext_store = false;
+    }
+  } else {
+    ef[0] = ef[1] = ef[2] = 0.0f;
+    et[0] = et[1] = et[2] = 0.0f;
+  }
+  return cmd_dirty;
+}
+
 // Called by a whole wave (the extras sums are wave reductions); lane = env n0 (lanes past num_envs shadow the
 // last env).  Returns this env's reset decision; on return X holds the post-callback state (root after a push,
 // resampled commands, incremented episode / phase counters, external force and torque) and bq the base
@@ -236,7 +272,7 @@ __device__ __forceinline__ void load_post_a_in(const t1env_buffers& B, size_t N,
 // state, extras sums) and zeroes the reward state of resetting envs itself; POST_A_STATE runs the same prefix
 // and the state-owned stores (counters, base quantities, commands, push, external force, reset / time-out
 // flags) for the wave that continues with post_b.  The prefix is deterministic, so both waves agree.
-enum : int { POST_A_ALL = 0, POST_A_REWARDS = 1, POST_A_STATE = 2 };
+enum : int { POST_A_ALL = 0, POST_A_REWARDS = 1, POST_A_STATE = 2, POST_OBS_PRIV = 3, POST_OBS_ACTOR = 4 };
 template <int PART = POST_A_ALL>
 __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
                                             const t1env_step_args& A, int n0, PostAIn& X, BaseQ& bq,
@@ -289,34 +325,9 @@ __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_confi
     euler_xyz(q1, fe + 3);
   }
   T1_PROF_MARK(16);
-  // ---- _post_physics_step_callback (t1_dh_stand_env.py:179-215)
-  const bool cmd_dirty = resample_commands_r(C, A, el, gt, cmd, genv, ctr);
-  if (A.push_call) {  // _push_robots (t1:217-231): drawn every call (is_first_push reset is commented out)
-    root[7] = rand_float(-C.push_vel_xy, C.push_vel_xy, K, SLOT_PUSH_VEL + 0);
-    root[8] = rand_float(-C.push_vel_xy, C.push_vel_xy, K, SLOT_PUSH_VEL + 1);
-    root[10] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 0);
-    root[11] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 1);
-    root[12] = rand_float(-C.push_ang, C.push_ang, K, SLOT_PUSH_ANG + 2);
-  }
-  float af[3] = {0.0f, 0.0f, 0.0f};
-  bool ext_store = true;
-  if (A.ext_force_call) {  // _add_ext_force (t1:233-247)
-    if (A.ext_force_first) {
-      ef[0] = rand_float(-C.ext_force_max[0] / 2, C.ext_force_max[0], K, SLOT_EXT_FORCE + 0);
-      ef[1] = rand_float(-C.ext_force_max[1], C.ext_force_max[1], K, SLOT_EXT_FORCE + 1);
-      ef[2] = rand_float(-C.ext_force_max[2], C.ext_force_max[2], K, SLOT_EXT_FORCE + 2);
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-        et[k] = rand_float(-C.ext_torque_max, C.ext_torque_max, K, SLOT_EXT_TORQUE + k);
-    } else {
-      const float st = is_stand(C, cmd) ? 1.0f : 0.0f;
-      af[0] = ef[0] * st; af[1] = ef[1] * st; af[2] = ef[2] * st;
-      ext_store = false;
-    }
-  } else {
-    ef[0] = ef[1] = ef[2] = 0.0f;
-    et[0] = et[1] = et[2] = 0.0f;
-  }
+  float af[3];
+  bool ext_store;
+  const bool cmd_dirty = post_callback(C, A, genv, ctr, K, el, gt, cmd, root, ef, et, af, ext_store);
   T1_PROF_MARK(17);
   // ---- check_termination (legged_robot.py:509-517)
   const bool term = norm3(cfb[0], cfb[1], cfb[2]) > 1.0f;
@@ -580,23 +591,62 @@ struct ObsIn {
 // =====================================================================================================
 // reset_idx for one env (t1_dh_stand_env.py:483-559 + legged_robot.py:604-651, 732-783, 1076-1120, 1138-1158)
 // =====================================================================================================
+// The observation inputs of an env that reset_idx restarts, from its draws alone (the slots reset_env below draws
+// them from): joint positions, zero actions, the initial root velocity and its base quantities (the root's position
+// does not enter them), gait start and times, lag lengths; el = pl = 0.  cmd is left as it is.  The fused epilogue's
+// observation waves take a resetting env's inputs from here while another wave stores its new state.
+__device__ __forceinline__ void reset_obs_inputs(const DynModel& M, const t1env_config& C, RngKey K, ObsIn& X,
+                                                 bool dof = true) {
+  if (dof)  // _reset_dofs (dof = false: not drawn, for a caller that does not read them)
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      X.dof[2 * j] = M.default_dof_pos[j] + rand_float(-C.reset_dof_range, C.reset_dof_range, K, SLOT_RESET_DOF + j);
+      X.dof[2 * j + 1] = 0.0f;
+    }
+#pragma unroll
+  for (int j = 0; j < 12; ++j) { X.act[j] = 0.0f; X.la[j] = 0.0f; }
+  float r[13];  // _reset_root_states without the origin / xy offsets (position only)
+#pragma unroll
+  for (int i = 0; i < 13; ++i) r[i] = M.base_init_state[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) X.rv[i] = r[7 + i];
+  base_quantities_r(r, X.bq);  // (t1:548-552) reads the quaternion and velocities only
+  X.dl = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, K, SLOT_LAG_DOF);
+  X.il = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, K, SLOT_LAG_IMU);
+  X.gstart = (float)rand_int(0, 2, K, SLOT_GAIT_START) * 0.5f;
+  float g[3];  // generate_gait_time (t1:109-124)
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    g[i] = rand_float(C.gait_time_range[i][0], C.gait_time_range[i][1], K, SLOT_GAIT_TIME + i);
+  const float gs = (g[0] + g[1]) + g[2];
+  const float f = C.max_episode_length / gs;
+  const float s0 = g[0] * f, s1 = g[1] * f;
+  X.gt[0] = 0;
+  X.gt[1] = (int32_t)(0.0f + s0);
+  X.gt[2] = (int32_t)((0.0f + s0) + s1);
+  X.el = 0;
+  X.pl = 0;
+}
+
 // zero_reward_state = false: the caller's reward pass zeroes feet_air_time and the episode sums itself (the fused
 // epilogue, where that pass runs on another wave concurrently: post_a_core<POST_A_REWARDS>)
-// X != nullptr: the new state's observation inputs are also returned in X from registers (post_b_core), instead of
-// being read back from the rows just written -- the same values (stores and loads do not change them), one dependent
-// memory round trip less; X->cmd is left as it is (reset_idx does not touch the commands)
-__device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B, const t1env_step_args& A,
+// (the new state's observation inputs: reset_obs_inputs, from the same draws, instead of reading back the rows just
+// written -- one dependent memory round trip less)
+// obs_elsewhere: the last_* rows are left to the wave that writes the observations (the fused epilogue's post_b
+// stores them after the reset, with the values reset_obs_inputs gives; two waves storing one row would race)
+// pos_cmd: the env's root position (x, y) and commands as they stand (the caller's registers) instead of memory
+__device__ __forceinline__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_buffers& B, const t1env_step_args& A,
                           int n, uint32_t genv, uint32_t ctr, bool do_terrain, bool zero_reward_state = true,
-                          ObsIn* X = nullptr) {
+                          bool obs_elsewhere = false, const float* pos_cmd = nullptr) {
   const RngKey K = rng_key(C.seed, genv, ctr);
   float org[3];
   bool org_known = false;
   if (do_terrain && C.terrain_curriculum) {  // _update_terrain_curriculum
-    const float* r = B.root_states + n * 13;
+    const float* r = pos_cmd ? pos_cmd : B.root_states + n * 13;
     const float* o = B.env_origins + n * 3;
     const float dist = norm2(r[0] - o[0], r[1] - o[1]);
     const bool up = dist > C.env_length / 2.0f;
-    const float* cmd = B.commands + n * 4;
+    const float* cmd = pos_cmd ? pos_cmd + 2 : B.commands + n * 4;
     const bool down = (dist < norm2(cmd[0], cmd[1]) * (C.episode_length_s * 0.5f)) && !up;
     int lv = B.terrain_levels[n] + (up ? 1 : 0) - (down ? 1 : 0);
     const int rnd = rand_int(0, C.num_terrain_rows, K, SLOT_TERRAIN_LEVEL_RAND);
@@ -613,17 +663,14 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   if (!org_known)
 #pragma unroll
     for (int i = 0; i < 3; ++i) org[i] = B.env_origins[n * 3 + i];
+  ObsIn R;
+  reset_obs_inputs(M, C, K, R);
   // the new episode starts in the air as far as restitution is concerned (no contact episode carried over)
 #pragma unroll
   for (int i = 0; i < NVIMP; ++i) B.contact_vimp[(size_t)n * NVIMP + i] = 0.0f;
   // _reset_dofs
 #pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    const float dp = M.default_dof_pos[j] + rand_float(-C.reset_dof_range, C.reset_dof_range, K, SLOT_RESET_DOF + j);
-    B.dof_state[n * 24 + 2 * j] = dp;
-    B.dof_state[n * 24 + 2 * j + 1] = 0.0f;
-    if (X) { X->dof[2 * j] = dp; X->dof[2 * j + 1] = 0.0f; }
-  }
+  for (int j = 0; j < 24; ++j) B.dof_state[n * 24 + j] = R.dof[j];
   // _reset_root_states (in registers, then stored)
   float r[13];
 #pragma unroll
@@ -658,20 +705,21 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   for (int i = 0; i < 16; ++i) B.imu_hist[(size_t)n * 16 + i] = 0.0f;
 #endif
   B.lag_timestep[n] = rand_int(C.lag_range[0], C.lag_range[1] + 1, K, SLOT_LAG_ACTION);
-  const int dl = rand_int(C.dof_lag_range[0], C.dof_lag_range[1] + 1, K, SLOT_LAG_DOF);
-  const int il = rand_int(C.imu_lag_range[0], C.imu_lag_range[1] + 1, K, SLOT_LAG_IMU);
-  B.dof_lag_timestep[n] = dl;
-  B.imu_lag_timestep[n] = il;
+  B.dof_lag_timestep[n] = R.dl;
+  B.imu_lag_timestep[n] = R.il;
   // buffers
 #pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    B.last_last_actions[n * 12 + j] = 0.0f;
-    B.actions[n * 12 + j] = 0.0f;
-    B.last_actions[n * 12 + j] = 0.0f;
-    B.last_dof_vel[n * 12 + j] = 0.0f;
-  }
+  for (int j = 0; j < 12; ++j) B.actions[n * 12 + j] = 0.0f;
+  if (!obs_elsewhere) {
 #pragma unroll
-  for (int i = 0; i < 6; ++i) B.last_root_vel[n * 6 + i] = 0.0f;
+    for (int j = 0; j < 12; ++j) {
+      B.last_last_actions[n * 12 + j] = 0.0f;
+      B.last_actions[n * 12 + j] = 0.0f;
+      B.last_dof_vel[n * 12 + j] = 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) B.last_root_vel[n * 6 + i] = 0.0f;
+  }
   if (zero_reward_state) {
     B.feet_air_time[n * 2 + 0] = 0.0f;
     B.feet_air_time[n * 2 + 1] = 0.0f;
@@ -679,42 +727,14 @@ __device__ void reset_env(const DynModel& M, const t1env_config& C, const t1env_
   B.episode_length_buf[n] = 0;
   B.phase_length_buf[n] = 0;
   B.reset_buf[n] = 1;
-  const float gstart = (float)rand_int(0, 2, K, SLOT_GAIT_START) * 0.5f;
-  B.gait_start[n] = gstart;
-  // generate_gait_time (t1:109-124)
-  float g[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-    g[i] = rand_float(C.gait_time_range[i][0], C.gait_time_range[i][1], K, SLOT_GAIT_TIME + i);
-  const float s = (g[0] + g[1]) + g[2];
-  const float f = C.max_episode_length / s;
-  const float s0 = g[0] * f, s1 = g[1] * f;
-  B.gait_time[n * 3 + 0] = 0;
-  B.gait_time[n * 3 + 1] = (int32_t)(0.0f + s0);
-  B.gait_time[n * 3 + 2] = (int32_t)((0.0f + s0) + s1);
+  B.gait_start[n] = R.gstart;
+  strow(B.gait_time + n * 3, R.gt);
   // episode sums are zeroed after the extras reduction; obs/critic history rows zeroed in the stack pass
   if (zero_reward_state)
 #pragma unroll
     for (int k = 0; k < T1_NREW; ++k) B.episode_sums[(size_t)k * C.num_envs + n] = 0.0f;
   // base quantities of the reset env from the fresh root state (t1:548-552)
-  BaseQ bq;
-  base_quantities_r(r, bq);
-  store_base_quantities(B, n, bq);
-  if (X) {
-#pragma unroll
-    for (int j = 0; j < 12; ++j) { X->act[j] = 0.0f; X->la[j] = 0.0f; }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) X->rv[i] = r[7 + i];
-    X->bq = bq;
-    X->gt[0] = 0;
-    X->gt[1] = (int32_t)(0.0f + s0);
-    X->gt[2] = (int32_t)((0.0f + s0) + s1);
-    X->el = 0;
-    X->pl = 0;
-    X->gstart = gstart;
-    X->dl = dl;
-    X->il = il;
-  }
+  store_base_quantities(B, n, R.bq);
 }
 
 // the actor-frame noise of observation i (legged_robot.py compute_observations: (2 u - 1) * noise_vec * level, u keyed
@@ -769,22 +789,145 @@ __device__ __forceinline__ void post_b_env(const DynModel& M, const t1env_config
   post_b_core(M, C, B, A, n, do_reset, any_reset, X, E);
 }
 
-// X: the inputs as they stand after post_a (reloaded here after a reset)
-__device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
-                                            const t1env_step_args& A, int n, bool do_reset, bool any_reset, ObsIn& X,
-                                            const ObsExtra& E, bool zero_reward_state) {
-  const uint32_t genv = (uint32_t)(C.env_offset + n);
-  const uint32_t ctr = A.counter + 1u;
-  const RngKey K = rng_key(C.seed, genv, ctr);
-  const float (&ef)[2] = E.ef;
-  const float (&et)[3] = E.et;
-  const float (&cfz)[2] = E.cfz;
-  const float fric = E.fric, mass = E.mass;
-  // lagged sensor samples, loaded before the reset: a resetting env's rings are zeroed by its reset, so its samples
-  // are 0 whatever its new lag lengths (below); the others keep their lag lengths
-  const float* ldp = B.dof_hist + ((size_t)n * 4 + ((A.counter - (uint32_t)(X.dl / 10)) & 3u)) * 24;
-  const float* lip = B.imu_hist + ((size_t)n * 2 + ((A.counter - (uint32_t)(X.il / 10)) & 1u)) * 8;
-  float ld[24], lraw[8], li[6];
+// compute_observations' gait terms (t1:250-274, 368-481): sin / cos of the phase, the reference joint positions and
+// the stance masks of an env whose phase counter X.pl is already zeroed for standing
+struct ObsPhase {
+  float sp, cp, ref[12];
+  Phase ph;
+};
+__device__ __forceinline__ void obs_phase(const DynModel& M, const t1env_config& C, const ObsIn& X, bool stand,
+                                          ObsPhase& P) {
+  const float phase = phase_value(C, X.pl, X.gstart, stand);
+  // compute_ref_state (t1:250-274)
+  P.sp = sinf(TWO_PI_F * phase);
+  P.cp = cosf(TWO_PI_F * phase);
+  const float sl = P.sp > 0.0f ? 0.0f : P.sp;
+  const float sr = P.sp < 0.0f ? 0.0f : P.sp;
+  const float s1 = C.target_joint_pos_scale, s2 = 2.0f * C.target_joint_pos_scale;
+  float* ref = P.ref;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) ref[j] = 0.0f;
+  ref[2] = sl * s1; ref[3] = -sl * s2; ref[4] = sl * s1;
+  ref[8] = -sr * s1; ref[9] = sr * s2; ref[10] = -sr * s1;
+  if (fabsf(P.sp) < 0.1f)
+#pragma unroll
+    for (int j = 0; j < 12; ++j) ref[j] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) ref[j] = ref[j] + M.default_dof_pos[j];
+  P.ph = gait_phase(phase);
+}
+
+// the newest frames: fp32, or rounded once to fp16 (round to nearest even, as torch's .half()) with obs_half
+// privileged frame (73)
+__device__ __forceinline__ void store_priv_frame(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                                 const t1env_step_args& A, int n, const ObsIn& X, const ObsExtra& E,
+                                                 const ObsPhase& P) {
+  const size_t priv_at = (size_t)n * (T1_NPRIV * T1_CHIST) + T1_NPRIV * (T1_CHIST - 1);
+  float* priv = B.priv_buf[A.obs_slot] + priv_at;
+  _Float16* priv_h = reinterpret_cast<_Float16*>(B.priv_buf[A.obs_slot]) + priv_at;
+  const float clipo = C.clip_obs;
+  const float* cmd = X.cmd;
+  const float* dof = X.dof;
+  int k = 0;
+  float v[T1_NPRIV];
+  v[k++] = P.sp;
+  v[k++] = P.cp;
+  v[k++] = cmd[0] * C.lin_vel_obs_scale;
+  v[k++] = cmd[1] * C.lin_vel_obs_scale;
+  v[k++] = cmd[2] * C.ang_vel_obs_scale;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[k++] = (dof[2 * j] - M.default_dof_pos[j]) * C.dof_pos_obs_scale;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[k++] = dof[2 * j + 1] * C.dof_vel_obs_scale;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[k++] = X.act[j];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[k++] = dof[2 * j] - P.ref[j];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v[k++] = X.bq.lin[i] * C.lin_vel_obs_scale;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v[k++] = X.bq.ang[i] * C.ang_vel_obs_scale;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v[k++] = X.bq.euler[i] * C.quat_obs_scale;
+  v[k++] = E.ef[0] / (C.ext_force_max[0] + 0.1f);
+  v[k++] = E.ef[1] / (C.ext_force_max[0] + 0.1f);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v[k++] = E.et[i] / (C.ext_torque_max + 0.1f);
+  v[k++] = E.fric;
+  v[k++] = E.mass / 30.0f;
+  v[k++] = P.ph.stance[0];
+  v[k++] = P.ph.stance[1];
+  v[k++] = E.cfz[0] > 5.0f ? 1.0f : 0.0f;
+  v[k++] = E.cfz[1] > 5.0f ? 1.0f : 0.0f;
+  if (C.obs_half) {
+#pragma unroll
+    for (int i = 0; i < T1_NPRIV; ++i) priv_h[i] = (_Float16)clampf(v[i], -clipo, clipo);
+  } else {
+#pragma unroll
+    for (int i = 0; i < T1_NPRIV; ++i) priv[i] = clampf(v[i], -clipo, clipo);
+  }
+}
+
+// actor frame (47) from the lagged sensor samples (ld: joint positions / velocities, li: imu angular velocity and
+// euler angles) + noise
+__device__ __forceinline__ void store_actor_frame(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                                  const t1env_step_args& A, int n, RngKey K, const ObsIn& X,
+                                                  const float ld[24], const float li[6], const ObsPhase& P) {
+  const size_t obs_at = (size_t)n * (T1_NOBS * T1_HIST) + T1_NOBS * (T1_HIST - 1);
+  float* obs = B.obs_buf[A.obs_slot] + obs_at;
+  _Float16* obs_h = reinterpret_cast<_Float16*>(B.obs_buf[A.obs_slot]) + obs_at;
+  const float clipo = C.clip_obs;
+  const float* cmd = X.cmd;
+  float v[T1_NOBS];
+  int k = 0;
+  v[k++] = P.sp;
+  v[k++] = P.cp;
+  v[k++] = cmd[0] * C.lin_vel_obs_scale;
+  v[k++] = cmd[1] * C.lin_vel_obs_scale;
+  v[k++] = cmd[2] * C.ang_vel_obs_scale;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[k++] = (ld[j] - M.default_dof_pos[j]) * C.dof_pos_obs_scale;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[k++] = ld[12 + j] * C.dof_vel_obs_scale;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[k++] = X.act[j];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v[k++] = li[i] * C.ang_vel_obs_scale;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v[k++] = li[3 + i] * C.quat_obs_scale;
+#pragma unroll
+  for (int i = 0; i < T1_NOBS; ++i) {
+#ifdef T1_WHATIF_NO_NOISE_DRAWS  // timing-only what-if build
+    const float nz = 0.0f;
+#else
+    const float nz = obs_noise(C, K, i);
+#endif
+    v[i] = clampf(v[i] + nz, -clipo, clipo);
+  }
+  if (C.obs_half) {
+#pragma unroll
+    for (int i = 0; i < T1_NOBS; ++i) obs_h[i] = (_Float16)v[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < T1_NOBS; ++i) obs[i] = v[i];
+  }
+}
+
+// ref_dof_pos and last_* (legged_robot.py:496-502)
+__device__ __forceinline__ void store_obs_last(const t1env_buffers& B, int n, const ObsIn& X, const float (&ref)[12]) {
+  strow(B.ref_dof_pos + n * 12, ref);
+  strow(B.last_last_actions + n * 12, X.la);
+  strow(B.last_actions + n * 12, X.act);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) B.last_dof_vel[n * 12 + j] = X.dof[2 * j + 1];
+  strow(B.last_root_vel + n * 6, X.rv);
+}
+
+// the lagged sensor samples of an env (lags dl / il as they stand before this step's reset)
+__device__ __forceinline__ void load_lagged(const t1env_buffers& B, const t1env_step_args& A, int n, int dl, int il,
+                                            float (&ld)[24], float (&lraw)[8]) {
+  const float* ldp = B.dof_hist + ((size_t)n * 4 + ((A.counter - (uint32_t)(dl / 10)) & 3u)) * 24;
+  const float* lip = B.imu_hist + ((size_t)n * 2 + ((A.counter - (uint32_t)(il / 10)) & 1u)) * 8;
 #ifdef T1_WHATIF_NO_LAG_LOADS  // timing-only what-if build: the lagged sensor samples not loaded
   (void)ldp;
   (void)lip;
@@ -797,8 +940,22 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
   ldrow(ld, ldp);
   ldrow(lraw, lip);
 #endif
+}
+
+// X: the inputs as they stand after post_a (reloaded here after a reset)
+__device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_config& C, const t1env_buffers& B,
+                                            const t1env_step_args& A, int n, bool do_reset, bool any_reset, ObsIn& X,
+                                            const ObsExtra& E, bool zero_reward_state) {
+  const uint32_t genv = (uint32_t)(C.env_offset + n);
+  const uint32_t ctr = A.counter + 1u;
+  const RngKey K = rng_key(C.seed, genv, ctr);
+  // lagged sensor samples, loaded before the reset: a resetting env's rings are zeroed by its reset, so its samples
+  // are 0 whatever its new lag lengths (below); the others keep their lag lengths
+  float ld[24], lraw[8], li[6];
+  load_lagged(B, A, n, X.dl, X.il, ld, lraw);
   if (do_reset) {
-    reset_env(M, C, B, A, n, genv, ctr, true, zero_reward_state, &X);
+    reset_env(M, C, B, A, n, genv, ctr, true, zero_reward_state);
+    reset_obs_inputs(M, C, K, X);
 #pragma unroll
     for (int i = 0; i < 24; ++i) ld[i] = 0.0f;
 #pragma unroll
@@ -808,122 +965,19 @@ __device__ __forceinline__ void post_b_core(const DynModel& M, const t1env_confi
   if (any_reset && resample_commands_r(C, A, X.el, X.gt, X.cmd, genv, ctr)) strow(B.commands + n * 4, X.cmd);
   imu_sample(lraw, li);
   // ---- compute_observations
-  const float* cmd = X.cmd;
-  const float* dof = X.dof;
-  const float* act = X.act;
-  const bool stand = is_stand(C, cmd);
+  const bool stand = is_stand(C, X.cmd);
   if (stand) {  // _get_phase zeroes the phase counter of standing envs
     X.pl = 0;
     B.phase_length_buf[n] = 0;
   }
-  const float phase = phase_value(C, X.pl, X.gstart, stand);
-  // compute_ref_state (t1:250-274)
-  const float sp = sinf(TWO_PI_F * phase);
-  const float cp = cosf(TWO_PI_F * phase);
-  float ref[12];
-  {
-    const float sl = sp > 0.0f ? 0.0f : sp;
-    const float sr = sp < 0.0f ? 0.0f : sp;
-    const float s1 = C.target_joint_pos_scale, s2 = 2.0f * C.target_joint_pos_scale;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) ref[j] = 0.0f;
-    ref[2] = sl * s1; ref[3] = -sl * s2; ref[4] = sl * s1;
-    ref[8] = -sr * s1; ref[9] = sr * s2; ref[10] = -sr * s1;
-    if (fabsf(sp) < 0.1f)
-#pragma unroll
-      for (int j = 0; j < 12; ++j) ref[j] = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) ref[j] = ref[j] + M.default_dof_pos[j];
-  }
-  const Phase ph = gait_phase(phase);
+  ObsPhase P;
+  obs_phase(M, C, X, stand, P);
   T1_PROF_MARK(21);
-  // newest frames: fp32, or rounded once to fp16 (round to nearest even, as torch's .half()) with obs_half
-  const size_t priv_at = (size_t)n * (T1_NPRIV * T1_CHIST) + T1_NPRIV * (T1_CHIST - 1);
-  const size_t obs_at = (size_t)n * (T1_NOBS * T1_HIST) + T1_NOBS * (T1_HIST - 1);
-  float* priv = B.priv_buf[A.obs_slot] + priv_at;
-  float* obs = B.obs_buf[A.obs_slot] + obs_at;
-  _Float16* priv_h = reinterpret_cast<_Float16*>(B.priv_buf[A.obs_slot]) + priv_at;
-  _Float16* obs_h = reinterpret_cast<_Float16*>(B.obs_buf[A.obs_slot]) + obs_at;
-  const float clipo = C.clip_obs;
-  float cin[5] = {sp, cp, cmd[0] * C.lin_vel_obs_scale, cmd[1] * C.lin_vel_obs_scale, cmd[2] * C.ang_vel_obs_scale};
-  {  // privileged frame (73)
-    int k = 0;
-    float v[T1_NPRIV];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) v[k++] = cin[i];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) v[k++] = (dof[2 * j] - M.default_dof_pos[j]) * C.dof_pos_obs_scale;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) v[k++] = dof[2 * j + 1] * C.dof_vel_obs_scale;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) v[k++] = act[j];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) v[k++] = dof[2 * j] - ref[j];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) v[k++] = X.bq.lin[i] * C.lin_vel_obs_scale;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) v[k++] = X.bq.ang[i] * C.ang_vel_obs_scale;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) v[k++] = X.bq.euler[i] * C.quat_obs_scale;
-    v[k++] = ef[0] / (C.ext_force_max[0] + 0.1f);
-    v[k++] = ef[1] / (C.ext_force_max[0] + 0.1f);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) v[k++] = et[i] / (C.ext_torque_max + 0.1f);
-    v[k++] = fric;
-    v[k++] = mass / 30.0f;
-    v[k++] = ph.stance[0];
-    v[k++] = ph.stance[1];
-    v[k++] = cfz[0] > 5.0f ? 1.0f : 0.0f;
-    v[k++] = cfz[1] > 5.0f ? 1.0f : 0.0f;
-    if (C.obs_half) {
-#pragma unroll
-      for (int i = 0; i < T1_NPRIV; ++i) priv_h[i] = (_Float16)clampf(v[i], -clipo, clipo);
-    } else {
-#pragma unroll
-      for (int i = 0; i < T1_NPRIV; ++i) priv[i] = clampf(v[i], -clipo, clipo);
-    }
-  }
+  store_priv_frame(M, C, B, A, n, X, E, P);
   T1_PROF_MARK(22);
-  {  // actor frame (47) from the lagged sensor rings + noise
-    float v[T1_NOBS];
-    int k = 0;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) v[k++] = cin[i];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) v[k++] = (ld[j] - M.default_dof_pos[j]) * C.dof_pos_obs_scale;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) v[k++] = ld[12 + j] * C.dof_vel_obs_scale;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) v[k++] = act[j];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) v[k++] = li[i] * C.ang_vel_obs_scale;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) v[k++] = li[3 + i] * C.quat_obs_scale;
-#pragma unroll
-    for (int i = 0; i < T1_NOBS; ++i) {
-#ifdef T1_WHATIF_NO_NOISE_DRAWS  // timing-only what-if build
-      const float nz = 0.0f;
-#else
-      const float nz = obs_noise(C, K, i);
-#endif
-      v[i] = clampf(v[i] + nz, -clipo, clipo);
-    }
-    if (C.obs_half) {
-#pragma unroll
-      for (int i = 0; i < T1_NOBS; ++i) obs_h[i] = (_Float16)v[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < T1_NOBS; ++i) obs[i] = v[i];
-    }
-  }
+  store_actor_frame(M, C, B, A, n, K, X, ld, li, P);
   T1_PROF_MARK(23);
-  strow(B.ref_dof_pos + n * 12, ref);
-  // last_* (legged_robot.py:496-502)
-  strow(B.last_last_actions + n * 12, X.la);
-  strow(B.last_actions + n * 12, X.act);
-#pragma unroll
-  for (int j = 0; j < 12; ++j) B.last_dof_vel[n * 12 + j] = dof[2 * j + 1];
-  strow(B.last_root_vel + n * 6, X.rv);
+  store_obs_last(B, n, X, P.ref);
 }
 
 }  // namespace t1
