@@ -89,6 +89,11 @@ int t1policy_conv1_wgrad_bf16(const void* x, const void* gy, void* workspace, fl
  * Returns 0, -1 on bad arguments, -2 on a launch error. */
 int t1policy_colsum_workspace_bytes(int rows, int cols);
 int t1policy_colsum(const void* g, int elem_bytes, int rows, int cols, void* workspace, float* out, void* stream);
+/* The split-K weight gradient's reduction (dh_policy.wgrad_splitk; replaces torch's part.sum(0) after the batched GEMM,
+ * the reduction inside dh_ppo.py:180's loss.backward() for every Linear weight, humanoid/algo/ppo/dh_ppo.py:112-205):
+ * out[i] = sum over s = 0 .. slices-1, in that order, of part[s * n + i] (fp32).  Returns 0, -1 bad arguments, -2 launch
+ * error. */
+int t1policy_slice_sum(const float* part, int slices, int n, float* out, void* stream);
 
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py

@@ -83,3 +83,32 @@ def test_bias_colsum_matches_fp64(rows, cols, dtype, monkeypatch):
     ref = gy.double().sum(0)
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-3)
     assert torch.equal(bias_grad(gy), out)
+
+
+@pytest.mark.parametrize("slices,shape", [(24, (512, 302)), (24, (3, 64)), (5, (7, 13)), (1, (768, 219)), (9, (128, 96))])
+def test_splitk_slice_sum_is_the_ordered_fp32_sum(slices, shape):
+    """The split-K weight gradient's reduction (dh_policy.slice_sum, t1policy_slice_sum): bit-identical to the fp32 sum
+    of the slices taken s = 0, 1, ... in order (float4 path for sizes divisible by 4, scalar path otherwise)."""
+    from ti5_isaacgym_amd.algo.dh_policy import slice_sum
+    g = torch.Generator(device=DEV).manual_seed(slices * 1000 + shape[0])
+    part = torch.randn(slices, *shape, device=DEV, generator=g) * 10.0
+    out = slice_sum(part)
+    ref = part[0].clone()
+    for s in range(1, slices):
+        ref += part[s]
+    assert out.shape == shape and out.dtype == torch.float32
+    assert torch.equal(out, ref)
+
+
+def test_wgrad_splitk_uses_slice_sum_and_matches_fp64():
+    """wgrad_splitk on the device (bf16 operands, fp32 partials, HIP slice sum) against fp64, at whole slices (the
+    update's 49,152 rows are 24 of them; a ragged tail's bf16 GEMM output is rounded to bf16 before the widening)."""
+    from ti5_isaacgym_amd.algo import dh_policy
+    g = torch.Generator(device=DEV).manual_seed(7)
+    K = 3 * dh_policy.SPLITK_ROWS
+    gy = torch.randn(K, 96, device=DEV, generator=g).to(torch.bfloat16)
+    x = torch.randn(K, 130, device=DEV, generator=g).to(torch.bfloat16)
+    gw = dh_policy.wgrad_splitk(gy, x)
+    ref = gy.double().t() @ x.double()
+    assert gw.dtype == torch.float32
+    torch.testing.assert_close(gw.double(), ref, rtol=1e-4, atol=1e-2)

@@ -39,6 +39,27 @@ SPLITK_ROWS = _splitk_rows(os.environ.get("T1_SPLITK_ROWS", "2048"))
 WGRAD_OUT_F32 = os.environ.get("T1_WGRAD_OUT_F32", "1") != "0"
 
 
+# the split-K partial products summed by the HIP slice sum (t1policy_slice_sum, slices in order) on the device;
+# T1_SLICE_SUM=0: torch's part.sum(0) (A/B)
+SLICE_SUM = os.environ.get("T1_SLICE_SUM", "1") != "0"
+
+
+def slice_sum(part):
+    """part.sum(0) of the (S, M, N) split-K partial products: on the device the HIP slice sum (fp32, s = 0, 1, ... in
+    order: one HBM pass instead of torch's dim-0 reduction kernel), on the host or for other dtypes torch's."""
+    if not (part.is_cuda and SLICE_SUM and part.dtype == torch.float32):
+        return part.sum(0)
+    from .. import _lib
+    lib = _lib.load()
+    part = part.contiguous()
+    out = torch.empty(part.shape[1:], device=part.device, dtype=torch.float32)
+    rc = lib.t1policy_slice_sum(part.data_ptr(), part.shape[0], out.numel(), out.data_ptr(),
+                                torch.cuda.current_stream(part.device).cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"t1policy_slice_sum failed (rc={rc})")
+    return out
+
+
 def wgrad_splitk(gy, x):
     """dW = gy^T x for a batch of K rows (gy: K x M, x: K x N) as a batched GEMM over K-slices of SPLITK_ROWS rows plus
     a sum: the PPO update's weight gradients have K = 49,152 (688,128 for the first conv) and M x N of a few hundred
@@ -64,9 +85,9 @@ def wgrad_splitk(gy, x):
         # bf16 operands, fp32 partial products straight from the GEMM (aten::bmm.dtype): no bf16 rounding of the
         # 2,048-row partial sums and no widening copy of them.  An fp32 saved input is rounded to the gradient's dtype
         # first, as autocast's bmm would (the once-per-update obs cast stays bit-identical to the per-minibatch one)
-        gw = torch.bmm(a, b if b.dtype == gy.dtype else b.to(gy.dtype), out_dtype=torch.float32).sum(0)
+        gw = slice_sum(torch.bmm(a, b if b.dtype == gy.dtype else b.to(gy.dtype), out_dtype=torch.float32))
     else:
-        gw = wide(torch.bmm(a, b)).sum(0)
+        gw = slice_sum(wide(torch.bmm(a, b)))
     if c < K:
         gw = gw + wide(gy[c:].t().mm(x[c:]))
     return gw

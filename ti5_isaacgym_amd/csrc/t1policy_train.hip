@@ -294,6 +294,38 @@ __global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ 
   out[c] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
 }
 
+// ---- the split-K weight gradient's partial products summed over the slices: out[i] = sum_s part[s][i], s in order
+// (fp32; the PPO update's wgrad_splitk: 24 slices of M x N fp32 at 49,152 rows).  One thread per 4 consecutive
+// outputs (float4 loads, 8 slices in flight); the sum runs s = 0, 1, ... exactly, so the result does not depend on the
+// launch shape.
+__global__ __launch_bounds__(256) void k_slice_sum4(const float4* __restrict__ part, int slices, int n4,
+                                                    float4* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  int k = 0;
+  for (; k + 8 <= slices; k += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(k + u) * n4 + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+  }
+  for (; k < slices; ++k) {
+    const float4 v = part[(size_t)k * n4 + i];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  out[i] = s;
+}
+__global__ __launch_bounds__(256) void k_slice_sum1(const float* __restrict__ part, int slices, int n,
+                                                    float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.0f;
+  for (int k = 0; k < slices; ++k) s += part[(size_t)k * n + i];
+  out[i] = s;
+}
+
 bool tc_shape(int channels, int length, int out_channels, int kernel, int stride) {
   return channels == TC_C && length == TC_L && out_channels == TC_O && kernel == TC_K && stride == TC_S;
 }
@@ -368,6 +400,18 @@ int t1policy_colsum(const void* g, int elem_bytes, int rows, int cols, void* wor
     return -1;
   hipLaunchKernelGGL(k_colsum_final, dim3((cols + 255) / 256), dim3(256), 0, (hipStream_t)stream, part, chunks, cols,
                      out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_slice_sum(const float* part, int slices, int n, float* out, void* stream) {
+  if (!part || !out || slices <= 0 || n <= 0) return -1;
+  if (n % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15u) == 0 && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+    const int n4 = n / 4;
+    hipLaunchKernelGGL(k_slice_sum4, dim3((n4 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(part), slices, n4, reinterpret_cast<float4*>(out));
+  } else {
+    hipLaunchKernelGGL(k_slice_sum1, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, part, slices, n, out);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
