@@ -702,6 +702,17 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
     q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
     qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
   }
+  // every per-env load of the prologue is issued before its first global store (the buffers may alias as far as the
+  // compiler knows, so a load after a store would cost another memory round trip)
+  const int lag = B.lag_timestep[n];
+  const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
+  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
+  float vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
+  int s_dof = 9 - B.dof_lag_timestep[n] % 10;
+#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
+  s_dof = s_dof > 0 ? s_dof - 1 : 0;
+#endif
+  const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
   {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged
     PdStage<64>& P = lds.pd;
     float a[NLEG];
@@ -733,16 +744,7 @@ __global__ __launch_bounds__(D5_BLOCK) void k_dyn5(const DynModel* __restrict__ 
       }
     }
   }
-  const int lag = B.lag_timestep[n];
-  const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
-  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
-  float vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
   lds.vift[lane] = vi_ft;
-  int s_dof = 9 - B.dof_lag_timestep[n] % 10;
-#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
-  s_dof = s_dof > 0 ? s_dof - 1 : 0;
-#endif
-  const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
   float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
   float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
   float tau[NLEG];
