@@ -98,7 +98,9 @@ __device__ __forceinline__ void epilogue_finalize_parts(const t1env_config& C, c
   const float4* P = reinterpret_cast<const float4*>(FA.ep_part);
   const int q = lane & 7;
   float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  constexpr int BATCH = 8;  // loads in flight per lane
+  // loads in flight per lane: 32 covers 256 workgroups in one memory round trip (8 took four, serialised at the very
+  // end of the launch); each lane still adds its rows in row order, so the sums do not depend on BATCH
+  constexpr int BATCH = 32;
   for (int r0 = lane >> 3; r0 < dyn_blocks; r0 += 8 * BATCH) {
     float4 v[BATCH];
 #pragma unroll
