@@ -89,9 +89,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--cpu-shards", type=int, default=32,
                    help="CPU baseline: env shards stepped on Python threads (at most the affinity's core count)")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r04fh.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r04fi.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
-    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r04fh_sq_counters.json"),
+    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r04fi_sq_counters.json"),
                    help="SQ instruction counters of the fused kernel (tools/pmc_sq_summary.py): the VALU-issue roofline")
     return p.parse_args()
 
