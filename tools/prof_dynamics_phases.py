@@ -39,16 +39,19 @@ HELPER_SUB = {16: "contacts: transforms + height queries (issue)", 17: "contacts
 NB = len(BUCKETS)
 NW = 4
 # k_dyn5 (t1env_dyn5.hip): per-role mark meanings (ids 13-15 epilogue and 16-23 sub-marks as above)
-D5 = {
-    0: ["prologue", "S1 wait", "forward chain (poses)", "CRBA backward pass", "S2 wait", "LDS reads + fold-in",
-        "elimination", "base system + solve + backsub + integrate", "log / captures / publish", "stores + R1 wait",
-        "rigid report", "epilogue barrier"],
-    1: ["prologue (actions, PD stage)", "S1 wait", "state + PD torques", "RNEA bias + rhs", "base block + base box",
-        "publish", "S2 wait", "history shift slice", "-", "R1 wait", "-", "epilogue barrier"],
-    2: ["prologue + epilogue staging", "S1 wait", "state + kinematics", "shank terrain", "foot terrain", "publish",
-        "S2 wait", "history shift slice", "-", "R1 wait", "-", "epilogue barrier"],
-    3: ["prologue + epilogue staging", "S1 wait", "state + kinematics", "capsule exchange", "self-contact terms",
-        "publish", "S2 wait", "history shift slice", "-", "R1 wait", "contact-force report", "epilogue barrier"],
+D5 = {  # bucket i = the time from the previous mark to mark i (t1env_dyn5.hip's T1_PROF_MARK ids)
+    0: ["prologue", "S1 wait", "base frame, PD torques, base block, leg chain", "CRBA backward pass", "S2 wait",
+        "LDS reads + fold-in", "elimination", "base system + solve + backsub + integrate", "log / captures / publish",
+        "stores + R1 wait", "rigid report", "epilogue barrier"],
+    1: ["prologue", "S1 wait", "state + base-box query issue", "RNEA bias + rhs", "base-box contact + halves",
+        "publish + shift DMA retire", "S2 wait", "history shift slice", "-", "R1 wait", "base-box report",
+        "epilogue barrier"],
+    2: ["prologue + epilogue staging", "S1 wait", "state + kinematics", "foot / shank queries + shank contact",
+        "foot contact (points 0-3)", "publish + shift DMA retire", "S2 wait", "history shift slice", "-", "R1 wait",
+        "terrain report", "epilogue barrier"],
+    3: ["prologue + epilogue staging", "S1 wait", "state + kinematics", "foot queries + self-contact terms",
+        "foot contact (points 4-7)", "publish + shift DMA retire", "S2 wait", "history shift slice", "-", "R1 wait",
+        "self-contact report", "epilogue barrier"],
 }
 
 
