@@ -44,7 +44,7 @@ def fused_kernel(num_envs, cus=256):
     """The step kernel t1env picks (t1_dyn_waves_default): k_dyn5 up to 32 envs per CU, k_dyn4 above; the
     T1ENV_DYN_KERNEL override wins."""
     k = os.environ.get("T1ENV_DYN_KERNEL")
-    if k in ("4", "5"):
+    if k in ("4", "5", "6"):
         return "k_dyn" + k
     return "k_dyn5" if (num_envs + 31) // 32 <= cus else "k_dyn4"
 # per-kernel algorithmic bytes per env (reads + writes it must do; DESIGN.md §3) for the split sequence

@@ -88,14 +88,16 @@ class ShardedCpuT1Env:
                        for s in range(S)]
         self.pool = ThreadPoolExecutor(S)
 
+    BARRIER_TIMEOUT_S = 600.0   # a stuck shard cannot hang the CPU baseline
+
     def _reduce(self, s, c):
-        if self._bar.wait() == 0:
+        if self._bar.wait(self.BARRIER_TIMEOUT_S) == 0:
             self._acc = [0.0, 0]
-        self._bar.wait()
+        self._bar.wait(self.BARRIER_TIMEOUT_S)
         with self._lock:
             self._acc[0] += s
             self._acc[1] += c
-        self._bar.wait()
+        self._bar.wait(self.BARRIER_TIMEOUT_S)
         return self._acc[0], self._acc[1]
 
     def threads(self):
@@ -106,4 +108,13 @@ class ShardedCpuT1Env:
 
     def step(self, actions):
         b = self.bounds
-        list(self.pool.map(lambda i: self.shards[i].step(actions[b[i]:b[i + 1]]), range(len(self.shards))))
+
+        def one(i):
+            try:
+                return self.shards[i].step(actions[b[i]:b[i + 1]])
+            except BaseException:
+                # a shard that fails before or inside the curriculum reduction breaks the barrier, so the other shards
+                # raise BrokenBarrierError instead of waiting forever; the first error propagates
+                self._bar.abort()
+                raise
+        list(self.pool.map(one, range(len(self.shards))))

@@ -68,6 +68,7 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
     for (int k = 0; k < nsub; ++k) {
       V3<R> ef = (ext_force && k == 0) ? v3<R>(ext_force[n * 3], ext_force[n * 3 + 1], ext_force[n * 3 + 2]) : v3<R>(0, 0, 0);
       if (mode == 2) substep_roles(M, T, P, s, t, ef, R(dt));  // k_dyn5's role composition
+      else if (mode == 3) substep_roles6(M, T, P, s, t, ef, R(dt));  // k_dyn6's
       else substep(M, T, P, s, t, ef, R(dt), mode == 1);
     }
     Writer<R> W{root + (size_t)n * 13, rigid ? rigid + (size_t)n * 169 : nullptr, contact ? contact + (size_t)n * 39 : nullptr};
@@ -83,7 +84,7 @@ int substep_batch(const t1env_model* model, int N, float* root, float* dof, cons
 extern "C" {
 // Advance N envs by nsub substeps with constant joint torques (root: Gym layout, COM velocity).
 // flags: bit 0 = fp64, bit 1 = the k_dyn4 split composition (compute_delta_split) instead of compute_delta,
-// bit 2 = k_dyn5's role composition (compute_delta_roles, t1_dyn5.h).
+// bit 2 = k_dyn5's role composition (compute_delta_roles, t1_dyn5.h), bit 3 = k_dyn6's (compute_delta_roles6).
 // restitution: the envs' shape restitution (null: 0); vimp: (N, 6) restitution episodes of the contact bodies, read
 // and updated (null: none carried across calls).
 int t1dyn_substeps(const t1env_model* model, int N, int flags, float* root, float* dof, const float* tau,
@@ -91,7 +92,7 @@ int t1dyn_substeps(const t1env_model* model, int N, int flags, float* root, floa
                    const float* friction, const float* restitution, float* vimp, const float* ext_force, float dt, int nsub,
                    const int16_t* hf, int rows, int cols, float hs, float vs, float border, int mesh, float* rigid,
                    float* contact) {
-  const int mode = (flags & 4) ? 2 : ((flags & 2) ? 1 : 0);
+  const int mode = (flags & 8) ? 3 : ((flags & 4) ? 2 : ((flags & 2) ? 1 : 0));
   return (flags & 1) ? substep_batch<double>(model, N, root, dof, tau, body_mass, link_scale, com_disp, armature,
                                              friction, restitution, vimp, ext_force, dt, nsub, hf, rows, cols, hs, vs, border,
                                              mesh, rigid, contact, mode)

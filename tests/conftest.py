@@ -29,7 +29,8 @@ def pytest_sessionfinish(session, exitstatus):
 
 # the step's dynamics kernels (T1ENV_DYN_KERNEL / T1ENV_D5_SHIFT, read when an env is created): k_dyn5 with its
 # in-workgroup history shift (the default), k_dyn5 beside the concurrent k_shift5 launch, and k_dyn4
-DYN_KERNELS = {"dyn5": {"T1ENV_DYN_KERNEL": "5", "T1ENV_D5_SHIFT": "0"},
+DYN_KERNELS = {"dyn6": {"T1ENV_DYN_KERNEL": "6"},
+               "dyn5": {"T1ENV_DYN_KERNEL": "5", "T1ENV_D5_SHIFT": "0"},
                "dyn5_concshift": {"T1ENV_DYN_KERNEL": "5", "T1ENV_D5_SHIFT": "1"},
                "dyn4": {"T1ENV_DYN_KERNEL": "4"}}
 
@@ -41,9 +42,9 @@ def dyn_kernel(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["dyn5", "dyn4"])
+@pytest.fixture(params=["dyn6", "dyn5", "dyn4"])
 def dyn_solver(request, monkeypatch):
-    """The two dynamics kernels (the shift mode does not touch the solver)."""
+    """The dynamics kernels (the shift mode does not touch the solver)."""
     for k, v in DYN_KERNELS[request.param].items():
         monkeypatch.setenv(k, v)
     return request.param

@@ -225,10 +225,11 @@ def _run_flags(dyn, m, flags, root, dof, tau, hf, mesh, nsub):
 
 @pytest.mark.parametrize("mesh", [0, 2])
 def test_split_composition_matches_assembled(dyn, model, mesh):
-    """k_dyn4's split composition (contact-free passes + contact fold-in, compute_delta_split) and k_dyn5's four-role
-    composition (bias / torque rhs from the RNEA wave, compute_delta_roles) are the same linear system as the
-    assembled one (compute_delta): in fp64 they agree to rounding, with the feet and shanks in contact on a plane
-    and on a rough height field."""
+    """k_dyn4's split composition (contact-free passes + contact fold-in, compute_delta_split), k_dyn5's four-role
+    composition (bias / torque rhs from the RNEA wave, compute_delta_roles) and k_dyn6's eight-role composition (each
+    terrain contact body as two halves of its points, its restitution episode from the halves' fastest approach,
+    compute_delta_roles6) are the same linear system as the assembled one (compute_delta): in fp64 they agree to
+    rounding, with the feet and shanks in contact on a plane and on a rough height field."""
     m, _ = model
     n = 48
     rng = np.random.default_rng(3)
@@ -245,8 +246,9 @@ def test_split_composition_matches_assembled(dyn, model, mesh):
     hf = (rng.integers(-20, 20, (40, 40)) if mesh else np.zeros((2, 2))).astype(np.int16)
     a = _run_flags(dyn, m, 1, root, dof, tau, hf, mesh, 20)
     assert np.abs(a[3]).sum() > 0, "no contact exercised"
-    # flags 3: k_dyn4's split composition; 5: k_dyn5's four-role composition (compute_delta_roles, t1_dyn5.h)
-    for flags in (3, 5):
+    # flags 3: k_dyn4's split composition; 5: k_dyn5's four-role composition (compute_delta_roles, t1_dyn5.h); 9:
+    # k_dyn6's eight-role composition (compute_delta_roles6)
+    for flags in (3, 5, 9):
         b = _run_flags(dyn, m, flags, root, dof, tau, hf, mesh, 20)
         for x, y, name in zip(a, b, ["root", "dof", "rigid", "contact"]):
             scale = np.abs(x).max() + 1.0

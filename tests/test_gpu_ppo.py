@@ -269,8 +269,9 @@ def test_graphed_act_follows_graphed_updates():
 def test_update_after_loading_plain_adam_state():
     """a checkpoint's optimizer state written by a plain (non-capturable) torch Adam -- the
     reference's, or an older build's -- replaces the param groups' flags on load; after_optimizer_load restores the
-    capturable fused Adam with the device learning rate, so the next update runs, and the loaded lr is the one used
-    unless the caller assigns another afterwards."""
+    capturable fused Adam with the device learning rate, so the next update runs.  The learning rate follows the
+    reference's runner.load: DHPPO.learning_rate keeps this process's value; under the adaptive schedule Adam
+    continues from it, under the fixed schedule Adam keeps the checkpoint's lr (the reference never writes it)."""
     from torch import optim
     from ti5_isaacgym_amd import task_registry
     from ti5_isaacgym_amd.algo.dh_policy import ActorCriticDH
@@ -288,10 +289,18 @@ def test_update_after_loading_plain_adam_state():
     sd = plain.state_dict()
     assert sd["param_groups"][0]["capturable"] is False
     alg = DHPPO(ac, device=str(dev), **cfg["algorithm"])
+    lr0 = float(cfg["algorithm"]["learning_rate"])
+    assert alg.schedule == "adaptive" and abs(lr0 - 3e-4) > 1e-6
     alg.init_storage(N, T, [3102], [219], [12], history=(47, 66))
     alg.optimizer.load_state_dict(sd)
     alg.after_optimizer_load()
-    assert abs(alg.learning_rate - 3e-4) < 1e-10
+    assert abs(alg.learning_rate - lr0) < 1e-12 and abs(float(alg._lr_t) - lr0) < 1e-9  # not the checkpoint's 3e-4
+    fixed = DHPPO(ActorCriticDH(235, 47, 219, 12, **cfg["policy"]).to(dev), device=str(dev),
+                  **dict(cfg["algorithm"], schedule="fixed"))
+    fixed.optimizer.load_state_dict(sd)
+    fixed.after_optimizer_load()
+    assert abs(fixed.learning_rate - lr0) < 1e-12 and abs(float(fixed._lr_t) - 3e-4) < 1e-10
+    assert fixed.optimizer.param_groups[0]["lr"] is fixed._lr_t
     _fill_storage(alg, N, T, dev, 5)
     ac.train()
     losses = alg.update()

@@ -339,6 +339,11 @@ def heads_forward(ac, obs, critic_obs, eps):
     if (layers is None or not obs.is_cuda or obs.dtype != torch.float32 or critic_obs.dtype != torch.float32
             or obs.dim() != 2 or critic_obs.dim() != 2 or eps.shape != (obs.shape[0], ac.std.numel())):
         return None
+    # the kernel reads critic_obs and obs row by row up to the batch: shapes it was not built for are refused here,
+    # not read out of bounds on the device
+    if (critic_obs.shape[0] != obs.shape[0] or obs.shape[1] != ac.in_channels * ac.num_proprio_obs
+            or critic_obs.shape[1] != layers[11].in_features):
+        return None
     lib = _lib.load()
     dims, ptrs = [], []
     for m in layers:

@@ -122,23 +122,36 @@ class DHPPO:
         """After optimizer.load_state_dict (a checkpoint resume): load_state_dict replaces every param-group
         hyperparameter with the saved one, so a state written by the reference (or by an older build) comes back with
         capturable=False / fused=None, under which the device-tensor learning rate is rejected.  Restore the flags this
-        optimizer was built with, move the step counters to the parameters' device as fp32 (capturable Adam keeps them
-        there), and bind the lr tensor to the loaded value now, so a later `learning_rate = x` wins."""
+        optimizer was built with and move the step counters to the parameters' device as fp32 (capturable Adam keeps
+        them there).
+
+        The learning rate follows the reference's runner.load (dh_on_policy_runner.py:311-318, dh_ppo.py:36, 141-151),
+        which loads the optimizer state but leaves DHPPO.learning_rate at this process's value (the constructor's after
+        a fresh start): under the adaptive schedule the first KL step overwrites the loaded lr with that value / 1.5,
+        * 1.5 or itself, so the device lr continues from learning_rate, not from the checkpoint; under
+        the fixed schedule the reference never writes the param groups' lr, so Adam keeps the checkpoint's lr while
+        learning_rate (what the runner logs) stays this process's value.  The host path (a plain Adam) does both by
+        itself."""
         if self._lr_t is None:
             return
+        loaded = float(self.optimizer.param_groups[0]["lr"])
         for g in self.optimizer.param_groups:
             g["capturable"] = True
             g["fused"] = True
             g["foreach"] = None
+            g["lr"] = self._lr_t
             for p in g["params"]:
                 st = self.optimizer.state.get(p)
                 if st and "step" in st:
                     st["step"] = torch.as_tensor(st["step"], dtype=torch.float32, device=p.device).reshape(())
-        self._bind_lr()
+        if self.desired_kl is not None and self.schedule == "adaptive":
+            self._lr_t.copy_(self._lr64)
+        else:
+            self._lr_t.fill_(loaded)
 
     def _bind_lr(self):
-        """Keep every param group's lr the device tensor (a loaded optimizer state or a caller may have put a float or
-        another tensor there: its value is taken over)."""
+        """Keep every param group's lr the device tensor (a caller may have put a float or another tensor there
+        without after_optimizer_load: its value is taken over)."""
         for g in self.optimizer.param_groups:
             if g["lr"] is not self._lr_t:
                 self._lr64.fill_(float(g["lr"]))
@@ -164,6 +177,7 @@ class DHPPO:
         torch.normal's std >= 0 test (the sample is drawn as mean + std * N(0, 1), the same distribution)."""
         ac = self.actor_critic
         obs, critic_obs = obs.float(), critic_obs.float()   # fp16 env histories (state_dtype="fp16"): no-op for fp32
+        eps = None
         if obs.is_cuda and FUSED_ACT:
             # the fused HIP heads (t1policy_heads_forward): the same draw (randn of the mean's shape), one kernel for
             # every layer after the first conv plus the sample and its log-prob
@@ -175,7 +189,9 @@ class DHPPO:
         mean = ac.actor(ac.actor_input(obs))
         std = mean * 0.0 + ac.std
         dist = Normal(mean, std, validate_args=False)
-        actions = mean + std * torch.randn_like(mean)
+        # a refused fused call (no compiled instance for this model / shape) keeps its draw: one draw per act() either
+        # way, so the RNG stream does not depend on the path
+        actions = mean + std * (eps if eps is not None else torch.randn_like(mean))
         return actions, ac.critic(critic_obs), dist.log_prob(actions).sum(dim=-1), mean, std
 
     def _graphed_act(self, obs, critic_obs):

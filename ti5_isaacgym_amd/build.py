@@ -12,7 +12,8 @@ CSRC = os.path.join(HERE, "csrc")
 # translation unit -> optimisation level.  The dynamics unit is built at -O1 (round 1's fastest level; on the round-2
 # kernel -O1/-O2/-O3 measure the same, profiles/r02bc_opt_levels.json).  Round 1's -O2/-O3 wrong dynamics bisected to the load/store vectorizer over the __restrict__
 # model-pointer loads; the -O3 guard build (OUT_O3) keeps every level under the fp64 check.
-UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1"), ("t1env_dyn5.hip", "-O1"), ("t1policy.hip", "-O3"),
+UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1"), ("t1env_dyn5.hip", "-O1"), ("t1env_dyn6.hip", "-O1"),
+         ("t1policy.hip", "-O3"),
          ("t1policy_heads.hip", "-O3"), ("t1policy_train.hip", "-O3")]
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
 # guard build: the dynamics unit at -O3 (tests/test_gpu_opt_levels.py keeps it under the fp64 dynamics check)
@@ -35,7 +36,7 @@ def build(force=False, extra=(), out=None, dyn_opt=None):
     common = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result", "-fno-slp-vectorize", *extra]
     objs, procs = [], []
     for src, opt in UNITS:  # the units compile concurrently
-        if dyn_opt and src in ("t1env_dynamics.hip", "t1env_dyn5.hip"):
+        if dyn_opt and src in ("t1env_dynamics.hip", "t1env_dyn5.hip", "t1env_dyn6.hip"):
             opt = dyn_opt
         obj = os.path.join(os.path.dirname(out), os.path.splitext(src)[0] + ".o")
         procs.append(subprocess.Popen([hipcc, opt, *common, "-c", "-o", obj, os.path.join(CSRC, src)]))

@@ -284,6 +284,132 @@ T1_HD void compute_delta_roles(const DynModel& M, const Terrain& T, const EnvPar
   for (int leg = 0; leg < 2; ++leg) backsub_leg(lb[leg], r, delta + 6 + 6 * leg);
 }
 
+// one half (NP points from c_begin) of a contact body against the terrain: contact_query + contact_apply, the fastest
+// approach of its points in amax (k_dyn6's contact_half, t1env_dyn6.hip, on one host thread)
+template <int NP, typename R>
+T1_HD void contact_points_half(const DynModel& M, const Terrain& T, int c_begin, const M3<R>& Rb, V3<R> pb,
+                               V3<R> base_abs, const R Vb[6], R mu, R vtg, R dt, Sym6<R>& A, R g[6], R& amax) {
+  ContactQuery<NP, R> Q;
+  if (T.type == 0) {
+    contact_query<false, NP>(M, T, c_begin, Rb, pb, base_abs, Q);
+    contact_apply<false, NP>(M, Q, Vb, mu, vtg, dt, A, g, amax);
+  } else {
+    contact_query<true, NP>(M, T, c_begin, Rb, pb, base_abs, Q);
+    contact_apply<true, NP>(M, Q, Vb, mu, vtg, dt, A, g, amax);
+  }
+}
+
+// k_dyn6's eight roles (t1env_dyn6.hip) composed on one thread: k_dyn5's composition with each terrain contact body
+// evaluated as two halves of its points (W2 / W6: the shank, W3 / W7: the foot) whose terms are summed, then the
+// self-contact terms added ((half 0 + half 1) + self), and the body's restitution episode taken from the larger of the
+// halves' fastest approach (the core wave, W0).  The base-box halves and the leg passes are k_dyn5's.
+template <typename R>
+T1_HD void compute_delta_roles6(const DynModel& M, const Terrain& T, const EnvParams<R>& P, EnvState<R>& s,
+                                const R tau[ND], V3<R> ext_f, R dt, R delta[6 + ND]) {
+  constexpr int KS = 3, KF = 5, NH = T1_POINTS_PER_BODY / 2;
+  static_assert(T1_LEG_CONTACT_MASK == ((1 << KS) | (1 << KF)), "roles assume shank + foot contacts");
+  BaseFrame<R> F;
+  base_frame(s, F);
+  const R mu = P.base.friction, e = ground_restitution(M, P.base.restitution);
+  // W0: the base block and the base-box contact halves, summed (left half first)
+  Sym6<R> Bs;
+  R rbs[6];
+  base_block(M, P.base, F, ext_f, dt, Bs, rbs);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) rbs[i] = -rbs[i];
+  const int32_t bound_b = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
+  for (int leg = 0; leg < 2; ++leg) {
+    int cb, ce;
+    base_contact_range(M, leg, cb, ce);
+    Sym6<R> Cb;
+    R gw[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+    sym_zero(Cb);
+    body_contact_fixed<T1_POINTS_PER_BODY / 2>(M, T, F.abs.z - R(M.contact_radius[0]), bound_b, cb, F.R0,
+                                               v3<R>(0, 0, 0), F.abs, F.V0, mu, e, s.vimp[vimp_base(leg)], dt, Cb, gw);
+    sym_add(Bs, Cb);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rbs[i] -= gw[i];
+  }
+  // W5: self-contact terms of both legs (from the substep's state)
+  SelfTerms<R> ST;
+  self_terms_env(M, F, s.q, s.qd, P.base, dt, ST);
+  LegBlock<R> lb[2];
+  Sym6<R> Ab[2];
+  R rb[2][6];
+  R vnew[2][2];  // the shank / foot episodes after this substep (W0 updates them after S2)
+  for (int leg = 0; leg < 2; ++leg) {
+    const R* q = s.q + 6 * leg;
+    const R* qd = s.qd + 6 * leg;
+    // W4
+    LegFK<R> fk;
+    leg_fk_chain(M, F.R0, q, leg, fk);
+    R S[NLEG][6];
+    sym_zero(Ab[leg]);
+    leg_backward_crba(M, P.leg[leg], q, qd, leg, dt, fk, S, lb[leg], Ab[leg]);
+    // W1
+    R rg[NLEG], G[6];
+    leg_bias_rhs(M, P.leg[leg], F, q, qd, tau + 6 * leg, leg, dt, rg, G);
+    // W2 / W6 (shank), W3 / W7 (foot): the terrain terms of each half of the body's points
+    BodyKin<R> K[2];
+    leg_body_kinematics(M, F, q, qd, leg, K);
+    Sym6<R> Ct[2];
+    R ct[2][6];
+    for (int i = 0; i < 2; ++i) {
+      const int b = 1 + 6 * leg + (i ? KF : KS);
+      const int vi = i ? vimp_foot(leg) : vimp_shank(leg);
+      const R vtg = restitution_target(M, e, s.vimp[vi]);
+      // the shank is skipped when out of the terrain's reach by its height bound (both halves: no contact)
+      const bool skip = i == 0 && K[i].p.z + F.abs.z - R(M.contact_radius[b]) >
+                                      bound_height<R>(T, terrain_bound_raw_any(T, K[i].p.x + F.abs.x, K[i].p.y + F.abs.y));
+      Sym6<R> Ch[2];
+      R ch[2][6], am[2] = {R(-1), R(-1)};
+      for (int h = 0; h < 2; ++h) {
+        sym_zero(Ch[h]);
+        for (int j = 0; j < 6; ++j) ch[h][j] = R(0);
+        if (!skip)
+          contact_points_half<NH>(M, T, M.contact_start[b] + h * NH, K[i].Rb, K[i].p, F.abs, K[i].V, mu, vtg, dt,
+                                  Ch[h], ch[h], am[h]);
+      }
+      vnew[leg][i] = restitution_episode(s.vimp[vi], am[0] > am[1] ? am[0] : am[1]);
+      // W0: (half 0 + half 1) + self
+      for (int j = 0; j < 21; ++j) Ct[i].a[j] = (Ch[0].a[j] + Ch[1].a[j]) + ST.C[leg][i].a[j];
+      for (int j = 0; j < 6; ++j) ct[i][j] = (ch[0][j] + ch[1][j]) + ST.c[leg][i][j];
+    }
+    // W0 after S2
+    R g6[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+    leg_apply_terms<KS, KF>(Ct[0], ct[0], Ct[1], ct[1], rg, G, S, lb[leg], Ab[leg], g6);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rb[leg][i] = -g6[i];
+    eliminate_leg(lb[leg], Ab[leg], rb[leg]);
+  }
+  for (int leg = 0; leg < 2; ++leg) {
+    s.vimp[vimp_shank(leg)] = vnew[leg][0];
+    s.vimp[vimp_foot(leg)] = vnew[leg][1];
+  }
+  // W0: base system = (base + base-box halves) + left leg + right leg
+  Sym6<R> Ac = Bs;
+  R r[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) r[i] = rbs[i];
+  for (int leg = 0; leg < 2; ++leg) {
+    sym_add(Ac, Ab[leg]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r[i] += rb[leg][i];
+  }
+  solve_base(Ac, r);
+  for (int i = 0; i < 6; ++i) delta[i] = r[i];
+  for (int leg = 0; leg < 2; ++leg) backsub_leg(lb[leg], r, delta + 6 + 6 * leg);
+}
+
+template <typename R>
+T1_HD void substep_roles6(const DynModel& M, const Terrain& T, const EnvParams<R>& P, EnvState<R>& s, const R tau[ND],
+                          V3<R> ext_f, R dt) {
+  R delta[6 + ND];
+  compute_delta_roles6(M, T, P, s, tau, ext_f, dt, delta);
+  integrate_base(s, delta, dt);
+  for (int leg = 0; leg < 2; ++leg) integrate_leg(M, leg, s.q + 6 * leg, s.qd + 6 * leg, delta + 6 + 6 * leg, dt);
+}
+
 template <typename R>
 T1_HD void substep_roles(const DynModel& M, const Terrain& T, const EnvParams<R>& P, EnvState<R>& s, const R tau[ND],
                          V3<R> ext_f, R dt) {

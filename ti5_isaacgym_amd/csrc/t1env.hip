@@ -482,8 +482,8 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
         hipSuccess) cus = 256;
     e->dyn.cus = cus;
     e->dyn.waves = t1_dyn_waves_default(cfg->num_envs, cus);
-    if (const char* dk = getenv("T1ENV_DYN_KERNEL"))  // A/B: 4 = k_dyn4, 5 = k_dyn5
-      if (atoi(dk) == 4 || atoi(dk) == 5) e->dyn.waves = atoi(dk);
+    if (const char* dk = getenv("T1ENV_DYN_KERNEL"))  // A/B: 4 = k_dyn4, 5 = k_dyn5, 6 = k_dyn6
+      if (atoi(dk) >= 4 && atoi(dk) <= 6) e->dyn.waves = atoi(dk);
     e->dyn.shift_blocks = 0;
     if (const char* sb = getenv("T1ENV_SHIFT_BLOCKS"))  // > 0: shift workgroups in the launch; -1: stand-alone shift
       if (atoi(sb) > 0 || atoi(sb) == -1) e->dyn.shift_blocks = atoi(sb);

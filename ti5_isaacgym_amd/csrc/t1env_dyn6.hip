@@ -1,0 +1,806 @@
+// t1env_dyn6.hip -- k_dyn6, the env step's main launch on eight waves: two waves per SIMD at 8192 envs
+// (legged_robot.py:399-434 + Isaac Gym simulate(), and in the fused step post-physics, legged_robot.py:458-506).
+//
+// k_dyn5 (t1env_dyn5.hip) runs 32 envs per workgroup on four role waves, one wave per SIMD: every role is issue-bound at
+// the lone-wave rate (one VALU instruction per 4 cycles, MI355X_MICROARCH.md constants table), and the step is the
+// longest pre-S2 role (the shank + foot-half terrain wave, ~3.4k VALU instructions per substep) plus the core wave's
+// post-S2 chain (~1.5k).  A SIMD issues a wave64 instruction in 2 cycles, so two waves per SIMD can double its VALU
+// rate; k_dyn6 keeps k_dyn5's lane layout (lane l of a wave: env blockIdx.x * 32 + (l & 31), leg l >> 5) and its
+// arithmetic, and spreads the pre-S2 work of the substep over eight roles of ~1.3-2k instructions, two per SIMD
+// (waves w and w + 4 share SIMD w):
+//
+//   wave  SIMD  S1 -> S2 (the terms of the published state)            S2 -> S1
+//   W0    0     PD torques, base block, base-box contacts (both halves)  core chain: fold-in, elimination, base system,
+//                                                                        solve, back-substitution, integration, publish
+//   W4    0     pose chain + contact-free CRBA backward pass (-> LDS)    --
+//   W1    1     RNEA bias and joint rhs                                  history shift slice
+//   W5    1     self-contacts (capsules, both legs' bodies by permlane)  history shift slice
+//   W2    2     shank terrain contact, points 0-3                        history shift slice
+//   W6    2     shank terrain contact, points 4-7                        history shift slice
+//   W3    3     foot terrain contact, points 0-3                         --
+//   W7    3     foot terrain contact, points 4-7                         --
+//
+// The core wave (W0) owns the restitution episodes of the shank, foot and base box: the contact halves publish the
+// fastest approach of their points (amx), and W0 folds the two halves of a body into its episode after S2.  The
+// history shift is no longer staged in LDS (the role hand-offs need it): the shift waves copy their slice of the
+// workgroup's rows through VGPRs (two aligned 16-B loads per output chunk, non-temporal stores) in the post-S2 window,
+// where their role state is dead.  The step's report and the fused epilogue are k_dyn5's, spread over the eight waves.
+//
+// Every value is computed by the same t1_dynamics.h / t1_dyn5.h functions as in k_dyn5; what differs is the order of a
+// few sums: a contact body's terms are the sum of its two point halves (and the self terms) instead of one 8-point
+// accumulation.  compute_delta_roles6 (t1_dyn5.h) is the same composition on one host thread (tests/test_dynamics.py).
+#include <hip/hip_runtime.h>
+
+#include "t1_dyn5.h"
+#include "t1env_device.h"
+#include "t1env_internal.h"
+#include "t1env_postphys.h"
+#include "t1env_fused.h"
+#include "t1env_roles.h"
+
+using namespace t1;
+
+constexpr int NE6 = 32;        // envs per workgroup
+constexpr int D6_BLOCK = 512;  // eight waves
+
+// W4 -> W0: the contact-free leg block (L, Bl, limit rhs) and the leg composite; the joint subspaces in rows of their own
+enum : int { CR_L = 0, CR_BL = 21, CR_RHS = 57, CR_AB = 63, CR_N = 84 };
+struct SubspaceRows { float4 r[NLEG][2][64]; };  // S_k = (r[k][0], r[k][1].xy)
+// W1 -> W0: the bias part of each joint rhs (-S_k . sum_{j>=k} g_j) and the leg's total bias
+enum : int { R_RG = 0, R_G = 6, R_N = 12 };
+// contact terms -> W0
+enum : int { WC_SHA = 0, WC_SHB = 1, WC_FTA = 2, WC_FTB = 3, WC_SSH = 4, WC_SFT = 5, WC_N = 6 };
+// the shift waves (post-S2) and their count
+constexpr int SHIFT6_MASK = (1 << 1) | (1 << 5) | (1 << 2) | (1 << 6);
+constexpr int SHIFT6_WAVES = 4;
+constexpr int SHIFT6_U = 4;  // output chunks per lane in flight
+
+struct Dyn6Lds {
+  DynModel model;
+  Rows4<Q_N> st;          // W0 -> all: substep state
+  Rows4<CR_N> crba;       // W4 -> W0
+  SubspaceRows sj;        // W4 -> W0
+  Rows4<R_N> w1;          // W1 -> W0
+  Rows4<XCH> wc[WC_N];    // contact roles -> W0
+  PdStage<64> pd;         // W0: PD constants and action ring of each lane's leg
+  float cap[CAP5_N][64];
+  float act[12][NE6];     // the clipped actions (epilogue)
+  float epi[EPI_N][NE6];  // staged post-physics inputs (epilogue)
+  float fr[FR_N][NE6];    // this step's outputs (epilogue)
+  float vish[64];         // the shank's restitution episode (W0 updates it after S2; W2 / W6 read it)
+  float vift[64];         // the foot's (W0; W3 / W7)
+  float vib[64];          // the base-box half's (W0; end of step: W4's report)
+  float amx[4][64];       // the fastest approach among the points of the shank halves [0, 1] and foot halves [2, 3]
+  float rtf[2][3][64];    // the report: terrain forces on the shank [0] (W2) / foot [1] (W3)
+  float rsf[2][3][64];    // the report: self-contact forces on the shank / foot (W5)
+};
+
+// ---- the history shift through VGPRs: output chunks [c_lo, c_hi) of the workgroup's rows [r0, r1) of one history,
+// lane t0 of `stride` lanes, U chunks per lane with their two aligned source loads issued before any store (the
+// in-launch form of shift_rows_f32 / shift_rows_f16, t1env_device.h, restricted to a chunk range)
+template <int F, int H, int U>
+__device__ __forceinline__ void shift6_f32(const float* __restrict__ in, float* __restrict__ out, int64_t total,
+                                           int64_t r0, int64_t r1, uint32_t c_lo, uint32_t c_hi, int t0, int stride) {
+  constexpr uint32_t ROW = F * H;
+  const float* __restrict__ in0 = in + r0 * ROW;
+  float* __restrict__ out0 = out + r0 * ROW;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
+  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
+  const uint32_t nel = span < lim ? span : lim;
+  const uint32_t n4 = (nel + 3) / 4;
+  const uint32_t hi = c_hi < n4 ? c_hi : n4;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  for (uint32_t base = c_lo + (uint32_t)t0; base < hi; base += U * (uint32_t)stride) {
+    float4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sa = ((base + u * stride) * 4 + F) & ~3u;
+      const uint32_t sc = sa + 8 <= lim ? sa : (lim - 8) & ~3u;  // tail: aligned in-bounds dummy
+      a[u] = *reinterpret_cast<const float4*>(in0 + sc);
+      b[u] = *reinterpret_cast<const float4*>(in0 + sc + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = base + u * stride;
+      if (c >= hi) break;
+      const uint32_t i = c * 4, sidx = i + F, sa = sidx & ~3u;
+      float4 x = a[u], y = b[u];
+      if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
+        float t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
+        x = make_float4(t[0], t[1], t[2], t[3]);
+        y = make_float4(t[4], t[5], t[6], t[7]);
+      }
+      const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+      constexpr int rem = (int)(F & 3u);
+      const uint32_t col0 = i - (i / ROW) * ROW;
+      if (col0 + 3 < ROW - F && i + 3 < lim) {  // 4 older-frame columns of one row
+        __builtin_nontemporal_store(f4v{src[rem], src[rem + 1], src[rem + 2], src[rem + 3]},
+                                    reinterpret_cast<f4v*>(out0 + i));
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t e = i + k;
+        if (e >= lim) break;
+        if (e - (e / ROW) * ROW < ROW - F) out0[e] = src[rem + k];
+      }
+    }
+  }
+}
+template <int F, int H, int U>
+__device__ __forceinline__ void shift6_f16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t total,
+                                           int64_t r0, int64_t r1, uint32_t c_lo, uint32_t c_hi, int t0, int stride) {
+  constexpr uint32_t ROW = F * H, REM = F % 8, M = REM / 2;
+  const uint16_t* __restrict__ in0 = in + r0 * ROW;
+  uint16_t* __restrict__ out0 = out + r0 * ROW;
+  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
+  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
+  const uint32_t nel = span < lim ? span : lim;
+  const uint32_t n8 = (nel + 7) / 8;
+  const uint32_t hi = c_hi < n8 ? c_hi : n8;
+  for (uint32_t base = c_lo + (uint32_t)t0; base < hi; base += U * (uint32_t)stride) {
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sa = ((base + u * stride) * 8 + F) & ~7u;
+      const uint32_t sc = sa + 16 <= lim ? sa : (lim - 16) & ~7u;
+      a[u] = *reinterpret_cast<const u32x4*>(in0 + sc);
+      b[u] = *reinterpret_cast<const u32x4*>(in0 + sc + 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c8 = base + u * stride;
+      if (c8 >= hi) break;
+      const uint32_t i = c8 * 8, sa = (i + F) & ~7u;
+      uint32_t w[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
+      if (sa + 16 > lim) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t lo = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
+          const uint32_t hh = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
+          w[k] = lo | (hh << 16);
+        }
+      }
+      u32x4 o;
+      if constexpr (REM % 2 == 0) {
+        o = u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
+      } else {
+        o = u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], 2), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], 2),
+                  __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], 2), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], 2)};
+      }
+      const uint32_t col0 = i - (i / ROW) * ROW;
+      if (col0 + 7 < ROW - F && i + 7 < lim) {
+        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out0 + i));
+        continue;
+      }
+      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t e = i + k;
+        if (e >= lim) break;
+        if (e - (e / ROW) * ROW < ROW - F) out0[e] = (uint16_t)(ow[k / 2] >> (16 * (k & 1)));
+      }
+    }
+  }
+}
+// slice `sl` of `nsl` of both histories of the rows [r0, r1), shift wave `wi` of SHIFT6_WAVES
+__device__ __forceinline__ void shift6_slice(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int wi,
+                                             int lane) {
+#ifdef T1_WHATIF_D6_NO_SHIFT  // timing-only what-if build: the history is not shifted
+  return;
+#endif
+  if (r1 <= r0 || sl >= nsl) return;
+  const int t0 = wi * 64 + lane, stride = 64 * SHIFT6_WAVES;
+  const int64_t ro = (int64_t)T1_NOBS * T1_HIST, rp = (int64_t)T1_NPRIV * T1_CHIST;
+  const int per = S.half ? 8 : 4;
+  // chunks of the rows (the buffer end clips the last workgroup's span; the range functions clip again)
+  auto chunks = [&](int64_t row, int64_t total) {
+    const int64_t lim = total - r0 * row, span = (r1 - r0) * row;
+    return (uint32_t)(((span < lim ? span : lim) + per - 1) / per);
+  };
+  const uint32_t no = chunks(ro, S.total_obs), np = chunks(rp, S.total_priv);
+  const uint32_t olo = no * sl / nsl, ohi = no * (sl + 1) / nsl, plo = np * sl / nsl, phi = np * (sl + 1) / nsl;
+  if (S.half) {
+    shift6_f16<T1_NOBS, T1_HIST, SHIFT6_U>(reinterpret_cast<const uint16_t*>(S.obs_in),
+                                            reinterpret_cast<uint16_t*>(S.obs_out), S.total_obs, r0, r1, olo, ohi, t0,
+                                            stride);
+    shift6_f16<T1_NPRIV, T1_CHIST, SHIFT6_U>(reinterpret_cast<const uint16_t*>(S.priv_in),
+                                              reinterpret_cast<uint16_t*>(S.priv_out), S.total_priv, r0, r1, plo, phi,
+                                              t0, stride);
+  } else {
+    shift6_f32<T1_NOBS, T1_HIST, SHIFT6_U>(S.obs_in, S.obs_out, S.total_obs, r0, r1, olo, ohi, t0, stride);
+    shift6_f32<T1_NPRIV, T1_CHIST, SHIFT6_U>(S.priv_in, S.priv_out, S.total_priv, r0, r1, plo, phi, t0, stride);
+  }
+}
+__device__ __forceinline__ int shift6_index(int wave) {  // the wave's index among the shift waves, -1: none
+  return (SHIFT6_MASK >> wave) & 1 ? __builtin_popcount(SHIFT6_MASK & ((1 << wave) - 1)) : -1;
+}
+
+// the other leg's capsule ends and velocity (from the other half of the wave) for the self-contact terms / forces
+__device__ __forceinline__ void self_bodies(const DynModel& M, int leg, const BodyKin<float> (&Ko)[2],
+                                            SelfBody<float> (&O)[2], SelfBody<float> (&X)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    O[s] = self_body(M, leg, s, Ko[s]);
+    const float mine[12] = {O[s].cap.p.x, O[s].cap.p.y, O[s].cap.p.z, O[s].cap.q.x, O[s].cap.q.y, O[s].cap.q.z,
+                            O[s].V[0],    O[s].V[1],    O[s].V[2],    O[s].V[3],    O[s].V[4],    O[s].V[5]};
+    float oth[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      float l, r;
+      halves(mine[i], l, r);
+      oth[i] = leg ? l : r;
+    }
+    X[s].cap.p = v3<float>(oth[0], oth[1], oth[2]);
+    X[s].cap.q = v3<float>(oth[3], oth[4], oth[5]);
+    X[s].cap.r = M.self_cap[1 - leg][s].r;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) X[s].V[i] = oth[6 + i];
+  }
+}
+
+// one contact half (4 points) of the shank or foot against the terrain: its terms and the fastest approach of its
+// points (amax < 0: none in contact, or the body out of the terrain's reach by its height bound -- the shank only)
+template <bool HF, bool BOUND>
+__device__ __forceinline__ void contact_half(const DynModel& M, const Terrain& T, int c0, const BodyKin<float>& K,
+                                             const BaseFrame<float>& F, int b, float mu, float vtg, float dt,
+                                             Sym6<float>& C, float c[6], float& amax) {
+  ContactQuery<T1_POINTS_PER_BODY / 2, float> Q;
+  contact_query<HF, T1_POINTS_PER_BODY / 2>(M, T, c0, K.Rb, K.p, F.abs, Q);
+  amax = -1.0f;
+  if constexpr (BOUND) {  // the body's height bound, loaded with the point queries (one memory round trip)
+    const int32_t bnd = terrain_bound_raw_any(T, K.p.x + F.abs.x, K.p.y + F.abs.y);
+    if (K.p.z + F.abs.z - M.contact_radius[b] > bound_height<float>(T, bnd)) return;
+  }
+  if (t1_wave_any(vtg > 0.0f)) contact_apply<HF, T1_POINTS_PER_BODY / 2>(M, Q, K.V, mu, vtg, dt, C, c, amax);
+  else contact_apply<HF, T1_POINTS_PER_BODY / 2>(M, Q, K.V, mu, 0.0f, dt, C, c, amax);
+}
+
+// leg_apply_terms (t1_dyn5.h) with the joint subspaces read from W4's LDS rows where they are used and the products
+// u_j = C S_j formed one joint at a time (leaf first): every element gets the same operations as there, in the same
+// order (the L, Bl and rhs updates of different joints are independent), with ~40 registers less at the core wave's
+// register peak
+template <int K0, int K1>
+__device__ __forceinline__ void leg_apply_terms_rows(const Sym6<float>& C0, const float c0[6], const Sym6<float>& C1,
+                                                     const float c1[6], const float rg[NLEG], const float G[6],
+                                                     const SubspaceRows& SR, int lane, LegBlock<float>& out,
+                                                     Sym6<float>& Ac_up, float gc_up[6]) {
+  static_assert(0 <= K0 && K0 < K1 && K1 < NLEG, "contact bodies K0 < K1 of the leg");
+  Sym6<float> Cs = C0;
+  sym_add(Cs, C1);
+  float cs[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) cs[i] = c0[i] + c1[i];
+  auto subspace = [&](int k, float (&Sk)[6]) {
+    const float4 a = SR.r[k][0][lane], b = SR.r[k][1][lane];
+    Sk[0] = a.x; Sk[1] = a.y; Sk[2] = a.z; Sk[3] = a.w; Sk[4] = b.x; Sk[5] = b.y;
+  };
+  auto joint = [&](auto jc) {
+    constexpr int jj = decltype(jc)::value;
+    float Sj[6], u[6];
+    subspace(jj, Sj);
+    if constexpr (jj <= K0) sym_mul(Cs, Sj, u);
+    else if constexpr (jj <= K1) sym_mul(C1, Sj, u);
+    else {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) u[i] = 0.0f;
+    }
+    const float sc = jj <= K0 ? dot6(Sj, cs) : (jj <= K1 ? dot6(Sj, c1) : 0.0f);
+    out.L[sidx(jj, jj)] += dot6(Sj, u);
+    out.rhs[jj] += rg[jj] - sc;
+#pragma unroll
+    for (int k = 0; k < jj; ++k) {
+      float Sk[6];
+      subspace(k, Sk);
+      out.L[sidx(k, jj)] += dot6(Sk, u);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) out.Bl[r][jj] += u[r];
+  };
+  joint(kconst<5>{});
+  joint(kconst<4>{});
+  joint(kconst<3>{});
+  joint(kconst<2>{});
+  joint(kconst<1>{});
+  joint(kconst<0>{});
+  sym_add(Ac_up, Cs);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) gc_up[i] += G[i] + cs[i];
+}
+
+template <bool HF, bool FUSED>
+__global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ Mg, const t1env_config* __restrict__ Cp,
+                                                   t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
+                                                   t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA,
+                                                   SubLog LG) {
+  __shared__ Dyn6Lds lds;
+  {  // the model to LDS
+    constexpr int NW = (int)(sizeof(DynModel) / 4);
+    static_assert(sizeof(DynModel) % 4 == 0, "the model copies as words");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(Mg);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&lds.model);
+    for (int i = threadIdx.x; i < NW; i += D6_BLOCK) dst[i] = src[i];
+  }
+  Terrain T = Tin;
+  T.type = HF ? 2 : 0;
+  const t1env_config& C = *Cp;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / 64);
+  const int lane = threadIdx.x & 63;
+  const int leg = lane >> 5;
+  const int e = lane & 31;
+  const int j0 = 6 * leg;
+  const int N = C.num_envs;
+  const int n0 = (int)blockIdx.x * NE6 + e;
+  const bool active = n0 < N;
+  const int n = active ? n0 : N - 1;
+  const float dt = C.sim_dt;
+  const uint32_t ctr = A.counter;
+  const int nsub = C.decimation;
+  const int64_t r0 = (int64_t)blockIdx.x * NE6, r1 = r0 + NE6 < N ? r0 + NE6 : N;
+  __syncthreads();  // the model in LDS
+  const DynModel& M = lds.model;
+
+  if (wave != 0) {
+    // ======== the term roles
+    const int wi = shift6_index(wave);
+    const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // robot shape vs ground (PhysX average)
+    const float mu_self = B.friction[n];                          // robot shape vs robot shape
+    const float eg = ground_restitution(M, B.restitution[n]);
+    LegParams<float> PL;
+    if (wave == 1 || wave == 4) load_leg_params(M, B, n, j0, PL);
+    // the epilogue's inputs the step does not change, staged by W4-W7 before their first substep
+    if (FUSED && wave >= 4) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
+    const int bsh = 1 + 6 * leg + K_SHANK, bft = 1 + 6 * leg + K_FOOT;
+    const int half = wave >= 4 ? 1 : 0;  // W2 / W3: points 0-3, W6 / W7: points 4-7
+    // each role its own substep loop (the register allocation of one role's loop does not carry the others' values)
+    if (wave == 4) {
+      // ---- W4: pose chain + contact-free CRBA backward pass
+      for (int sub = 0; sub < nsub; ++sub) {
+        __syncthreads();  // S1: the substep state published
+        BaseState<float> sb;
+        float q[NLEG], qd[NLEG];
+        read_state_rows(lds.st, lane, sb, q, qd);
+        const M3<float> R0 = quat_to_mat(sb.quat[0], sb.quat[1], sb.quat[2], sb.quat[3]);  // base_frame's F.R0
+        LegFK<float> fk;
+        leg_fk_chain(M, R0, q, leg, fk);
+        float Sj[NLEG][6];
+        LegBlock<float> lb;
+        Sym6<float> Ab;
+        sym_zero(Ab);
+        leg_backward_crba(M, PL, q, qd, leg, dt, fk, Sj, lb, Ab);
+        float v[CR_N];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) { v[CR_L + i] = lb.L[i]; v[CR_AB + i] = Ab.a[i]; }
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+          for (int k = 0; k < NLEG; ++k) v[CR_BL + 6 * r + k] = lb.Bl[r][k];
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) {
+          v[CR_RHS + k] = lb.rhs[k];
+          lds.sj.r[k][0][lane] = make_float4(Sj[k][0], Sj[k][1], Sj[k][2], Sj[k][3]);
+          lds.sj.r[k][1][lane] = make_float4(Sj[k][4], Sj[k][5], 0.0f, 0.0f);
+        }
+        put4(lds.crba, lane, v);
+        __syncthreads();  // S2: the terms published
+        if (wi >= 0) shift6_slice(S, r0, r1, sub, nsub, wi, lane);
+      }
+    } else if (wave == 1) {
+      // ---- W1: RNEA bias terms of the leg
+      for (int sub = 0; sub < nsub; ++sub) {
+        __syncthreads();  // S1
+        BaseState<float> sb;
+        float q[NLEG], qd[NLEG];
+        read_state_rows(lds.st, lane, sb, q, qd);
+        BaseFrame<float> F;
+        base_frame(sb, F);
+        const float zero6[NLEG] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        float rg[NLEG], G[6], v[R_N];
+        leg_bias_rhs(M, PL, F, q, qd, zero6, leg, dt, rg, G);  // -S_k . sum g (W0 adds dt tau_k)
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) v[R_RG + k] = rg[k];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[R_G + i] = G[i];
+        put4(lds.w1, lane, v);
+        __syncthreads();  // S2
+        if (wi >= 0) shift6_slice(S, r0, r1, sub, nsub, wi, lane);
+      }
+    } else if (wave == 5) {
+      // ---- W5: self-contact terms of the shank and foot
+      for (int sub = 0; sub < nsub; ++sub) {
+        __syncthreads();  // S1
+        BaseState<float> sb;
+        float q[NLEG], qd[NLEG];
+        read_state_rows(lds.st, lane, sb, q, qd);
+        BaseFrame<float> F;
+        base_frame(sb, F);
+        BodyKin<float> Ko[2];
+        leg_body_kinematics(M, F, q, qd, leg, Ko);
+        Sym6<float> Cs[2];
+        float cs[2][6];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          sym_zero(Cs[i]);
+#pragma unroll
+          for (int j = 0; j < 6; ++j) cs[i][j] = 0.0f;
+        }
+        if (M.self_collisions) {
+          SelfBody<float> O[2], X[2];
+          self_bodies(M, leg, Ko, O, X);
+          self_terms_bodies(M, leg, O, X, mu_self, dt, Cs, cs);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          float v[XCH];
+          sym_pack(Cs[i], cs[i], v);
+          put4(lds.wc[WC_SSH + i], lane, v);
+        }
+        __syncthreads();  // S2
+        if (wi >= 0) shift6_slice(S, r0, r1, sub, nsub, wi, lane);
+      }
+    } else {
+      // ---- W2 / W6: shank terrain, W3 / W7: foot terrain (one half of the body's points each)
+      const bool shank = wave == 2 || wave == 6;
+      const int slot = (shank ? WC_SHA : WC_FTA) + half;
+      const int b = shank ? bsh : bft;
+      const int c0 = M.contact_start[b] + half * (T1_POINTS_PER_BODY / 2);
+      for (int sub = 0; sub < nsub; ++sub) {
+        __syncthreads();  // S1
+        BaseState<float> sb;
+        float q[NLEG], qd[NLEG];
+        read_state_rows(lds.st, lane, sb, q, qd);
+        BaseFrame<float> F;
+        base_frame(sb, F);
+        BodyKin<float> Ko[2];
+        leg_body_kinematics(M, F, q, qd, leg, Ko);
+        Sym6<float> Cc;
+        float cc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        sym_zero(Cc);
+        float amax;
+        if (shank) {
+          const float vtg = restitution_target(M, eg, lds.vish[lane]);
+          contact_half<HF, true>(M, T, c0, Ko[0], F, b, mu, vtg, dt, Cc, cc, amax);
+        } else {
+          const float vtg = restitution_target(M, eg, lds.vift[lane]);
+          contact_half<HF, false>(M, T, c0, Ko[1], F, b, mu, vtg, dt, Cc, cc, amax);
+        }
+        float v[XCH];
+        sym_pack(Cc, cc, v);
+        put4(lds.wc[slot], lane, v);
+        lds.amx[slot][lane] = amax;
+        __syncthreads();  // S2
+        if (wi >= 0) shift6_slice(S, r0, r1, sub, nsub, wi, lane);
+      }
+    }
+    if (wi >= 0) __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
+    __syncthreads();  // R1: the end-of-step state and episodes published
+    {  // the contact-force report from the end-of-step state: W2 the shank's terrain force, W3 the foot's, W5 their
+       // self-contact forces, W4 the base box (leg-0 lanes); W6 sums and stores the shank / foot rows after RB
+      BaseState<float> sb;
+      float q[NLEG], qd[NLEG];
+      read_state_rows(lds.st, lane, sb, q, qd);
+      BaseFrame<float> F;
+      base_frame(sb, F);
+      V3<float> fb = v3<float>(0.0f, 0.0f, 0.0f);
+      if (wave == 4) {
+        if (leg == 0) {
+          const float vt0 = restitution_target(M, eg, lds.vib[lane]), vt1 = restitution_target(M, eg, lds.vib[lane ^ 32]);
+          fb = body_contact_force(M, T, 0, F.R0, v3<float>(0, 0, 0), F.abs, F.V0, mu, vt0 > vt1 ? vt0 : vt1);
+        }
+      } else if (wave == 2 || wave == 3 || wave == 5) {
+        BodyKin<float> Ko[2];
+        leg_body_kinematics(M, F, q, qd, leg, Ko);
+        if (wave == 5) {
+          V3<float> fself[2] = {v3<float>(0.0f, 0.0f, 0.0f), v3<float>(0.0f, 0.0f, 0.0f)};
+          if (M.self_collisions) {
+            SelfBody<float> O[2], X[2];
+            self_bodies(M, leg, Ko, O, X);
+            self_forces_bodies(M, leg, O, X, mu_self, fself);
+          }
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            lds.rsf[s][0][lane] = fself[s].x; lds.rsf[s][1][lane] = fself[s].y; lds.rsf[s][2][lane] = fself[s].z;
+          }
+        } else {
+          const int s = wave == 2 ? 0 : 1;
+          const int b = s == 0 ? bsh : bft;
+          const float vt = restitution_target(M, eg, s == 0 ? lds.vish[lane] : lds.vift[lane]);
+          const V3<float> f = body_contact_force(M, T, b, Ko[s].Rb, Ko[s].p, F.abs, Ko[s].V, mu, vt);
+          lds.rtf[s][0][lane] = f.x; lds.rtf[s][1][lane] = f.y; lds.rtf[s][2][lane] = f.z;
+        }
+      }
+      __syncthreads();  // RB: the report's parts in LDS
+      if (wave == 4 && leg == 0) {
+        if (active) {
+          float* cf = B.contact_forces + (size_t)n * 39;
+          cf[0] = fb.x; cf[1] = fb.y; cf[2] = fb.z;
+        }
+        if constexpr (FUSED) { lds.fr[F_CFB][e] = fb.x; lds.fr[F_CFB + 1][e] = fb.y; lds.fr[F_CFB + 2][e] = fb.z; }
+      }
+      if (wave == 6) {
+        float* cf = B.contact_forces + (size_t)n * 39;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int b = s == 0 ? bsh : bft;
+          const float f[3] = {lds.rtf[s][0][lane] + lds.rsf[s][0][lane], lds.rtf[s][1][lane] + lds.rsf[s][1][lane],
+                              lds.rtf[s][2][lane] + lds.rsf[s][2][lane]};
+          if (active) { cf[b * 3 + 0] = f[0]; cf[b * 3 + 1] = f[1]; cf[b * 3 + 2] = f[2]; }
+          if (FUSED && s == 1) {
+            const int r = leg == 0 ? F_C0 : F_C1;
+            lds.fr[r][e] = f[0]; lds.fr[r + 1][e] = f[1]; lds.fr[r + 2][e] = f[2];
+          }
+        }
+      }
+    }
+    if constexpr (FUSED) {
+      __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
+      if (wave == 1)
+        fused_epilogue_staged<POST_A_STATE, NE6, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
+                                                       lds.act + NLEG);
+      else if (wave == 2)
+        fused_epilogue_obs<POST_OBS_PRIV, NE6>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
+      else if (wave == 3)
+        fused_epilogue_obs<POST_OBS_ACTOR, NE6>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
+    }
+    return;
+  }
+
+  // ======== W0: core -- PD torques, base block, base-box contacts; after S2 fold-in, elimination, base system,
+  // integration; owns the actions, the PD staging and the restitution episodes of the shank, foot and base-box half
+  BaseParams<float> PB;
+  BaseState<float> sb;
+  float q[NLEG], qd[NLEG];
+  load_base_params(M, B, n, PB);
+  load_base_state(M, PB, B.root_states + (size_t)n * 13, sb);
+#pragma unroll
+  for (int k = 0; k < NLEG; ++k) {
+    q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
+    qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
+  }
+  // every per-env load of the prologue is issued before its first global store (k_dyn5)
+  const int lag = B.lag_timestep[n];
+  const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
+  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
+  float vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
+  float vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
+  float vi_b = B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)];
+  int s_dof = 9 - B.dof_lag_timestep[n] % 10;
+#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
+  s_dof = s_dof > 0 ? s_dof - 1 : 0;
+#endif
+  const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
+  {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged
+    PdStage<64>& P = lds.pd;
+    float a[NLEG];
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) a[k] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
+    const int cs = (int)(ctr & 3u);
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      const int j = j0 + k;
+      P.kp[k][lane] = B.kp[n * 12 + j];
+      P.kd[k][lane] = B.kd[n * 12 + j];
+      P.off[k][lane] = B.motor_offsets[n * 12 + j];
+      P.visc[k][lane] = B.viscous[n * 12 + j];
+      P.coul[k][lane] = B.coulomb[n * 12 + j];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k)
+        P.act[s][k][lane] = s == cs ? a[k] * C.action_scale : B.act_hist[((size_t)n * 4 + s) * 12 + j0 + k];
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) lds.act[j0 + k][e] = a[k];
+    if (active) {
+      float* slot = B.act_hist + ((size_t)n * 4 + cs) * 12;
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) {
+        B.actions[n * 12 + j0 + k] = a[k];
+        slot[j0 + k] = a[k] * C.action_scale;
+      }
+    }
+  }
+  lds.vift[lane] = vi_ft;
+  lds.vish[lane] = vi_sh;
+  const float mu = PB.friction, eg = ground_restitution(M, PB.restitution);
+  int cb, ce;
+  base_contact_range(M, leg, cb, ce);
+  float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
+  float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
+  float tau[NLEG];
+  {
+    float v[Q_N];
+    state_pack(sb, q, qd, v);
+    put4(lds.st, lane, v);
+  }
+  for (int sub = 0; sub < nsub; ++sub) {
+    __syncthreads();  // S1: the substep state published
+    BaseFrame<float> F;
+    base_frame(sb, F);
+    pd_torques_staged(M, C, lds.pd, lane, K, ctr, sub, lag, j0, q, qd, tau);
+    Sym6<float> Ac;  // the base body's block (both halves compute it: the same values)
+    float r[6];
+    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
+    {  // the base-box halves, summed left first (the same sum in both halves), into the base block before S2
+      const int32_t bound_b = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
+      ContactQuery<T1_POINTS_PER_BODY / 2, float> Qb;
+      contact_query<HF, T1_POINTS_PER_BODY / 2>(M, T, cb, F.R0, v3<float>(0, 0, 0), F.abs, Qb);
+      Sym6<float> Cb;
+      float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+      sym_zero(Cb);
+      body_contact_fixed_q<HF, T1_POINTS_PER_BODY / 2>(M, Qb, F.abs.z - M.contact_radius[0], bound_b, T, F.V0, mu, eg,
+                                                       vi_b, dt, Cb, gw);
+#pragma unroll
+      for (int i = 0; i < 21; ++i) {
+        float l, rr;
+        halves(Cb.a[i], l, rr);
+        Ac.a[i] = Ac.a[i] + (l + rr);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        float l, rr;
+        halves(gw[i], l, rr);
+        r[i] = -r[i] + (-l - rr);
+      }
+    }
+    __syncthreads();  // S2: the terms published
+    {  // the episodes of the shank and foot from the two halves of their points
+      vi_sh = restitution_episode(vi_sh, fmaxf(lds.amx[WC_SHA][lane], lds.amx[WC_SHB][lane]));
+      vi_ft = restitution_episode(vi_ft, fmaxf(lds.amx[WC_FTA][lane], lds.amx[WC_FTB][lane]));
+      lds.vish[lane] = vi_sh;  // W2 / W6 read it after the next S1
+      lds.vift[lane] = vi_ft;  // W3 / W7
+    }
+    LegBlock<float> lb;
+    Sym6<float> Ab;
+    {
+      float v[CR_N];
+      get4(lds.crba, lane, v);
+#pragma unroll
+      for (int i = 0; i < 21; ++i) { lb.L[i] = v[CR_L + i]; Ab.a[i] = v[CR_AB + i]; }
+#pragma unroll
+      for (int rr = 0; rr < 6; ++rr)
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) lb.Bl[rr][k] = v[CR_BL + 6 * rr + k];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) lb.rhs[k] = v[CR_RHS + k];
+    }
+    float g6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    {
+      float w1v[R_N];
+      get4(lds.w1, lane, w1v);
+      float rg[NLEG], G[6];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) rg[k] = dt * tau[k] + w1v[R_RG + k];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) G[i] = w1v[R_G + i];
+      Sym6<float> Cb[2];
+      float cbv[2][6];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // shank [0]: (points 0-3 + 4-7) + self; foot [1]: the same
+        float va[XCH], vb[XCH], vs[XCH];
+        get4(lds.wc[2 * i], lane, va);
+        get4(lds.wc[2 * i + 1], lane, vb);
+        get4(lds.wc[WC_SSH + i], lane, vs);
+#pragma unroll
+        for (int k = 0; k < XCH; ++k) va[k] = (va[k] + vb[k]) + vs[k];
+        sym_unpack(va, Cb[i], cbv[i]);
+      }
+      leg_apply_terms_rows<K_SHANK, K_FOOT>(Cb[0], cbv[0], Cb[1], cbv[1], rg, G, lds.sj, lane, lb, Ab, g6);
+    }
+    float rb[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rb[i] = -g6[i];
+    eliminate_leg(lb, Ab, rb);
+    // the base system: (base block + both base-box halves) + the left leg + the right leg, in every lane
+#pragma unroll
+    for (int i = 0; i < 21; ++i) {
+      float l, rr;
+      halves(Ab.a[i], l, rr);
+      Ac.a[i] = (Ac.a[i] + l) + rr;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      float l, rr;
+      halves(rb[i], l, rr);
+      r[i] = (r[i] + l) + rr;
+    }
+    solve_base(Ac, r);
+    float dq[NLEG];
+    backsub_leg(lb, r, dq);
+    integrate_base(sb, r, dt);
+    integrate_leg(M, leg, q, qd, dq, dt);
+    if (LG.root != nullptr) {  // wave-uniform (a kernel argument)
+      if (active) {
+        const size_t row = (size_t)sub * N + n;
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) {
+          LG.torque[row * 12 + j0 + k] = tau[k];
+          LG.dof[row * 24 + 2 * (j0 + k)] = q[k];
+          LG.dof[row * 24 + 2 * (j0 + k) + 1] = qd[k];
+        }
+        if (leg == 0) {
+          BaseFrame<float> FL;
+          base_frame(sb, FL);
+          float body[13];
+          root_row(M, PB, sb, FL, body);
+#pragma unroll
+          for (int i = 0; i < 13; ++i) LG.root[row * 13 + i] = body[i];
+        }
+      }
+    }
+    if (sub == s_dof) {
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { lds.cap[k][lane] = q[k]; lds.cap[NLEG + k][lane] = qd[k]; }
+    }
+    if (leg == 0 && sub == s_imu) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lds.cap[2 * NLEG + i][lane] = sb.quat[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) lds.cap[2 * NLEG + 4 + i][lane] = sb.w[i];
+    }
+    float v[Q_N];
+    state_pack(sb, q, qd, v);
+    put4(lds.st, lane, v);  // the roles read the previous state before S2; after the last substep: the report's
+  }
+  lds.vib[lane] = vi_b;  // the end-of-step episodes for the report (W4: base box; W2 / W3 read vish / vift)
+  if (active) {
+    B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)] = vi_ft;
+    B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
+    B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)] = vi_b;
+    if (s_dof < nsub) {  // the sensor-lag samples captured in the loop
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) { dof_dst[j0 + k] = lds.cap[k][lane]; dof_dst[12 + j0 + k] = lds.cap[NLEG + k][lane]; }
+    }
+    if (leg == 0 && s_imu < nsub) {
+      const float quat[4] = {lds.cap[2 * NLEG][lane], lds.cap[2 * NLEG + 1][lane], lds.cap[2 * NLEG + 2][lane],
+                             lds.cap[2 * NLEG + 3][lane]};
+      const float w[3] = {lds.cap[2 * NLEG + 4][lane], lds.cap[2 * NLEG + 5][lane], lds.cap[2 * NLEG + 6][lane]};
+      capture_imu(quat, w, imu_dst);
+    }
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
+      B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
+      B.torques[n * 12 + j0 + k] = tau[k];
+    }
+  }
+  float (*FR)[NE6] = FUSED ? lds.fr : nullptr;
+  if constexpr (FUSED) {
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      lds.fr[F_DOF + 2 * (j0 + k)][e] = q[k];
+      lds.fr[F_DOF + 2 * (j0 + k) + 1][e] = qd[k];
+      lds.fr[F_TQ + j0 + k][e] = tau[k];
+    }
+  }
+  __syncthreads();  // R1: the end-of-step state published (the report's contact forces meanwhile)
+  {
+    BaseFrame<float> F;
+    base_frame(sb, F);
+    leg_report_rigid<NE6>(M, B, PB, sb, F, q, qd, n, leg, active, e, FR);
+  }
+  __syncthreads();  // RB: the contact-force report's parts in LDS
+  if constexpr (FUSED) {
+    __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
+    fused_epilogue_staged<POST_A_REWARDS, NE6, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
+                                                     lds.act + NLEG);
+  }
+}
+
+int t1_launch_dyn6(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
+                   const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
+                   const FusedArgs* fused, hipStream_t s, const SubLog* log) {
+  const int blocks = (num_envs + NE6 - 1) / NE6;
+  const FusedArgs FA = fused ? *fused : FusedArgs{};
+  const SubLog LG = log ? *log : SubLog{};
+  const bool hf = T.type != 0;
+  if (log && !fused) return (int)hipErrorInvalidValue;  // the substep log: fused steps only (the caller checks)
+#define T1_LAUNCH6(HF, FU) \
+  hipLaunchKernelGGL((k_dyn6<HF, FU>), dim3(blocks), dim3(D6_BLOCK), 0, s, d_model, d_cfg, B, T, actions, A, S, blocks, FA, LG)
+  if (fused) { if (hf) T1_LAUNCH6(true, true); else T1_LAUNCH6(false, true); }
+  else { if (hf) T1_LAUNCH6(true, false); else T1_LAUNCH6(false, false); }
+#undef T1_LAUNCH6
+  return (int)hipGetLastError();
+}

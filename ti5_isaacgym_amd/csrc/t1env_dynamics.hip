@@ -630,7 +630,7 @@ int t1_dyn_waves_default(int num_envs, int cus) { return (num_envs + 31) / 32 <=
 
 constexpr int MIN_SHIFT_BLOCKS = 64;
 bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg) {
-  if (cfg.waves == 5) return false;        // k_dyn5: every workgroup shifts its own rows
+  if (cfg.waves >= 5) return false;        // k_dyn5 / k_dyn6: every workgroup shifts its own rows
   if (cfg.shift_blocks < 0) return true;   // forced stand-alone shift (tuning: T1ENV_SHIFT_BLOCKS=-1)
   if (cfg.shift_blocks > 0) return false;  // explicit shift-workgroup count (tuning)
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;
@@ -641,6 +641,7 @@ int t1_launch_dynamics(const DynModel* d_model, const t1env_config* d_cfg, const
                        const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,
                        const DynLaunch& cfg, const FusedArgs* fused, hipStream_t s, bool shift_prelaunched,
                        const SubLog* log) {
+  if (cfg.waves == 6) return t1_launch_dyn6(d_model, d_cfg, B, T, actions, A, num_envs, S, fused, s, log);
   if (cfg.waves == 5)  // the shift in the workgroup (d5_shift 0) or the caller's concurrent k_shift5 launch (1)
     return t1_launch_dyn5(d_model, d_cfg, B, T, actions, A, num_envs, S, fused, s, log, cfg.d5_shift == 0);
   const int dyn_blocks = (num_envs + DYN_ENVS - 1) / DYN_ENVS;

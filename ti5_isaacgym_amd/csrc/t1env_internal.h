@@ -34,9 +34,10 @@ constexpr int T1_SHIFT_DELAY_DEFAULT = 3000;
 
 // launch shape of the dynamics kernel
 struct DynLaunch {
-  int waves;         // 5: k_dyn5 (t1env_dyn5.hip: 32 envs per workgroup, four roles, in-workgroup history shift; the
-                     //    default up to 32 envs per CU), 4: k_dyn4 (64 envs per workgroup, leg + contact helper waves;
-                     //    the default above; T1ENV_DYN_KERNEL=4|5 overrides)
+  int waves;         // 6: k_dyn6 (t1env_dyn6.hip: 32 envs per workgroup, eight role waves, two per SIMD), 5: k_dyn5
+                     //    (t1env_dyn5.hip: 32 envs per workgroup, four roles, in-workgroup history shift), 4: k_dyn4
+                     //    (64 envs per workgroup, leg + contact helper waves); t1_dyn_waves_default picks by env
+                     //    count, T1ENV_DYN_KERNEL=4|5|6 overrides
   int cus;           // compute units of the device (default history-shift grid)
   int shift_blocks;  // > 0: history-shift workgroups override (tuning)
   int shift_delay;   // in-launch shift workgroups start this many 100 MHz ticks late (T1ENV_SHIFT_DELAY; 0 = at once)
@@ -60,6 +61,11 @@ bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg);
 int t1_launch_dyn5(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const t1::Terrain& T,
                    const float* actions, const t1env_step_args& A, int num_envs, const t1::ShiftArgs& S,
                    const FusedArgs* fused, hipStream_t s, const SubLog* log, bool inwg_shift);
+// k_dyn6 (t1env_dyn6.hip): k_dyn5's roles on eight waves (two per SIMD), the same contract; each workgroup shifts its own
+// history rows
+int t1_launch_dyn6(const t1::DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const t1::Terrain& T,
+                   const float* actions, const t1env_step_args& A, int num_envs, const t1::ShiftArgs& S,
+                   const FusedArgs* fused, hipStream_t s, const SubLog* log);
 // k_dyn5's history shift as its own launch (k_shift5), for a second stream beside k_dyn5 (d5_shift = 1); fused: the
 // unit handoff with the fused epilogue, else plain (k_post_b zeroes the reset rows)
 int t1_launch_shift5(const t1::ShiftArgs& S, const FusedArgs* fused, int num_envs, int cus, hipStream_t s);
