@@ -84,8 +84,8 @@ def parse():
     p.add_argument("--time-every", type=int, default=8,
                    help="record per-kernel HIP events on every k-th timed step (event records cost host time; "
                         "0 = never, 1 = every step)")
-    p.add_argument("--cpu-envs", type=int, default=4096,
-                   help="CPU-baseline sample size (BASELINE configs[1]'s 4096 envs; 256 understated the CPU by ~2x)")
+    p.add_argument("--cpu-envs", type=int, default=None,
+                   help="CPU-baseline env count (default: --num-envs, the metric's 8192; VERDICT r4 #7)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--cpu-shards", type=int, default=32,
                    help="CPU baseline: env shards stepped on Python threads (at most the affinity's core count)")
@@ -123,7 +123,10 @@ def effective_cores():
 
 
 def cpu_baseline(env, args):
-    """Bounded sample of the same workload on the host cores (the build's CPU restatement)."""
+    """Bounded sample of the same workload on the host cores (the build's CPU restatement), at the metric's env count
+    unless --cpu-envs says otherwise."""
+    if args.cpu_envs is None:
+        args.cpu_envs = args.num_envs
     from oracle.cpu_env import ShardedCpuT1Env
     terrain = None
     if env.mesh_type in ("heightfield", "trimesh"):

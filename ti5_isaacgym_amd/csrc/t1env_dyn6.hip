@@ -10,9 +10,9 @@
 // (waves w and w + 4 share SIMD w):
 //
 //   wave  SIMD  S1 -> S2 (the terms of the published state)            S2 -> S1
-//   W0    0     PD torques, base block, base-box contacts (both halves)  core chain: fold-in, elimination, base system,
+//   W0    0     pose chain + contact-free CRBA backward pass             core chain: fold-in, elimination, base system,
 //                                                                        solve, back-substitution, integration, publish
-//   W4    0     pose chain + contact-free CRBA backward pass (-> LDS)    --
+//   W4    0     PD torques, base block, base-box contacts (both halves)  --
 //   W1    1     RNEA bias and joint rhs                                  history shift slice
 //   W5    1     self-contacts (capsules, both legs' bodies by permlane)  history shift slice
 //   W2    2     shank terrain contact, points 0-3                        history shift slice
@@ -20,8 +20,9 @@
 //   W3    3     foot terrain contact, points 0-3                         --
 //   W7    3     foot terrain contact, points 4-7                         --
 //
-// The core wave (W0) owns the restitution episodes of the shank, foot and base box: the contact halves publish the
-// fastest approach of their points (amx), and W0 folds the two halves of a body into its episode after S2.  The
+// The core wave (W0) owns the restitution episodes of the shank and foot: the contact halves publish the fastest
+// approach of their points (amx), and W0 folds the two halves of a body into its episode after S2 (W4 keeps the base
+// box's, as k_dyn5's W1).  The
 // history shift is no longer staged in LDS (the role hand-offs need it): the shift waves copy their slice of the
 // workgroup's rows through VGPRs (two aligned 16-B loads per output chunk, non-temporal stores) in the post-S2 window,
 // where their role state is dead.  The step's report and the fused epilogue are k_dyn5's, spread over the eight waves.
@@ -43,8 +44,9 @@ using namespace t1;
 constexpr int NE6 = 32;        // envs per workgroup
 constexpr int D6_BLOCK = 512;  // eight waves
 
-// W4 -> W0: the contact-free leg block (L, Bl, limit rhs) and the leg composite; the joint subspaces in rows of their own
-enum : int { CR_L = 0, CR_BL = 21, CR_RHS = 57, CR_AB = 63, CR_N = 84 };
+// W4 -> W0: the substep's PD torques, the base block with both base-box halves, its rhs
+enum : int { WB_TAU = 0, WB_AC = 8, WB_R = 29, WB_N = 35 };
+// W0's joint subspaces (its CRBA pass -> its fold-in), in rows of their own
 struct SubspaceRows { float4 r[NLEG][2][64]; };  // S_k = (r[k][0], r[k][1].xy)
 // W1 -> W0: the bias part of each joint rhs (-S_k . sum_{j>=k} g_j) and the leg's total bias
 enum : int { R_RG = 0, R_G = 6, R_N = 12 };
@@ -58,19 +60,20 @@ constexpr int SHIFT6_U = 4;  // output chunks per lane in flight
 struct Dyn6Lds {
   DynModel model;
   Rows4<Q_N> st;          // W0 -> all: substep state
-  Rows4<CR_N> crba;       // W4 -> W0
-  SubspaceRows sj;        // W4 -> W0
+  Rows4<WB_N> wb;         // W4 -> W0
+  SubspaceRows sj;        // W0
   Rows4<R_N> w1;          // W1 -> W0
   Rows4<XCH> wc[WC_N];    // contact roles -> W0
-  PdStage<64> pd;         // W0: PD constants and action ring of each lane's leg
+  PdStage<64> pd;         // W4: PD constants and action ring of each lane's leg
   float cap[CAP5_N][64];
   float act[12][NE6];     // the clipped actions (epilogue)
   float epi[EPI_N][NE6];  // staged post-physics inputs (epilogue)
   float fr[FR_N][NE6];    // this step's outputs (epilogue)
   float vish[64];         // the shank's restitution episode (W0 updates it after S2; W2 / W6 read it)
   float vift[64];         // the foot's (W0; W3 / W7)
-  float vib[64];          // the base-box half's (W0; end of step: W4's report)
   float amx[4][64];       // the fastest approach among the points of the shank halves [0, 1] and foot halves [2, 3]
+  LegParams<float> pl[64];   // W0's per-lane leg parameters (CRBA) and base parameters (report, log): LDS, not
+  BaseParams<float> pb[64];  // registers held across the substep loop
   float rtf[2][3][64];    // the report: terrain forces on the shank [0] (W2) / foot [1] (W3)
   float rsf[2][3][64];    // the report: self-contact forces on the shank / foot (W5)
 };
@@ -218,6 +221,16 @@ __device__ __forceinline__ int shift6_index(int wave) {  // the wave's index amo
   return (SHIFT6_MASK >> wave) & 1 ? __builtin_popcount(SHIFT6_MASK & ((1 << wave) - 1)) : -1;
 }
 
+// The model in LDS as the loop sees it: the address passes through an empty asm each substep, so its per-lane reads (the
+// leg index is a lane value) are not hoisted out of the substep loop as invariants -- at two waves per SIMD (256
+// registers) the hoisted model values would be spilled to scratch, and an LDS read is the cheaper re-load
+__device__ __forceinline__ const DynModel& model_in_loop(const DynModel& m) {
+  typedef __attribute__((address_space(3))) const DynModel* lds_model_ptr;
+  lds_model_ptr p = (lds_model_ptr)&m;
+  asm volatile("" : "+s"(p));
+  return *(const DynModel*)p;
+}
+
 // the other leg's capsule ends and velocity (from the other half of the wave) for the self-contact terms / forces
 __device__ __forceinline__ void self_bodies(const DynModel& M, int leg, const BodyKin<float> (&Ko)[2],
                                             SelfBody<float> (&O)[2], SelfBody<float> (&X)[2]) {
@@ -258,36 +271,45 @@ __device__ __forceinline__ void contact_half(const DynModel& M, const Terrain& T
   else contact_apply<HF, T1_POINTS_PER_BODY / 2>(M, Q, K.V, mu, 0.0f, dt, C, c, amax);
 }
 
-// leg_apply_terms (t1_dyn5.h) with the joint subspaces read from W4's LDS rows where they are used and the products
-// u_j = C S_j formed one joint at a time (leaf first): every element gets the same operations as there, in the same
-// order (the L, Bl and rhs updates of different joints are independent), with ~40 registers less at the core wave's
-// register peak
+// leg_apply_terms (t1_dyn5.h) with its inputs read from LDS where they are used, to hold the core wave's register peak:
+// the joint subspaces (W0's own CRBA rows) per joint, the foot's terms ((points 0-3 + 4-7) + self) for joints 5 and 4,
+// then the shank's, added to them in place for joints 3-0 (Cs = C0 + C1, the same sums), the bias G last.  Every
+// element gets leg_apply_terms' operations in its order (the L, Bl and rhs updates of different joints are independent).
 template <int K0, int K1>
-__device__ __forceinline__ void leg_apply_terms_rows(const Sym6<float>& C0, const float c0[6], const Sym6<float>& C1,
-                                                     const float c1[6], const float rg[NLEG], const float G[6],
-                                                     const SubspaceRows& SR, int lane, LegBlock<float>& out,
-                                                     Sym6<float>& Ac_up, float gc_up[6]) {
-  static_assert(0 <= K0 && K0 < K1 && K1 < NLEG, "contact bodies K0 < K1 of the leg");
-  Sym6<float> Cs = C0;
-  sym_add(Cs, C1);
-  float cs[6];
+__device__ __forceinline__ void leg_apply_terms_rows(const Rows4<XCH> (&W)[WC_N], const Rows4<R_N>& W1,
+                                                     const float rg[NLEG], const SubspaceRows& SR, int lane,
+                                                     LegBlock<float>& out, Sym6<float>& Ac_up, float gc_up[6]) {
+  static_assert(K0 == K_SHANK && K1 == K_FOOT && K1 == NLEG - 1, "the foot's terms first, then the shank's");
+  auto terms = [&](int i, Sym6<float>& Cb, float cb[6]) {  // contact body i (0 shank, 1 foot): (half 0 + half 1) + self
+    float va[XCH];
+    get4(W[2 * i], lane, va);
+    {
+      float vb[XCH];
+      get4(W[2 * i + 1], lane, vb);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) cs[i] = c0[i] + c1[i];
-  auto subspace = [&](int k, float (&Sk)[6]) {
-    const float4 a = SR.r[k][0][lane], b = SR.r[k][1][lane];
-    Sk[0] = a.x; Sk[1] = a.y; Sk[2] = a.z; Sk[3] = a.w; Sk[4] = b.x; Sk[5] = b.y;
+      for (int k = 0; k < XCH; ++k) va[k] = va[k] + vb[k];
+    }
+    {
+      float vs[XCH];
+      get4(W[WC_SSH + i], lane, vs);
+#pragma unroll
+      for (int k = 0; k < XCH; ++k) va[k] = va[k] + vs[k];
+    }
+    sym_unpack(va, Cb, cb);
   };
+  auto subspace = [&](int k, float (&Sk)[6]) {
+    const float4 x = SR.r[k][0][lane], y = SR.r[k][1][lane];
+    Sk[0] = x.x; Sk[1] = x.y; Sk[2] = x.z; Sk[3] = x.w; Sk[4] = y.x; Sk[5] = y.y;
+  };
+  Sym6<float> C;  // C1 (the foot), then Cs = C0 + C1
+  float c[6];
+  terms(1, C, c);
   auto joint = [&](auto jc) {
     constexpr int jj = decltype(jc)::value;
     float Sj[6], u[6];
     subspace(jj, Sj);
-    if constexpr (jj <= K0) sym_mul(Cs, Sj, u);
-    else if constexpr (jj <= K1) sym_mul(C1, Sj, u);
-    else {
-#pragma unroll
-      for (int i = 0; i < 6; ++i) u[i] = 0.0f;
-    }
-    const float sc = jj <= K0 ? dot6(Sj, cs) : (jj <= K1 ? dot6(Sj, c1) : 0.0f);
+    sym_mul(C, Sj, u);
+    const float sc = dot6(Sj, c);
     out.L[sidx(jj, jj)] += dot6(Sj, u);
     out.rhs[jj] += rg[jj] - sc;
 #pragma unroll
@@ -301,13 +323,24 @@ __device__ __forceinline__ void leg_apply_terms_rows(const Sym6<float>& C0, cons
   };
   joint(kconst<5>{});
   joint(kconst<4>{});
+  {
+    Sym6<float> C0;
+    float c0[6];
+    terms(0, C0, c0);
+#pragma unroll
+    for (int i = 0; i < 21; ++i) C.a[i] = C0.a[i] + C.a[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) c[i] = c0[i] + c[i];
+  }
   joint(kconst<3>{});
   joint(kconst<2>{});
   joint(kconst<1>{});
   joint(kconst<0>{});
-  sym_add(Ac_up, Cs);
+  sym_add(Ac_up, C);
+  float w1v[R_N];
+  get4(W1, lane, w1v);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) gc_up[i] += G[i] + cs[i];
+  for (int i = 0; i < 6; ++i) gc_up[i] += w1v[R_G + i] + c[i];
 }
 
 template <bool HF, bool FUSED>
@@ -342,53 +375,149 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   __syncthreads();  // the model in LDS
   const DynModel& M = lds.model;
 
+  if (wave == 4) {
+    // ======== W4: base -- the actions, PD torques, the base block and both base-box halves (their restitution episode)
+    BaseParams<float> PB;
+    load_base_params(M, B, n, PB);
+    const int lag = B.lag_timestep[n];
+    const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
+    const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
+    float vi_b = B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)];
+    {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged (every per-env
+       // load before the first global store: the buffers may alias as far as the compiler knows)
+      PdStage<64>& P = lds.pd;
+      float a[NLEG];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) a[k] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
+      const int cs = (int)(ctr & 3u);
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) {
+        const int j = j0 + k;
+        P.kp[k][lane] = B.kp[n * 12 + j];
+        P.kd[k][lane] = B.kd[n * 12 + j];
+        P.off[k][lane] = B.motor_offsets[n * 12 + j];
+        P.visc[k][lane] = B.viscous[n * 12 + j];
+        P.coul[k][lane] = B.coulomb[n * 12 + j];
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k)
+          P.act[s][k][lane] = s == cs ? a[k] * C.action_scale : B.act_hist[((size_t)n * 4 + s) * 12 + j0 + k];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) lds.act[j0 + k][e] = a[k];
+      if (active) {
+        float* slot = B.act_hist + ((size_t)n * 4 + cs) * 12;
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) {
+          B.actions[n * 12 + j0 + k] = a[k];
+          slot[j0 + k] = a[k] * C.action_scale;
+        }
+      }
+    }
+    // the epilogue's inputs the step does not change, staged by W4-W7 before their first substep
+    if (FUSED) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
+    const float mu = PB.friction, eg = ground_restitution(M, PB.restitution);
+    int cb, ce;
+    base_contact_range(M, leg, cb, ce);
+    float tau[NLEG];
+    for (int sub = 0; sub < nsub; ++sub) {
+      __syncthreads();  // S1: the substep state published
+      BaseState<float> sb;
+      float q[NLEG], qd[NLEG];
+      read_state_rows(lds.st, lane, sb, q, qd);
+      BaseFrame<float> F;
+      base_frame(sb, F);
+      // the base box half's queries issued first, under the PD torques and the base block
+      const int32_t bound_b = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
+      ContactQuery<T1_POINTS_PER_BODY / 2, float> Qb;
+      contact_query<HF, T1_POINTS_PER_BODY / 2>(M, T, cb, F.R0, v3<float>(0, 0, 0), F.abs, Qb);
+      pd_torques_staged(M, C, lds.pd, lane, K, ctr, sub, lag, j0, q, qd, tau);
+      Sym6<float> Ac;  // the base body's block (both halves compute it: the same values)
+      float r[6];
+      base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
+      {  // the base-box halves, summed left first (the same sum in both halves), into the base block
+        Sym6<float> Cb;
+        float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        sym_zero(Cb);
+        body_contact_fixed_q<HF, T1_POINTS_PER_BODY / 2>(M, Qb, F.abs.z - M.contact_radius[0], bound_b, T, F.V0, mu, eg,
+                                                         vi_b, dt, Cb, gw);
+#pragma unroll
+        for (int i = 0; i < 21; ++i) {
+          float l, rr;
+          halves(Cb.a[i], l, rr);
+          Ac.a[i] = Ac.a[i] + (l + rr);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          float l, rr;
+          halves(gw[i], l, rr);
+          r[i] = -r[i] + (-l - rr);
+        }
+      }
+      float v[WB_N];
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) v[WB_TAU + k] = tau[k];
+      v[NLEG] = 0.0f;
+      v[NLEG + 1] = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 21; ++i) v[WB_AC + i] = Ac.a[i];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) v[WB_R + i] = r[i];
+      put4(lds.wb, lane, v);
+      if (LG.root != nullptr && active)  // the substep log's torques (tests only; wave-uniform kernel argument)
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) LG.torque[((size_t)sub * N + n) * 12 + j0 + k] = tau[k];
+      __syncthreads();  // S2: the terms published
+    }
+    if (active) {
+      B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)] = vi_b;
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) B.torques[n * 12 + j0 + k] = tau[k];
+    }
+    if constexpr (FUSED)
+#pragma unroll
+      for (int k = 0; k < NLEG; ++k) lds.fr[F_TQ + j0 + k][e] = tau[k];
+    float vl, vr;
+    halves(vi_b, vl, vr);  // the base box's two halves' end-of-step episodes (leg-0 lanes report the whole box)
+    __syncthreads();  // R1: the end-of-step state published
+    V3<float> fb = v3<float>(0.0f, 0.0f, 0.0f);
+    if (leg == 0) {
+      BaseState<float> sb;
+      float q[NLEG], qd[NLEG];
+      read_state_rows(lds.st, lane, sb, q, qd);
+      BaseFrame<float> F;
+      base_frame(sb, F);
+      const float vt0 = restitution_target(M, eg, vl), vt1 = restitution_target(M, eg, vr);
+      fb = body_contact_force(M, T, 0, F.R0, v3<float>(0, 0, 0), F.abs, F.V0, mu, vt0 > vt1 ? vt0 : vt1);
+    }
+    __syncthreads();  // RB: the report's parts in LDS
+    if (leg == 0) {
+      if (active) {
+        float* cf = B.contact_forces + (size_t)n * 39;
+        cf[0] = fb.x; cf[1] = fb.y; cf[2] = fb.z;
+      }
+      if constexpr (FUSED) { lds.fr[F_CFB][e] = fb.x; lds.fr[F_CFB + 1][e] = fb.y; lds.fr[F_CFB + 2][e] = fb.z; }
+    }
+    if constexpr (FUSED) __syncthreads();  // the epilogue barrier
+    return;
+  }
+
   if (wave != 0) {
-    // ======== the term roles
+    // ======== the term roles W1-W3, W5-W7
     const int wi = shift6_index(wave);
     const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // robot shape vs ground (PhysX average)
     const float mu_self = B.friction[n];                          // robot shape vs robot shape
     const float eg = ground_restitution(M, B.restitution[n]);
-    LegParams<float> PL;
-    if (wave == 1 || wave == 4) load_leg_params(M, B, n, j0, PL);
     // the epilogue's inputs the step does not change, staged by W4-W7 before their first substep
-    if (FUSED && wave >= 4) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
+    if (FUSED && wave >= 5) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
     const int bsh = 1 + 6 * leg + K_SHANK, bft = 1 + 6 * leg + K_FOOT;
     const int half = wave >= 4 ? 1 : 0;  // W2 / W3: points 0-3, W6 / W7: points 4-7
     // each role its own substep loop (the register allocation of one role's loop does not carry the others' values)
-    if (wave == 4) {
-      // ---- W4: pose chain + contact-free CRBA backward pass
-      for (int sub = 0; sub < nsub; ++sub) {
-        __syncthreads();  // S1: the substep state published
-        BaseState<float> sb;
-        float q[NLEG], qd[NLEG];
-        read_state_rows(lds.st, lane, sb, q, qd);
-        const M3<float> R0 = quat_to_mat(sb.quat[0], sb.quat[1], sb.quat[2], sb.quat[3]);  // base_frame's F.R0
-        LegFK<float> fk;
-        leg_fk_chain(M, R0, q, leg, fk);
-        float Sj[NLEG][6];
-        LegBlock<float> lb;
-        Sym6<float> Ab;
-        sym_zero(Ab);
-        leg_backward_crba(M, PL, q, qd, leg, dt, fk, Sj, lb, Ab);
-        float v[CR_N];
-#pragma unroll
-        for (int i = 0; i < 21; ++i) { v[CR_L + i] = lb.L[i]; v[CR_AB + i] = Ab.a[i]; }
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-          for (int k = 0; k < NLEG; ++k) v[CR_BL + 6 * r + k] = lb.Bl[r][k];
-#pragma unroll
-        for (int k = 0; k < NLEG; ++k) {
-          v[CR_RHS + k] = lb.rhs[k];
-          lds.sj.r[k][0][lane] = make_float4(Sj[k][0], Sj[k][1], Sj[k][2], Sj[k][3]);
-          lds.sj.r[k][1][lane] = make_float4(Sj[k][4], Sj[k][5], 0.0f, 0.0f);
-        }
-        put4(lds.crba, lane, v);
-        __syncthreads();  // S2: the terms published
-        if (wi >= 0) shift6_slice(S, r0, r1, sub, nsub, wi, lane);
-      }
-    } else if (wave == 1) {
+    if (wave == 1) {
       // ---- W1: RNEA bias terms of the leg
+      LegParams<float> PL;
+      load_leg_params(M, B, n, j0, PL);
       for (int sub = 0; sub < nsub; ++sub) {
         __syncthreads();  // S1
         BaseState<float> sb;
@@ -477,19 +606,13 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     if (wi >= 0) __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
     __syncthreads();  // R1: the end-of-step state and episodes published
     {  // the contact-force report from the end-of-step state: W2 the shank's terrain force, W3 the foot's, W5 their
-       // self-contact forces, W4 the base box (leg-0 lanes); W6 sums and stores the shank / foot rows after RB
-      BaseState<float> sb;
-      float q[NLEG], qd[NLEG];
-      read_state_rows(lds.st, lane, sb, q, qd);
-      BaseFrame<float> F;
-      base_frame(sb, F);
-      V3<float> fb = v3<float>(0.0f, 0.0f, 0.0f);
-      if (wave == 4) {
-        if (leg == 0) {
-          const float vt0 = restitution_target(M, eg, lds.vib[lane]), vt1 = restitution_target(M, eg, lds.vib[lane ^ 32]);
-          fb = body_contact_force(M, T, 0, F.R0, v3<float>(0, 0, 0), F.abs, F.V0, mu, vt0 > vt1 ? vt0 : vt1);
-        }
-      } else if (wave == 2 || wave == 3 || wave == 5) {
+       // self-contact forces; W6 sums and stores the shank / foot rows after RB (the base box: W4)
+      if (wave == 2 || wave == 3 || wave == 5) {
+        BaseState<float> sb;
+        float q[NLEG], qd[NLEG];
+        read_state_rows(lds.st, lane, sb, q, qd);
+        BaseFrame<float> F;
+        base_frame(sb, F);
         BodyKin<float> Ko[2];
         leg_body_kinematics(M, F, q, qd, leg, Ko);
         if (wave == 5) {
@@ -512,13 +635,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         }
       }
       __syncthreads();  // RB: the report's parts in LDS
-      if (wave == 4 && leg == 0) {
-        if (active) {
-          float* cf = B.contact_forces + (size_t)n * 39;
-          cf[0] = fb.x; cf[1] = fb.y; cf[2] = fb.z;
-        }
-        if constexpr (FUSED) { lds.fr[F_CFB][e] = fb.x; lds.fr[F_CFB + 1][e] = fb.y; lds.fr[F_CFB + 2][e] = fb.z; }
-      }
       if (wave == 6) {
         float* cf = B.contact_forces + (size_t)n * 39;
 #pragma unroll
@@ -547,69 +663,35 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     return;
   }
 
-  // ======== W0: core -- PD torques, base block, base-box contacts; after S2 fold-in, elimination, base system,
-  // integration; owns the actions, the PD staging and the restitution episodes of the shank, foot and base-box half
-  BaseParams<float> PB;
+  // ======== W0: core -- pose chain + contact-free CRBA backward pass; after S2 fold-in, elimination, base system,
+  // integration; owns the joint state and the restitution episodes of the shank and foot
+  BaseParams<float>& PB = lds.pb[lane];
+  LegParams<float>& PL = lds.pl[lane];
   BaseState<float> sb;
   float q[NLEG], qd[NLEG];
-  load_base_params(M, B, n, PB);
-  load_base_state(M, PB, B.root_states + (size_t)n * 13, sb);
+  {
+    BaseParams<float> pb;
+    LegParams<float> pl;
+    load_base_params(M, B, n, pb);
+    load_leg_params(M, B, n, j0, pl);
+    load_base_state(M, pb, B.root_states + (size_t)n * 13, sb);
+    PB = pb;
+    PL = pl;
+  }
 #pragma unroll
   for (int k = 0; k < NLEG; ++k) {
     q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
     qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
   }
-  // every per-env load of the prologue is issued before its first global store (k_dyn5)
-  const int lag = B.lag_timestep[n];
-  const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
-  const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
   float vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
   float vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
-  float vi_b = B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)];
   int s_dof = 9 - B.dof_lag_timestep[n] % 10;
 #ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
   s_dof = s_dof > 0 ? s_dof - 1 : 0;
 #endif
   const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
-  {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged
-    PdStage<64>& P = lds.pd;
-    float a[NLEG];
-#pragma unroll
-    for (int k = 0; k < NLEG; ++k) a[k] = fminf(fmaxf(actions[n * 12 + j0 + k], -C.clip_actions), C.clip_actions);
-    const int cs = (int)(ctr & 3u);
-#pragma unroll
-    for (int k = 0; k < NLEG; ++k) {
-      const int j = j0 + k;
-      P.kp[k][lane] = B.kp[n * 12 + j];
-      P.kd[k][lane] = B.kd[n * 12 + j];
-      P.off[k][lane] = B.motor_offsets[n * 12 + j];
-      P.visc[k][lane] = B.viscous[n * 12 + j];
-      P.coul[k][lane] = B.coulomb[n * 12 + j];
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k)
-        P.act[s][k][lane] = s == cs ? a[k] * C.action_scale : B.act_hist[((size_t)n * 4 + s) * 12 + j0 + k];
-#pragma unroll
-    for (int k = 0; k < NLEG; ++k) lds.act[j0 + k][e] = a[k];
-    if (active) {
-      float* slot = B.act_hist + ((size_t)n * 4 + cs) * 12;
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) {
-        B.actions[n * 12 + j0 + k] = a[k];
-        slot[j0 + k] = a[k] * C.action_scale;
-      }
-    }
-  }
   lds.vift[lane] = vi_ft;
   lds.vish[lane] = vi_sh;
-  const float mu = PB.friction, eg = ground_restitution(M, PB.restitution);
-  int cb, ce;
-  base_contact_range(M, leg, cb, ce);
-  float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
-  float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
-  float tau[NLEG];
   {
     float v[Q_N];
     state_pack(sb, q, qd, v);
@@ -617,32 +699,20 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   }
   for (int sub = 0; sub < nsub; ++sub) {
     __syncthreads();  // S1: the substep state published
-    BaseFrame<float> F;
-    base_frame(sb, F);
-    pd_torques_staged(M, C, lds.pd, lane, K, ctr, sub, lag, j0, q, qd, tau);
-    Sym6<float> Ac;  // the base body's block (both halves compute it: the same values)
-    float r[6];
-    base_block(M, PB, F, sub == 0 ? ef : v3<float>(0, 0, 0), dt, Ac, r);
-    {  // the base-box halves, summed left first (the same sum in both halves), into the base block before S2
-      const int32_t bound_b = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
-      ContactQuery<T1_POINTS_PER_BODY / 2, float> Qb;
-      contact_query<HF, T1_POINTS_PER_BODY / 2>(M, T, cb, F.R0, v3<float>(0, 0, 0), F.abs, Qb);
-      Sym6<float> Cb;
-      float gw[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-      sym_zero(Cb);
-      body_contact_fixed_q<HF, T1_POINTS_PER_BODY / 2>(M, Qb, F.abs.z - M.contact_radius[0], bound_b, T, F.V0, mu, eg,
-                                                       vi_b, dt, Cb, gw);
+    const DynModel& M = model_in_loop(lds.model);
+    LegBlock<float> lb;
+    Sym6<float> Ab;
+    {
+      const M3<float> R0 = quat_to_mat(sb.quat[0], sb.quat[1], sb.quat[2], sb.quat[3]);  // base_frame's F.R0
+      LegFK<float> fk;
+      leg_fk_chain(M, R0, q, leg, fk);
+      float Sj[NLEG][6];
+      sym_zero(Ab);
+      leg_backward_crba(M, PL, q, qd, leg, dt, fk, Sj, lb, Ab);
 #pragma unroll
-      for (int i = 0; i < 21; ++i) {
-        float l, rr;
-        halves(Cb.a[i], l, rr);
-        Ac.a[i] = Ac.a[i] + (l + rr);
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        float l, rr;
-        halves(gw[i], l, rr);
-        r[i] = -r[i] + (-l - rr);
+      for (int k = 0; k < NLEG; ++k) {  // the joint subspaces to LDS for the fold-in (registers at its peak)
+        lds.sj.r[k][0][lane] = make_float4(Sj[k][0], Sj[k][1], Sj[k][2], Sj[k][3]);
+        lds.sj.r[k][1][lane] = make_float4(Sj[k][4], Sj[k][5], 0.0f, 0.0f);
       }
     }
     __syncthreads();  // S2: the terms published
@@ -652,48 +722,31 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       lds.vish[lane] = vi_sh;  // W2 / W6 read it after the next S1
       lds.vift[lane] = vi_ft;  // W3 / W7
     }
-    LegBlock<float> lb;
-    Sym6<float> Ab;
-    {
-      float v[CR_N];
-      get4(lds.crba, lane, v);
-#pragma unroll
-      for (int i = 0; i < 21; ++i) { lb.L[i] = v[CR_L + i]; Ab.a[i] = v[CR_AB + i]; }
-#pragma unroll
-      for (int rr = 0; rr < 6; ++rr)
-#pragma unroll
-        for (int k = 0; k < NLEG; ++k) lb.Bl[rr][k] = v[CR_BL + 6 * rr + k];
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) lb.rhs[k] = v[CR_RHS + k];
-    }
     float g6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     {
-      float w1v[R_N];
-      get4(lds.w1, lane, w1v);
-      float rg[NLEG], G[6];
+      float rg[NLEG];  // dt tau_k (W4's torques, the first two rows of wb) + the bias part (W1)
+      const float4 t0 = lds.wb.r[0][lane], t1 = lds.wb.r[1][lane], g0 = lds.w1.r[0][lane], g1 = lds.w1.r[1][lane];
+      const float tv[NLEG] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y}, gv[NLEG] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y};
+      static_assert(WB_TAU == 0 && R_RG == 0, "the torques and the bias rhs lead their rows");
 #pragma unroll
-      for (int k = 0; k < NLEG; ++k) rg[k] = dt * tau[k] + w1v[R_RG + k];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) G[i] = w1v[R_G + i];
-      Sym6<float> Cb[2];
-      float cbv[2][6];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {  // shank [0]: (points 0-3 + 4-7) + self; foot [1]: the same
-        float va[XCH], vb[XCH], vs[XCH];
-        get4(lds.wc[2 * i], lane, va);
-        get4(lds.wc[2 * i + 1], lane, vb);
-        get4(lds.wc[WC_SSH + i], lane, vs);
-#pragma unroll
-        for (int k = 0; k < XCH; ++k) va[k] = (va[k] + vb[k]) + vs[k];
-        sym_unpack(va, Cb[i], cbv[i]);
-      }
-      leg_apply_terms_rows<K_SHANK, K_FOOT>(Cb[0], cbv[0], Cb[1], cbv[1], rg, G, lds.sj, lane, lb, Ab, g6);
+      for (int k = 0; k < NLEG; ++k) rg[k] = dt * tv[k] + gv[k];
+      leg_apply_terms_rows<K_SHANK, K_FOOT>(lds.wc, lds.w1, rg, lds.sj, lane, lb, Ab, g6);
     }
     float rb[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) rb[i] = -g6[i];
     eliminate_leg(lb, Ab, rb);
-    // the base system: (base block + both base-box halves) + the left leg + the right leg, in every lane
+    // the base system: (base block + both base-box halves, W4) + the left leg + the right leg, in every lane
+    Sym6<float> Ac;
+    float r[6];
+    {
+      float v[WB_N];
+      get4(lds.wb, lane, v);
+#pragma unroll
+      for (int i = 0; i < 21; ++i) Ac.a[i] = v[WB_AC + i];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) r[i] = v[WB_R + i];
+    }
 #pragma unroll
     for (int i = 0; i < 21; ++i) {
       float l, rr;
@@ -711,12 +764,11 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     backsub_leg(lb, r, dq);
     integrate_base(sb, r, dt);
     integrate_leg(M, leg, q, qd, dq, dt);
-    if (LG.root != nullptr) {  // wave-uniform (a kernel argument)
+    if (LG.root != nullptr) {  // wave-uniform (a kernel argument); the torques: W4
       if (active) {
         const size_t row = (size_t)sub * N + n;
 #pragma unroll
         for (int k = 0; k < NLEG; ++k) {
-          LG.torque[row * 12 + j0 + k] = tau[k];
           LG.dof[row * 24 + 2 * (j0 + k)] = q[k];
           LG.dof[row * 24 + 2 * (j0 + k) + 1] = qd[k];
         }
@@ -744,11 +796,11 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     state_pack(sb, q, qd, v);
     put4(lds.st, lane, v);  // the roles read the previous state before S2; after the last substep: the report's
   }
-  lds.vib[lane] = vi_b;  // the end-of-step episodes for the report (W4: base box; W2 / W3 read vish / vift)
   if (active) {
+    float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
+    float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
     B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)] = vi_ft;
     B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
-    B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)] = vi_b;
     if (s_dof < nsub) {  // the sensor-lag samples captured in the loop
 #pragma unroll
       for (int k = 0; k < NLEG; ++k) { dof_dst[j0 + k] = lds.cap[k][lane]; dof_dst[12 + j0 + k] = lds.cap[NLEG + k][lane]; }
@@ -763,7 +815,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     for (int k = 0; k < NLEG; ++k) {
       B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
       B.dof_state[n * 24 + 2 * (j0 + k) + 1] = qd[k];
-      B.torques[n * 12 + j0 + k] = tau[k];
     }
   }
   float (*FR)[NE6] = FUSED ? lds.fr : nullptr;
@@ -772,7 +823,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     for (int k = 0; k < NLEG; ++k) {
       lds.fr[F_DOF + 2 * (j0 + k)][e] = q[k];
       lds.fr[F_DOF + 2 * (j0 + k) + 1][e] = qd[k];
-      lds.fr[F_TQ + j0 + k][e] = tau[k];
     }
   }
   __syncthreads();  // R1: the end-of-step state published (the report's contact forces meanwhile)
