@@ -97,7 +97,8 @@ class DHPPO:
         # graphed rollout act(): {(obs ptr, critic obs ptr, shapes): (graph, static outputs)}; None = eager
         self.graph_act = cuda
         self._act_graphs = {}
-        # graphed update minibatch step (single process; the DP all-reduce stays eager): (key, graph) once captured
+        # graphed update minibatch step: (key, graph) once captured; under data parallelism (key, (graph A, graph B))
+        # with the gradient / KL all-reduce eager between them
         self.graph_update = cuda
         if cuda:
             _init_graph_rng(device)
@@ -105,6 +106,8 @@ class DHPPO:
         self._upd_warm = 0
         self._idx = None
         self._sums = torch.zeros(3, device=device)
+        self._kl = torch.zeros(1, device=device)   # this rank's KL mean, then the all-reduced one (DP graphed step)
+        self._kl_deferred = False
 
     @property
     def learning_rate(self):
@@ -255,19 +258,14 @@ class DHPPO:
             kl = torch.sum(torch.log(sigma / old_sigma + 1.0e-5)
                            + (torch.square(old_sigma) + torch.square(old_mu - mu)) / (2.0 * torch.square(sigma)) - 0.5,
                            axis=-1)
+            if self._kl_deferred:
+                # the data-parallel graphed step (_dp_part_a): this rank's KL mean, all-reduced between the two graphs
+                # and decided on in _dp_part_b (the lr only matters at the optimizer step: the same decision)
+                self._kl.copy_(torch.mean(kl).reshape(1))
+                return
             kl_mean = dist_util.all_reduce_mean_(torch.mean(kl).reshape(1))[0]
             if self._lr_t is not None:
-                # the same decision on the device (no host sync; capturable): lr / 1.5 floored at 1e-5 above twice the
-                # target KL, lr * 1.5 capped at 1e-2 below half of it (a KL of exactly 0 keeps lr); the KL compared in
-                # fp32 as the reference's tensor comparisons, the lr stepped in fp64 as its Python float
-                lr = self._lr64
-                # a tensor divisor: torch divides by a host scalar as a multiply by its reciprocal (one more rounding
-                # than the reference's Python lr / 1.5)
-                down = torch.clamp(lr / self._c15, min=1e-5)
-                up = torch.clamp(lr * 1.5, max=1e-2)
-                low = (kl_mean > 0.0) & (kl_mean < self.desired_kl / 2.0)
-                lr.copy_(torch.where(kl_mean > self.desired_kl * 2.0, down, torch.where(low, up, lr)))
-                self._lr_t.copy_(lr)
+                self._lr_decide(kl_mean)
                 return
             kl_mean = float(kl_mean)
         if kl_mean > self.desired_kl * 2.0:
@@ -276,6 +274,54 @@ class DHPPO:
             self.learning_rate = min(1e-2, self.learning_rate * 1.5)
         for g in self.optimizer.param_groups:
             g["lr"] = self.learning_rate
+
+    def _lr_decide(self, kl_mean):
+        """The adaptive decision on the device (no host sync; capturable): lr / 1.5 floored at 1e-5 above twice the
+        target KL, lr * 1.5 capped at 1e-2 below half of it (a KL of exactly 0 keeps lr); the KL compared in fp32 as
+        the reference's tensor comparisons, the lr stepped in fp64 as its Python float."""
+        lr = self._lr64
+        # a tensor divisor: torch divides by a host scalar as a multiply by its reciprocal (one more rounding than the
+        # reference's Python lr / 1.5)
+        down = torch.clamp(lr / self._c15, min=1e-5)
+        up = torch.clamp(lr * 1.5, max=1e-2)
+        low = (kl_mean > 0.0) & (kl_mean < self.desired_kl / 2.0)
+        lr.copy_(torch.where(kl_mean > self.desired_kl * 2.0, down, torch.where(low, up, lr)))
+        self._lr_t.copy_(lr)
+
+    # ---- the data-parallel minibatch step on the device, in two parts around the exchange (dh_ppo.py:139-151,
+    # 180-182): part A forward, losses, this rank's KL mean and backward into the gradient bucket; the exchange all-reduces
+    # the bucket and the KL mean (RCCL on MI355X; it cannot sit inside a captured graph with gloo, and stays outside
+    # with RCCL too); part B the adaptive lr decision, clipping and Adam.  Graphed, A and B are two captured graphs.
+    def _dp_part_a(self, batch, amp, mse):
+        ac = self.actor_critic
+        (obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b, hid_b,
+         masks_b) = batch
+        self._kl_deferred = True
+        try:
+            with amp:
+                loss, value_loss, surrogate_loss, se_loss = self._losses(
+                    ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
+                    old_sigma_b, hid_b, masks_b, mse)
+        finally:
+            self._kl_deferred = False
+        self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
+        loss.backward()
+        self._sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), se_loss.detach()])
+
+    def _dp_exchange(self):
+        self.grads.all_reduce_()
+        if self._adaptive():
+            dist_util.all_reduce_mean_(self._kl)
+
+    def _dp_part_b(self):
+        if self._adaptive():
+            with torch.no_grad():
+                self._lr_decide(self._kl[0])
+        nn.utils.clip_grad_norm_(self.actor_critic.parameters(), self.max_grad_norm)
+        self.optimizer.step()
+
+    def _adaptive(self):
+        return self.desired_kl is not None and self.schedule == "adaptive"
 
     def _minibatch_step(self, batch, amp, mse):
         """One minibatch of the update: losses, backward, gradient all-reduce, clipping, Adam; the losses summed into
@@ -293,6 +339,16 @@ class DHPPO:
         nn.utils.clip_grad_norm_(ac.parameters(), self.max_grad_norm)
         self.optimizer.step()
         self._sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), se_loss.detach()])
+
+    def _step_eager(self, batch, amp, mse):
+        """One eager minibatch step: the single-process / host step, or on the device under data parallelism the two
+        parts of the graphed step around the exchange (the same kernels as its graph replays)."""
+        if self._lr_t is not None and dist_util.active():
+            self._dp_part_a(batch, amp, mse)
+            self._dp_exchange()
+            self._dp_part_b()
+        else:
+            self._minibatch_step(batch, amp, mse)
 
     def update(self):
         ac = self.actor_critic
@@ -314,12 +370,12 @@ class DHPPO:
         if cuda:
             ac.validate_args = False
         try:
-            if cuda and self.graph_update and not dist_util.active():
+            if cuda and self.graph_update:
                 self._update_graphed(amp, mse, obs_dtype)
             else:
                 for batch in self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs,
                                                                obs_dtype=obs_dtype):
-                    self._minibatch_step(batch, amp, mse)
+                    self._step_eager(batch, amp, mse)
         finally:
             ac.validate_args = validate
         if cuda:  # the optimizer steps were graph replays (no version bump): repack the conv's fragments now
@@ -334,8 +390,10 @@ class DHPPO:
     WARMUP_STEPS = 2   # eager minibatch steps (on a side stream) before the capture
 
     def _update_graphed(self, amp, mse, obs_dtype):
-        """The minibatches of mini_batch_generator, each as (copy its indices into a static buffer, replay)."""
+        """The minibatches of mini_batch_generator, each as (copy its indices into a static buffer, replay); under data
+        parallelism each as (copy, replay part A, exchange, replay part B)."""
         st = self.storage
+        dp = dist_util.active()
         mb = st.num_envs * st.num_transitions_per_env // self.num_mini_batches
         perm = torch.randperm(self.num_mini_batches * mb, requires_grad=False, device=self.device)
         take = st.minibatch_source(obs_dtype)
@@ -351,15 +409,30 @@ class DHPPO:
             for i in range(self.num_mini_batches):
                 self._idx.copy_(perm[i * mb:(i + 1) * mb])
                 if self._upd is not None:
-                    self._upd[1].replay()
+                    if dp:
+                        self._upd[1][0].replay()
+                        self._dp_exchange()
+                        self._upd[1][1].replay()
+                    else:
+                        self._upd[1].replay()
                 elif self._upd_warm < self.WARMUP_STEPS or any(len(self.optimizer.state.get(p, {})) == 0
                                                                for p in self.grads.params):
                     side = torch.cuda.Stream(device=self._idx.device)
                     side.wait_stream(cur)
                     with torch.cuda.stream(side):
-                        self._minibatch_step(take(self._idx), amp, mse)
+                        self._step_eager(take(self._idx), amp, mse)
                     cur.wait_stream(side)
                     self._upd_warm += 1
+                elif dp:
+                    ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(ga):
+                        self._dp_part_a(take(self._idx), amp, mse)
+                    ga.replay()
+                    self._dp_exchange()
+                    with torch.cuda.graph(gb):
+                        self._dp_part_b()
+                    gb.replay()
+                    self._upd = (self._graph_key(mb, take), (ga, gb))
                 else:
                     graph = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(graph):
@@ -379,7 +452,7 @@ class DHPPO:
                 opt.extend(st[k].data_ptr() if k in st else None for k in ("step", "exp_avg", "exp_avg_sq"))
         return (mb, take.key, tuple(opt), str(self.amp_dtype), self.schedule, self.desired_kl, self.clip_param,
                 self.value_loss_coef, self.entropy_coef, self.max_grad_norm, self.use_clipped_value_loss,
-                self.lin_vel_idx)
+                self.lin_vel_idx, dist_util.active())
 
     def _losses(self, ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
                 old_sigma_b, hid_b, masks_b, mse):
