@@ -12,7 +12,8 @@
 //   wave  SIMD  S1 -> S2 (the terms of the published state)            S2 -> S1
 //   W0    0     pose chain + contact-free CRBA backward pass             core chain: fold-in, elimination, base system,
 //                                                                        solve, back-substitution, integration, publish
-//   W4    0     PD torques, base block, base-box contacts (both halves)  --
+//   W4    0     PD torques, base block, base-box contacts (both halves)  --  (at S1: the sensor-lag capture of the
+//                                                                        previous substep's state)
 //   W1    1     RNEA bias and joint rhs                                  history shift slice
 //   W5    1     self-contacts (capsules, both legs' bodies by permlane)  history shift slice
 //   W2    2     shank terrain contact, points 0-3                        history shift slice
@@ -65,7 +66,7 @@ struct Dyn6Lds {
   Rows4<R_N> w1;          // W1 -> W0
   Rows4<XCH> wc[WC_N];    // contact roles -> W0
   PdStage<64> pd;         // W4: PD constants and action ring of each lane's leg
-  float cap[CAP5_N][64];
+  float cap[CAP5_N][64];  // W4: the sensor-lag samples captured in the loop
   float act[12][NE6];     // the clipped actions (epilogue)
   float epi[EPI_N][NE6];  // staged post-physics inputs (epilogue)
   float fr[FR_N][NE6];    // this step's outputs (epilogue)
@@ -377,12 +378,47 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
 
   if (wave == 4) {
     // ======== W4: base -- the actions, PD torques, the base block and both base-box halves (their restitution episode)
-    BaseParams<float> PB;
-    load_base_params(M, B, n, PB);
+    const BaseParams<float>& PB = lds.pb[lane];  // W0 stores it before the first S1 (LDS, not registers held across
+                                                 // the loop); read from the first substep on
     const int lag = B.lag_timestep[n];
     const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
     const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
     float vi_b = B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)];
+    int s_dof = 9 - B.dof_lag_timestep[n] % 10;
+#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
+    s_dof = s_dof > 0 ? s_dof - 1 : 0;
+#endif
+    const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
+    // the state after substep s (W4 reads it at the next S1, the last one after R1): the sensor-lag samples the next
+    // observation reads (dof at substep 9 - lag % 10, the raw IMU sample likewise) and the substep log's rows
+    auto record = [&](int s, const BaseState<float>& sb, const float (&q)[NLEG], const float (&qd)[NLEG]) {
+      if (LG.root != nullptr && active) {  // tests only (a wave-uniform kernel argument)
+        const size_t row = (size_t)s * N + n;
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) {
+          LG.dof[row * 24 + 2 * (j0 + k)] = q[k];
+          LG.dof[row * 24 + 2 * (j0 + k) + 1] = qd[k];
+        }
+        if (leg == 0) {
+          BaseFrame<float> FL;
+          base_frame(sb, FL);
+          float body[13];
+          root_row(M, PB, sb, FL, body);
+#pragma unroll
+          for (int i = 0; i < 13; ++i) LG.root[row * 13 + i] = body[i];
+        }
+      }
+      if (s == s_dof) {
+#pragma unroll
+        for (int k = 0; k < NLEG; ++k) { lds.cap[k][lane] = q[k]; lds.cap[NLEG + k][lane] = qd[k]; }
+      }
+      if (leg == 0 && s == s_imu) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lds.cap[2 * NLEG + i][lane] = sb.quat[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) lds.cap[2 * NLEG + 4 + i][lane] = sb.w[i];
+      }
+    };
     {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged (every per-env
        // load before the first global store: the buffers may alias as far as the compiler knows)
       PdStage<64>& P = lds.pd;
@@ -417,15 +453,18 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     }
     // the epilogue's inputs the step does not change, staged by W4-W7 before their first substep
     if (FUSED) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
-    const float mu = PB.friction, eg = ground_restitution(M, PB.restitution);
+    const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // load_base_params' friction, restitution
+    const float eg = ground_restitution(M, B.restitution[n]);
     int cb, ce;
     base_contact_range(M, leg, cb, ce);
     float tau[NLEG];
     for (int sub = 0; sub < nsub; ++sub) {
       __syncthreads();  // S1: the substep state published
+      const DynModel& M = model_in_loop(lds.model);
       BaseState<float> sb;
       float q[NLEG], qd[NLEG];
       read_state_rows(lds.st, lane, sb, q, qd);
+      if (sub > 0) record(sub - 1, sb, q, qd);
       BaseFrame<float> F;
       base_frame(sb, F);
       // the base box half's queries issued first, under the PD torques and the base block
@@ -482,14 +521,34 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     halves(vi_b, vl, vr);  // the base box's two halves' end-of-step episodes (leg-0 lanes report the whole box)
     __syncthreads();  // R1: the end-of-step state published
     V3<float> fb = v3<float>(0.0f, 0.0f, 0.0f);
-    if (leg == 0) {
+    {
       BaseState<float> sb;
       float q[NLEG], qd[NLEG];
       read_state_rows(lds.st, lane, sb, q, qd);
+      record(nsub - 1, sb, q, qd);
+      if (active) {  // the sensor-lag samples into the step's ring slots
+        float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
+        float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
+        if (s_dof < nsub) {
+#pragma unroll
+          for (int k = 0; k < NLEG; ++k) {
+            dof_dst[j0 + k] = lds.cap[k][lane];
+            dof_dst[12 + j0 + k] = lds.cap[NLEG + k][lane];
+          }
+        }
+        if (leg == 0 && s_imu < nsub) {
+          const float quat[4] = {lds.cap[2 * NLEG][lane], lds.cap[2 * NLEG + 1][lane], lds.cap[2 * NLEG + 2][lane],
+                                 lds.cap[2 * NLEG + 3][lane]};
+          const float w[3] = {lds.cap[2 * NLEG + 4][lane], lds.cap[2 * NLEG + 5][lane], lds.cap[2 * NLEG + 6][lane]};
+          capture_imu(quat, w, imu_dst);
+        }
+      }
+      if (leg == 0) {
       BaseFrame<float> F;
       base_frame(sb, F);
       const float vt0 = restitution_target(M, eg, vl), vt1 = restitution_target(M, eg, vr);
       fb = body_contact_force(M, T, 0, F.R0, v3<float>(0, 0, 0), F.abs, F.V0, mu, vt0 > vt1 ? vt0 : vt1);
+      }
     }
     __syncthreads();  // RB: the report's parts in LDS
     if (leg == 0) {
@@ -685,11 +744,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   }
   float vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
   float vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
-  int s_dof = 9 - B.dof_lag_timestep[n] % 10;
-#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
-  s_dof = s_dof > 0 ? s_dof - 1 : 0;
-#endif
-  const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
   lds.vift[lane] = vi_ft;
   lds.vish[lane] = vi_sh;
   {
@@ -764,53 +818,13 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     backsub_leg(lb, r, dq);
     integrate_base(sb, r, dt);
     integrate_leg(M, leg, q, qd, dq, dt);
-    if (LG.root != nullptr) {  // wave-uniform (a kernel argument); the torques: W4
-      if (active) {
-        const size_t row = (size_t)sub * N + n;
-#pragma unroll
-        for (int k = 0; k < NLEG; ++k) {
-          LG.dof[row * 24 + 2 * (j0 + k)] = q[k];
-          LG.dof[row * 24 + 2 * (j0 + k) + 1] = qd[k];
-        }
-        if (leg == 0) {
-          BaseFrame<float> FL;
-          base_frame(sb, FL);
-          float body[13];
-          root_row(M, PB, sb, FL, body);
-#pragma unroll
-          for (int i = 0; i < 13; ++i) LG.root[row * 13 + i] = body[i];
-        }
-      }
-    }
-    if (sub == s_dof) {
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) { lds.cap[k][lane] = q[k]; lds.cap[NLEG + k][lane] = qd[k]; }
-    }
-    if (leg == 0 && sub == s_imu) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) lds.cap[2 * NLEG + i][lane] = sb.quat[i];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) lds.cap[2 * NLEG + 4 + i][lane] = sb.w[i];
-    }
     float v[Q_N];
     state_pack(sb, q, qd, v);
     put4(lds.st, lane, v);  // the roles read the previous state before S2; after the last substep: the report's
   }
   if (active) {
-    float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
-    float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
     B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)] = vi_ft;
     B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
-    if (s_dof < nsub) {  // the sensor-lag samples captured in the loop
-#pragma unroll
-      for (int k = 0; k < NLEG; ++k) { dof_dst[j0 + k] = lds.cap[k][lane]; dof_dst[12 + j0 + k] = lds.cap[NLEG + k][lane]; }
-    }
-    if (leg == 0 && s_imu < nsub) {
-      const float quat[4] = {lds.cap[2 * NLEG][lane], lds.cap[2 * NLEG + 1][lane], lds.cap[2 * NLEG + 2][lane],
-                             lds.cap[2 * NLEG + 3][lane]};
-      const float w[3] = {lds.cap[2 * NLEG + 4][lane], lds.cap[2 * NLEG + 5][lane], lds.cap[2 * NLEG + 6][lane]};
-      capture_imu(quat, w, imu_dst);
-    }
 #pragma unroll
     for (int k = 0; k < NLEG; ++k) {
       B.dof_state[n * 24 + 2 * (j0 + k)] = q[k];
