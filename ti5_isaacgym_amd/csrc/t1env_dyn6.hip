@@ -12,12 +12,12 @@
 //   wave  SIMD  S1 -> S2 (the terms of the published state)            S2 -> S1
 //   W0    0     pose chain + contact-free CRBA backward pass             core chain: fold-in, elimination, base system,
 //                                                                        solve, back-substitution, integration, publish
-//   W4    0     PD torques, base block, base-box contacts (both halves)  --  (at S1: the sensor-lag capture of the
-//                                                                        previous substep's state)
+//   W4    0     PD torques, base block, base-box contacts (both halves)  --
 //   W1    1     RNEA bias and joint rhs                                  history shift slice
 //   W5    1     self-contacts (capsules, both legs' bodies by permlane)  history shift slice
 //   W2    2     shank terrain contact, points 0-3                        history shift slice
-//   W6    2     shank terrain contact, points 4-7                        history shift slice
+//   W6    2     shank terrain contact, points 4-7 (at S1: the sensor-lag  history shift slice
+//               capture of the previous substep's state)
 //   W3    3     foot terrain contact, points 0-3                         --
 //   W7    3     foot terrain contact, points 4-7                         --
 //
@@ -32,6 +32,53 @@
 // few sums: a contact body's terms are the sum of its two point halves (and the self terms) instead of one 8-point
 // accumulation.  compute_delta_roles6 (t1_dyn5.h) is the same composition on one host thread (tests/test_dynamics.py).
 #include <hip/hip_runtime.h>
+
+// -DT1_PHASE_PROF (tools/prof_dynamics_phases.py --kernel 6): lane 0 of every wave accumulates shader-clock deltas
+// between T1_PROF_MARK points into per-phase buckets; never part of the product build.
+#ifdef T1_PHASE_PROF
+constexpr int T1_NPROF6 = 24, T1_PROF_WAVES6 = 8;
+__device__ unsigned long long g_t1_prof6[T1_PROF_WAVES6][T1_NPROF6];
+__shared__ unsigned long long t1_prof_acc6[T1_PROF_WAVES6][T1_NPROF6 + 1];  // [wave][bucket], last = previous mark
+__device__ __forceinline__ unsigned long long t1_stamp6() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+__device__ __forceinline__ void t1_prof_mark6(int i) {
+  const int w = threadIdx.x / 64;
+  const unsigned long long now = t1_stamp6();
+  if ((threadIdx.x & 63) == 0) {
+    t1_prof_acc6[w][i] += now - t1_prof_acc6[w][T1_NPROF6];
+    t1_prof_acc6[w][T1_NPROF6] = now;
+  }
+}
+__device__ __forceinline__ void t1_prof_begin6() {
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    for (int i = 0; i < T1_NPROF6; ++i) t1_prof_acc6[w][i] = 0;
+    t1_prof_acc6[w][T1_NPROF6] = t1_stamp6();
+  }
+}
+__device__ __forceinline__ void t1_prof_end6() {
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < T1_NPROF6; ++i) atomicAdd(&g_t1_prof6[w][i], t1_prof_acc6[w][i]);
+}
+#define T1_PROF_MARK(i) t1_prof_mark6(i)
+#define T1_PROF_BEGIN() t1_prof_begin6()
+#define T1_PROF_END() t1_prof_end6()
+#elif defined(T1_ASM_MARKS)  // ISA analysis build (tools/isa_phases.py): the marks as assembly comments
+#define T1_ASM_STR2(x) #x
+#define T1_ASM_STR(x) T1_ASM_STR2(x)
+#define T1_PROF_MARK(i) asm volatile(";@@MARK " #i "@L" T1_ASM_STR(__LINE__))
+#define T1_PROF_BEGIN() asm volatile(";@@MARK begin")
+#define T1_PROF_END() asm volatile(";@@MARK end")
+#else
+#define T1_PROF_BEGIN() ((void)0)
+#define T1_PROF_END() ((void)0)
+#endif
 
 #include "t1_dyn5.h"
 #include "t1env_device.h"
@@ -54,9 +101,18 @@ enum : int { R_RG = 0, R_G = 6, R_N = 12 };
 // contact terms -> W0
 enum : int { WC_SHA = 0, WC_SHB = 1, WC_FTA = 2, WC_FTB = 3, WC_SSH = 4, WC_SFT = 5, WC_N = 6 };
 // the shift waves (post-S2) and their count
-constexpr int SHIFT6_MASK = (1 << 1) | (1 << 5) | (1 << 2) | (1 << 6);
-constexpr int SHIFT6_WAVES = 4;
-constexpr int SHIFT6_U = 4;  // output chunks per lane in flight
+#ifndef T1_D6_SHIFT_MASK  // A/B builds: -DT1_D6_SHIFT_MASK=... -DT1_D6_SHIFT_U=...
+#define T1_D6_SHIFT_MASK ((1 << 1) | (1 << 5) | (1 << 2) | (1 << 6) | (1 << 3) | (1 << 7))
+#endif
+#ifndef T1_D6_SHIFT_U
+#define T1_D6_SHIFT_U 8
+#endif
+constexpr int SHIFT6_MASK = T1_D6_SHIFT_MASK;
+constexpr int SHIFT6_WAVES = __builtin_popcount(SHIFT6_MASK);
+// output chunks per lane in flight: the shift waves' role state is dead after S2, so a slice's loads (two 16-B loads
+// per output chunk) can all be in flight at once -- one memory round trip per substep
+constexpr int SHIFT6_U = T1_D6_SHIFT_U;
+static_assert((SHIFT6_MASK & 0x11) == 0, "W0 / W4 (the core chain's SIMD) do not shift");
 
 struct Dyn6Lds {
   DynModel model;
@@ -66,7 +122,7 @@ struct Dyn6Lds {
   Rows4<R_N> w1;          // W1 -> W0
   Rows4<XCH> wc[WC_N];    // contact roles -> W0
   PdStage<64> pd;         // W4: PD constants and action ring of each lane's leg
-  float cap[CAP5_N][64];  // W4: the sensor-lag samples captured in the loop
+  float cap[CAP5_N][64];  // W6: the sensor-lag samples captured in the loop
   float act[12][NE6];     // the clipped actions (epilogue)
   float epi[EPI_N][NE6];  // staged post-physics inputs (epilogue)
   float fr[FR_N][NE6];    // this step's outputs (epilogue)
@@ -218,6 +274,166 @@ __device__ __forceinline__ void shift6_slice(const ShiftArgs& S, int64_t r0, int
     shift6_f32<T1_NPRIV, T1_CHIST, SHIFT6_U>(S.priv_in, S.priv_out, S.total_priv, r0, r1, plo, phi, t0, stride);
   }
 }
+// ---- the shift pipelined across the substep: a shift wave issues the source loads of slice s + 1 right after it
+// stores slice s (after S2), holds them in registers through substep s + 1's role work (the HBM stream then spans the
+// whole substep instead of the post-S2 window alone, where its burst outlasted the core chain) and forms and stores
+// the outputs after the next S2.  A lane holds U_O chunks of the actor history and one of the critic history; a slice
+// with more chunks (fewer than 10 substeps) does the rest through shift6_f32 / _f16 at commit time.
+constexpr int SHP_UO = 7, SHP_UP = 1;  // 32 rows / 10 slices / (6 x 64) lanes: 6.5 actor chunks, 0.5 critic
+struct ShiftHold {
+  float4 a[SHP_UO + SHP_UP], b[SHP_UO + SHP_UP];  // the two aligned 16-B source blocks of each held chunk
+};
+// the chunk range [lo, hi) of slice sl of one history of the rows [r0, r1)
+template <int F, int H, bool HALF>
+__device__ __forceinline__ void shp_range(int64_t total, int64_t r0, int64_t r1, int sl, int nsl, uint32_t& lo,
+                                          uint32_t& hi, uint32_t& lim) {
+  constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4;
+  lim = (uint32_t)(total - r0 * (int64_t)ROW);
+  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
+  const uint32_t n = ((span < lim ? span : lim) + PER - 1) / PER;
+  lo = n * (uint32_t)sl / (uint32_t)nsl;
+  hi = n * (uint32_t)(sl + 1) / (uint32_t)nsl;
+}
+template <int F, int H, bool HALF, int U>
+__device__ __forceinline__ void shp_issue(const void* in, int64_t total, int64_t r0, int64_t r1, int sl, int nsl,
+                                          int t0, int stride, float4* a, float4* b) {
+  constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4, ES = HALF ? 2 : 4;
+  uint32_t lo, hi, lim;
+  shp_range<F, H, HALF>(total, r0, r1, sl, nsl, lo, hi, lim);
+  const uint8_t* in0 = reinterpret_cast<const uint8_t*>(in) + (size_t)(r0 * ROW) * ES;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = lo + (uint32_t)(t0 + u * stride);
+    const uint32_t sa = (c * PER + F) & ~(PER - 1);
+    const uint32_t sc = sa + 2 * PER <= lim ? sa : (lim - 2 * PER) & ~(PER - 1);  // tail: an aligned in-bounds dummy
+    a[u] = *reinterpret_cast<const float4*>(in0 + (size_t)sc * ES);
+    b[u] = *reinterpret_cast<const float4*>(in0 + (size_t)(sc + PER) * ES);
+  }
+}
+template <int F, int H, bool HALF, int U>
+__device__ __forceinline__ void shp_commit(const void* in, void* out, int64_t total, int64_t r0, int64_t r1, int sl,
+                                           int nsl, int t0, int stride, const float4* a, const float4* b) {
+  constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4;
+  uint32_t lo, hi, lim;
+  shp_range<F, H, HALF>(total, r0, r1, sl, nsl, lo, hi, lim);
+  if constexpr (!HALF) {
+    const float* in0 = reinterpret_cast<const float*>(in) + r0 * ROW;
+    float* out0 = reinterpret_cast<float*>(out) + r0 * ROW;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = lo + (uint32_t)(t0 + u * stride);
+      if (c >= hi) break;
+      const uint32_t i = c * 4, sa = (i + F) & ~3u;
+      float4 x = a[u], y = b[u];
+      if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
+        float t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
+        x = make_float4(t[0], t[1], t[2], t[3]);
+        y = make_float4(t[4], t[5], t[6], t[7]);
+      }
+      const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+      constexpr int rem = (int)(F & 3u);
+      const uint32_t col0 = i - (i / ROW) * ROW;
+      if (col0 + 3 < ROW - F && i + 3 < lim) {
+        __builtin_nontemporal_store(f4v{src[rem], src[rem + 1], src[rem + 2], src[rem + 3]},
+                                    reinterpret_cast<f4v*>(out0 + i));
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t e = i + k;
+        if (e >= lim) break;
+        if (e - (e / ROW) * ROW < ROW - F) out0[e] = src[rem + k];
+      }
+    }
+    // chunks past the held ones (a slice larger than the lanes hold)
+    const uint32_t rest = lo + (uint32_t)(U * stride);
+    if (rest < hi) shift6_f32<F, H, 1>(reinterpret_cast<const float*>(in), reinterpret_cast<float*>(out), total,
+                                              r0, r1, rest, hi, t0, stride);
+  } else {
+    constexpr uint32_t REM = F % 8, M = REM / 2;
+    const uint16_t* in0 = reinterpret_cast<const uint16_t*>(in) + r0 * ROW;
+    uint16_t* out0 = reinterpret_cast<uint16_t*>(out) + r0 * ROW;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = lo + (uint32_t)(t0 + u * stride);
+      if (c >= hi) break;
+      const uint32_t i = c * 8, sa = (i + F) & ~7u;
+      const u32x4 xa = __builtin_bit_cast(u32x4, a[u]), xb = __builtin_bit_cast(u32x4, b[u]);
+      uint32_t w[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+      if (sa + 16 > lim) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t l0 = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
+          const uint32_t hh = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
+          w[k] = l0 | (hh << 16);
+        }
+      }
+      u32x4 o;
+      if constexpr (REM % 2 == 0) {
+        o = u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
+      } else {
+        o = u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], 2), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], 2),
+                  __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], 2), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], 2)};
+      }
+      const uint32_t col0 = i - (i / ROW) * ROW;
+      if (col0 + 7 < ROW - F && i + 7 < lim) {
+        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out0 + i));
+        continue;
+      }
+      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t e = i + k;
+        if (e >= lim) break;
+        if (e - (e / ROW) * ROW < ROW - F) out0[e] = (uint16_t)(ow[k / 2] >> (16 * (k & 1)));
+      }
+    }
+    const uint32_t rest = lo + (uint32_t)(U * stride);
+    if (rest < hi) shift6_f16<F, H, 1>(reinterpret_cast<const uint16_t*>(in), reinterpret_cast<uint16_t*>(out),
+                                              total, r0, r1, rest, hi, t0, stride);
+  }
+}
+// issue slice sl's loads into H (shift wave wi); commit slice sl from H
+__device__ __forceinline__ void shp_issue_slice(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int wi,
+                                                int lane, ShiftHold& Hd) {
+#ifdef T1_WHATIF_D6_NO_SHIFT
+  return;
+#endif
+  if (r1 <= r0 || sl >= nsl) return;
+  const int t0 = wi * 64 + lane, stride = 64 * SHIFT6_WAVES;
+  if (S.half) {
+    shp_issue<T1_NOBS, T1_HIST, true, SHP_UO>(S.obs_in, S.total_obs, r0, r1, sl, nsl, t0, stride, Hd.a, Hd.b);
+    shp_issue<T1_NPRIV, T1_CHIST, true, SHP_UP>(S.priv_in, S.total_priv, r0, r1, sl, nsl, t0, stride, Hd.a + SHP_UO,
+                                                Hd.b + SHP_UO);
+  } else {
+    shp_issue<T1_NOBS, T1_HIST, false, SHP_UO>(S.obs_in, S.total_obs, r0, r1, sl, nsl, t0, stride, Hd.a, Hd.b);
+    shp_issue<T1_NPRIV, T1_CHIST, false, SHP_UP>(S.priv_in, S.total_priv, r0, r1, sl, nsl, t0, stride, Hd.a + SHP_UO,
+                                                 Hd.b + SHP_UO);
+  }
+}
+__device__ __forceinline__ void shp_commit_slice(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int wi,
+                                                 int lane, const ShiftHold& Hd) {
+#ifdef T1_WHATIF_D6_NO_SHIFT
+  return;
+#endif
+  if (r1 <= r0 || sl >= nsl) return;
+  const int t0 = wi * 64 + lane, stride = 64 * SHIFT6_WAVES;
+  if (S.half) {
+    shp_commit<T1_NOBS, T1_HIST, true, SHP_UO>(S.obs_in, S.obs_out, S.total_obs, r0, r1, sl, nsl, t0, stride, Hd.a,
+                                               Hd.b);
+    shp_commit<T1_NPRIV, T1_CHIST, true, SHP_UP>(S.priv_in, S.priv_out, S.total_priv, r0, r1, sl, nsl, t0, stride,
+                                                 Hd.a + SHP_UO, Hd.b + SHP_UO);
+  } else {
+    shp_commit<T1_NOBS, T1_HIST, false, SHP_UO>(S.obs_in, S.obs_out, S.total_obs, r0, r1, sl, nsl, t0, stride, Hd.a,
+                                                Hd.b);
+    shp_commit<T1_NPRIV, T1_CHIST, false, SHP_UP>(S.priv_in, S.priv_out, S.total_priv, r0, r1, sl, nsl, t0, stride,
+                                                  Hd.a + SHP_UO, Hd.b + SHP_UO);
+  }
+}
+
 __device__ __forceinline__ int shift6_index(int wave) {  // the wave's index among the shift waves, -1: none
   return (SHIFT6_MASK >> wave) & 1 ? __builtin_popcount(SHIFT6_MASK & ((1 << wave) - 1)) : -1;
 }
@@ -344,6 +560,41 @@ __device__ __forceinline__ void leg_apply_terms_rows(const Rows4<XCH> (&W)[WC_N]
   for (int i = 0; i < 6; ++i) gc_up[i] += w1v[R_G + i] + c[i];
 }
 
+// The state after substep s, recorded by W6 (it reads that state at the next S1, the last one after R1): the sensor-lag
+// samples the next observation reads (the joint state at substep 9 - lag % 10, the raw IMU sample likewise) into LDS,
+// and the substep log's rows (tests only; LG.root is a wave-uniform kernel argument)
+__device__ __forceinline__ void record_substep(const DynModel& M, const BaseParams<float>& PB, const SubLog& LG,
+                                               Dyn6Lds& L, int s, int s_dof, int s_imu, int N, int n, int j0, int leg,
+                                               int lane, bool active, const BaseState<float>& sb,
+                                               const float (&q)[NLEG], const float (&qd)[NLEG]) {
+  if (LG.root != nullptr && active) {
+    const size_t row = (size_t)s * N + n;
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) {
+      LG.dof[row * 24 + 2 * (j0 + k)] = q[k];
+      LG.dof[row * 24 + 2 * (j0 + k) + 1] = qd[k];
+    }
+    if (leg == 0) {
+      BaseFrame<float> FL;
+      base_frame(sb, FL);
+      float body[13];
+      root_row(M, PB, sb, FL, body);
+#pragma unroll
+      for (int i = 0; i < 13; ++i) LG.root[row * 13 + i] = body[i];
+    }
+  }
+  if (s == s_dof) {
+#pragma unroll
+    for (int k = 0; k < NLEG; ++k) { L.cap[k][lane] = q[k]; L.cap[NLEG + k][lane] = qd[k]; }
+  }
+  if (leg == 0 && s == s_imu) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L.cap[2 * NLEG + i][lane] = sb.quat[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) L.cap[2 * NLEG + 4 + i][lane] = sb.w[i];
+  }
+}
+
 template <bool HF, bool FUSED>
 __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ Mg, const t1env_config* __restrict__ Cp,
                                                    t1env_buffers B, Terrain Tin, const float* __restrict__ actions,
@@ -373,6 +624,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   const uint32_t ctr = A.counter;
   const int nsub = C.decimation;
   const int64_t r0 = (int64_t)blockIdx.x * NE6, r1 = r0 + NE6 < N ? r0 + NE6 : N;
+  T1_PROF_BEGIN();
   __syncthreads();  // the model in LDS
   const DynModel& M = lds.model;
 
@@ -384,41 +636,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
     const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
     float vi_b = B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)];
-    int s_dof = 9 - B.dof_lag_timestep[n] % 10;
-#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
-    s_dof = s_dof > 0 ? s_dof - 1 : 0;
-#endif
-    const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
-    // the state after substep s (W4 reads it at the next S1, the last one after R1): the sensor-lag samples the next
-    // observation reads (dof at substep 9 - lag % 10, the raw IMU sample likewise) and the substep log's rows
-    auto record = [&](int s, const BaseState<float>& sb, const float (&q)[NLEG], const float (&qd)[NLEG]) {
-      if (LG.root != nullptr && active) {  // tests only (a wave-uniform kernel argument)
-        const size_t row = (size_t)s * N + n;
-#pragma unroll
-        for (int k = 0; k < NLEG; ++k) {
-          LG.dof[row * 24 + 2 * (j0 + k)] = q[k];
-          LG.dof[row * 24 + 2 * (j0 + k) + 1] = qd[k];
-        }
-        if (leg == 0) {
-          BaseFrame<float> FL;
-          base_frame(sb, FL);
-          float body[13];
-          root_row(M, PB, sb, FL, body);
-#pragma unroll
-          for (int i = 0; i < 13; ++i) LG.root[row * 13 + i] = body[i];
-        }
-      }
-      if (s == s_dof) {
-#pragma unroll
-        for (int k = 0; k < NLEG; ++k) { lds.cap[k][lane] = q[k]; lds.cap[NLEG + k][lane] = qd[k]; }
-      }
-      if (leg == 0 && s == s_imu) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) lds.cap[2 * NLEG + i][lane] = sb.quat[i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) lds.cap[2 * NLEG + 4 + i][lane] = sb.w[i];
-      }
-    };
     {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged (every per-env
        // load before the first global store: the buffers may alias as far as the compiler knows)
       PdStage<64>& P = lds.pd;
@@ -457,20 +674,21 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     const float eg = ground_restitution(M, B.restitution[n]);
     int cb, ce;
     base_contact_range(M, leg, cb, ce);
-    float tau[NLEG];
+    T1_PROF_MARK(0);
     for (int sub = 0; sub < nsub; ++sub) {
       __syncthreads();  // S1: the substep state published
+      T1_PROF_MARK(1);
       const DynModel& M = model_in_loop(lds.model);
       BaseState<float> sb;
       float q[NLEG], qd[NLEG];
       read_state_rows(lds.st, lane, sb, q, qd);
-      if (sub > 0) record(sub - 1, sb, q, qd);
       BaseFrame<float> F;
       base_frame(sb, F);
       // the base box half's queries issued first, under the PD torques and the base block
       const int32_t bound_b = terrain_bound_raw_any(T, F.abs.x, F.abs.y);
       ContactQuery<T1_POINTS_PER_BODY / 2, float> Qb;
       contact_query<HF, T1_POINTS_PER_BODY / 2>(M, T, cb, F.R0, v3<float>(0, 0, 0), F.abs, Qb);
+      float tau[NLEG];
       pd_torques_staged(M, C, lds.pd, lane, K, ctr, sub, lag, j0, q, qd, tau);
       Sym6<float> Ac;  // the base body's block (both halves compute it: the same values)
       float r[6];
@@ -507,7 +725,14 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       if (LG.root != nullptr && active)  // the substep log's torques (tests only; wave-uniform kernel argument)
 #pragma unroll
         for (int k = 0; k < NLEG; ++k) LG.torque[((size_t)sub * N + n) * 12 + j0 + k] = tau[k];
+      T1_PROF_MARK(2);
       __syncthreads();  // S2: the terms published
+      T1_PROF_MARK(3);
+    }
+    float tau[8];  // the last substep's torques, from the wb rows
+    {
+      const float4 t0 = lds.wb.r[0][lane], t1 = lds.wb.r[1][lane];
+      tau[0] = t0.x; tau[1] = t0.y; tau[2] = t0.z; tau[3] = t0.w; tau[4] = t1.x; tau[5] = t1.y;
     }
     if (active) {
       B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)] = vi_b;
@@ -525,24 +750,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       BaseState<float> sb;
       float q[NLEG], qd[NLEG];
       read_state_rows(lds.st, lane, sb, q, qd);
-      record(nsub - 1, sb, q, qd);
-      if (active) {  // the sensor-lag samples into the step's ring slots
-        float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
-        float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
-        if (s_dof < nsub) {
-#pragma unroll
-          for (int k = 0; k < NLEG; ++k) {
-            dof_dst[j0 + k] = lds.cap[k][lane];
-            dof_dst[12 + j0 + k] = lds.cap[NLEG + k][lane];
-          }
-        }
-        if (leg == 0 && s_imu < nsub) {
-          const float quat[4] = {lds.cap[2 * NLEG][lane], lds.cap[2 * NLEG + 1][lane], lds.cap[2 * NLEG + 2][lane],
-                                 lds.cap[2 * NLEG + 3][lane]};
-          const float w[3] = {lds.cap[2 * NLEG + 4][lane], lds.cap[2 * NLEG + 5][lane], lds.cap[2 * NLEG + 6][lane]};
-          capture_imu(quat, w, imu_dst);
-        }
-      }
       if (leg == 0) {
       BaseFrame<float> F;
       base_frame(sb, F);
@@ -558,7 +765,9 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       }
       if constexpr (FUSED) { lds.fr[F_CFB][e] = fb.x; lds.fr[F_CFB + 1][e] = fb.y; lds.fr[F_CFB + 2][e] = fb.z; }
     }
+    T1_PROF_MARK(10);
     if constexpr (FUSED) __syncthreads();  // the epilogue barrier
+    T1_PROF_END();
     return;
   }
 
@@ -577,8 +786,12 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       // ---- W1: RNEA bias terms of the leg
       LegParams<float> PL;
       load_leg_params(M, B, n, j0, PL);
+      ShiftHold hold;  // the pipelined history shift's loads in flight (its own live range per role loop)
+      if (wi >= 0) shp_issue_slice(S, r0, r1, 0, nsub, wi, lane, hold);
       for (int sub = 0; sub < nsub; ++sub) {
+        T1_PROF_MARK(4);
         __syncthreads();  // S1
+        T1_PROF_MARK(1);
         BaseState<float> sb;
         float q[NLEG], qd[NLEG];
         read_state_rows(lds.st, lane, sb, q, qd);
@@ -592,13 +805,22 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 6; ++i) v[R_G + i] = G[i];
         put4(lds.w1, lane, v);
+        T1_PROF_MARK(2);
         __syncthreads();  // S2
-        if (wi >= 0) shift6_slice(S, r0, r1, sub, nsub, wi, lane);
+        T1_PROF_MARK(3);
+        if (wi >= 0) {  // slice sub (its loads issued a substep ago), then slice sub + 1's loads
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+          shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
+        }
       }
     } else if (wave == 5) {
       // ---- W5: self-contact terms of the shank and foot
+      ShiftHold hold;  // the pipelined history shift's loads in flight (its own live range per role loop)
+      if (wi >= 0) shp_issue_slice(S, r0, r1, 0, nsub, wi, lane, hold);
       for (int sub = 0; sub < nsub; ++sub) {
+        T1_PROF_MARK(4);
         __syncthreads();  // S1
+        T1_PROF_MARK(1);
         BaseState<float> sb;
         float q[NLEG], qd[NLEG];
         read_state_rows(lds.st, lane, sb, q, qd);
@@ -625,20 +847,38 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
           sym_pack(Cs[i], cs[i], v);
           put4(lds.wc[WC_SSH + i], lane, v);
         }
+        T1_PROF_MARK(2);
         __syncthreads();  // S2
-        if (wi >= 0) shift6_slice(S, r0, r1, sub, nsub, wi, lane);
+        T1_PROF_MARK(3);
+        if (wi >= 0) {  // slice sub (its loads issued a substep ago), then slice sub + 1's loads
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+          shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
+        }
       }
     } else {
-      // ---- W2 / W6: shank terrain, W3 / W7: foot terrain (one half of the body's points each)
+      // ---- W2 / W6: shank terrain, W3 / W7: foot terrain (one half of the body's points each); W6 also records the
+      // sensor-lag samples and the substep log from the state it reads at S1
       const bool shank = wave == 2 || wave == 6;
+      int s_dof = 9 - B.dof_lag_timestep[n] % 10;
+#ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
+      s_dof = s_dof > 0 ? s_dof - 1 : 0;
+#endif
+      const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
+
       const int slot = (shank ? WC_SHA : WC_FTA) + half;
       const int b = shank ? bsh : bft;
       const int c0 = M.contact_start[b] + half * (T1_POINTS_PER_BODY / 2);
+      ShiftHold hold;  // the pipelined history shift's loads in flight (its own live range per role loop)
+      if (wi >= 0) shp_issue_slice(S, r0, r1, 0, nsub, wi, lane, hold);
       for (int sub = 0; sub < nsub; ++sub) {
+        T1_PROF_MARK(4);
         __syncthreads();  // S1
+        T1_PROF_MARK(1);
         BaseState<float> sb;
         float q[NLEG], qd[NLEG];
         read_state_rows(lds.st, lane, sb, q, qd);
+        if (wave == 6 && sub > 0)
+          record_substep(M, lds.pb[lane], LG, lds, sub - 1, s_dof, s_imu, N, n, j0, leg, lane, active, sb, q, qd);
         BaseFrame<float> F;
         base_frame(sb, F);
         BodyKin<float> Ko[2];
@@ -658,12 +898,20 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         sym_pack(Cc, cc, v);
         put4(lds.wc[slot], lane, v);
         lds.amx[slot][lane] = amax;
+        T1_PROF_MARK(2);
         __syncthreads();  // S2
-        if (wi >= 0) shift6_slice(S, r0, r1, sub, nsub, wi, lane);
+        T1_PROF_MARK(3);
+        if (wi >= 0) {  // slice sub (its loads issued a substep ago), then slice sub + 1's loads
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+          shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
+        }
       }
     }
+    T1_PROF_MARK(4);
     if (wi >= 0) __builtin_amdgcn_s_waitcnt(0);  // the shift's stores complete before the epilogue zeroes reset rows
+    T1_PROF_MARK(8);
     __syncthreads();  // R1: the end-of-step state and episodes published
+    T1_PROF_MARK(9);
     {  // the contact-force report from the end-of-step state: W2 the shank's terrain force, W3 the foot's, W5 their
        // self-contact forces; W6 sums and stores the shank / foot rows after RB (the base box: W4)
       if (wave == 2 || wave == 3 || wave == 5) {
@@ -693,7 +941,37 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
           lds.rtf[s][0][lane] = f.x; lds.rtf[s][1][lane] = f.y; lds.rtf[s][2][lane] = f.z;
         }
       }
+      T1_PROF_MARK(10);
+      if (wave == 6) {  // the last substep's state (published before R1): its log row, then the lag samples' stores
+        int s_dof = 9 - B.dof_lag_timestep[n] % 10;
+#ifdef T1_MUTANT_CAPTURE
+        s_dof = s_dof > 0 ? s_dof - 1 : 0;
+#endif
+        const int s_imu = 9 - B.imu_lag_timestep[n] % 10;
+        BaseState<float> sb;
+        float q[NLEG], qd[NLEG];
+        read_state_rows(lds.st, lane, sb, q, qd);
+        record_substep(M, lds.pb[lane], LG, lds, nsub - 1, s_dof, s_imu, N, n, j0, leg, lane, active, sb, q, qd);
+        if (active) {  // the sensor-lag samples into the step's ring slots
+          float* const dof_dst = B.dof_hist + ((size_t)n * 4 + (ctr & 3u)) * 24;
+          float* const imu_dst = B.imu_hist + ((size_t)n * 2 + (ctr & 1u)) * 8;
+          if (s_dof < nsub) {
+#pragma unroll
+            for (int k = 0; k < NLEG; ++k) {
+              dof_dst[j0 + k] = lds.cap[k][lane];
+              dof_dst[12 + j0 + k] = lds.cap[NLEG + k][lane];
+            }
+          }
+          if (leg == 0 && s_imu < nsub) {
+            const float quat[4] = {lds.cap[2 * NLEG][lane], lds.cap[2 * NLEG + 1][lane], lds.cap[2 * NLEG + 2][lane],
+                                   lds.cap[2 * NLEG + 3][lane]};
+            const float w[3] = {lds.cap[2 * NLEG + 4][lane], lds.cap[2 * NLEG + 5][lane], lds.cap[2 * NLEG + 6][lane]};
+            capture_imu(quat, w, imu_dst);
+          }
+        }
+      }
       __syncthreads();  // RB: the report's parts in LDS
+      T1_PROF_MARK(11);
       if (wave == 6) {
         float* cf = B.contact_forces + (size_t)n * 39;
 #pragma unroll
@@ -711,6 +989,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     }
     if constexpr (FUSED) {
       __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
+      T1_PROF_MARK(12);
       if (wave == 1)
         fused_epilogue_staged<POST_A_STATE, NE6, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
                                                        lds.act + NLEG);
@@ -718,7 +997,9 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         fused_epilogue_obs<POST_OBS_PRIV, NE6>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
       else if (wave == 3)
         fused_epilogue_obs<POST_OBS_ACTOR, NE6>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
+      T1_PROF_MARK(15);
     }
+    T1_PROF_END();
     return;
   }
 
@@ -726,9 +1007,9 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   // integration; owns the joint state and the restitution episodes of the shank and foot
   BaseParams<float>& PB = lds.pb[lane];
   LegParams<float>& PL = lds.pl[lane];
-  BaseState<float> sb;
-  float q[NLEG], qd[NLEG];
-  {
+  {  // the state is held in LDS (lds.st, which W0 alone writes), not in registers across the substep loop
+    BaseState<float> sb;
+    float q[NLEG], qd[NLEG];
     BaseParams<float> pb;
     LegParams<float> pl;
     load_base_params(M, B, n, pb);
@@ -736,27 +1017,30 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     load_base_state(M, pb, B.root_states + (size_t)n * 13, sb);
     PB = pb;
     PL = pl;
-  }
 #pragma unroll
-  for (int k = 0; k < NLEG; ++k) {
-    q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
-    qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
+    for (int k = 0; k < NLEG; ++k) {
+      q[k] = B.dof_state[n * 24 + 2 * (j0 + k)];
+      qd[k] = B.dof_state[n * 24 + 2 * (j0 + k) + 1];
+    }
+    float v[Q_N];
+    state_pack(sb, q, qd, v);
+    put4(lds.st, lane, v);
   }
   float vi_ft = B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)];
   float vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
   lds.vift[lane] = vi_ft;
   lds.vish[lane] = vi_sh;
-  {
-    float v[Q_N];
-    state_pack(sb, q, qd, v);
-    put4(lds.st, lane, v);
-  }
+  T1_PROF_MARK(0);
   for (int sub = 0; sub < nsub; ++sub) {
     __syncthreads();  // S1: the substep state published
+    T1_PROF_MARK(1);
     const DynModel& M = model_in_loop(lds.model);
     LegBlock<float> lb;
     Sym6<float> Ab;
     {
+      BaseState<float> sb;
+      float q[NLEG], qd[NLEG];
+      read_state_rows(lds.st, lane, sb, q, qd);
       const M3<float> R0 = quat_to_mat(sb.quat[0], sb.quat[1], sb.quat[2], sb.quat[3]);  // base_frame's F.R0
       LegFK<float> fk;
       leg_fk_chain(M, R0, q, leg, fk);
@@ -769,7 +1053,9 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         lds.sj.r[k][1][lane] = make_float4(Sj[k][4], Sj[k][5], 0.0f, 0.0f);
       }
     }
+    T1_PROF_MARK(2);
     __syncthreads();  // S2: the terms published
+    T1_PROF_MARK(3);
     {  // the episodes of the shank and foot from the two halves of their points
       vi_sh = restitution_episode(vi_sh, fmaxf(lds.amx[WC_SHA][lane], lds.amx[WC_SHB][lane]));
       vi_ft = restitution_episode(vi_ft, fmaxf(lds.amx[WC_FTA][lane], lds.amx[WC_FTB][lane]));
@@ -786,10 +1072,12 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       for (int k = 0; k < NLEG; ++k) rg[k] = dt * tv[k] + gv[k];
       leg_apply_terms_rows<K_SHANK, K_FOOT>(lds.wc, lds.w1, rg, lds.sj, lane, lb, Ab, g6);
     }
+    T1_PROF_MARK(5);
     float rb[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) rb[i] = -g6[i];
     eliminate_leg(lb, Ab, rb);
+    T1_PROF_MARK(6);
     // the base system: (base block + both base-box halves, W4) + the left leg + the right leg, in every lane
     Sym6<float> Ac;
     float r[6];
@@ -816,12 +1104,19 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     solve_base(Ac, r);
     float dq[NLEG];
     backsub_leg(lb, r, dq);
+    BaseState<float> sb;
+    float q[NLEG], qd[NLEG];
+    read_state_rows(lds.st, lane, sb, q, qd);
     integrate_base(sb, r, dt);
     integrate_leg(M, leg, q, qd, dq, dt);
     float v[Q_N];
     state_pack(sb, q, qd, v);
     put4(lds.st, lane, v);  // the roles read the previous state before S2; after the last substep: the report's
+    T1_PROF_MARK(7);
   }
+  BaseState<float> sb;
+  float q[NLEG], qd[NLEG];
+  read_state_rows(lds.st, lane, sb, q, qd);
   if (active) {
     B.contact_vimp[(size_t)n * NVIMP + vimp_foot(leg)] = vi_ft;
     B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)] = vi_sh;
@@ -839,19 +1134,37 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       lds.fr[F_DOF + 2 * (j0 + k) + 1][e] = qd[k];
     }
   }
+  T1_PROF_MARK(8);
   __syncthreads();  // R1: the end-of-step state published (the report's contact forces meanwhile)
+  T1_PROF_MARK(9);
   {
     BaseFrame<float> F;
     base_frame(sb, F);
     leg_report_rigid<NE6>(M, B, PB, sb, F, q, qd, n, leg, active, e, FR);
   }
+  T1_PROF_MARK(10);
   __syncthreads();  // RB: the contact-force report's parts in LDS
+  T1_PROF_MARK(11);
   if constexpr (FUSED) {
     __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
+    T1_PROF_MARK(12);
     fused_epilogue_staged<POST_A_REWARDS, NE6, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
                                                      lds.act + NLEG);
   }
+  T1_PROF_END();
 }
+
+#ifdef T1_PHASE_PROF
+// profiling build only: summed clock deltas per [wave][bucket] since the last reset
+extern "C" int t1env_debug_phase_cycles6(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_prof6), sizeof(g_t1_prof6));
+  if (e == hipSuccess && reset) {
+    static const unsigned long long zero[T1_PROF_WAVES6][T1_NPROF6] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_t1_prof6), zero, sizeof(zero));
+  }
+  return (int)e;
+}
+#endif
 
 int t1_launch_dyn6(const DynModel* d_model, const t1env_config* d_cfg, const t1env_buffers& B, const Terrain& T,
                    const float* actions, const t1env_step_args& A, int num_envs, const ShiftArgs& S,

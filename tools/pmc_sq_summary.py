@@ -51,7 +51,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("dbs", nargs="+")
     p.add_argument("--envs", type=int, default=8192)
-    p.add_argument("--kernel", default="k_dyn5", choices=["k_dyn5", "k_dyn4"])
+    p.add_argument("--kernel", default="k_dyn5", choices=["k_dyn6", "k_dyn5", "k_dyn4"])
     p.add_argument("-o", "--out")
     a = p.parse_args()
     global KERNEL
@@ -65,7 +65,8 @@ def main():
             durs += durations_ns(db)
         except sqlite3.Error:
             pass
-    dyn_waves = 4 * ((a.envs + 31) // 32) if a.kernel == "k_dyn5" else 4 * ((a.envs + 63) // 64)
+    dyn_waves = {"k_dyn6": 8 * ((a.envs + 31) // 32), "k_dyn5": 4 * ((a.envs + 31) // 32)}.get(
+        a.kernel, 4 * ((a.envs + 63) // 64))
     d = {}
     if "SQ_INSTS_VALU" in vals:
         d["valu_insts_per_dyn_wave"] = vals["SQ_INSTS_VALU"] / dyn_waves
@@ -83,6 +84,10 @@ def main():
         d["valu_active_frac_all_waves"] = vals["SQ_ACTIVE_INST_VALU"] / vals["SQ_WAVE_CYCLES"]
     if "SQ_WAIT_ANY" in vals and "SQ_WAVE_CYCLES" in vals:
         d["wait_any_frac"] = vals["SQ_WAIT_ANY"] / vals["SQ_WAVE_CYCLES"]
+    if "SQ_WAIT_INST_ANY" in vals and "SQ_WAVE_CYCLES" in vals:
+        d["wait_inst_any_frac"] = vals["SQ_WAIT_INST_ANY"] / vals["SQ_WAVE_CYCLES"]
+    if "SQC_ICACHE_MISSES" in vals and "SQC_ICACHE_HITS" in vals:
+        d["icache_miss_rate"] = vals["SQC_ICACHE_MISSES"] / max(1.0, vals["SQC_ICACHE_HITS"] + vals["SQC_ICACHE_MISSES"])
     out = {"kernel": a.kernel, "envs": a.envs, "dispatches": n, "counters": vals, "derived": d,
            "sources": a.dbs}
     print(json.dumps(out, indent=1))

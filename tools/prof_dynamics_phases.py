@@ -55,6 +55,17 @@ D5 = {  # bucket i = the time from the previous mark to mark i (t1env_dyn5.hip's
 }
 
 
+# k_dyn6 (t1env_dyn6.hip, eight waves): mark meanings
+D6_W0 = ["prologue", "S1 wait", "chain + CRBA", "S2 wait", "-", "LDS reads + fold-in", "elimination",
+         "base system + solve + backsub + integrate + publish", "stores", "R1 wait", "rigid report", "RB wait",
+         "epilogue barrier", "post_a (fused)", "post_a tail", "handoff + zeroing + finalize"]
+D6_W4 = ["prologue + epilogue staging", "S1 wait", "capture, PD, base block, base box", "S2 wait", "-", "-", "-", "-",
+         "-", "R1 wait", "capture stores + base-box report", "epilogue barrier"]
+D6_R = ["-", "S1 wait", "role terms (pre-S2)", "S2 wait", "shift slice / prologue", "-", "-", "-",
+        "shift store drain", "R1 wait", "report", "RB wait", "epilogue barrier", "-", "-", "epilogue (obs / state)"]
+D6_ROLES = ["W0 core", "W1 RNEA", "W2 shank A", "W3 foot A", "W4 base", "W5 self", "W6 shank B", "W7 foot B"]
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--build", action="store_true")
@@ -63,14 +74,15 @@ def main():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--split", action="store_true", help="time the split path (k_dynamics without epilogue)")
     p.add_argument("--no-self-collision", action="store_true", help="asset.self_collisions = 1 (A/B)")
-    p.add_argument("--kernel", type=int, default=5, choices=[4, 5], help="k_dyn5 (default) or k_dyn4")
+    p.add_argument("--kernel", type=int, default=5, choices=[4, 5, 6], help="k_dyn5 (default), k_dyn6 or k_dyn4")
+    p.add_argument("--lib", default=PROF_LIB, help="a profiling build (-DT1_PHASE_PROF), e.g. a what-if variant")
     a = p.parse_args()
     sys.path.insert(0, REPO)
     if a.build:
         from ti5_isaacgym_amd import build
         print(build.build(force=True, extra=["-DT1_PHASE_PROF"], out=PROF_LIB))
         return
-    os.environ["T1ENV_LIB"] = PROF_LIB
+    os.environ["T1ENV_LIB"] = a.lib
     os.environ["T1ENV_DYN_KERNEL"] = str(a.kernel)
     import torch
     from ti5_isaacgym_amd import make_t1_env
@@ -79,15 +91,17 @@ def main():
             cfg.asset.self_collisions = 1
     env = make_t1_env(num_envs=a.num_envs, mesh_type=a.mesh, seed=5, device="cuda:0", cfg_hook=hook)
     env.set_fused(not a.split)
-    lib = ctypes.CDLL(PROF_LIB)
-    buf = (ctypes.c_ulonglong * (NW * NB))()
+    lib = ctypes.CDLL(a.lib)
+    nw = 8 if a.kernel == 6 else NW
+    buf = (ctypes.c_ulonglong * (nw * (24 if a.kernel == 6 else NB)))()
     env.reset()
     g = torch.Generator(device="cuda:0").manual_seed(0)
     acts = [torch.randn(a.num_envs, 12, device="cuda:0", generator=g) for _ in range(8)]
     for i in range(50):
         env.step(acts[i % 8])
     torch.cuda.synchronize()
-    read = lib.t1env_debug_phase_cycles5 if a.kernel == 5 else lib.t1env_debug_phase_cycles
+    read = {5: lib.t1env_debug_phase_cycles5, 6: getattr(lib, "t1env_debug_phase_cycles6", None)}.get(
+        a.kernel, lib.t1env_debug_phase_cycles)
     assert read(buf, 1) == 0
     env.set_timing(True)
     for i in range(a.steps):
@@ -100,6 +114,17 @@ def main():
     waves = (a.num_envs + 63) // 64 if a.kernel == 4 else (a.num_envs + 31) // 32
     print(f"k_dynamics {kern_us:.1f} us/launch (events), {a.mesh}, {a.num_envs} envs, {a.steps} steps, "
           f"{'split' if a.split else 'fused'}")
+    if a.kernel == 6:
+        for w in range(8):
+            cyc = [buf[w * 24 + i] / (waves * a.steps) for i in range(24)]
+            tot = sum(cyc)
+            names = D6_W0 if w == 0 else (D6_W4 if w == 4 else D6_R)
+            print(f"wave {w} ({D6_ROLES[w]}): {tot:.0f} cycles/launch")
+            for i, c in sorted(enumerate(cyc), key=lambda x: -x[1]):
+                if c > 0:
+                    nm = names[i] if i < len(names) else f"mark {i}"
+                    print(f"   {nm:40s} {c:10.0f} cyc  {100 * c / tot:5.1f}%  ~{kern_us * c / tot:6.1f} us")
+        return
     four = True
     names = BUCKETS4
     roles = ["left leg", "right leg", "left contact helper", "right contact helper"]
