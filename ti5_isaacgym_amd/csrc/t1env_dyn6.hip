@@ -101,17 +101,19 @@ enum : int { R_RG = 0, R_G = 6, R_N = 12 };
 // contact terms -> W0
 enum : int { WC_SHA = 0, WC_SHB = 1, WC_FTA = 2, WC_FTB = 3, WC_SSH = 4, WC_SFT = 5, WC_N = 6 };
 // the shift waves (post-S2) and their count
-#ifndef T1_D6_SHIFT_MASK  // A/B builds: -DT1_D6_SHIFT_MASK=... -DT1_D6_SHIFT_U=...
+#ifndef T1_D6_SHIFT_MASK  // A/B builds: -DT1_D6_SHIFT_MASK=...
 #define T1_D6_SHIFT_MASK ((1 << 1) | (1 << 5) | (1 << 2) | (1 << 6) | (1 << 3) | (1 << 7))
 #endif
-#ifndef T1_D6_SHIFT_U
-#define T1_D6_SHIFT_U 8
+constexpr int SHIFT6_MASK = T1_D6_SHIFT_MASK;  // by role (below)
+// The role of each wave: role ids are the wave numbers of the table at the top (0 core, 4 base, 1 RNEA, 5 self, 2 / 6
+// shank halves, 3 / 7 foot halves); T1_D6_ROLE_MAP holds the role of wave w in hex digit w, so the SIMD pairs (w, w + 4)
+// can be re-dealt for A/B (the core stays wave 0: its partner is wave 4's role)
+#ifndef T1_D6_ROLE_MAP
+#define T1_D6_ROLE_MAP 0x76543210u
 #endif
-constexpr int SHIFT6_MASK = T1_D6_SHIFT_MASK;
+__device__ __forceinline__ int role_of(int wave) { return (int)((T1_D6_ROLE_MAP >> (4 * wave)) & 0xFu); }
+static_assert((T1_D6_ROLE_MAP & 0xFu) == 0, "the core role is wave 0");
 constexpr int SHIFT6_WAVES = __builtin_popcount(SHIFT6_MASK);
-// output chunks per lane in flight: the shift waves' role state is dead after S2, so a slice's loads (two 16-B loads
-// per output chunk) can all be in flight at once -- one memory round trip per substep
-constexpr int SHIFT6_U = T1_D6_SHIFT_U;
 static_assert((SHIFT6_MASK & 0x11) == 0, "W0 / W4 (the core chain's SIMD) do not shift");
 
 struct Dyn6Lds {
@@ -135,143 +137,99 @@ struct Dyn6Lds {
   float rsf[2][3][64];    // the report: self-contact forces on the shank / foot (W5)
 };
 
-// ---- the history shift through VGPRs: output chunks [c_lo, c_hi) of the workgroup's rows [r0, r1) of one history,
-// lane t0 of `stride` lanes, U chunks per lane with their two aligned source loads issued before any store (the
-// in-launch form of shift_rows_f32 / shift_rows_f16, t1env_device.h, restricted to a chunk range)
-template <int F, int H, int U>
-__device__ __forceinline__ void shift6_f32(const float* __restrict__ in, float* __restrict__ out, int64_t total,
-                                           int64_t r0, int64_t r1, uint32_t c_lo, uint32_t c_hi, int t0, int stride) {
-  constexpr uint32_t ROW = F * H;
-  const float* __restrict__ in0 = in + r0 * ROW;
-  float* __restrict__ out0 = out + r0 * ROW;
-  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
-  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
-  const uint32_t nel = span < lim ? span : lim;
-  const uint32_t n4 = (nel + 3) / 4;
-  const uint32_t hi = c_hi < n4 ? c_hi : n4;
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  for (uint32_t base = c_lo + (uint32_t)t0; base < hi; base += U * (uint32_t)stride) {
-    float4 a[U], b[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t sa = ((base + u * stride) * 4 + F) & ~3u;
-      const uint32_t sc = sa + 8 <= lim ? sa : (lim - 8) & ~3u;  // tail: aligned in-bounds dummy
-      a[u] = *reinterpret_cast<const float4*>(in0 + sc);
-      b[u] = *reinterpret_cast<const float4*>(in0 + sc + 4);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t c = base + u * stride;
-      if (c >= hi) break;
-      const uint32_t i = c * 4, sidx = i + F, sa = sidx & ~3u;
-      float4 x = a[u], y = b[u];
-      if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
-        float t[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
-        x = make_float4(t[0], t[1], t[2], t[3]);
-        y = make_float4(t[4], t[5], t[6], t[7]);
-      }
-      const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-      constexpr int rem = (int)(F & 3u);
-      const uint32_t col0 = i - (i / ROW) * ROW;
-      if (col0 + 3 < ROW - F && i + 3 < lim) {  // 4 older-frame columns of one row
-        __builtin_nontemporal_store(f4v{src[rem], src[rem + 1], src[rem + 2], src[rem + 3]},
-                                    reinterpret_cast<f4v*>(out0 + i));
-        continue;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t e = i + k;
-        if (e >= lim) break;
-        if (e - (e / ROW) * ROW < ROW - F) out0[e] = src[rem + k];
-      }
-    }
-  }
-}
-template <int F, int H, int U>
-__device__ __forceinline__ void shift6_f16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t total,
-                                           int64_t r0, int64_t r1, uint32_t c_lo, uint32_t c_hi, int t0, int stride) {
-  constexpr uint32_t ROW = F * H, REM = F % 8, M = REM / 2;
-  const uint16_t* __restrict__ in0 = in + r0 * ROW;
-  uint16_t* __restrict__ out0 = out + r0 * ROW;
-  const uint32_t lim = (uint32_t)(total - r0 * (int64_t)ROW);
-  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
-  const uint32_t nel = span < lim ? span : lim;
-  const uint32_t n8 = (nel + 7) / 8;
-  const uint32_t hi = c_hi < n8 ? c_hi : n8;
-  for (uint32_t base = c_lo + (uint32_t)t0; base < hi; base += U * (uint32_t)stride) {
-    u32x4 a[U], b[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t sa = ((base + u * stride) * 8 + F) & ~7u;
-      const uint32_t sc = sa + 16 <= lim ? sa : (lim - 16) & ~7u;
-      a[u] = *reinterpret_cast<const u32x4*>(in0 + sc);
-      b[u] = *reinterpret_cast<const u32x4*>(in0 + sc + 8);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t c8 = base + u * stride;
-      if (c8 >= hi) break;
-      const uint32_t i = c8 * 8, sa = (i + F) & ~7u;
-      uint32_t w[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
-      if (sa + 16 > lim) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t lo = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
-          const uint32_t hh = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
-          w[k] = lo | (hh << 16);
-        }
-      }
-      u32x4 o;
-      if constexpr (REM % 2 == 0) {
-        o = u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
-      } else {
-        o = u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], 2), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], 2),
-                  __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], 2), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], 2)};
-      }
-      const uint32_t col0 = i - (i / ROW) * ROW;
-      if (col0 + 7 < ROW - F && i + 7 < lim) {
-        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out0 + i));
-        continue;
-      }
-      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t e = i + k;
-        if (e >= lim) break;
-        if (e - (e / ROW) * ROW < ROW - F) out0[e] = (uint16_t)(ow[k / 2] >> (16 * (k & 1)));
-      }
-    }
-  }
-}
-// slice `sl` of `nsl` of both histories of the rows [r0, r1), shift wave `wi` of SHIFT6_WAVES
-__device__ __forceinline__ void shift6_slice(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int wi,
-                                             int lane) {
-#ifdef T1_WHATIF_D6_NO_SHIFT  // timing-only what-if build: the history is not shifted
-  return;
-#endif
-  if (r1 <= r0 || sl >= nsl) return;
-  const int t0 = wi * 64 + lane, stride = 64 * SHIFT6_WAVES;
-  const int64_t ro = (int64_t)T1_NOBS * T1_HIST, rp = (int64_t)T1_NPRIV * T1_CHIST;
-  const int per = S.half ? 8 : 4;
-  // chunks of the rows (the buffer end clips the last workgroup's span; the range functions clip again)
-  auto chunks = [&](int64_t row, int64_t total) {
-    const int64_t lim = total - r0 * row, span = (r1 - r0) * row;
-    return (uint32_t)(((span < lim ? span : lim) + per - 1) / per);
-  };
-  const uint32_t no = chunks(ro, S.total_obs), np = chunks(rp, S.total_priv);
-  const uint32_t olo = no * sl / nsl, ohi = no * (sl + 1) / nsl, plo = np * sl / nsl, phi = np * (sl + 1) / nsl;
-  if (S.half) {
-    shift6_f16<T1_NOBS, T1_HIST, SHIFT6_U>(reinterpret_cast<const uint16_t*>(S.obs_in),
-                                            reinterpret_cast<uint16_t*>(S.obs_out), S.total_obs, r0, r1, olo, ohi, t0,
-                                            stride);
-    shift6_f16<T1_NPRIV, T1_CHIST, SHIFT6_U>(reinterpret_cast<const uint16_t*>(S.priv_in),
-                                              reinterpret_cast<uint16_t*>(S.priv_out), S.total_priv, r0, r1, plo, phi,
-                                              t0, stride);
+// ---- the history shift through VGPRs.  Output element e of a row-major history (rows of ROW = F * H) is input element
+// e + F unless e is in the row's newest frame (column >= ROW - F), which the epilogue (or k_post_b) of the same
+// workgroup writes after the shift has completed.  So a 16-B output chunk is stored whole -- its newest-frame elements
+// are don't-cares -- whenever it lies inside the workgroup's rows and its two aligned 16-B source blocks inside the
+// buffer; only a chunk crossing into the next workgroup's first row (whose epilogue may zero it for a reset: the race
+// the whole-chunk store must not enter) or sourcing past the buffer's end takes the element path.
+// bytes [OFF, OFF + 16) of the 32-B window a:b
+template <uint32_t OFF>
+__device__ __forceinline__ u32x4 shift_window(const float4& a, const float4& b) {
+  const u32x4 xa = __builtin_bit_cast(u32x4, a), xb = __builtin_bit_cast(u32x4, b);
+  const uint32_t w[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+  constexpr uint32_t M = OFF / 4, R = OFF % 4;
+  if constexpr (R == 0) {
+    return u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
   } else {
-    shift6_f32<T1_NOBS, T1_HIST, SHIFT6_U>(S.obs_in, S.obs_out, S.total_obs, r0, r1, olo, ohi, t0, stride);
-    shift6_f32<T1_NPRIV, T1_CHIST, SHIFT6_U>(S.priv_in, S.priv_out, S.total_priv, r0, r1, plo, phi, t0, stride);
+    return u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], R), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], R),
+                 __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], R), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], R)};
+  }
+}
+// the element path of one chunk (elements [i, i + PER) of the workgroup's nel): older-frame columns only
+template <int F, int H, bool HALF>
+__device__ __forceinline__ void shift_chunk_elems(const uint8_t* in0, uint8_t* out0, uint32_t i, uint32_t nel) {
+  constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4;
+#pragma unroll 1
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t e = i + k;
+    if (e < nel && e % ROW < ROW - F) {
+      if constexpr (HALF)
+        reinterpret_cast<uint16_t*>(out0)[e] = reinterpret_cast<const uint16_t*>(in0)[e + F];
+      else
+        reinterpret_cast<float*>(out0)[e] = reinterpret_cast<const float*>(in0)[e + F];
+    }
+  }
+}
+// the chunk range [lo, hi) of slice sl of one history of the rows [r0, r1); lim: elements to the buffer's end, nel:
+// the workgroup's elements (its rows, clipped to the buffer)
+template <int F, int H, bool HALF>
+__device__ __forceinline__ void shp_range(int64_t total, int64_t r0, int64_t r1, int sl, int nsl, uint32_t& lo,
+                                          uint32_t& hi, uint32_t& lim, uint32_t& nel) {
+  constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4;
+  lim = (uint32_t)(total - r0 * (int64_t)ROW);
+  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
+  nel = span < lim ? span : lim;
+  const uint32_t n = (nel + PER - 1) / PER;
+  lo = n * (uint32_t)sl / (uint32_t)nsl;
+  hi = n * (uint32_t)(sl + 1) / (uint32_t)nsl;
+}
+// the source loads of U chunks (lane t0's, `stride` apart from chunk lo)
+template <int F, bool HALF, int U>
+__device__ __forceinline__ void shift_loads(const uint8_t* in0, uint32_t lo, uint32_t lim, int t0, int stride,
+                                            float4* a, float4* b) {
+  constexpr uint32_t PER = HALF ? 8 : 4, ES = HALF ? 2 : 4;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = lo + (uint32_t)(t0 + u * stride);
+    const uint32_t sa = (c * PER + F) & ~(PER - 1);
+    const uint32_t sc = sa + 2 * PER <= lim ? sa : (lim - 2 * PER) & ~(PER - 1);  // tail: an aligned in-bounds dummy
+    a[u] = *reinterpret_cast<const float4*>(in0 + (size_t)sc * ES);
+    b[u] = *reinterpret_cast<const float4*>(in0 + (size_t)(sc + PER) * ES);
+  }
+}
+// the stores of U chunks from their loaded source blocks (whole chunks; the rest by the element path)
+template <int F, int H, bool HALF, int U>
+__device__ __forceinline__ void shift_stores(const uint8_t* in0, uint8_t* out0, uint32_t lo, uint32_t hi,
+                                             uint32_t lim, uint32_t nel, int t0, int stride, const float4* a,
+                                             const float4* b) {
+  constexpr uint32_t PER = HALF ? 8 : 4, ES = HALF ? 2 : 4, OFF = (F * ES) % 16;
+  uint32_t slow = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = lo + (uint32_t)(t0 + u * stride), i = c * PER;
+    const uint32_t sa = (i + F) & ~(PER - 1);
+    if (c < hi) {
+      if (i + PER <= nel && sa + 2 * PER <= lim)
+        __builtin_nontemporal_store(shift_window<OFF>(a[u], b[u]), reinterpret_cast<u32x4*>(out0 + (size_t)i * ES));
+      else
+        slow |= 1u << u;
+    }
+  }
+  if (slow) {
+#pragma unroll 1
+    for (int u = 0; u < U; ++u)
+      if ((slow >> u) & 1u) shift_chunk_elems<F, H, HALF>(in0, out0, (lo + (uint32_t)(t0 + u * stride)) * PER, nel);
+  }
+}
+// chunks [c_lo, c_hi) of the workgroup's rows, U per lane per round, every round's loads before its stores
+template <int F, int H, bool HALF, int U>
+__device__ __forceinline__ void shift6_range(const uint8_t* in0, uint8_t* out0, uint32_t c_lo, uint32_t c_hi,
+                                             uint32_t lim, uint32_t nel, int t0, int stride) {
+  for (uint32_t base = c_lo; base + (uint32_t)t0 < c_hi; base += U * (uint32_t)stride) {
+    float4 a[U], b[U];
+    shift_loads<F, HALF, U>(in0, base, lim, t0, stride, a, b);
+    shift_stores<F, H, HALF, U>(in0, out0, base, c_hi, lim, nel, t0, stride, a, b);
   }
 }
 // ---- the shift pipelined across the substep: a shift wave issues the source loads of slice s + 1 right after it
@@ -283,118 +241,26 @@ constexpr int SHP_UO = 7, SHP_UP = 1;  // 32 rows / 10 slices / (6 x 64) lanes: 
 struct ShiftHold {
   float4 a[SHP_UO + SHP_UP], b[SHP_UO + SHP_UP];  // the two aligned 16-B source blocks of each held chunk
 };
-// the chunk range [lo, hi) of slice sl of one history of the rows [r0, r1)
-template <int F, int H, bool HALF>
-__device__ __forceinline__ void shp_range(int64_t total, int64_t r0, int64_t r1, int sl, int nsl, uint32_t& lo,
-                                          uint32_t& hi, uint32_t& lim) {
-  constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4;
-  lim = (uint32_t)(total - r0 * (int64_t)ROW);
-  const uint32_t span = (uint32_t)((r1 - r0) * ROW);
-  const uint32_t n = ((span < lim ? span : lim) + PER - 1) / PER;
-  lo = n * (uint32_t)sl / (uint32_t)nsl;
-  hi = n * (uint32_t)(sl + 1) / (uint32_t)nsl;
-}
 template <int F, int H, bool HALF, int U>
 __device__ __forceinline__ void shp_issue(const void* in, int64_t total, int64_t r0, int64_t r1, int sl, int nsl,
                                           int t0, int stride, float4* a, float4* b) {
-  constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4, ES = HALF ? 2 : 4;
-  uint32_t lo, hi, lim;
-  shp_range<F, H, HALF>(total, r0, r1, sl, nsl, lo, hi, lim);
-  const uint8_t* in0 = reinterpret_cast<const uint8_t*>(in) + (size_t)(r0 * ROW) * ES;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint32_t c = lo + (uint32_t)(t0 + u * stride);
-    const uint32_t sa = (c * PER + F) & ~(PER - 1);
-    const uint32_t sc = sa + 2 * PER <= lim ? sa : (lim - 2 * PER) & ~(PER - 1);  // tail: an aligned in-bounds dummy
-    a[u] = *reinterpret_cast<const float4*>(in0 + (size_t)sc * ES);
-    b[u] = *reinterpret_cast<const float4*>(in0 + (size_t)(sc + PER) * ES);
-  }
+  constexpr uint32_t ROW = F * H, ES = HALF ? 2 : 4;
+  uint32_t lo, hi, lim, nel;
+  shp_range<F, H, HALF>(total, r0, r1, sl, nsl, lo, hi, lim, nel);
+  shift_loads<F, HALF, U>(reinterpret_cast<const uint8_t*>(in) + (size_t)(r0 * ROW) * ES, lo, lim, t0, stride, a, b);
 }
 template <int F, int H, bool HALF, int U>
 __device__ __forceinline__ void shp_commit(const void* in, void* out, int64_t total, int64_t r0, int64_t r1, int sl,
                                            int nsl, int t0, int stride, const float4* a, const float4* b) {
-  constexpr uint32_t ROW = F * H, PER = HALF ? 8 : 4;
-  uint32_t lo, hi, lim;
-  shp_range<F, H, HALF>(total, r0, r1, sl, nsl, lo, hi, lim);
-  if constexpr (!HALF) {
-    const float* in0 = reinterpret_cast<const float*>(in) + r0 * ROW;
-    float* out0 = reinterpret_cast<float*>(out) + r0 * ROW;
-    typedef float f4v __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t c = lo + (uint32_t)(t0 + u * stride);
-      if (c >= hi) break;
-      const uint32_t i = c * 4, sa = (i + F) & ~3u;
-      float4 x = a[u], y = b[u];
-      if (sa + 8 > lim) {  // the last chunks of the buffer: element loads, zero past the end
-        float t[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = sa + k < lim ? in0[sa + k] : 0.0f;
-        x = make_float4(t[0], t[1], t[2], t[3]);
-        y = make_float4(t[4], t[5], t[6], t[7]);
-      }
-      const float src[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-      constexpr int rem = (int)(F & 3u);
-      const uint32_t col0 = i - (i / ROW) * ROW;
-      if (col0 + 3 < ROW - F && i + 3 < lim) {
-        __builtin_nontemporal_store(f4v{src[rem], src[rem + 1], src[rem + 2], src[rem + 3]},
-                                    reinterpret_cast<f4v*>(out0 + i));
-        continue;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t e = i + k;
-        if (e >= lim) break;
-        if (e - (e / ROW) * ROW < ROW - F) out0[e] = src[rem + k];
-      }
-    }
-    // chunks past the held ones (a slice larger than the lanes hold)
-    const uint32_t rest = lo + (uint32_t)(U * stride);
-    if (rest < hi) shift6_f32<F, H, 1>(reinterpret_cast<const float*>(in), reinterpret_cast<float*>(out), total,
-                                              r0, r1, rest, hi, t0, stride);
-  } else {
-    constexpr uint32_t REM = F % 8, M = REM / 2;
-    const uint16_t* in0 = reinterpret_cast<const uint16_t*>(in) + r0 * ROW;
-    uint16_t* out0 = reinterpret_cast<uint16_t*>(out) + r0 * ROW;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t c = lo + (uint32_t)(t0 + u * stride);
-      if (c >= hi) break;
-      const uint32_t i = c * 8, sa = (i + F) & ~7u;
-      const u32x4 xa = __builtin_bit_cast(u32x4, a[u]), xb = __builtin_bit_cast(u32x4, b[u]);
-      uint32_t w[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-      if (sa + 16 > lim) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t l0 = sa + 2 * k < lim ? in0[sa + 2 * k] : 0u;
-          const uint32_t hh = sa + 2 * k + 1 < lim ? in0[sa + 2 * k + 1] : 0u;
-          w[k] = l0 | (hh << 16);
-        }
-      }
-      u32x4 o;
-      if constexpr (REM % 2 == 0) {
-        o = u32x4{w[M], w[M + 1], w[M + 2], w[M + 3]};
-      } else {
-        o = u32x4{__builtin_amdgcn_alignbyte(w[M + 1], w[M], 2), __builtin_amdgcn_alignbyte(w[M + 2], w[M + 1], 2),
-                  __builtin_amdgcn_alignbyte(w[M + 3], w[M + 2], 2), __builtin_amdgcn_alignbyte(w[M + 4], w[M + 3], 2)};
-      }
-      const uint32_t col0 = i - (i / ROW) * ROW;
-      if (col0 + 7 < ROW - F && i + 7 < lim) {
-        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out0 + i));
-        continue;
-      }
-      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t e = i + k;
-        if (e >= lim) break;
-        if (e - (e / ROW) * ROW < ROW - F) out0[e] = (uint16_t)(ow[k / 2] >> (16 * (k & 1)));
-      }
-    }
-    const uint32_t rest = lo + (uint32_t)(U * stride);
-    if (rest < hi) shift6_f16<F, H, 1>(reinterpret_cast<const uint16_t*>(in), reinterpret_cast<uint16_t*>(out),
-                                              total, r0, r1, rest, hi, t0, stride);
-  }
+  constexpr uint32_t ROW = F * H, ES = HALF ? 2 : 4;
+  uint32_t lo, hi, lim, nel;
+  shp_range<F, H, HALF>(total, r0, r1, sl, nsl, lo, hi, lim, nel);
+  const uint8_t* in0 = reinterpret_cast<const uint8_t*>(in) + (size_t)(r0 * ROW) * ES;
+  uint8_t* out0 = reinterpret_cast<uint8_t*>(out) + (size_t)(r0 * ROW) * ES;
+  shift_stores<F, H, HALF, U>(in0, out0, lo, hi, lim, nel, t0, stride, a, b);
+  // chunks past the held ones (a slice larger than the lanes hold: fewer than 10 substeps)
+  const uint32_t rest = lo + (uint32_t)(U * stride);
+  if (rest < hi) shift6_range<F, H, HALF, 1>(in0, out0, rest, hi, lim, nel, t0, stride);
 }
 // issue slice sl's loads into H (shift wave wi); commit slice sl from H
 __device__ __forceinline__ void shp_issue_slice(const ShiftArgs& S, int64_t r0, int64_t r1, int sl, int nsl, int wi,
@@ -421,21 +287,22 @@ __device__ __forceinline__ void shp_commit_slice(const ShiftArgs& S, int64_t r0,
 #endif
   if (r1 <= r0 || sl >= nsl) return;
   const int t0 = wi * 64 + lane, stride = 64 * SHIFT6_WAVES;
+  const ShiftHold& H = Hd;
   if (S.half) {
-    shp_commit<T1_NOBS, T1_HIST, true, SHP_UO>(S.obs_in, S.obs_out, S.total_obs, r0, r1, sl, nsl, t0, stride, Hd.a,
-                                               Hd.b);
+    shp_commit<T1_NOBS, T1_HIST, true, SHP_UO>(S.obs_in, S.obs_out, S.total_obs, r0, r1, sl, nsl, t0, stride, H.a,
+                                               H.b);
     shp_commit<T1_NPRIV, T1_CHIST, true, SHP_UP>(S.priv_in, S.priv_out, S.total_priv, r0, r1, sl, nsl, t0, stride,
-                                                 Hd.a + SHP_UO, Hd.b + SHP_UO);
+                                                 H.a + SHP_UO, H.b + SHP_UO);
   } else {
-    shp_commit<T1_NOBS, T1_HIST, false, SHP_UO>(S.obs_in, S.obs_out, S.total_obs, r0, r1, sl, nsl, t0, stride, Hd.a,
-                                                Hd.b);
+    shp_commit<T1_NOBS, T1_HIST, false, SHP_UO>(S.obs_in, S.obs_out, S.total_obs, r0, r1, sl, nsl, t0, stride, H.a,
+                                                H.b);
     shp_commit<T1_NPRIV, T1_CHIST, false, SHP_UP>(S.priv_in, S.priv_out, S.total_priv, r0, r1, sl, nsl, t0, stride,
-                                                  Hd.a + SHP_UO, Hd.b + SHP_UO);
+                                                  H.a + SHP_UO, H.b + SHP_UO);
   }
 }
 
-__device__ __forceinline__ int shift6_index(int wave) {  // the wave's index among the shift waves, -1: none
-  return (SHIFT6_MASK >> wave) & 1 ? __builtin_popcount(SHIFT6_MASK & ((1 << wave) - 1)) : -1;
+__device__ __forceinline__ int shift6_index(int role) {  // the role's index among the shifting roles, -1: none
+  return (SHIFT6_MASK >> role) & 1 ? __builtin_popcount(SHIFT6_MASK & ((1 << role) - 1)) : -1;
 }
 
 // The model in LDS as the loop sees it: the address passes through an empty asm each substep, so its per-lane reads (the
@@ -612,6 +479,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   T.type = HF ? 2 : 0;
   const t1env_config& C = *Cp;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / 64);
+  const int role = role_of(wave);
   const int lane = threadIdx.x & 63;
   const int leg = lane >> 5;
   const int e = lane & 31;
@@ -628,7 +496,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   __syncthreads();  // the model in LDS
   const DynModel& M = lds.model;
 
-  if (wave == 4) {
+  if (role == 4) {
     // ======== W4: base -- the actions, PD torques, the base block and both base-box halves (their restitution episode)
     const BaseParams<float>& PB = lds.pb[lane];  // W0 stores it before the first S1 (LDS, not registers held across
                                                  // the loop); read from the first substep on
@@ -669,7 +537,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       }
     }
     // the epilogue's inputs the step does not change, staged by W4-W7 before their first substep
-    if (FUSED) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
+    if (FUSED && wave >= 4) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
     const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // load_base_params' friction, restitution
     const float eg = ground_restitution(M, B.restitution[n]);
     int cb, ce;
@@ -771,18 +639,18 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     return;
   }
 
-  if (wave != 0) {
+  if (role != 0) {
     // ======== the term roles W1-W3, W5-W7
-    const int wi = shift6_index(wave);
+    const int wi = shift6_index(role);
     const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // robot shape vs ground (PhysX average)
     const float mu_self = B.friction[n];                          // robot shape vs robot shape
     const float eg = ground_restitution(M, B.restitution[n]);
     // the epilogue's inputs the step does not change, staged by W4-W7 before their first substep
-    if (FUSED && wave >= 5) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
+    if (FUSED && wave >= 4) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
     const int bsh = 1 + 6 * leg + K_SHANK, bft = 1 + 6 * leg + K_FOOT;
-    const int half = wave >= 4 ? 1 : 0;  // W2 / W3: points 0-3, W6 / W7: points 4-7
+    const int half = role >= 4 ? 1 : 0;  // roles 2 / 3: points 0-3, 6 / 7: points 4-7
     // each role its own substep loop (the register allocation of one role's loop does not carry the others' values)
-    if (wave == 1) {
+    if (role == 1) {
       // ---- W1: RNEA bias terms of the leg
       LegParams<float> PL;
       load_leg_params(M, B, n, j0, PL);
@@ -813,7 +681,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
           shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
         }
       }
-    } else if (wave == 5) {
+    } else if (role == 5) {
       // ---- W5: self-contact terms of the shank and foot
       ShiftHold hold;  // the pipelined history shift's loads in flight (its own live range per role loop)
       if (wi >= 0) shp_issue_slice(S, r0, r1, 0, nsub, wi, lane, hold);
@@ -858,7 +726,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     } else {
       // ---- W2 / W6: shank terrain, W3 / W7: foot terrain (one half of the body's points each); W6 also records the
       // sensor-lag samples and the substep log from the state it reads at S1
-      const bool shank = wave == 2 || wave == 6;
+      const bool shank = role == 2 || role == 6;
       int s_dof = 9 - B.dof_lag_timestep[n] % 10;
 #ifdef T1_MUTANT_CAPTURE  // mutation check of tests/test_gpu_product_parity.py only (tools/gpu): capture a substep early
       s_dof = s_dof > 0 ? s_dof - 1 : 0;
@@ -877,7 +745,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         BaseState<float> sb;
         float q[NLEG], qd[NLEG];
         read_state_rows(lds.st, lane, sb, q, qd);
-        if (wave == 6 && sub > 0)
+        if (role == 6 && sub > 0)
           record_substep(M, lds.pb[lane], LG, lds, sub - 1, s_dof, s_imu, N, n, j0, leg, lane, active, sb, q, qd);
         BaseFrame<float> F;
         base_frame(sb, F);
@@ -914,7 +782,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     T1_PROF_MARK(9);
     {  // the contact-force report from the end-of-step state: W2 the shank's terrain force, W3 the foot's, W5 their
        // self-contact forces; W6 sums and stores the shank / foot rows after RB (the base box: W4)
-      if (wave == 2 || wave == 3 || wave == 5) {
+      if (role == 2 || role == 3 || role == 5) {
         BaseState<float> sb;
         float q[NLEG], qd[NLEG];
         read_state_rows(lds.st, lane, sb, q, qd);
@@ -922,7 +790,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         base_frame(sb, F);
         BodyKin<float> Ko[2];
         leg_body_kinematics(M, F, q, qd, leg, Ko);
-        if (wave == 5) {
+        if (role == 5) {
           V3<float> fself[2] = {v3<float>(0.0f, 0.0f, 0.0f), v3<float>(0.0f, 0.0f, 0.0f)};
           if (M.self_collisions) {
             SelfBody<float> O[2], X[2];
@@ -934,7 +802,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
             lds.rsf[s][0][lane] = fself[s].x; lds.rsf[s][1][lane] = fself[s].y; lds.rsf[s][2][lane] = fself[s].z;
           }
         } else {
-          const int s = wave == 2 ? 0 : 1;
+          const int s = role == 2 ? 0 : 1;
           const int b = s == 0 ? bsh : bft;
           const float vt = restitution_target(M, eg, s == 0 ? lds.vish[lane] : lds.vift[lane]);
           const V3<float> f = body_contact_force(M, T, b, Ko[s].Rb, Ko[s].p, F.abs, Ko[s].V, mu, vt);
@@ -942,7 +810,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         }
       }
       T1_PROF_MARK(10);
-      if (wave == 6) {  // the last substep's state (published before R1): its log row, then the lag samples' stores
+      if (role == 6) {  // the last substep's state (published before R1): its log row, then the lag samples' stores
         int s_dof = 9 - B.dof_lag_timestep[n] % 10;
 #ifdef T1_MUTANT_CAPTURE
         s_dof = s_dof > 0 ? s_dof - 1 : 0;
@@ -972,7 +840,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       }
       __syncthreads();  // RB: the report's parts in LDS
       T1_PROF_MARK(11);
-      if (wave == 6) {
+      if (role == 6) {
         float* cf = B.contact_forces + (size_t)n * 39;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -990,12 +858,12 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     if constexpr (FUSED) {
       __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
       T1_PROF_MARK(12);
-      if (wave == 1)
+      if (role == 1)
         fused_epilogue_staged<POST_A_STATE, NE6, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
                                                        lds.act + NLEG);
-      else if (wave == 2)
+      else if (role == 2)
         fused_epilogue_obs<POST_OBS_PRIV, NE6>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
-      else if (wave == 3)
+      else if (role == 3)
         fused_epilogue_obs<POST_OBS_ACTOR, NE6>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
       T1_PROF_MARK(15);
     }

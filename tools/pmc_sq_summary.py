@@ -4,7 +4,10 @@
         --envs 8192 -o profiles/<tag>_sq_counters.json
 
 Per counter: the value summed over the kernel's per-SE instances of one dispatch, averaged over the dispatches
-of --kernel (k_dyn5, the default step kernel; k_dyn4).  Derived ("Roofline"):
+of --kernel (k_dyn6, the default step kernel up to 32 envs per CU; k_dyn5; k_dyn4).  Derived ("Roofline"):
+  * k_dyn6 (two role waves per SIMD): valu_insts_per_simd = SQ_INSTS_VALU / (4 SIMDs x workgroups) and
+    simd_issue_frac = 2 valu_insts_per_simd / kernel_cycles, against the SIMD's one wave64 VALU instruction per 2
+    cycles (what bench.py's roofline.issue reports for k_dyn6);
   * valu_insts_per_dyn_wave: SQ_INSTS_VALU over the dynamics waves: k_dyn5 4 ceil(N / 32) (four role waves per 32
     envs, each also shifting history rows), k_dyn4 4 ceil(N / 64) (the shift waves issue a few hundred VALU each, so
     this slightly overstates a dynamics wave);
@@ -51,7 +54,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("dbs", nargs="+")
     p.add_argument("--envs", type=int, default=8192)
-    p.add_argument("--kernel", default="k_dyn5", choices=["k_dyn6", "k_dyn5", "k_dyn4"])
+    p.add_argument("--kernel", default="k_dyn6", choices=["k_dyn6", "k_dyn5", "k_dyn4"])
     p.add_argument("-o", "--out")
     a = p.parse_args()
     global KERNEL
@@ -79,6 +82,9 @@ def main():
             d["shader_clock_ghz"] = d["kernel_cycles"] / (sum(durs) / len(durs))
         if "valu_insts_per_dyn_wave" in d:
             d["dyn_wave_issue_frac"] = 4.0 * d["valu_insts_per_dyn_wave"] / d["kernel_cycles"]
+        if a.kernel == "k_dyn6" and "SQ_INSTS_VALU" in vals:
+            d["valu_insts_per_simd"] = vals["SQ_INSTS_VALU"] / (4 * ((a.envs + 31) // 32))
+            d["simd_issue_frac"] = 2.0 * d["valu_insts_per_simd"] / d["kernel_cycles"]
     if "SQ_ACTIVE_INST_VALU" in vals and "SQ_WAVE_CYCLES" in vals:
         # VALU quad-cycles over wave quad-cycles, averaged over every wave of the launch (shift waves included)
         d["valu_active_frac_all_waves"] = vals["SQ_ACTIVE_INST_VALU"] / vals["SQ_WAVE_CYCLES"]
