@@ -42,12 +42,12 @@ SIMD_VALU_PER_CYCLE = 0.5        # a SIMD with two or more waves: one wave64 VAL
 # k_post_a / k_post_b only launch on the split (command-curriculum, 1 in 2400) steps
 KERNELS = ["k_dynamics", "k_post_a", "k_post_b"]
 def fused_kernel(num_envs, cus=256):
-    """The step kernel t1env picks (t1_dyn_waves_default): k_dyn6 up to 32 envs per CU, k_dyn4 above; the
-    T1ENV_DYN_KERNEL override wins."""
+    """The step kernel t1env picks (t1_dyn_waves_default): k_dyn6 at every env count; the T1ENV_DYN_KERNEL override
+    wins."""
     k = os.environ.get("T1ENV_DYN_KERNEL")
     if k in ("4", "5", "6"):
         return "k_dyn" + k
-    return "k_dyn6" if (num_envs + 31) // 32 <= cus else "k_dyn4"
+    return "k_dyn6"
 # per-kernel algorithmic bytes per env (reads + writes it must do; DESIGN.md §3) for the split sequence
 SHIFT_BYTES = 2 * 4 * ((3102 - 47) + (219 - 73))
 KERNEL_BYTES = {

@@ -27,9 +27,8 @@ def pytest_sessionfinish(session, exitstatus):
         json.dump({"rtol": mod.RTOL, "atol": mod.ATOL, "fields": rep}, f, indent=1)
 
 
-# the step's dynamics kernels (T1ENV_DYN_KERNEL / T1ENV_D5_SHIFT, read when an env is created): k_dyn6 (the default
-# up to 32 envs per CU), k_dyn5 with its in-workgroup history shift, k_dyn5 beside the concurrent k_shift5 launch, and
-# k_dyn4 (the default above)
+# the step's dynamics kernels (T1ENV_DYN_KERNEL / T1ENV_D5_SHIFT, read when an env is created): k_dyn6 (the default),
+# k_dyn5 with its in-workgroup history shift, k_dyn5 beside the concurrent k_shift5 launch, and k_dyn4
 DYN_KERNELS = {"dyn6": {"T1ENV_DYN_KERNEL": "6"},
                "dyn5": {"T1ENV_DYN_KERNEL": "5", "T1ENV_D5_SHIFT": "0"},
                "dyn5_concshift": {"T1ENV_DYN_KERNEL": "5", "T1ENV_D5_SHIFT": "1"},

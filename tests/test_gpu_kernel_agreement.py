@@ -1,7 +1,8 @@
-"""The step kernels the product picks between agree with each other -- needs the MI355X.
+"""The selectable step kernels agree with each other -- needs the MI355X.
 
-t1_dyn_waves_default picks the step kernel by env count (k_dyn6 / k_dyn5 up to 32 envs per CU, k_dyn4 above), so the
-same global envs run on different kernels in an 8-GPU run (8192 per GPU) and on one GPU (65,536).  The kernels solve
+The product runs k_dyn6 at every env count (t1_dyn_waves_default, since r05; until r04 the choice went by env count,
+so the same global envs ran on different kernels in an 8-GPU run and on one GPU), and T1ENV_DYN_KERNEL=4|5 selects
+the older kernels.  The kernels solve
 the same linear system per substep (compute_delta / _split / _roles / _roles6 agree in fp64, tests/test_dynamics.py)
 but sum it in different fp32 orders, so their trajectories are not bit-identical, and contact dynamics amplify
 rounding chaotically over a trajectory.  The bound is therefore on the ONE-STEP gap, as in tests/test_gpu_dynamics.py:

@@ -902,43 +902,50 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   for (int sub = 0; sub < nsub; ++sub) {
     __syncthreads();  // S1: the substep state published
     T1_PROF_MARK(1);
+    // the lane and leg as the loop sees them (through an empty asm each substep): the lane- and leg-indexed LDS
+    // addresses are formed in the loop, not hoisted out of it as invariants and spilled to scratch
+    int lane_s = lane, leg_s = leg;
+#ifndef T1_D6_NO_LAUNDER  // A/B builds
+    asm volatile("" : "+v"(lane_s), "+v"(leg_s));
+#endif
     const DynModel& M = model_in_loop(lds.model);
     LegBlock<float> lb;
     Sym6<float> Ab;
     {
       BaseState<float> sb;
       float q[NLEG], qd[NLEG];
-      read_state_rows(lds.st, lane, sb, q, qd);
+      read_state_rows(lds.st, lane_s, sb, q, qd);
       const M3<float> R0 = quat_to_mat(sb.quat[0], sb.quat[1], sb.quat[2], sb.quat[3]);  // base_frame's F.R0
       LegFK<float> fk;
-      leg_fk_chain(M, R0, q, leg, fk);
+      leg_fk_chain(M, R0, q, leg_s, fk);
       float Sj[NLEG][6];
       sym_zero(Ab);
-      leg_backward_crba(M, PL, q, qd, leg, dt, fk, Sj, lb, Ab);
+      leg_backward_crba(M, PL, q, qd, leg_s, dt, fk, Sj, lb, Ab);
 #pragma unroll
       for (int k = 0; k < NLEG; ++k) {  // the joint subspaces to LDS for the fold-in (registers at its peak)
-        lds.sj.r[k][0][lane] = make_float4(Sj[k][0], Sj[k][1], Sj[k][2], Sj[k][3]);
-        lds.sj.r[k][1][lane] = make_float4(Sj[k][4], Sj[k][5], 0.0f, 0.0f);
+        lds.sj.r[k][0][lane_s] = make_float4(Sj[k][0], Sj[k][1], Sj[k][2], Sj[k][3]);
+        lds.sj.r[k][1][lane_s] = make_float4(Sj[k][4], Sj[k][5], 0.0f, 0.0f);
       }
     }
     T1_PROF_MARK(2);
     __syncthreads();  // S2: the terms published
     T1_PROF_MARK(3);
     {  // the episodes of the shank and foot from the two halves of their points
-      vi_sh = restitution_episode(vi_sh, fmaxf(lds.amx[WC_SHA][lane], lds.amx[WC_SHB][lane]));
-      vi_ft = restitution_episode(vi_ft, fmaxf(lds.amx[WC_FTA][lane], lds.amx[WC_FTB][lane]));
-      lds.vish[lane] = vi_sh;  // W2 / W6 read it after the next S1
-      lds.vift[lane] = vi_ft;  // W3 / W7
+      vi_sh = restitution_episode(vi_sh, fmaxf(lds.amx[WC_SHA][lane_s], lds.amx[WC_SHB][lane_s]));
+      vi_ft = restitution_episode(vi_ft, fmaxf(lds.amx[WC_FTA][lane_s], lds.amx[WC_FTB][lane_s]));
+      lds.vish[lane_s] = vi_sh;  // W2 / W6 read it after the next S1
+      lds.vift[lane_s] = vi_ft;  // W3 / W7
     }
     float g6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     {
       float rg[NLEG];  // dt tau_k (W4's torques, the first two rows of wb) + the bias part (W1)
-      const float4 t0 = lds.wb.r[0][lane], t1 = lds.wb.r[1][lane], g0 = lds.w1.r[0][lane], g1 = lds.w1.r[1][lane];
+      const float4 t0 = lds.wb.r[0][lane_s], t1 = lds.wb.r[1][lane_s];
+      const float4 g0 = lds.w1.r[0][lane_s], g1 = lds.w1.r[1][lane_s];
       const float tv[NLEG] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y}, gv[NLEG] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y};
       static_assert(WB_TAU == 0 && R_RG == 0, "the torques and the bias rhs lead their rows");
 #pragma unroll
       for (int k = 0; k < NLEG; ++k) rg[k] = dt * tv[k] + gv[k];
-      leg_apply_terms_rows<K_SHANK, K_FOOT>(lds.wc, lds.w1, rg, lds.sj, lane, lb, Ab, g6);
+      leg_apply_terms_rows<K_SHANK, K_FOOT>(lds.wc, lds.w1, rg, lds.sj, lane_s, lb, Ab, g6);
     }
     T1_PROF_MARK(5);
     float rb[6];
@@ -951,7 +958,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     float r[6];
     {
       float v[WB_N];
-      get4(lds.wb, lane, v);
+      get4(lds.wb, lane_s, v);
 #pragma unroll
       for (int i = 0; i < 21; ++i) Ac.a[i] = v[WB_AC + i];
 #pragma unroll
@@ -974,12 +981,12 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     backsub_leg(lb, r, dq);
     BaseState<float> sb;
     float q[NLEG], qd[NLEG];
-    read_state_rows(lds.st, lane, sb, q, qd);
+    read_state_rows(lds.st, lane_s, sb, q, qd);
     integrate_base(sb, r, dt);
-    integrate_leg(M, leg, q, qd, dq, dt);
+    integrate_leg(M, leg_s, q, qd, dq, dt);
     float v[Q_N];
     state_pack(sb, q, qd, v);
-    put4(lds.st, lane, v);  // the roles read the previous state before S2; after the last substep: the report's
+    put4(lds.st, lane_s, v);  // the roles read the previous state before S2; after the last substep: the report's
     T1_PROF_MARK(7);
   }
   BaseState<float> sb;

@@ -622,11 +622,14 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
   T1_PROF_END();
 }
 
-// k_dyn6 while its 32-env workgroups fit the device in one round (N <= 32 x CUs: 8192 envs on 256 CUs), k_dyn4 above:
-// both run one workgroup per CU, and once every CU is busy k_dyn4's 64 envs per workgroup cost less than two rounds of
-// 32 (r04j, k_dyn5: 16384 envs 0.271 vs 0.289 ms).  At 8192 trimesh envs k_dyn6 0.127 ms, k_dyn5 0.141, k_dyn4 0.150
-// (r05).  T1ENV_DYN_KERNEL=4|5|6 overrides (A/B).
-int t1_dyn_waves_default(int num_envs, int cus) { return (num_envs + 31) / 32 <= cus ? 6 : 4; }
+// k_dyn6 at every env count: at 8192 trimesh envs (one round of 32-env workgroups on 256 CUs) k_dyn6 0.127 ms,
+// k_dyn5 0.141, k_dyn4 0.150; above one round k_dyn6's rounds still beat k_dyn4's 64-env workgroups (r05full: 16384
+// trimesh 0.247 vs 0.268 ms, 32768 0.485 vs 0.519).  T1ENV_DYN_KERNEL=4|5|6 overrides (A/B).
+int t1_dyn_waves_default(int num_envs, int cus) {
+  (void)num_envs;
+  (void)cus;
+  return 6;
+}
 
 constexpr int MIN_SHIFT_BLOCKS = 64;
 bool t1_shift_prelaunch(int num_envs, const DynLaunch& cfg) {

@@ -559,9 +559,14 @@ __device__ __forceinline__ bool post_a_core(const DynModel& M, const t1env_confi
 #pragma unroll
     for (int k = 0; k < T1_NREW; ++k) part[k] = contrib[k];
     part[T1_NREW] = do_reset ? 1.0f : 0.0f;
-    if (ep_row)  // the fused k_dyn4 step: this workgroup's partial row (FusedArgs::ep_part)
-      wave_sum_store_n(ep_row, part);
-    else
+    if (ep_row) {  // the fused step: this workgroup's partial row (FusedArgs::ep_part)
+      if (__ballot(do_reset) != 0) {
+        wave_sum_store_n(ep_row, part);
+      } else if ((threadIdx.x & 63) == 0) {  // no env of the wave resets (most steps): the sums are all +0
+#pragma unroll
+        for (int k = 0; k <= T1_NREW; ++k) __hip_atomic_store(ep_row + k, 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else
       wave_atomic_add_n(B.ep_accum, part);  // ep_accum[0..23] episode sums, [24] reset count
   }
   X.el = el;
