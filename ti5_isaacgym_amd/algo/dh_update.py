@@ -100,6 +100,10 @@ class DHPPO:
         # graphed update minibatch step: (key, graph) once captured; under data parallelism (key, (graph A, graph B))
         # with the gradient / KL all-reduce eager between them
         self.graph_update = cuda
+        # graphed process_env_step: {(storage slot, every input's address): graph}, one per rollout slot and env
+        # buffer parity (the env's observation buffers alternate between two addresses); False = eager
+        self.graph_store = cuda
+        self._store_graphs = {}
         if cuda:
             _init_graph_rng(device)
         self._upd = None
@@ -239,13 +243,49 @@ class DHPPO:
         t.critic_observations = critic_obs
         return t.actions
 
-    def process_env_step(self, rewards, dones, infos):
+    def _store_body(self, rewards, dones, time_outs, k):
+        """process_env_step's device work for rollout slot k: the time-out bootstrap and the transition's copies."""
         t = self.transition
         t.rewards = rewards.clone()
         t.dones = dones
-        if "time_outs" in infos:  # bootstrap on time-outs
-            t.rewards += self.gamma * torch.squeeze(t.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
-        self.storage.add_transitions(t)
+        if time_outs is not None:  # bootstrap on time-outs
+            t.rewards += self.gamma * torch.squeeze(t.values * time_outs.unsqueeze(1).to(self.device), 1)
+        self.storage.write_transition(t, k)
+
+    def _graphed_store(self, rewards, dones, time_outs):
+        """The slot's store as a captured graph (a dozen small copies and element-wise kernels a step: their launch
+        gaps, not their bytes, set the eager time).  Keyed by the slot and every input's address, so a replay reads
+        the tensors it was captured on; anything else stays eager."""
+        t, k = self.transition, self.storage.step
+        ins = (rewards, dones, time_outs, t.observations, t.critic_observations, t.actions, t.values,
+               t.actions_log_prob, t.action_mean, t.action_sigma)
+        if any(x is not None and not x.is_cuda for x in ins) or t.next_proprio_obs is not None:
+            return False
+        key = (k,) + tuple(x.data_ptr() if x is not None else 0 for x in ins)
+        g = self._store_graphs.get(key)
+        if g is None:
+            if len(self._store_graphs) >= 4 * self.storage.num_transitions_per_env:
+                return False   # not the rollout's fixed buffers
+            self._store_body(rewards, dones, time_outs, k)   # this step eagerly; capture for the next time
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g):
+                    self._store_body(rewards, dones, time_outs, k)
+            except RuntimeError as e:
+                warnings.warn(f"DHPPO: process_env_step graph capture failed, running eager: {e}")
+                self.graph_store = False
+                return True
+            self._store_graphs[key] = g
+            return True
+        g.replay()
+        return True
+
+    def process_env_step(self, rewards, dones, infos):
+        t = self.transition
+        time_outs = infos.get("time_outs")
+        if not (self.graph_store and rewards.is_cuda and self._graphed_store(rewards, dones, time_outs)):
+            self._store_body(rewards, dones, time_outs, self.storage.step)
+        self.storage.step += 1
         t.clear()
         self.actor_critic.reset(dones)
 

@@ -64,13 +64,20 @@ class RolloutStorage:
         self.saved_hidden_states_a = None
         self.saved_hidden_states_c = None
         self.step = 0
+        self.graph_gae = True   # compute_returns' backward pass as a captured graph on a HIP device
+        self._gae_graph = None
+        self._gae_lv = None
         self._rows = None       # the frame-history rows source (_HistoryRows), rebuilt in place every update
         self._obs_cast = None   # the full storage's observations cast to the update's dtype, in place every update
 
     def add_transitions(self, t):
-        if self.step >= self.num_transitions_per_env:
+        self.write_transition(t, self.step)
+        self.step += 1
+
+    def write_transition(self, t, k):
+        """The transition's copies into slot k (add_transitions without the step count: DHPPO's graphed store)."""
+        if k >= self.num_transitions_per_env:
             raise AssertionError("Rollout buffer overflow")
-        k = self.step
         if self.history is not None:
             if k == 0:
                 self.obs0.copy_(t.observations)
@@ -88,13 +95,11 @@ class RolloutStorage:
         self.sigma[k].copy_(t.action_sigma)
         if self.next_proprio_obs is not None:
             self.next_proprio_obs[k].copy_(t.next_proprio_obs)
-        self.step += 1
 
     def clear(self):
         self.step = 0
 
-    def compute_returns(self, last_values, gamma, lam):
-        """Generalised advantage estimation, backwards over the rollout (rollout_storage.py:91-116)."""
+    def _gae(self, last_values, gamma, lam):
         adv = torch.zeros_like(last_values)
         next_values = last_values
         for k in range(self.num_transitions_per_env - 1, -1, -1):
@@ -105,6 +110,25 @@ class RolloutStorage:
             next_values = self.values[k]
         # in place: the minibatch sources keep their addresses across updates (a captured update graph reads them)
         torch.sub(self.returns, self.values, out=self.advantages)
+
+    def compute_returns(self, last_values, gamma, lam):
+        """Generalised advantage estimation, backwards over the rollout (rollout_storage.py:91-116).  On a HIP device
+        the backward pass (about 200 small element-wise kernels) replays a captured graph over the storage's own
+        buffers and a static copy of last_values: the same kernels, without their launch gaps."""
+        if last_values.is_cuda and self.graph_gae:
+            key = (tuple(last_values.shape), last_values.dtype, float(gamma), float(lam))
+            if self._gae_graph is None or self._gae_graph[0] != key:
+                self._gae_lv = last_values.clone()
+                self._gae(self._gae_lv, gamma, lam)   # this call eagerly; captured for the next ones
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._gae(self._gae_lv, gamma, lam)
+                self._gae_graph = (key, g)
+            else:
+                self._gae_lv.copy_(last_values)
+                self._gae_graph[1].replay()
+        else:
+            self._gae(last_values, gamma, lam)
         mean, std = dist_util.global_mean_std(self.advantages)
         self.advantages.sub_(mean).div_(std + 1e-8)
 

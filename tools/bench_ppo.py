@@ -8,7 +8,8 @@ DH-PPO update, on one GPU or data-parallel over N GPUs of one node.
 One process per GPU (RCCL = torch.distributed "nccl"): rank r steps global envs [r*N, (r+1)*N) and the update
 all-reduces the flat policy gradient once per minibatch (8 per iteration, ti5_isaacgym_amd/algo/distributed.py) --
 the exchange config 4 names.  Timed: --iters whole learn() iterations after one warm-up iteration, bracketed by a
-barrier + synchronize, max over ranks; then a phase breakdown (rollout / env.step inside it / update) and the mean
+barrier + synchronize, max over ranks; then a phase breakdown (the rollout as learn() runs it, compute_returns, the
+rollout again with a sync around every env.step for the env share, the update) and the mean
 gradient all-reduce time (CUDA events around every all-reduce of the timed iterations).  Rank 0 prints one JSON line.
 """
 import argparse
@@ -85,8 +86,24 @@ steps = a.iters * T * N * world
 # phase breakdown: rollout (policy inference + env.step + storage) vs the PPO update
 alg = r.alg
 obs, cobs = env.get_observations(), env.get_privileged_observations()
-t_roll = t_env = t_upd = 0.0
+t_roll = t_env = t_upd = t_free = t_ret = 0.0
 for _ in range(a.iters):
+    # the rollout as learn() runs it (no sync inside): act + env.step + process_env_step, then compute_returns
+    barrier()
+    t0 = time.perf_counter()
+    with torch.inference_mode():
+        for i in range(T):
+            act = alg.act(obs, cobs)
+            obs, cobs, rew, dones, infos = env.step(act)
+            alg.process_env_step(rew, dones, infos)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        alg.compute_returns(cobs)
+    barrier()
+    t_free += t1 - t0
+    t_ret += time.perf_counter() - t1
+    alg.storage.clear()
+    # the same with a sync around every env.step: the env's share (the syncs add their own idle time)
     barrier()
     t0 = time.perf_counter()
     with torch.inference_mode():
@@ -105,12 +122,14 @@ for _ in range(a.iters):
     barrier()
     t_upd += time.perf_counter() - t1
     t_roll += t1 - t0
-t_roll, t_env, t_upd = (max_over_ranks(x) for x in (t_roll, t_env, t_upd))
+t_roll, t_env, t_upd, t_free, t_ret = (max_over_ranks(x) for x in (t_roll, t_env, t_upd, t_free, t_ret))
 line = {"bench": "ppo_iteration", "n_gpus": 1 if a.one_gpu else world, "ranks": world, "num_envs_per_gpu": N,
         "global_envs": N * world, "mesh": a.mesh, "iters": a.iters, "graph_act": r.alg.graph_act,
         "update_dtype": "bf16" if a.bf16 else "fp32", "env_steps_per_s_incl_update": round(steps / dt, 1),
         "env_steps_per_s_per_gpu": round(steps / dt / world, 1), "s_per_iter": round(dt / a.iters, 4),
-        "phases_s_per_iter": {"rollout": round(t_roll / a.iters, 4), "env_step_in_rollout": round(t_env / a.iters, 4),
+        "phases_s_per_iter": {"rollout": round(t_free / a.iters, 4), "compute_returns": round(t_ret / a.iters, 4),
+                              "rollout_synced": round(t_roll / a.iters, 4),
+                              "env_step_in_rollout_synced": round(t_env / a.iters, 4),
                               "update": round(t_upd / a.iters, 4)},
         "grad_allreduce": {"bytes": r.alg.grads.flat.numel() * 4, "per_iter": cfg["algorithm"]["num_learning_epochs"]
                            * cfg["algorithm"]["num_mini_batches"],
