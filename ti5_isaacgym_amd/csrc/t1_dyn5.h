@@ -101,9 +101,22 @@ T1_HD void leg_backward_crba(const DynModel& M, const LegParams<R>& P, const R q
 #pragma unroll
     for (int r = 0; r < 6; ++r) out.Bl[r][k] = Fk[r];
   };
+#ifndef T1_WHATIF_CRBA_HALF  // timing-only what-if build (never the product): the distal half of the pass skipped
   step(kconst<5>{});
   step(kconst<4>{});
   step(kconst<3>{});
+#else  // joints 3-5 decoupled with a unit inertia (a bounded, wrong system: timing only)
+#pragma unroll
+  for (int k = 3; k < NLEG; ++k) {
+#pragma unroll
+    for (int jj = 0; jj < NLEG; ++jj) out.L[sidx(jj < k ? jj : k, jj < k ? k : jj)] = jj == k ? R(1) : R(0);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) out.Bl[r][k] = R(0);
+    out.rhs[k] = R(0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) S[k][i] = R(0);
+  }
+#endif
   step(kconst<2>{});
   step(kconst<1>{});
   step(kconst<0>{});

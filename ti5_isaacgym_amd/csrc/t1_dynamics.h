@@ -515,10 +515,14 @@ T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, con
     if constexpr (std::is_same<R, float>::value && CH % 2 == 0) {
 #pragma unroll
       for (int i = 0; i < CH; i += 2) {
-        const bool c0 = dz[i] > R(0), c1 = dz[i + 1] > R(0);  // below the surface (the normal's z is positive)
+        // the pair's inputs as values before the branch: the unrolled pairs' identical bodies may be merged into one
+        // block, which then takes phis of these values instead of indexing the arrays (a scratch copy at -O2)
+        const V3<R> x0 = xs[i], x1 = xs[i + 1];
+        const R dz0 = dz[i], dz1 = dz[i + 1], gx0 = gxs[i], gy0 = gys[i], gx1 = gxs[i + 1], gy1 = gys[i + 1];
+        const bool c0 = dz0 > R(0), c1 = dz1 > R(0);  // below the surface (the normal's z is positive)
         if (c0 || c1) {
-          const V3<R> n0 = terrain_normal<HF>(gxs[i], gys[i]), n1 = terrain_normal<HF>(gxs[i + 1], gys[i + 1]);
-          contact_pair(M, xs[i], xs[i + 1], n0, n1, dz[i] * n0.z, dz[i + 1] * n1.z, c0, c1, Vb, mu, vtg, dt, pacc, amax);
+          const V3<R> n0 = terrain_normal<HF>(gx0, gy0), n1 = terrain_normal<HF>(gx1, gy1);
+          contact_pair(M, x0, x1, n0, n1, dz0 * n0.z, dz1 * n1.z, c0, c1, Vb, mu, vtg, dt, pacc, amax);
         }
       }
     } else
@@ -538,6 +542,20 @@ T1_HD void body_contact_np(const DynModel& M, const Terrain& T, int c_begin, con
 #endif
   moments_flush(fric, A);
 }
+
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(T1_SCALAR_CONTACT)
+// one pair of queried points into the pair accumulators (contact_apply), every input by value
+template <bool HF>
+__device__ __forceinline__ void contact_pair_q(const DynModel& M, V3<float> x0, V3<float> x1, float dz0, float dz1,
+                                               float gx0, float gy0, float gx1, float gy1, const float Vb[6], float mu,
+                                               float vtg, float dt, PairAcc& pacc, float& amax) {
+  const bool c0 = dz0 > 0.0f, c1 = dz1 > 0.0f;  // below the surface (the normal's z is positive)
+  if (c0 || c1) {
+    const V3<float> n0 = terrain_normal<HF>(gx0, gy0), n1 = terrain_normal<HF>(gx1, gy1);
+    contact_pair(M, x0, x1, n0, n1, dz0 * n0.z, dz1 * n1.z, c0, c1, Vb, mu, vtg, dt, pacc, amax);
+  }
+}
+#endif
 
 // body_contact_np in two halves, for a caller with independent work to run while the height loads are in flight:
 // contact_query (phase 1: transforms and terrain queries, one batch of NP <= T1_CONTACT_BATCH points) and
@@ -567,14 +585,18 @@ T1_HD void contact_apply(const DynModel& M, const ContactQuery<NP, R>& Q, const 
   if constexpr (std::is_same<R, float>::value && NP % 2 == 0) {
     PairAcc pacc;
     pair_acc_zero(pacc);
-#pragma unroll
-    for (int i = 0; i < NP; i += 2) {
-      const bool c0 = Q.dz[i] > R(0), c1 = Q.dz[i + 1] > R(0);
-      if (c0 || c1) {
-        const V3<R> n0 = terrain_normal<HF>(Q.gx[i], Q.gy[i]), n1 = terrain_normal<HF>(Q.gx[i + 1], Q.gy[i + 1]);
-        contact_pair(M, Q.xs[i], Q.xs[i + 1], n0, n1, Q.dz[i] * n0.z, Q.dz[i + 1] * n1.z, c0, c1, Vb, mu, vtg, dt, pacc,
-                     amax);
-      }
+    // the pairs unrolled by hand, their inputs passed by value (at -O2 the pragma'd loop, and a lambda capturing Q,
+    // kept a scratch copy of Q indexed per pair)
+    static_assert(NP == 4 || NP == 8, "two or four pairs");
+    contact_pair_q<HF>(M, Q.xs[0], Q.xs[1], Q.dz[0], Q.dz[1], Q.gx[0], Q.gy[0], Q.gx[1], Q.gy[1], Vb, mu, vtg, dt, pacc,
+                       amax);
+    contact_pair_q<HF>(M, Q.xs[2], Q.xs[3], Q.dz[2], Q.dz[3], Q.gx[2], Q.gy[2], Q.gx[3], Q.gy[3], Vb, mu, vtg, dt, pacc,
+                       amax);
+    if constexpr (NP == 8) {
+      contact_pair_q<HF>(M, Q.xs[4], Q.xs[5], Q.dz[4], Q.dz[5], Q.gx[4], Q.gy[4], Q.gx[5], Q.gy[5], Vb, mu, vtg, dt,
+                         pacc, amax);
+      contact_pair_q<HF>(M, Q.xs[6], Q.xs[7], Q.dz[6], Q.dz[7], Q.gx[6], Q.gy[6], Q.gx[7], Q.gy[7], Vb, mu, vtg, dt,
+                         pacc, amax);
     }
     pair_acc_flush(pacc, A, g);
   } else
@@ -991,8 +1013,12 @@ T1_HD void body_contact_fixed_q(const DynModel& M, const ContactQuery<NP, R>& Q,
   }
   const R vtg = restitution_target(M, e, vimp);
   R amax = R(-1);
+#ifdef T1_CONTACT_ONE_COPY  // one copy of the contact law (k_dyn6's unit: see t1env_dyn6.hip)
+  contact_apply<HF, NP>(M, Q, Vb, mu, vtg, dt, A, g, amax);
+#else
   if (t1_wave_any(vtg > R(0))) contact_apply<HF, NP>(M, Q, Vb, mu, vtg, dt, A, g, amax);
   else contact_apply<HF, NP>(M, Q, Vb, mu, R(0), dt, A, g, amax);
+#endif
   vimp = restitution_episode(vimp, amax);
 }
 // body_contact_fixed for a body that is always evaluated (no height bound), with `between()` run after its terrain

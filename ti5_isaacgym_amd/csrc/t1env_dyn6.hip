@@ -17,21 +17,30 @@
 //   W5    1     self-contacts (capsules, both legs' bodies by permlane)  history shift slice
 //   W2    2     shank terrain contact, points 0-3                        history shift slice
 //   W6    2     shank terrain contact, points 4-7 (at S1: the sensor-lag  history shift slice
-//               capture of the previous substep's state)
-//   W3    3     foot terrain contact, points 0-3                         --
-//   W7    3     foot terrain contact, points 4-7                         --
+//               capture and substep log of the previous substep's state)
+//   W3    3     foot terrain contact, points 0-3                         history shift slice
+//   W7    3     foot terrain contact, points 4-7                         history shift slice
 //
 // The core wave (W0) owns the restitution episodes of the shank and foot: the contact halves publish the fastest
 // approach of their points (amx), and W0 folds the two halves of a body into its episode after S2 (W4 keeps the base
-// box's, as k_dyn5's W1).  The
-// history shift is no longer staged in LDS (the role hand-offs need it): the shift waves copy their slice of the
-// workgroup's rows through VGPRs (two aligned 16-B loads per output chunk, non-temporal stores) in the post-S2 window,
-// where their role state is dead.  The step's report and the fused epilogue are k_dyn5's, spread over the eight waves.
+// box's, as k_dyn5's W1).  The history shift is not staged in LDS (the role hand-offs need it): each of the six shift
+// waves copies one tenth of its share of the workgroup's rows per substep through VGPRs, pipelined across the substep
+// -- slice s + 1's two aligned 16-B source loads per output chunk are issued right after slice s's stores and held in
+// registers through the next substep's role work (ShiftHold), so the HBM stream spans the whole substep -- and stores
+// whole 16-B chunks (the newest frame of a row is a don't-care the epilogue rewrites; only the workgroup's last chunk
+// takes an element path).  The step's report and the fused epilogue are k_dyn5's, spread over the eight waves.
 //
 // Every value is computed by the same t1_dynamics.h / t1_dyn5.h functions as in k_dyn5; what differs is the order of a
 // few sums: a contact body's terms are the sum of its two point halves (and the self terms) instead of one 8-point
 // accumulation.  compute_delta_roles6 (t1_dyn5.h) is the same composition on one host thread (tests/test_dynamics.py).
 #include <hip/hip_runtime.h>
+
+// one inlined copy of the contact law per call site (body_contact_fixed_q, contact_half) instead of a copy
+// specialised for waves without a restitution set point: the -O2 build merged the two and indexed a scratch copy of
+// the query (-DT1_D6_VTG_SPECIALIZE: the two copies, A/B)
+#ifndef T1_D6_VTG_SPECIALIZE
+#define T1_CONTACT_ONE_COPY
+#endif
 
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py --kernel 6): lane 0 of every wave accumulates shader-clock deltas
 // between T1_PROF_MARK points into per-phase buckets; never part of the product build.
@@ -351,8 +360,12 @@ __device__ __forceinline__ void contact_half(const DynModel& M, const Terrain& T
     const int32_t bnd = terrain_bound_raw_any(T, K.p.x + F.abs.x, K.p.y + F.abs.y);
     if (K.p.z + F.abs.z - M.contact_radius[b] > bound_height<float>(T, bnd)) return;
   }
+#ifdef T1_D6_VTG_SPECIALIZE  // A/B: the contact law specialised for a wave without a restitution set point
   if (t1_wave_any(vtg > 0.0f)) contact_apply<HF, T1_POINTS_PER_BODY / 2>(M, Q, K.V, mu, vtg, dt, C, c, amax);
   else contact_apply<HF, T1_POINTS_PER_BODY / 2>(M, Q, K.V, mu, 0.0f, dt, C, c, amax);
+#else  // one copy of the contact law (the -O2 build merged the two and indexed a scratch copy of Q)
+  contact_apply<HF, T1_POINTS_PER_BODY / 2>(M, Q, K.V, mu, vtg, dt, C, c, amax);
+#endif
 }
 
 // leg_apply_terms (t1_dyn5.h) with its inputs read from LDS where they are used, to hold the core wave's register peak:
@@ -500,12 +513,19 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     // ======== W4: base -- the actions, PD torques, the base block and both base-box halves (their restitution episode)
     const BaseParams<float>& PB = lds.pb[lane];  // W0 stores it before the first S1 (LDS, not registers held across
                                                  // the loop); read from the first substep on
+    // the friction and restitution, lag, force and episode loads, then the actions and PD constants below, before the
+    // first global store (the buffers may alias as far as the compiler knows)
+#ifdef T1_D6_STAGE_FIRST  // A/B: the staging loads first (0.1275 vs 0.1270 ms, r05st: not kept)
+    EpiStage<NE6, 256> EV;
+    if (FUSED) epi_stage_load<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, EV);
+#endif
+    const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // load_base_params' friction, restitution
+    const float eg = ground_restitution(M, B.restitution[n]);
     const int lag = B.lag_timestep[n];
     const RngKey K = rng_key(C.seed, (uint32_t)(C.env_offset + n), ctr);
     const V3<float> ef = v3<float>(B.applied_force[n * 3 + 0], B.applied_force[n * 3 + 1], B.applied_force[n * 3 + 2]);
     float vi_b = B.contact_vimp[(size_t)n * NVIMP + vimp_base(leg)];
-    {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged (every per-env
-       // load before the first global store: the buffers may alias as far as the compiler knows)
+    {  // actions = clip(actions) into the step's history slot, the PD constants and action ring staged
       PdStage<64>& P = lds.pd;
       float a[NLEG];
 #pragma unroll
@@ -536,10 +556,13 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         }
       }
     }
-    // the epilogue's inputs the step does not change, staged by W4-W7 before their first substep
-    if (FUSED && wave >= 4) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
-    const float mu = 0.5f * (B.friction[n] + M.ground_friction);  // load_base_params' friction, restitution
-    const float eg = ground_restitution(M, B.restitution[n]);
+    // the epilogue's inputs the step does not change, staged by W4-W7 before their first substep (staged by W4 alone
+    // in the first substep's idle S2 -> S1 window instead: 0.1301 vs 0.1269 ms, its loop's registers spill, r05stage)
+#ifdef T1_D6_STAGE_FIRST
+    if (FUSED) epi_stage_store<NE6, 256>(N, (int)r0, (int)threadIdx.x - 256, EV, lds.epi);
+#else
+    if (FUSED) stage_epilogue_inputs<NE6, 256>(B, N, (int)r0, (int)threadIdx.x - 256, lds.epi);
+#endif
     int cb, ce;
     base_contact_range(M, leg, cb, ce);
     T1_PROF_MARK(0);
@@ -858,7 +881,11 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     if constexpr (FUSED) {
       __syncthreads();  // the epilogue barrier: every output of the workgroup is in LDS / memory
       T1_PROF_MARK(12);
-      if (role == 1)
+#ifndef T1_WHATIF_D6_EPI_SKIP  // timing-only what-if builds: bit r set = role r skips its epilogue part
+#define T1_WHATIF_D6_EPI_SKIP 0
+#endif
+      if ((T1_WHATIF_D6_EPI_SKIP >> role) & 1) {
+      } else if (role == 1)
         fused_epilogue_staged<POST_A_STATE, NE6, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
                                                        lds.act + NLEG);
       else if (role == 2)
@@ -902,10 +929,11 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   for (int sub = 0; sub < nsub; ++sub) {
     __syncthreads();  // S1: the substep state published
     T1_PROF_MARK(1);
-    // the lane and leg as the loop sees them (through an empty asm each substep): the lane- and leg-indexed LDS
-    // addresses are formed in the loop, not hoisted out of it as invariants and spilled to scratch
+    // -DT1_D6_LAUNDER (A/B): the lane and leg through an empty asm each substep, so the lane- and leg-indexed LDS
+    // addresses are formed in the loop instead of hoisted and spilled: no scratch reloads in the loop, yet measured
+    // 0.5-1% slower (r05ab2, r05o2)
     int lane_s = lane, leg_s = leg;
-#ifndef T1_D6_NO_LAUNDER  // A/B builds
+#ifdef T1_D6_LAUNDER
     asm volatile("" : "+v"(lane_s), "+v"(leg_s));
 #endif
     const DynModel& M = model_in_loop(lds.model);
@@ -945,7 +973,11 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       static_assert(WB_TAU == 0 && R_RG == 0, "the torques and the bias rhs lead their rows");
 #pragma unroll
       for (int k = 0; k < NLEG; ++k) rg[k] = dt * tv[k] + gv[k];
+#ifndef T1_WHATIF_D6_NO_FOLDIN  // timing-only what-if build: the contact / bias terms not folded in
       leg_apply_terms_rows<K_SHANK, K_FOOT>(lds.wc, lds.w1, rg, lds.sj, lane_s, lb, Ab, g6);
+#else
+      for (int k = 0; k < NLEG; ++k) lb.rhs[k] += rg[k];
+#endif
     }
     T1_PROF_MARK(5);
     float rb[6];
