@@ -41,13 +41,13 @@ SIMD_VALU_PER_CYCLE = 0.5        # a SIMD with two or more waves: one wave64 VAL
 # whole fused step (k_dyn6: dynamics + in-workgroup history shift + post-physics epilogue, t1env_dyn6.hip);
 # k_post_a / k_post_b only launch on the split (command-curriculum, 1 in 2400) steps
 KERNELS = ["k_dynamics", "k_post_a", "k_post_b"]
-def fused_kernel(num_envs, cus=256):
-    """The step kernel t1env picks (t1_dyn_waves_default): k_dyn6 at every env count; the T1ENV_DYN_KERNEL override
-    wins."""
+def fused_kernel(num_envs, cus=256, obs_half=False):
+    """The step kernel t1env picks (t1_dyn_waves_default): k_dyn6, k_dyn4 for fp16 histories above one round of 32-env
+    workgroups; the T1ENV_DYN_KERNEL override wins."""
     k = os.environ.get("T1ENV_DYN_KERNEL")
     if k in ("4", "5", "6"):
         return "k_dyn" + k
-    return "k_dyn6"
+    return "k_dyn4" if obs_half and (num_envs + 31) // 32 > cus else "k_dyn6"
 # per-kernel algorithmic bytes per env (reads + writes it must do; DESIGN.md §3) for the split sequence
 SHIFT_BYTES = 2 * 4 * ((3102 - 47) + (219 - 73))
 KERNEL_BYTES = {
@@ -90,9 +90,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--cpu-shards", type=int, default=32,
                    help="CPU baseline: env shards stepped on Python threads (at most the affinity's core count)")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r04fi.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r05fa.json"),
                    help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
-    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r04fi_sq_counters.json"),
+    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r05fa_sq_counters.json"),
                    help="SQ instruction counters of the fused kernel (tools/pmc_sq_summary.py): the VALU-issue roofline")
     return p.parse_args()
 
@@ -225,7 +225,7 @@ def main():
     pre_shift = kt["k_shift"]["launches"] > 0
     per_kernel = {}
     cus = torch.cuda.get_device_properties(dev).multi_processor_count if torch.cuda.is_available() else 256
-    FUSED_KERNEL = fused_kernel(N, cus)
+    FUSED_KERNEL = fused_kernel(N, cus, args.state_dtype == "fp16")
     for k in KERNELS + (["k_shift"] if pre_shift else []):
         ms = kt[k]["ms"] / max(1, kt[k]["launches"])
         if k == "k_shift":

@@ -28,8 +28,12 @@ def _make(n, mesh, dtype):
     return make_t1_env(num_envs=n, mesh_type=mesh, seed=4, device="cuda:0", cfg_hook=hook)
 
 
+@pytest.mark.parametrize("kernel", ["6", "4"])
 @pytest.mark.parametrize("n,mesh", [(32768, "heightfield"), (777, "trimesh")], ids=["config5_32768_hf", "ragged777"])
-def test_fp16_histories_equal_rounded_fp32(n, mesh):
+def test_fp16_histories_equal_rounded_fp32(n, mesh, kernel, monkeypatch):
+    # one step kernel for both envs (the default takes k_dyn4 for fp16 histories above one workgroup round, k_dyn6
+    # for fp32: different fp32 summation orders, t1_dyn_waves_default)
+    monkeypatch.setenv("T1ENV_DYN_KERNEL", kernel)
     e32, e16 = _make(n, mesh, "fp32"), _make(n, mesh, "fp16")
     assert e16.obs_buf.dtype == torch.float16 and e32.obs_buf.dtype == torch.float32
     for e in (e32, e16):

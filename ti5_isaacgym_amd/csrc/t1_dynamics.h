@@ -413,8 +413,8 @@ __device__ __forceinline__ void pair_acc_zero(PairAcc& P) {
   for (int k = 0; k < 6; ++k) P.g[k] = t1f2{0.0f, 0.0f};
   P.m = P.hx = P.hy = P.hz = P.sxx = P.syy = P.szz = P.sxy = P.sxz = P.syz = t1f2{0.0f, 0.0f};
 }
-__device__ __forceinline__ void contact_pair(const DynModel& M, const V3<float> x0, const V3<float> x1, const V3<float> n0,
-                                             const V3<float> n1, float pen0, float pen1, bool c0, bool c1,
+__device__ __forceinline__ void contact_pair(const DynModel& M, const V3<float>& x0, const V3<float>& x1, const V3<float>& n0,
+                                             const V3<float>& n1, float pen0, float pen1, bool c0, bool c1,
                                              const float Vb[6], float mu, float vtg, float dt, PairAcc& P,
                                              float& amax) {
   const float k = M.k_contact, d = M.d_contact;

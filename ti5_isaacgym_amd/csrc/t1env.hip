@@ -481,7 +481,7 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
         hipSuccess) cus = 256;
     e->dyn.cus = cus;
-    e->dyn.waves = t1_dyn_waves_default(cfg->num_envs, cus);
+    e->dyn.waves = t1_dyn_waves_default(cfg->num_envs, cus, cfg->obs_half != 0);
     if (const char* dk = getenv("T1ENV_DYN_KERNEL"))  // A/B: 4 = k_dyn4, 5 = k_dyn5, 6 = k_dyn6
       if (atoi(dk) >= 4 && atoi(dk) <= 6) e->dyn.waves = atoi(dk);
     e->dyn.shift_blocks = 0;

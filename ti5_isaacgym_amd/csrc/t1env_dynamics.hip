@@ -622,13 +622,13 @@ __global__ __launch_bounds__(D4_BLOCK) T1_DYN4_ATTR void k_dyn4(const DynModel* 
   T1_PROF_END();
 }
 
-// k_dyn6 at every env count: at 8192 trimesh envs (one round of 32-env workgroups on 256 CUs) k_dyn6 0.127 ms,
-// k_dyn5 0.141, k_dyn4 0.150; above one round k_dyn6's rounds still beat k_dyn4's 64-env workgroups (r05full: 16384
-// trimesh 0.247 vs 0.268 ms, 32768 0.485 vs 0.519).  T1ENV_DYN_KERNEL=4|5|6 overrides (A/B).
-int t1_dyn_waves_default(int num_envs, int cus) {
-  (void)num_envs;
-  (void)cus;
-  return 6;
+// k_dyn6 at 8192 trimesh envs (one round of 32-env workgroups on 256 CUs): 0.127 ms, k_dyn5 0.141, k_dyn4 0.150.
+// Above one round k_dyn6's rounds still beat k_dyn4's 64-env workgroups with fp32 histories (r05full: 16384 trimesh
+// 0.247 vs 0.268 ms, 32768 hf + push 0.485 vs 0.519), but not with fp16 histories, where k_dyn4's stand-alone shift
+// launch halves and k_dyn4's 64 envs per workgroup are the better throughput (r05cfg5: 32768 hf + push 0.437 vs 0.471,
+// 16384 0.216 vs 0.240).  T1ENV_DYN_KERNEL=4|5|6 overrides (A/B).
+int t1_dyn_waves_default(int num_envs, int cus, bool obs_half) {
+  return obs_half && (num_envs + 31) / 32 > cus ? 4 : 6;
 }
 
 constexpr int MIN_SHIFT_BLOCKS = 64;

@@ -36,15 +36,15 @@ constexpr int T1_SHIFT_DELAY_DEFAULT = 3000;
 struct DynLaunch {
   int waves;         // 6: k_dyn6 (t1env_dyn6.hip: 32 envs per workgroup, eight role waves, two per SIMD), 5: k_dyn5
                      //    (t1env_dyn5.hip: 32 envs per workgroup, four roles, in-workgroup history shift), 4: k_dyn4
-                     //    (64 envs per workgroup, leg + contact helper waves); t1_dyn_waves_default picks by env
-                     //    count, T1ENV_DYN_KERNEL=4|5|6 overrides
+                     //    (64 envs per workgroup, leg + contact helper waves); t1_dyn_waves_default picks k_dyn6
+                     //    (k_dyn4 for fp16 histories above one round), T1ENV_DYN_KERNEL=4|5|6 overrides
   int cus;           // compute units of the device (default history-shift grid)
   int shift_blocks;  // > 0: history-shift workgroups override (tuning)
   int shift_delay;   // in-launch shift workgroups start this many 100 MHz ticks late (T1ENV_SHIFT_DELAY; 0 = at once)
   int d5_shift;      // k_dyn5's history shift: 0 = in the workgroup through LDS-DMA (default), 1 = a concurrent launch
                      // on a second stream (k_shift5; T1ENV_D5_SHIFT=1, A/B: the same step time, r04e)
 };
-int t1_dyn_waves_default(int num_envs, int cus);
+int t1_dyn_waves_default(int num_envs, int cus, bool obs_half);
 
 // dynamics launch (t1env_dynamics.hip) plus history-shift workgroups running the shift S; fused != nullptr:
 // the whole step (post-physics in the epilogue).  shift_prelaunched: the caller already enqueued the shift as
