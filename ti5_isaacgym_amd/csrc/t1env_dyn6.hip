@@ -120,14 +120,15 @@ constexpr int SHIFT6_MASK = T1_D6_SHIFT_MASK;  // by role (below)
 #ifndef T1_D6_ROLE_MAP
 #define T1_D6_ROLE_MAP 0x76543210u
 #endif
-__device__ __forceinline__ int role_of(int wave) { return (int)((T1_D6_ROLE_MAP >> (4 * wave)) & 0xFu); }
+__device__ __forceinline__ int role_of(int wave) {
+#ifdef T1_PROBE_ROLE  // register-probe builds only (every wave one role: the others' code compiled out)
+  return T1_PROBE_ROLE;
+#endif
+  return (int)((T1_D6_ROLE_MAP >> (4 * wave)) & 0xFu);
+}
 static_assert((T1_D6_ROLE_MAP & 0xFu) == 0, "the core role is wave 0");
 constexpr int SHIFT6_WAVES = __builtin_popcount(SHIFT6_MASK);
 static_assert((SHIFT6_MASK & 0x11) == 0, "W0 / W4 (the core chain's SIMD) do not shift");
-
-// the fold-in split (T1_D6_FOLD_SPLIT): joint columns 0-2 of the leg block, L (6: sidx(k, j), k <= j <= 2), Bl (18:
-// [r][j]), rhs (3)
-constexpr int FS_NL = 6, FS_NB = 18, FS_N = FS_NL + FS_NB + 3;
 
 struct Dyn6Lds {
   DynModel model;
@@ -148,10 +149,6 @@ struct Dyn6Lds {
   BaseParams<float> pb[64];  // registers held across the substep loop
   float rtf[2][3][64];    // the report: terrain forces on the shank [0] (W2) / foot [1] (W3)
   float rsf[2][3][64];    // the report: self-contact forces on the shank / foot (W5)
-#ifdef T1_D6_FOLD_SPLIT
-  Rows4<FS_N> fs;         // W0 -> W4 -> W0: joint columns 0-2 of the leg block (the CRBA's, then with the terms folded)
-  int fsflag;             // W4 -> W0: the substep (+1) whose folded columns are in fs
-#endif
 };
 
 // ---- the history shift through VGPRs.  Output element e of a row-major history (rows of ROW = F * H) is input element
@@ -380,7 +377,7 @@ __device__ __forceinline__ void contact_half(const DynModel& M, const Terrain& T
 // the joint subspaces (W0's own CRBA rows) per joint, the foot's terms ((points 0-3 + 4-7) + self) for joints 5 and 4,
 // then the shank's, added to them in place for joints 3-0 (Cs = C0 + C1, the same sums), the bias G last.  Every
 // element gets leg_apply_terms' operations in its order (the L, Bl and rhs updates of different joints are independent).
-template <int K0, int K1, int JMIN = 0>
+template <int K0, int K1>
 __device__ __forceinline__ void leg_apply_terms_rows(const Rows4<XCH> (&W)[WC_N], const Rows4<R_N>& W1,
                                                      const float rg[NLEG], const SubspaceRows& SR, int lane,
                                                      LegBlock<float>& out, Sym6<float>& Ac_up, float gc_up[6]) {
@@ -438,126 +435,15 @@ __device__ __forceinline__ void leg_apply_terms_rows(const Rows4<XCH> (&W)[WC_N]
     for (int i = 0; i < 6; ++i) c[i] = c0[i] + c[i];
   }
   joint(kconst<3>{});
-  if constexpr (JMIN <= 2) {  // (T1_D6_FOLD_SPLIT: joints 2-0 on W4, fold_low_columns)
-    joint(kconst<2>{});
-    joint(kconst<1>{});
-    joint(kconst<0>{});
-  }
+  joint(kconst<2>{});
+  joint(kconst<1>{});
+  joint(kconst<0>{});
   sym_add(Ac_up, C);
   float w1v[R_N];
   get4(W1, lane, w1v);
 #pragma unroll
   for (int i = 0; i < 6; ++i) gc_up[i] += w1v[R_G + i] + c[i];
 }
-
-#ifdef T1_D6_FOLD_SPLIT
-// spin until the LDS word *flag equals target (wave-uniform): the poll as one asm block, not a loop of the kernel's
-// (a loop there made the register allocator spill the core wave's leg block around it)
-__device__ __forceinline__ void lds_wait_flag(int* flag, int target) {
-  typedef __attribute__((address_space(3))) int* lds_int_ptr;
-  const uint32_t addr = (uint32_t)(uintptr_t)(lds_int_ptr)flag;
-  int v;
-  asm volatile(
-      "1:\n\t"
-      "ds_read_b32 %0, %1\n\t"
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "v_cmp_eq_u32 vcc, %2, %0\n\t"
-      "s_and_b64 vcc, vcc, exec\n\t"
-      "s_cbranch_vccnz 2f\n\t"
-      "s_sleep 1\n\t"
-      "s_branch 1b\n\t"
-      "2:"
-      : "=&v"(v)
-      : "v"(addr), "s"(target)
-      : "vcc", "scc", "memory");
-}
-// joint columns 0-2 of the leg block <-> FS_N floats
-__device__ __forceinline__ void fs_pack(const LegBlock<float>& lb, float (&v)[FS_N]) {
-  int i = 0;
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-#pragma unroll
-    for (int k = 0; k <= j; ++k) v[i++] = lb.L[sidx(k, j)];
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) v[FS_NL + 3 * r + j] = lb.Bl[r][j];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) v[FS_NL + FS_NB + j] = lb.rhs[j];
-}
-__device__ __forceinline__ void fs_unpack(const float (&v)[FS_N], LegBlock<float>& lb) {
-  int i = 0;
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-#pragma unroll
-    for (int k = 0; k <= j; ++k) lb.L[sidx(k, j)] = v[i++];
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) lb.Bl[r][j] = v[FS_NL + 3 * r + j];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) lb.rhs[j] = v[FS_NL + FS_NB + j];
-}
-// W4 after S2: leg_apply_terms_rows' fold-in of joints 2-0 (every element the same operations in the same order: the
-// columns of different joints are independent) into the CRBA's columns v, from the same LDS rows
-__device__ __forceinline__ void fold_low_columns(const Rows4<XCH> (&W)[WC_N], const float (&rg)[3],
-                                                 const SubspaceRows& SR, int lane, float (&v)[FS_N]) {
-  auto terms = [&](int i, Sym6<float>& Cb, float cb[6]) {
-    float va[XCH];
-    get4(W[2 * i], lane, va);
-    {
-      float vb[XCH];
-      get4(W[2 * i + 1], lane, vb);
-#pragma unroll
-      for (int k = 0; k < XCH; ++k) va[k] = va[k] + vb[k];
-    }
-    {
-      float vs[XCH];
-      get4(W[WC_SSH + i], lane, vs);
-#pragma unroll
-      for (int k = 0; k < XCH; ++k) va[k] = va[k] + vs[k];
-    }
-    sym_unpack(va, Cb, cb);
-  };
-  auto subspace = [&](int k, float (&Sk)[6]) {
-    const float4 x = SR.r[k][0][lane], y = SR.r[k][1][lane];
-    Sk[0] = x.x; Sk[1] = x.y; Sk[2] = x.z; Sk[3] = x.w; Sk[4] = y.x; Sk[5] = y.y;
-  };
-  Sym6<float> C;
-  float c[6];
-  terms(1, C, c);
-  {
-    Sym6<float> C0;
-    float c0[6];
-    terms(0, C0, c0);
-#pragma unroll
-    for (int i = 0; i < 21; ++i) C.a[i] = C0.a[i] + C.a[i];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) c[i] = c0[i] + c[i];
-  }
-  auto joint = [&](auto jc) {
-    constexpr int jj = decltype(jc)::value;
-    constexpr int L0 = jj * (jj + 1) / 2;  // v's first L entry of column jj (k = 0 .. jj)
-    float Sj[6], u[6];
-    subspace(jj, Sj);
-    sym_mul(C, Sj, u);
-    const float sc = dot6(Sj, c);
-    v[L0 + jj] += dot6(Sj, u);
-    v[FS_NL + FS_NB + jj] += rg[jj] - sc;
-#pragma unroll
-    for (int k = 0; k < jj; ++k) {
-      float Sk[6];
-      subspace(k, Sk);
-      v[L0 + k] += dot6(Sk, u);
-    }
-#pragma unroll
-    for (int r = 0; r < 6; ++r) v[FS_NL + 3 * r + jj] += u[r];
-  };
-  joint(kconst<2>{});
-  joint(kconst<1>{});
-  joint(kconst<0>{});
-}
-#endif
 
 // The state after substep s, recorded by W6 (it reads that state at the next S1, the last one after R1): the sensor-lag
 // samples the next observation reads (the joint state at substep 9 - lag % 10, the raw IMU sample likewise) into LDS,
@@ -745,20 +631,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       T1_PROF_MARK(2);
       __syncthreads();  // S2: the terms published
       T1_PROF_MARK(3);
-#ifdef T1_D6_FOLD_SPLIT
-      {  // joints 2-0 of the fold-in (W0 folds 5-3 meanwhile): rg as W0 forms it, from the same rows.  The lane
-         // through an empty asm: the rows' addresses are formed here, not hoisted out of the loop (and spilled)
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const float4 t0 = lds.wb.r[0][ln], g0 = lds.w1.r[0][ln];
-        const float rg[3] = {dt * t0.x + g0.x, dt * t0.y + g0.y, dt * t0.z + g0.z};
-        float v[FS_N];
-        get4(lds.fs, ln, v);
-        fold_low_columns(lds.wc, rg, lds.sj, ln, v);
-        put4(lds.fs, ln, v);
-        if (ln == 0) __hip_atomic_store(&lds.fsflag, sub + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-#endif
     }
     float tau[8];  // the last substep's torques, from the wb rows
     {
@@ -1065,9 +937,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   float vi_sh = B.contact_vimp[(size_t)n * NVIMP + vimp_shank(leg)];
   lds.vift[lane] = vi_ft;
   lds.vish[lane] = vi_sh;
-#ifdef T1_D6_FOLD_SPLIT
-  if (lane == 0) lds.fsflag = 0;  // before the first S1
-#endif
   T1_PROF_MARK(0);
   for (int sub = 0; sub < nsub; ++sub) {
     __syncthreads();  // S1: the substep state published
@@ -1097,13 +966,6 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         lds.sj.r[k][0][lane_s] = make_float4(Sj[k][0], Sj[k][1], Sj[k][2], Sj[k][3]);
         lds.sj.r[k][1][lane_s] = make_float4(Sj[k][4], Sj[k][5], 0.0f, 0.0f);
       }
-#ifdef T1_D6_FOLD_SPLIT
-      {  // joint columns 0-2 to W4, which folds their terms in after S2
-        float v[FS_N];
-        fs_pack(lb, v);
-        put4(lds.fs, lane_s, v);
-      }
-#endif
     }
     T1_PROF_MARK(2);
     __syncthreads();  // S2: the terms published
@@ -1124,18 +986,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
 #pragma unroll
       for (int k = 0; k < NLEG; ++k) rg[k] = dt * tv[k] + gv[k];
 #ifndef T1_WHATIF_D6_NO_FOLDIN  // timing-only what-if build: the contact / bias terms not folded in
-#ifndef T1_D6_FOLD_SPLIT
       leg_apply_terms_rows<K_SHANK, K_FOOT>(lds.wc, lds.w1, rg, lds.sj, lane_s, lb, Ab, g6);
-#else
-      leg_apply_terms_rows<K_SHANK, K_FOOT, 3>(lds.wc, lds.w1, rg, lds.sj, lane_s, lb, Ab, g6);
-      // joints 2-0 folded by W4 (fold_low_columns): wait for its columns of this substep
-      lds_wait_flag(&lds.fsflag, sub + 1);
-      {
-        float v[FS_N];
-        get4(lds.fs, lane_s, v);
-        fs_unpack(v, lb);
-      }
-#endif
 #else
       for (int k = 0; k < NLEG; ++k) lb.rhs[k] += rg[k];
 #endif
