@@ -42,6 +42,10 @@
 #define T1_CONTACT_ONE_COPY
 #endif
 
+#ifdef T1_PROBE_SIMD
+// probe build only: the hardware placement of every wave of the last launch (HW_ID: SIMD, CU, SE), [block][wave]
+__device__ unsigned g_t1_simd6[4096][8];
+#endif
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py --kernel 6): lane 0 of every wave accumulates shader-clock deltas
 // between T1_PROF_MARK points into per-phase buckets; never part of the product build.
 #ifdef T1_PHASE_PROF
@@ -498,6 +502,9 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   const t1env_config& C = *Cp;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / 64);
   const int role = role_of(wave);
+#ifdef T1_PROBE_SIMD
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) g_t1_simd6[blockIdx.x][wave] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+#endif
   const int lane = threadIdx.x & 63;
   const int leg = lane >> 5;
   const int e = lane & 31;
@@ -1072,6 +1079,12 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   }
   T1_PROF_END();
 }
+
+#ifdef T1_PROBE_SIMD
+extern "C" int t1env_debug_simd6(unsigned* out, int blocks) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_simd6), sizeof(unsigned) * 8 * (size_t)blocks);
+}
+#endif
 
 #ifdef T1_PHASE_PROF
 // profiling build only: summed clock deltas per [wave][bucket] since the last reset
