@@ -80,7 +80,7 @@ def test_env_refuses_cpu_device():
 def test_policy_header_exports(lib):
     """include/t1policy.h's entry points are exported by the same library, and _lib binds them."""
     src = open(os.path.join(REPO, "include", "t1policy.h")).read()
-    names = sorted(set(re.findall(r"^\s*int\s+(t1policy_\w+)\s*\(", src, re.M)))
+    names = sorted(set(re.findall(r"^\s*(?:int|long long)\s+(t1policy_\w+)\s*\(", src, re.M)))
     from ti5_isaacgym_amd import _lib
     assert names == sorted(_lib.POLICY_EXPORTS) and names
     for n in names:
@@ -90,6 +90,8 @@ def test_policy_header_exports(lib):
     assert lib.t1policy_conv1d_forward_packed(None, None, None, None, 1, 66, 47, 32, 6, 3, None) == -1
     assert lib.t1policy_conv1d_pack_weights(None, None, 66, 32, 6, None) == -1
     assert lib.t1policy_conv1d_frag_bytes() == 17 * 2 * 2 * 64 * 16
+    assert lib.t1policy_linear_wgrad_workspace_bytes(0, 4, 4) == -1
+    assert lib.t1policy_linear_wgrad_bf16(None, None, 8, 4, 4, None, 0, None, None, None) == -1
     # fused heads: 1,768 step-tiles (32 outputs x 16 inputs) of hi + lo fragments, 90 output tiles of bias
     assert lib.t1policy_heads_frag_bytes() == 1768 * 2 * 64 * 16 + 90 * 4 * 64 * 16   # + the bias fragments
     assert lib.t1policy_heads_pack(None, None, None, None) == -1

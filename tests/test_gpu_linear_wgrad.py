@@ -1,0 +1,98 @@
+"""The bf16 update's Linear weight + bias gradients as one HIP MFMA kernel (t1policy_linear_wgrad_bf16,
+ti5_isaacgym_amd/csrc/t1policy_wgrad.hip; dh_policy._LinearSplitK.backward) against fp64 torch on the same bf16
+operands -- needs the MI355X.
+
+Bound: the kernel sums exact bf16 products in fp32 (MFMA accumulation over a slice's rows, then the slices in order),
+so each output is within a few hundred fp32 roundings of |gy|^T |x|: the test holds it to 1e-5 of that magnitude sum
+(about 170 ulps), element by element.  Determinism: a second call gives the same bits (the graphed == eager update
+relies on it)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+# (rows, M = outputs, N = inputs): the update's layers at the 49,152-row minibatch (the odd widths take the 16-bit
+# load path: the state estimator's 235 inputs, the critic's 219, the estimator head's 3 outputs, the value head's 1),
+# the second conv as a GEMM (294,912 rows), and ragged / tiny shapes
+SHAPES = [(49152, 768, 219), (49152, 256, 235), (49152, 512, 302), (49152, 3, 64), (49152, 1, 128),
+          (294912, 16, 128), (49152, 256, 768), (1000, 12, 128), (31, 5, 7), (4097, 130, 97), (64, 300, 2)]
+
+
+def _operands(rows, M, N, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    gy = (torch.randn(rows, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(rows, N, device=DEV, generator=g).to(torch.bfloat16)
+    return gy, x
+
+
+def _check(gw, gb, gy, x):
+    gyd, xd = gy.double(), x.double()
+    ref_w = gyd.t() @ xd
+    mag_w = gyd.abs().t() @ xd.abs()
+    err = (gw.double() - ref_w).abs()
+    assert (err <= 1e-5 * mag_w + 1e-30).all(), float((err / (mag_w + 1e-30)).max())
+    if gb is not None:
+        ref_b = gyd.sum(0)
+        mag_b = gyd.abs().sum(0)
+        errb = (gb.double() - ref_b).abs()
+        assert (errb <= 1e-5 * mag_b + 1e-30).all(), float((errb / (mag_b + 1e-30)).max())
+
+
+@pytest.mark.parametrize("rows,M,N", SHAPES)
+def test_linear_wgrad_matches_fp64(rows, M, N):
+    from ti5_isaacgym_amd.algo.dh_policy import linear_wgrad_bf16
+    gy, x = _operands(rows, M, N, rows + 7 * M + N)
+    gw, gb = linear_wgrad_bf16(gy, x)
+    assert gw.shape == (M, N) and gw.dtype == torch.float32 and gb.shape == (M,) and gb.dtype == torch.float32
+    _check(gw, gb, gy, x)
+    gw2, gb2 = linear_wgrad_bf16(gy, x)
+    assert torch.equal(gw, gw2) and torch.equal(gb, gb2)
+    gw3, gb3 = linear_wgrad_bf16(gy, x, need_bias=False)   # no bias: the same weight gradient
+    assert gb3 is None and torch.equal(gw3, gw)
+
+
+def test_linear_wgrad_rounds_fp32_inputs_to_bf16():
+    """An fp32 saved input is rounded to bf16 first, as autocast's GEMM would round it."""
+    from ti5_isaacgym_amd.algo.dh_policy import linear_wgrad_bf16
+    gy, _ = _operands(5000, 64, 1, 3)
+    x = torch.randn(5000, 235, device=DEV)
+    gw, _ = linear_wgrad_bf16(gy, x)
+    gw16, _ = linear_wgrad_bf16(gy, x.to(torch.bfloat16))
+    assert torch.equal(gw, gw16)
+
+
+def test_linear_backward_uses_the_kernel_under_bf16_autocast(monkeypatch):
+    """A Linear of the policy under the bf16 update's autocast: the kernel's gradients (fp32, within the fp64 bound of
+    the bf16 operands autograd saved) and the split-K path's agree to bf16-GEMM precision."""
+    from ti5_isaacgym_amd.algo import dh_policy
+    torch.manual_seed(0)
+    lin = dh_policy.Linear(302, 512).to(DEV)
+    x = torch.randn(49152, 302, device=DEV).to(torch.bfloat16)
+    g = torch.randn(49152, 512, device=DEV).to(torch.bfloat16) * 0.01
+
+    def grads(flag):
+        monkeypatch.setattr(dh_policy, "LINEAR_WGRAD", flag)
+        lin.weight.grad = lin.bias.grad = None
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+            y = lin(x)
+        y.backward(g)
+        return lin.weight.grad.clone(), lin.bias.grad.clone()
+
+    gw, gb = grads(True)
+    _check(gw, gb, g, x)
+    gw0, gb0 = grads(False)
+    torch.testing.assert_close(gw, gw0, rtol=1e-2, atol=1e-3 * gw0.abs().max().item())
+    torch.testing.assert_close(gb, gb0, rtol=1e-2, atol=1e-3 * gb0.abs().max().item())
+
+
+def test_linear_wgrad_rejects_bad_arguments():
+    from ti5_isaacgym_amd import _lib
+    lib = _lib.load()
+    assert lib.t1policy_linear_wgrad_workspace_bytes(0, 4, 4) == -1
+    gy, x = _operands(64, 8, 8, 1)
+    ws = torch.empty(16, device=DEV, dtype=torch.uint8)
+    gw = torch.empty(8, 8, device=DEV)
+    # a workspace smaller than workspace_bytes is refused, not overrun
+    assert lib.t1policy_linear_wgrad_bf16(gy.data_ptr(), x.data_ptr(), 64, 8, 8, ws.data_ptr(), 16, gw.data_ptr(),
+                                          None, torch.cuda.current_stream().cuda_stream) == -1

@@ -116,6 +116,36 @@ def bias_grad(gy):
     return out
 
 
+# the bf16 update's Linear weight + bias gradients as one HIP MFMA kernel (t1policy_linear_wgrad_bf16); T1_LINEAR_WGRAD=0:
+# the split-K batched GEMM + slice sum + torch's bias sum (A/B)
+LINEAR_WGRAD = os.environ.get("T1_LINEAR_WGRAD", "1") != "0"
+
+
+def linear_wgrad_bf16(gy, x, need_bias=True):
+    """(gy^T x, gy.sum(0)) in fp32 for bf16 gy (K, M) and x (K, N) (x in fp32 is rounded to bf16 first, as autocast's
+    GEMM would): the HIP wgrad kernel, fixed-order fp32 sums of the exact bf16 products.  Device tensors only."""
+    from .. import _lib
+    lib = _lib.load()
+    gy = gy.contiguous()
+    x = (x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)).contiguous()
+    K, M = gy.shape
+    N = x.shape[1]
+    if x.shape[0] != K:
+        raise ValueError(f"linear_wgrad_bf16: {K} gradient rows against {x.shape[0]} input rows")
+    nbytes = lib.t1policy_linear_wgrad_workspace_bytes(K, M, N)
+    if nbytes <= 0:
+        raise RuntimeError(f"t1policy_linear_wgrad_workspace_bytes failed ({nbytes})")
+    ws = torch.empty(nbytes, device=gy.device, dtype=torch.uint8)
+    gw = torch.empty(M, N, device=gy.device, dtype=torch.float32)
+    gb = torch.empty(M, device=gy.device, dtype=torch.float32) if need_bias else None
+    rc = lib.t1policy_linear_wgrad_bf16(gy.data_ptr(), x.data_ptr(), K, M, N, ws.data_ptr(), nbytes, gw.data_ptr(),
+                                        gb.data_ptr() if gb is not None else None,
+                                        torch.cuda.current_stream(gy.device).cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"t1policy_linear_wgrad_bf16 failed (rc={rc})")
+    return gw, gb
+
+
 class _LinearSplitK(torch.autograd.Function):
     # custom_fwd / custom_bwd: under torch.autocast (the opt-in bf16 update) the GEMMs run in the autocast dtype in
     # both passes; autograd casts the returned gradients to the fp32 parameters' dtype
@@ -131,6 +161,9 @@ class _LinearSplitK(torch.autograd.Function):
         x, w = ctx.saved_tensors
         gy = gy.contiguous()
         gx = gy.mm(w) if ctx.needs_input_grad[0] else None
+        if LINEAR_WGRAD and gy.is_cuda and gy.dtype == torch.bfloat16 and ctx.needs_input_grad[1]:
+            gw, gb = linear_wgrad_bf16(gy, x, need_bias=ctx.needs_input_grad[2])
+            return gx, gw, gb
         gw = wgrad_splitk(gy, x) if ctx.needs_input_grad[1] else None
         gb = bias_grad(gy) if ctx.needs_input_grad[2] else None
         return gx, gw, gb

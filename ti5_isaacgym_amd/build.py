@@ -14,7 +14,8 @@ CSRC = os.path.join(HERE, "csrc")
 # model-pointer loads; the -O3 guard build (OUT_O3) keeps every level under the fp64 check.
 UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1"), ("t1env_dyn5.hip", "-O1"), ("t1env_dyn6.hip", "-O1"),
          ("t1policy.hip", "-O3"),
-         ("t1policy_heads.hip", "-O3"), ("t1policy_train.hip", "-O3")]
+         ("t1policy_heads.hip", "-O3"), ("t1policy_train.hip", "-O3"),
+         ("t1policy_wgrad.hip", "-O3")]
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
 # guard build: the dynamics unit at -O3 (tests/test_gpu_opt_levels.py keeps it under the fp64 dynamics check)
 OUT_O3 = os.path.join(HERE, "_lib", "var", "libt1env_hip_dyn_o3.so")

@@ -9,7 +9,8 @@
 // plus the Normal sample, its log-prob and the broadcast sigma (DHPPO._act_body), from the first conv's output
 // (t1policy_conv1d_forward_packed), the actor and critic observations and a standard-normal draw.
 //
-// A workgroup owns 32 envs and one role (actor chain or critic); every layer is a chain of
+// A workgroup owns 32 envs and one role (actor chain or critic), eight waves (two per SIMD) splitting each layer's
+// 32-output tiles; every layer is a chain of
 // v_mfma_f32_32x32x16_f16 with the WEIGHTS as the A operand (32 output features x 16 inputs) and the ACTIVATIONS as
 // the B operand (16 inputs x 32 envs), so a layer's 32 x 32 result has the env on the lane and the features in the
 // 16 accumulator registers -- exactly the B fragments of the next layer's two k-steps (permuted k order, cdna guide
@@ -39,7 +40,12 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr float PH_SPLIT = 2048.0f;
 constexpr int PH_M = 32;      // envs per workgroup (one MFMA column tile)
-constexpr int PH_WAVES = 4;
+// waves per workgroup: 8 = two per SIMD, each with half the output tiles and a shallower fragment ring (act() 0.177 ->
+// 0.147 ms at 8192 envs, profiles/r05h8_*); 4 = one per SIMD, the round-4 kernel (A/B)
+#ifndef T1_HEADS_WAVES
+#define T1_HEADS_WAVES 8
+#endif
+constexpr int PH_WAVES = T1_HEADS_WAVES;
 constexpr int PH_OBS_SHORT = 235, PH_CRITIC = 219, PH_Y1 = 14 * 32;
 constexpr int PH_NLAYER = 15;
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2 };
@@ -263,15 +269,17 @@ struct PhOut {  // the global outputs (OUT_MEAN / OUT_VALUE layers)
   bool live;
 };
 
-// one dense layer for this wave's output tiles nt = wave + 4 i: B fragments from `in` (LDS), A fragments streamed
+// one dense layer for this wave's output tiles nt = wave + PH_WAVES i: B fragments from `in` (LDS), A fragments streamed
 // from the packed buffer, result + bias through the activation into `out` (LDS, k-steps out0 + 2 nt + {0, 1}) or the
-// global outputs.  Waves past the layer's tile count recompute the last tile and store nothing.
+// global outputs.  Waves past the layer's tile count skip the products and store nothing.
 // the weight-fragment register ring of layer L: its loads run D k-steps ahead of their MFMAs through D + 1 slots
 // (about 16 x 96 MFMA cycles of cover over an L2 hit under load); its first D steps are issued during the previous
 // layer (ph_prologue), so no layer starts on an empty pipeline
 template <int L> struct PhRing {
   static constexpr int NT = ph_nt(L), KS = PH_L[L].ks, T = (NT + PH_WAVES - 1) / PH_WAVES;
-  static constexpr int D0 = T >= 4 ? 4 : (T >= 2 ? 8 : 16);
+  // two waves per SIMD (PH_WAVES 8): the other wave covers part of the latency, and 256 VGPRs hold the accumulators
+  // and a ring of 2-8 steps without spills (4 waves: 512 registers, 4-16 steps)
+  static constexpr int D0 = PH_WAVES == 8 ? (T >= 3 ? 2 : (T >= 2 ? 4 : 8)) : (T >= 4 ? 4 : (T >= 2 ? 8 : 16));
   static constexpr int D = D0 < KS ? D0 : KS - 1;
   static constexpr int R = D + 1;
   h8 w[R][T][2];
@@ -299,10 +307,11 @@ __device__ __forceinline__ void ph_prologue(const h8* __restrict__ frag, PhRing<
   for (int s = 0; s < PhRing<L>::D; ++s) ph_load<L>(frag, rg, s, s, wave, lane);
 }
 
-// one dense layer for this wave's output tiles nt = wave + 4 i: B fragments from `in` (LDS), A fragments through
+// one dense layer for this wave's output tiles nt = wave + PH_WAVES i: B fragments from `in` (LDS), A fragments through
 // the ring rg (prologue already issued), result + bias through the activation into `out` (LDS, k-steps
 // out0 + 2 nt + {0, 1}) or the global outputs.  LN >= 0: layer LN's prologue is issued into *nx before this layer's
-// epilogue.  Waves past the layer's tile count recompute the last tile and store nothing.
+// epilogue.  Waves past the layer's tile count (8 waves, layers of < 8 tiles) skip the products and store nothing;
+// at 4 waves every layer has a tile per wave except the narrow heads, whose spare waves recompute the last tile.
 template <int L, int OUT, int LN>
 __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhParams& P, const Frag* in, Frag* out,
                                          int out0, const PhOut& G, int wave, int lane, PhRing<L>& rg,
@@ -320,6 +329,8 @@ __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhPa
   h8 bq[2][2];
   bq[0][0] = in[0][0][lane];
   bq[0][1] = in[0][1][lane];
+  // a wave past the layer's tile count (PH_WAVES 8 on the narrow layers) skips the K loop (it stores nothing)
+  if (PH_WAVES == 4 || wave < NT)
 #pragma clang loop unroll(full)
   for (int s = 0; s < KS; ++s) {
     if (s + D < KS) ph_load<L>(frag, rg, (s + D) % R, s + D, wave, lane);
@@ -400,7 +411,7 @@ __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhPa
   }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ __launch_bounds__(64 * PH_WAVES) __attribute__((amdgpu_waves_per_eu(PH_WAVES / 4, PH_WAVES / 4)))
 void k_heads(PhParams P, const h8* __restrict__ frag, const float* __restrict__ y1, const float* __restrict__ obs,
              int obs_cols, const float* __restrict__ cobs, int cobs_cols, PhOut G, int batch, int xcd_split) {
   __shared__ PhLds S;

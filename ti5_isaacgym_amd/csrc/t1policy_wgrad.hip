@@ -1,0 +1,271 @@
+// The PPO update's Linear weight and bias gradients under the opt-in bf16 update (include/t1policy.h,
+// t1policy_linear_wgrad_bf16): gW = gy^T x and gb = sum_r gy[r] for a batch of rows, in one MFMA kernel plus one
+// fixed-order reduction -- what loss.backward() computes for every nn.Linear of the policy (dh_ppo.py:180,
+// actor_critic_dh.py:45-111), at the update's 49,152-row minibatch.
+//
+// The build's path before this (dh_policy.wgrad_splitk + bias_grad): a hipBLASLt strided-batched GEMM over 24 slices
+// of 2,048 rows, the slices summed by t1policy_slice_sum, and torch's dim-0 sum for the bias -- three launches per
+// layer and 10 ms of device time per update (bmm 5.4 ms + sums 4.7 ms, profiles/r04q_ppo_update_profile_bf16_eager.txt)
+// for ~0.7 TFLOP.
+//
+// Both operands are row-major with the REDUCTION (the batch row) as their slow index, so the MFMA fragments -- a lane
+// holds 8 consecutive k of one output row / column -- are columns of the staged tiles: each 32-row chunk of gy and x is
+// staged into LDS row-major as loaded (coalesced dword loads; 16-bit loads for an odd width), and the fragments come
+// back with ds_read_b64_tr_b16 (the gfx950 transposing LDS read: a 16-lane group reads 4 rows x 16 columns and gets
+// the columns in its lanes).  A workgroup owns a 128 x 128 output tile and a slice of rows; its four waves own 64 x 64
+// quarters (2 x 2 v_mfma_f32_32x32x16_bf16 accumulators).  The bias sum rides on the A fragments of the n-tile-0
+// workgroups.  Partials go to a workspace [slice][M x N | M]; k_wgrad_reduce sums the slices in order s = 0, 1, ...,
+// so the result is deterministic (eager and graph-replayed updates stay bit-identical).  Products of bf16 operands are
+// exact in fp32; the sums are fp32.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int WG_T = 128;             // output tile (m and n)
+constexpr int WG_ROWS = 32;           // rows per staged chunk (two k-steps of 16)
+constexpr int WG_PITCH = WG_T + 32;   // LDS row pitch in 16-bit elements: 320 B, rows 16 banks apart (conflict-free
+                                      // transposed reads: a 32-lane half's two groups x 4 rows cover the 64 banks once)
+constexpr int WG_IMG = WG_ROWS * WG_PITCH;  // one staged operand chunk (elements)
+constexpr int WG_MIN_ROWS = 256;      // rows per slice at least
+
+__device__ __forceinline__ float bf16_float(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
+
+// a 32-row chunk of columns [c0, c0 + 128) of a (rows, W) bf16 matrix in registers: thread t holds the column pair
+// 2 (t & 63) of rows (t >> 6) + 4 i, zero past the width or the slice end
+template <bool PAIR>
+__device__ __forceinline__ void wg_load(const uint16_t* __restrict__ z, int W, int c0, int r0, int r1, int t,
+                                        uint32_t (&v)[8]) {
+  const int col = c0 + 2 * (t & 63);
+  const bool c_ok = col < W, c1_ok = col + 1 < W;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = r0 + (t >> 6) + 4 * i;
+    const uint16_t* p = z + (size_t)r * W + col;
+    uint32_t u = 0u;
+    if (r < r1) {
+      if constexpr (PAIR) {  // W even: the pair is one aligned dword
+        if (c_ok) u = *reinterpret_cast<const uint32_t*>(p);
+      } else {
+        if (c_ok) u = p[0];
+        if (c1_ok) u |= (uint32_t)p[1] << 16;
+      }
+    }
+    v[i] = u;
+  }
+}
+
+__device__ __forceinline__ void wg_store(uint32_t* img, int t, const uint32_t (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) img[((t >> 6) + 4 * i) * (WG_PITCH / 2) + (t & 63)] = v[i];
+}
+
+// the 32 x 16 (A) or 16 x 32 (B) fragment of k-step ks for columns [col0, col0 + 32) of a staged chunk: lane
+// (r = l & 31, h = l >> 5) gets rows 16 ks + 8 h + j, j = 0 .. 7, of column col0 + r -- two transposed reads of
+// 4 rows each (lane 4 q + p of a 16-lane group addresses row q, columns 4 p .. 4 p + 3 of its 16-column block)
+__device__ __forceinline__ bf8 wg_frag(const uint16_t* img, int ks, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, h = g >> 1;
+  const int row = 16 * ks + 8 * h + (i >> 2);
+  const int col = col0 + 16 * (g & 1) + 4 * (i & 3);
+  typedef __attribute__((address_space(3))) s4 lds_s4;
+  const uint16_t* p = img + row * WG_PITCH + col;
+  const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p));
+  const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p + 4 * WG_PITCH));
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  const s8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf8, v);
+}
+
+// grid: x = output tile (tm + tiles_m tn), y = slice of rows_per_slice rows.  part: [slice][M][N], bpart: [slice][M]
+template <bool GY_PAIR, bool X_PAIR>
+__global__ __launch_bounds__(256, 2) void k_linear_wgrad_bf16(const uint16_t* __restrict__ gy,
+                                                              const uint16_t* __restrict__ x, int rows, int M, int N,
+                                                              int tiles_m, int rows_per_slice,
+                                                              float* __restrict__ part, float* __restrict__ bpart) {
+  __shared__ __attribute__((aligned(16))) uint16_t IMG[2][2][WG_IMG];  // [buffer][gy, x]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, h = lane >> 5;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int tm = blockIdx.x % tiles_m, tn = blockIdx.x / tiles_m, s = blockIdx.y;
+  const int m0 = WG_T * tm, n0 = WG_T * tn;
+  const int r0 = s * rows_per_slice;
+  const int r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
+  // this wave's 32-wide blocks that hold outputs (wave-uniform)
+  const int m_rem = M - (m0 + 64 * wm), n_rem = N - (n0 + 64 * wn);
+  const int mb_n = m_rem <= 0 ? 0 : (m_rem > 32 ? 2 : 1), nb_n = n_rem <= 0 ? 0 : (n_rem > 32 ? 2 : 1);
+  const bool bias = bpart != nullptr && tn == 0 && wn == 0;  // (nb_n >= 1 there)
+  f16v acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+  float bsum[2] = {0.0f, 0.0f};
+  uint32_t vg[8], vx[8];
+  wg_load<GY_PAIR>(gy, M, m0, r0, r1, t, vg);
+  wg_load<X_PAIR>(x, N, n0, r0, r1, t, vx);
+  int buf = 0;
+  for (int c = r0; c < r1; c += WG_ROWS, buf ^= 1) {
+    wg_store(reinterpret_cast<uint32_t*>(IMG[buf][0]), t, vg);
+    wg_store(reinterpret_cast<uint32_t*>(IMG[buf][1]), t, vx);
+    if (c + WG_ROWS < r1) {  // the next chunk's loads in flight behind this chunk's products
+      wg_load<GY_PAIR>(gy, M, m0, c + WG_ROWS, r1, t, vg);
+      wg_load<X_PAIR>(x, N, n0, c + WG_ROWS, r1, t, vx);
+    }
+    __syncthreads();  // staged; double-buffered, so the chunk before last's readers are done
+    if (mb_n > 0 && nb_n > 0) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf8 fa[2], fb[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) fa[a] = wg_frag(IMG[buf][0], ks, 64 * wm + 32 * a, lane);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) fb[b] = wg_frag(IMG[buf][1], ks, 64 * wn + 32 * b, lane);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          if (a >= mb_n) break;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if (b >= nb_n) break;
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+          }
+          if (bias) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bsum[a] += (float)fa[a][j];
+          }
+        }
+      }
+    }
+  }
+  // C/D: column n = lane & 31, row m = (r & 3) + 8 (r >> 2) + 4 h
+  float* P = part + (size_t)s * M * N;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    if (a >= mb_n) break;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if (b >= nb_n) break;
+      const int n = n0 + 64 * wn + 32 * b + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 64 * wm + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M && n < N) P[(size_t)m * N + n] = acc[a][b][r];
+      }
+    }
+  }
+  if (bias) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      if (a >= mb_n) break;
+      const float v = bsum[a] + __shfl_xor(bsum[a], 32);  // the two row halves of column m, in a fixed order
+      const int m = m0 + 64 * wm + 32 * a + (lane & 31);
+      if (h == 0 && m < M) bpart[(size_t)s * M + m] = v;
+    }
+  }
+}
+
+// gW[i] = sum_s part[s][i] (i < M N) and gb[m] = sum_s bpart[s][m], s = 0, 1, ... in order
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, const float* __restrict__ bpart,
+                                                      int slices, int mn, int m, float* __restrict__ gw,
+                                                      float* __restrict__ gb) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool w = e < mn;
+  if (!w && (gb == nullptr || e >= mn + m)) return;
+  const float* src = w ? part + e : bpart + (e - mn);
+  const size_t stride = w ? (size_t)mn : (size_t)m;
+  float acc = 0.0f;
+  int k = 0;
+  for (; k + 8 <= slices; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(k + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; k < slices; ++k) acc += src[(size_t)k * stride];
+  if (w) gw[e] = acc;
+  else gb[e - mn] = acc;
+}
+
+struct WgPlan {
+  int tiles_m, tiles, slices, rows_per_slice;
+};
+
+WgPlan wg_plan(int rows, int M, int N, int cus) {
+  WgPlan p;
+  p.tiles_m = (M + WG_T - 1) / WG_T;
+  p.tiles = p.tiles_m * ((N + WG_T - 1) / WG_T);
+  // about two workgroups per CU, slices of at least WG_MIN_ROWS rows, a multiple of the chunk
+  const int want = (2 * cus + p.tiles - 1) / p.tiles;
+  const int most = (rows + WG_MIN_ROWS - 1) / WG_MIN_ROWS;
+  int sl = want < most ? want : most;
+  if (sl < 1) sl = 1;
+  int rps = (rows + sl - 1) / sl;
+  rps = (rps + WG_ROWS - 1) / WG_ROWS * WG_ROWS;
+  p.rows_per_slice = rps;
+  p.slices = (rows + rps - 1) / rps;
+  return p;
+}
+
+int wg_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return -1;
+  return cus;
+}
+
+}  // namespace
+
+extern "C" {
+
+long long t1policy_linear_wgrad_workspace_bytes(int rows, int M, int N) {
+  if (rows <= 0 || M <= 0 || N <= 0) return -1;
+  const int cus = wg_cus();
+  if (cus <= 0) return -2;
+  const WgPlan p = wg_plan(rows, M, N, cus);
+  return (long long)p.slices * ((long long)M * N + M) * 4;
+}
+
+int t1policy_linear_wgrad_bf16(const void* gy, const void* x, int rows, int M, int N, void* workspace,
+                               long long workspace_bytes, float* grad_weight, float* grad_bias, void* stream) {
+  if (!gy || !x || !workspace || !grad_weight || rows <= 0 || M <= 0 || N <= 0) return -1;
+  if ((reinterpret_cast<uintptr_t>(gy) & 3u) != 0 || (reinterpret_cast<uintptr_t>(x) & 3u) != 0 ||
+      (reinterpret_cast<uintptr_t>(workspace) & 15u) != 0)
+    return -1;
+  if ((long long)M * N >= (1LL << 31) - M) return -1;
+  const int cus = wg_cus();
+  if (cus <= 0) return -2;
+  const WgPlan p = wg_plan(rows, M, N, cus);
+  if (workspace_bytes < (long long)p.slices * ((long long)M * N + M) * 4) return -1;
+  float* part = reinterpret_cast<float*>(workspace);
+  float* bpart = grad_bias ? part + (size_t)p.slices * M * N : nullptr;
+  const dim3 grid(p.tiles, p.slices);
+  const uint16_t* g16 = reinterpret_cast<const uint16_t*>(gy);
+  const uint16_t* x16 = reinterpret_cast<const uint16_t*>(x);
+  const bool gp = (M & 1) == 0, xp = (N & 1) == 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (gp && xp)
+    hipLaunchKernelGGL((k_linear_wgrad_bf16<true, true>), grid, dim3(256), 0, st, g16, x16, rows, M, N, p.tiles_m,
+                       p.rows_per_slice, part, bpart);
+  else if (gp)
+    hipLaunchKernelGGL((k_linear_wgrad_bf16<true, false>), grid, dim3(256), 0, st, g16, x16, rows, M, N, p.tiles_m,
+                       p.rows_per_slice, part, bpart);
+  else if (xp)
+    hipLaunchKernelGGL((k_linear_wgrad_bf16<false, true>), grid, dim3(256), 0, st, g16, x16, rows, M, N, p.tiles_m,
+                       p.rows_per_slice, part, bpart);
+  else
+    hipLaunchKernelGGL((k_linear_wgrad_bf16<false, false>), grid, dim3(256), 0, st, g16, x16, rows, M, N, p.tiles_m,
+                       p.rows_per_slice, part, bpart);
+  const int total = M * N + (grad_bias ? M : 0);
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + 255) / 256), dim3(256), 0, st, part, bpart, p.slices, M * N, M,
+                     grad_weight, grad_bias);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+"""Per-layer timing of the bf16 update's Linear weight + bias gradients: the HIP kernel (t1policy_linear_wgrad_bf16)
+against the split-K batched GEMM + slice sum + torch's bias sum it replaces, on the update's layer shapes at the
+49,152-row minibatch.  Prints one JSON line.
+
+    python tools/wgrad_bench.py [--reps 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ti5_isaacgym_amd.algo import dh_policy  # noqa: E402
+
+# (rows, outputs M, inputs N) of every Linear in one minibatch's backward (actor_critic_dh.py:45-111), the second
+# history conv as its GEMM
+LAYERS = [(294912, 16, 128), (49152, 128, 96), (49152, 64, 128),
+          (49152, 256, 235), (49152, 128, 256), (49152, 64, 128), (49152, 3, 64),
+          (49152, 512, 302), (49152, 256, 512), (49152, 128, 256), (49152, 12, 128),
+          (49152, 768, 219), (49152, 256, 768), (49152, 128, 256), (49152, 1, 128)]
+
+
+def timed(fn, reps):
+    for _ in range(3):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3   # us
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--reps", type=int, default=20)
+    a = p.parse_args()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    rows_out, tot_new, tot_old = [], 0.0, 0.0
+    for rows, M, N in LAYERS:
+        gy = (torch.randn(rows, M, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+        x = torch.randn(rows, N, device=dev, generator=g).to(torch.bfloat16)
+        t_new = timed(lambda: dh_policy.linear_wgrad_bf16(gy, x), a.reps)
+        t_old = timed(lambda: (dh_policy.wgrad_splitk(gy, x), dh_policy.bias_grad(gy)), a.reps)
+        flops = 2.0 * rows * M * N
+        rows_out.append({"rows": rows, "M": M, "N": N, "us_kernel": round(t_new, 2), "us_splitk": round(t_old, 2),
+                         "tflops_kernel": round(flops / t_new * 1e-6, 1)})
+        tot_new += t_new
+        tot_old += t_old
+    print(json.dumps({"bench": "linear_wgrad_bf16", "layers": rows_out, "us_per_minibatch_kernel": round(tot_new, 1),
+                      "us_per_minibatch_splitk": round(tot_old, 1)}))
+
+
+if __name__ == "__main__":
+    main()
