@@ -358,8 +358,28 @@ void k_conv1d_pair(const float* __restrict__ x, const h8* __restrict__ frag, con
 // The PPO minibatch's actor observations rebuilt from the frame-history rollout storage (algo/rollout.py
 // _HistoryRows): row m is the window of frames k .. k + F - 1 of env n's sequence seq[n] ((F + T - 1) frames of `frame`
 // values, k = idx[m] / N, n = idx[m] % N), with the frames older than the env's latest reset at or before step k
-// (time < first[k, n], time = k - F + 1 + j for window frame j) zeroed -- a prefix of the window.  One wave per row;
-// 16-bit (bf16 / fp16 storage) or 32-bit elements copied as raw bits.
+// (time < first[k, n], time = k - F + 1 + j for window frame j) zeroed -- a prefix of the window.  One wave per row,
+// copied as 32-bit words in bursts of 8 per lane (eight loads in flight before the stores; the one-element-per-lane
+// loop waited a full memory latency per 128 B, 181 us per 49,152-row minibatch, profiles/r05upd_*).  16-bit elements
+// with an even row length: the row's words realigned from the source's parity (one extra aligned word, a 16-bit
+// shift; the source window of an odd offset reaches one element past its last, inside the same aligned word);
+// otherwise one element per lane.
+struct HrRow {
+  int64_t src;  // element offset of the window in seq
+  int zlen;     // zeroed leading elements
+};
+__device__ __forceinline__ HrRow hr_row(const int64_t* __restrict__ first, const int64_t* __restrict__ idx, int m, int N,
+                                        int T, int frames, int frame) {
+  const int64_t g = idx[m];
+  const int k = (int)(g / N), n = (int)(g % N);
+  const int64_t f = first[(int64_t)k * N + n];
+  const int64_t z = f - ((int64_t)k - frames + 1);  // frames before the reset (window frame 0 at time k - F + 1)
+  const int zero_frames = z <= 0 ? 0 : (z >= frames ? frames : (int)z);
+  return HrRow{((int64_t)n * (frames + T - 1) + k) * frame, zero_frames * frame};
+}
+
+constexpr int HR_BURST = 8;
+
 template <typename E>
 __global__ __launch_bounds__(256) void k_history_rows(const E* __restrict__ seq, const int64_t* __restrict__ first,
                                                       const int64_t* __restrict__ idx, E* __restrict__ out, int rows,
@@ -367,16 +387,57 @@ __global__ __launch_bounds__(256) void k_history_rows(const E* __restrict__ seq,
   const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= rows) return;
   const int lane = threadIdx.x & 63;
-  const int64_t g = idx[m];
-  const int k = (int)(g / N), n = (int)(g % N);
-  const int64_t f = first[(int64_t)k * N + n];
-  const int64_t t0 = (int64_t)k - frames + 1;  // time of window frame 0
-  const int64_t z = f - t0;
-  const int zero_frames = z <= 0 ? 0 : (z >= frames ? frames : (int)z);
-  const int len = frames * frame, zlen = zero_frames * frame;
-  const E* src = seq + ((int64_t)n * (frames + T - 1) + k) * frame;
+  const HrRow r = hr_row(first, idx, m, N, T, frames, frame);
+  const int len = frames * frame;
+  const E* src = seq + r.src;
   E* dst = out + (int64_t)m * len;
-  for (int i = lane; i < len; i += 64) dst[i] = i < zlen ? E(0) : src[i];
+  for (int i0 = 0; i0 < len; i0 += 64 * HR_BURST) {
+    E v[HR_BURST];
+#pragma unroll
+    for (int u = 0; u < HR_BURST; ++u) {
+      const int i = i0 + 64 * u + lane;
+      v[u] = src[i < len ? i : len - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < HR_BURST; ++u) {
+      const int i = i0 + 64 * u + lane;
+      if (i < len) dst[i] = i < r.zlen ? E(0) : v[u];
+    }
+  }
+}
+
+// 16-bit elements, even row length (dst rows start on 4-byte boundaries): 32-bit words
+__global__ __launch_bounds__(256) void k_history_rows_w16(const uint16_t* __restrict__ seq,
+                                                          const int64_t* __restrict__ first,
+                                                          const int64_t* __restrict__ idx, uint16_t* __restrict__ out,
+                                                          int rows, int N, int T, int frames, int frame) {
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const HrRow r = hr_row(first, idx, m, N, T, frames, frame);
+  const int nw = frames * frame / 2;
+  const bool odd = (r.src & 1) != 0;  // wave-uniform
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(seq) + (r.src >> 1);  // the word holding the first element
+  uint32_t* dw = reinterpret_cast<uint32_t*>(out + (int64_t)m * 2 * nw);
+  for (int j0 = 0; j0 < nw; j0 += 64 * HR_BURST) {
+    uint32_t lo[HR_BURST], hi[HR_BURST];
+#pragma unroll
+    for (int u = 0; u < HR_BURST; ++u) {
+      int j = j0 + 64 * u + lane;
+      j = j < nw ? j : nw - 1;
+      lo[u] = sw[j];
+      hi[u] = sw[odd ? j + 1 : j];
+    }
+#pragma unroll
+    for (int u = 0; u < HR_BURST; ++u) {
+      const int j = j0 + 64 * u + lane;
+      if (j >= nw) continue;
+      uint32_t w = odd ? (lo[u] >> 16) | (hi[u] << 16) : lo[u];
+      if (2 * j + 1 < r.zlen) w = 0u;
+      else if (2 * j < r.zlen) w &= 0xffff0000u;
+      dw[j] = w;
+    }
+  }
 }
 
 }  // namespace
@@ -388,7 +449,11 @@ int t1policy_history_rows(const void* seq, const int64_t* first, const int64_t* 
   if (!seq || !first || !idx || !out || rows < 0 || num_envs <= 0 || steps <= 0 || frames <= 0 || frame <= 0) return -1;
   if (rows == 0) return 0;
   const dim3 grid((rows + 3) / 4), block(256);
-  if (elem_bytes == 2)
+  if (elem_bytes == 2 && (frames * frame) % 2 == 0 && (reinterpret_cast<uintptr_t>(seq) & 3u) == 0 &&
+      (reinterpret_cast<uintptr_t>(out) & 3u) == 0)
+    hipLaunchKernelGGL(k_history_rows_w16, grid, block, 0, (hipStream_t)stream, (const uint16_t*)seq, first, idx,
+                       (uint16_t*)out, rows, num_envs, steps, frames, frame);
+  else if (elem_bytes == 2)
     hipLaunchKernelGGL(k_history_rows<uint16_t>, grid, block, 0, (hipStream_t)stream, (const uint16_t*)seq, first, idx,
                        (uint16_t*)out, rows, num_envs, steps, frames, frame);
   else if (elem_bytes == 4)

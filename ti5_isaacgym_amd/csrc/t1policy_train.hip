@@ -16,7 +16,7 @@
 //   k_conv1_wgrad_bf16  gW[o, c, t] = sum_{b, l} gy[b, l, o] x[b, c, 3 l + t], gb[o] = sum gy: per sample ONE k-step of
 //                       v_mfma_f32_32x32x16_bf16 (k = the 14 output positions + 2 zero rows) for each of the 13 32-column
 //                       tiles of the 396 (c, t) columns; a workgroup accumulates a run of samples in registers and
-//                       stores one fp32 partial; k_conv1_wgrad_reduce sums the partials in a fixed order
+//                       stores one fp32 partial; k_conv1_wgrad_reduce sums the partials in a fixed tree
 //                       (deterministic, so eager and graph-replayed updates stay bit-identical).
 #include <hip/hip_runtime.h>
 
@@ -234,22 +234,44 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf16(const uint16_t* __rest
   }
 }
 
-// gW[o, c, t] (the (32, 66, 6) fp32 weight layout) and gb[o]: the partials summed in workgroup order
+// gW[o, c, t] (the (32, 66, 6) fp32 weight layout) and gb[o]: the partials summed in a fixed tree -- 16 groups per
+// output (thread (g, o) sums partials g, g + 16, ... in order, eight loads in flight), then the 16 group sums in order
+// (the one-thread-per-output chain of 512 dependent loads took 120 us, profiles/r05upd_*)
+constexpr int TR_GROUPS = 16, TR_PER = 256 / TR_GROUPS;
 __global__ __launch_bounds__(256) void k_conv1_wgrad_reduce(const float* __restrict__ part, int parts,
                                                             float* __restrict__ gw, float* __restrict__ gb) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= TC_O * TC_COLS + TC_O) return;
-  int src;
-  if (e < TC_O * TC_COLS) {
-    const int o = e / TC_COLS, col = e % TC_COLS;
-    src = o * (TC_CT * 32) + col;
-  } else {
+  __shared__ float red[256];
+  const int g = threadIdx.x / TR_PER, o = threadIdx.x % TR_PER;
+  const int e = blockIdx.x * TR_PER + o;
+  const bool live = e < TC_O * TC_COLS + TC_O;
+  int src = 0;
+  if (live && e < TC_O * TC_COLS) {
+    const int oc = e / TC_COLS, col = e % TC_COLS;
+    src = oc * (TC_CT * 32) + col;
+  } else if (live) {
     src = TC_O * TC_CT * 32 + (e - TC_O * TC_COLS);
   }
   float s = 0.0f;
-  for (int g = 0; g < parts; ++g) s += part[(size_t)g * TC_PART + src];
-  if (e < TC_O * TC_COLS) gw[e] = s;
-  else gb[e - TC_O * TC_COLS] = s;
+  if (live) {
+    int k = g;
+    for (; k + 7 * TR_GROUPS < parts; k += 8 * TR_GROUPS) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(k + u * TR_GROUPS) * TC_PART + src];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < parts; k += TR_GROUPS) s += part[(size_t)k * TC_PART + src];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (g == 0 && live) {
+    float sum = red[o];
+#pragma unroll
+    for (int q = 1; q < TR_GROUPS; ++q) sum += red[q * TR_PER + o];
+    if (e < TC_O * TC_COLS) gw[e] = sum;
+    else gb[e - TC_O * TC_COLS] = sum;
+  }
 }
 
 // ---- column sums of a (rows, cols) gradient (the Linear bias gradients gy.sum(0) of the PPO update: 49,152 rows),
@@ -375,7 +397,7 @@ int t1policy_conv1_wgrad_bf16(const void* x, const void* gy, void* workspace, fl
   float* part = reinterpret_cast<float*>(workspace);
   hipLaunchKernelGGL(k_conv1_wgrad_bf16, dim3(parts), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(gy), part, batch);
-  hipLaunchKernelGGL(k_conv1_wgrad_reduce, dim3((TC_O * TC_COLS + TC_O + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(k_conv1_wgrad_reduce, dim3((TC_O * TC_COLS + TC_O + TR_PER - 1) / TR_PER), dim3(256), 0,
                      (hipStream_t)stream, part, parts, grad_weight, grad_bias);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -10,16 +10,18 @@
 //
 // Both operands are row-major with the REDUCTION (the batch row) as their slow index, so the MFMA fragments -- a lane
 // holds 8 consecutive k of one output row / column -- are columns of the staged tiles: each 32-row chunk of gy and x is
-// staged into LDS row-major as loaded (coalesced dword loads; 16-bit loads for an odd width), and the fragments come
+// staged into LDS row-major as loaded (coalesced dword loads, realigned for an odd width; three chunks of loads in
+// flight through a register ring), and the fragments come
 // back with ds_read_b64_tr_b16 (the gfx950 transposing LDS read: a 16-lane group reads 4 rows x 16 columns and gets
 // the columns in its lanes).  A workgroup owns a 128 x 128 output tile and a slice of rows; its four waves own 64 x 64
 // quarters (2 x 2 v_mfma_f32_32x32x16_bf16 accumulators).  The bias sum rides on the A fragments of the n-tile-0
-// workgroups.  Partials go to a workspace [slice][M x N | M]; k_wgrad_reduce sums the slices in order s = 0, 1, ...,
-// so the result is deterministic (eager and graph-replayed updates stay bit-identical).  Products of bf16 operands are
+// workgroups.  Partials go to a workspace [slice][M x N | M]; k_wgrad_reduce sums the slices in a fixed tree, so the
+// result is deterministic (eager and graph-replayed updates stay bit-identical).  Products of bf16 operands are
 // exact in fp32; the sums are fp32.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace {
 
@@ -36,33 +38,46 @@ constexpr int WG_MIN_ROWS = 256;      // rows per slice at least
 
 __device__ __forceinline__ float bf16_float(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
 
-// a 32-row chunk of columns [c0, c0 + 128) of a (rows, W) bf16 matrix in registers: thread t holds the column pair
-// 2 (t & 63) of rows (t >> 6) + 4 i, zero past the width or the slice end
+// a 32-row chunk of columns [c0, c0 + 128) of a (rows, W) bf16 matrix: thread t loads the column pair 2 (t & 63) of
+// rows r0 + (t >> 6) + 4 i.  W even: the pair is an aligned dword.  W odd (c0, r0 even): a row starts at an element of
+// the row's parity, the wave's parity: even rows take the aligned dword, odd rows the two aligned dwords around the
+// pair, realigned by a 16-bit shift.  Every load is issued unconditionally at a clamped in-matrix index, and the raw
+// dwords stay in the register ring until the chunk is staged (wg_store applies the realignment and zeroes the pairs past
+// the slice end or the width): a conditional load, or a select right behind the load, makes the compiler wait for it
+// there and drains the ring.
+template <bool PAIR> struct WgStage {
+  uint32_t lo[8];
+  uint32_t hi[PAIR ? 1 : 8];
+};
 template <bool PAIR>
-__device__ __forceinline__ void wg_load(const uint16_t* __restrict__ z, int W, int c0, int r0, int r1, int t,
-                                        uint32_t (&v)[8]) {
+__device__ __forceinline__ void wg_load(const uint16_t* __restrict__ z, int W, int c0, int r0, int r1, int rows, int t,
+                                        WgStage<PAIR>& v) {
   const int col = c0 + 2 * (t & 63);
-  const bool c_ok = col < W, c1_ok = col + 1 < W;
+  const int colc = col < W ? col : (W - 1) & ~1;
+  const uint32_t* zw = reinterpret_cast<const uint32_t*>(z);
+  const size_t last = ((size_t)rows * W - 1) >> 1;  // the dword holding the matrix's last element
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int r = r0 + (t >> 6) + 4 * i;
-    const uint16_t* p = z + (size_t)r * W + col;
-    uint32_t u = 0u;
-    if (r < r1) {
-      if constexpr (PAIR) {  // W even: the pair is one aligned dword
-        if (c_ok) u = *reinterpret_cast<const uint32_t*>(p);
-      } else {
-        if (c_ok) u = p[0];
-        if (c1_ok) u |= (uint32_t)p[1] << 16;
-      }
+    const size_t e = (size_t)(r < r1 ? r : r1 - 1) * W + colc;
+    v.lo[i] = zw[e >> 1];
+    if constexpr (!PAIR) {
+      const size_t ih = (e >> 1) + 1;
+      v.hi[i] = zw[ih < last ? ih : last];
     }
-    v[i] = u;
   }
 }
 
-__device__ __forceinline__ void wg_store(uint32_t* img, int t, const uint32_t (&v)[8]) {
+template <bool PAIR>
+__device__ __forceinline__ void wg_store(uint32_t* img, int W, int c0, int r0, int r1, int t, const WgStage<PAIR>& v) {
+  const bool c_ok = c0 + 2 * (t & 63) < W;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) img[((t >> 6) + 4 * i) * (WG_PITCH / 2) + (t & 63)] = v[i];
+  for (int i = 0; i < 8; ++i) {
+    const bool ok = c_ok && r0 + (t >> 6) + 4 * i < r1;
+    uint32_t u = v.lo[i];
+    if constexpr (!PAIR) u = ((t >> 6) & 1) ? (u >> 16) | (v.hi[i] << 16) : u;
+    img[((t >> 6) + 4 * i) * (WG_PITCH / 2) + (t & 63)] = ok ? u : 0u;
+  }
 }
 
 // the 32 x 16 (A) or 16 x 32 (B) fragment of k-step ks for columns [col0, col0 + 32) of a staged chunk: lane
@@ -106,17 +121,25 @@ __global__ __launch_bounds__(256, 2) void k_linear_wgrad_bf16(const uint16_t* __
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
   float bsum[2] = {0.0f, 0.0f};
-  uint32_t vg[8], vx[8];
-  wg_load<GY_PAIR>(gy, M, m0, r0, r1, t, vg);
-  wg_load<X_PAIR>(x, N, n0, r0, r1, t, vx);
+  // three chunks of loads in flight: register slots 0, 1, 2 hold chunks c, c + 1, c + 2; a slot is refilled with chunk
+  // c + 3 as soon as it is staged into LDS (two LDS buffers, one barrier per chunk)
+  WgStage<GY_PAIR> vg[3];
+  WgStage<X_PAIR> vx[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    wg_load<GY_PAIR>(gy, M, m0, r0 + k * WG_ROWS, r1, rows, t, vg[k]);
+    wg_load<X_PAIR>(x, N, n0, r0 + k * WG_ROWS, r1, rows, t, vx[k]);
+    __builtin_amdgcn_sched_barrier(0);  // slot order = issue order (the waits count on it)
+  }
   int buf = 0;
-  for (int c = r0; c < r1; c += WG_ROWS, buf ^= 1) {
-    wg_store(reinterpret_cast<uint32_t*>(IMG[buf][0]), t, vg);
-    wg_store(reinterpret_cast<uint32_t*>(IMG[buf][1]), t, vx);
-    if (c + WG_ROWS < r1) {  // the next chunk's loads in flight behind this chunk's products
-      wg_load<GY_PAIR>(gy, M, m0, c + WG_ROWS, r1, t, vg);
-      wg_load<X_PAIR>(x, N, n0, c + WG_ROWS, r1, t, vx);
-    }
+  auto chunk = [&](WgStage<GY_PAIR>& rg, WgStage<X_PAIR>& rx, int c) {
+    wg_store<GY_PAIR>(reinterpret_cast<uint32_t*>(IMG[buf][0]), M, m0, c, r1, t, rg);
+    wg_store<X_PAIR>(reinterpret_cast<uint32_t*>(IMG[buf][1]), N, n0, c, r1, t, rx);
+    // refill unconditionally (past the slice end: the slice's last row again, never stored), so the wait before
+    // each store counts only this slot's loads
+    wg_load<GY_PAIR>(gy, M, m0, c + 3 * WG_ROWS, r1, rows, t, rg);
+    wg_load<X_PAIR>(x, N, n0, c + 3 * WG_ROWS, r1, rows, t, rx);
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();  // staged; double-buffered, so the chunk before last's readers are done
     if (mb_n > 0 && nb_n > 0) {
 #pragma unroll
@@ -141,6 +164,14 @@ __global__ __launch_bounds__(256, 2) void k_linear_wgrad_bf16(const uint16_t* __
         }
       }
     }
+    buf ^= 1;
+  };
+  for (int c = r0; c < r1; c += 3 * WG_ROWS) {
+    chunk(vg[0], vx[0], c);
+    if (c + WG_ROWS >= r1) break;
+    chunk(vg[1], vx[1], c + WG_ROWS);
+    if (c + 2 * WG_ROWS >= r1) break;
+    chunk(vg[2], vx[2], c + 2 * WG_ROWS);
   }
   // C/D: column n = lane & 31, row m = (r & 3) + 8 (r >> 2) + 4 h
   float* P = part + (size_t)s * M * N;
@@ -169,27 +200,50 @@ __global__ __launch_bounds__(256, 2) void k_linear_wgrad_bf16(const uint16_t* __
   }
 }
 
-// gW[i] = sum_s part[s][i] (i < M N) and gb[m] = sum_s bpart[s][m], s = 0, 1, ... in order
+// gW[i] = sum_s part[s][i] (i < M N) and gb[m] = sum_s bpart[s][m]: G slice groups per output (thread (g, o) sums
+// slices g, g + G, ... in order, eight loads in flight), then the G group sums in order -- a fixed tree for a given
+// slice count, so the result is deterministic
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, const float* __restrict__ bpart,
-                                                      int slices, int mn, int m, float* __restrict__ gw,
+                                                      int slices, int groups, int mn, int m, float* __restrict__ gw,
                                                       float* __restrict__ gb) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool w = e < mn;
-  if (!w && (gb == nullptr || e >= mn + m)) return;
-  const float* src = w ? part + e : bpart + (e - mn);
-  const size_t stride = w ? (size_t)mn : (size_t)m;
+  __shared__ float red[256];
+  const int per = 256 / groups, g = threadIdx.x / per, o = threadIdx.x % per;
+  const int e = blockIdx.x * per + o;
+  const int total = mn + (gb ? m : 0);
   float acc = 0.0f;
-  int k = 0;
-  for (; k + 8 <= slices; k += 8) {
-    float v[8];
+  if (e < total) {
+    const bool w = e < mn;
+    const float* src = w ? part + e : bpart + (e - mn);
+    const size_t stride = w ? (size_t)mn : (size_t)m;
+    int k = g;
+    for (; k + 7 * groups < slices; k += 8 * groups) {
+      float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(k + u) * stride];
+      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(k + u * groups) * stride];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc += v[u];
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; k < slices; k += groups) acc += src[(size_t)k * stride];
   }
-  for (; k < slices; ++k) acc += src[(size_t)k * stride];
-  if (w) gw[e] = acc;
-  else gb[e - mn] = acc;
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (g == 0 && e < total) {
+    float sum = red[o];
+    for (int q = 1; q < groups; ++q) sum += red[q * per + o];
+    if (e < mn) gw[e] = sum;
+    else gb[e - mn] = sum;
+  }
+}
+
+// workgroups per CU the slicing aims at (T1_WGRAD_WG_PER_CU, 1-4: A/B; fewer means fewer, longer slices and
+// less partial traffic)
+int wg_per_cu() {
+  static const int v = [] {
+    const char* e = getenv("T1_WGRAD_WG_PER_CU");
+    const int k = e ? atoi(e) : 2;
+    return k >= 1 && k <= 4 ? k : 2;
+  }();
+  return v;
 }
 
 struct WgPlan {
@@ -200,8 +254,8 @@ WgPlan wg_plan(int rows, int M, int N, int cus) {
   WgPlan p;
   p.tiles_m = (M + WG_T - 1) / WG_T;
   p.tiles = p.tiles_m * ((N + WG_T - 1) / WG_T);
-  // about two workgroups per CU, slices of at least WG_MIN_ROWS rows, a multiple of the chunk
-  const int want = (2 * cus + p.tiles - 1) / p.tiles;
+  // about wg_per_cu() workgroups per CU, slices of at least WG_MIN_ROWS rows, a multiple of the chunk
+  const int want = (wg_per_cu() * cus + p.tiles - 1) / p.tiles;
   const int most = (rows + WG_MIN_ROWS - 1) / WG_MIN_ROWS;
   int sl = want < most ? want : most;
   if (sl < 1) sl = 1;
@@ -263,8 +317,9 @@ int t1policy_linear_wgrad_bf16(const void* gy, const void* x, int rows, int M, i
     hipLaunchKernelGGL((k_linear_wgrad_bf16<false, false>), grid, dim3(256), 0, st, g16, x16, rows, M, N, p.tiles_m,
                        p.rows_per_slice, part, bpart);
   const int total = M * N + (grad_bias ? M : 0);
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + 255) / 256), dim3(256), 0, st, part, bpart, p.slices, M * N, M,
-                     grad_weight, grad_bias);
+  const int groups = p.slices <= 8 ? 1 : (p.slices <= 64 ? 4 : 16), per = 256 / groups;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + per - 1) / per), dim3(256), 0, st, part, bpart, p.slices, groups,
+                     M * N, M, grad_weight, grad_bias);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
