@@ -95,6 +95,15 @@ int t1policy_colsum(const void* g, int elem_bytes, int rows, int cols, void* wor
  * error. */
 int t1policy_slice_sum(const float* part, int slices, int n, float* out, void* stream);
 
+/* The input gradient of a channels-last Conv1d run as unfold + GEMM (the history encoder's second conv in the PPO
+ * update, actor_critic_dh.py:83-96; replaces torch's unfold backward inside dh_ppo.py:180's loss.backward()):
+ *   gx[b, l, c] = sum over taps t (ascending) with l - t = stride * p, 0 <= p < lout, of g[b, p, c, t]
+ * g: (batch, lout, channels, kernel) row-major, gx: (batch, length, channels), lout = (length - kernel) / stride + 1;
+ * elem_bytes 2 (bf16) or 4 (fp32), summed in fp32 and rounded once.  Returns 0, -1 on bad arguments, -2 on a launch
+ * error. */
+int t1policy_fold_rows(const void* g, void* gx, int batch, int length, int channels, int kernel, int stride,
+                       int elem_bytes, void* stream);
+
 /* A Linear layer's weight and bias gradients in the PPO update under the opt-in bf16 update (the gradients
  * loss.backward() forms for every nn.Linear of actor_critic_dh.py:45-111 at dh_ppo.py:180; replaces the split-K
  * batched GEMM + t1policy_slice_sum + torch's dim-0 bias sum of dh_policy._LinearSplitK.backward):

@@ -419,12 +419,48 @@ def heads_forward(ac, obs, critic_obs, eps):
     return mean, actions, sigma, logp, value
 
 
+# the unfolded rows' input gradient as the HIP gather (t1policy_fold_rows) instead of torch's unfold backward
+# (T1_FOLD_ROWS=0: torch's, A/B)
+FOLD_ROWS = os.environ.get("T1_FOLD_ROWS", "1") != "0"
+
+
+class _UnfoldRows(torch.autograd.Function):
+    """The (B * Lout, C * k) window rows of a channels-last (B, L, C) device tensor (x.unfold(1, k, st), copied); the
+    backward is the HIP gather t1policy_fold_rows -- each input element sums its (at most k / st) window entries in
+    fp32 and rounds once, bit-identical to torch's scatter-add when at most two windows meet (k = 4, st = 2 here)."""
+
+    @staticmethod
+    def forward(ctx, x, k, st):
+        ctx.geom = (tuple(x.shape), k, st)
+        win = x.unfold(1, k, st)
+        B, Lout, C, _ = win.shape
+        return win.reshape(B * Lout, C * k)
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _lib
+        lib = _lib.load()
+        (B, L, C), k, st = ctx.geom
+        g = g.contiguous()
+        gx = torch.empty(B, L, C, device=g.device, dtype=g.dtype)
+        rc = lib.t1policy_fold_rows(g.data_ptr(), gx.data_ptr(), B, L, C, k, st, g.element_size(),
+                                    torch.cuda.current_stream(g.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"t1policy_fold_rows failed (rc={rc})")
+        return gx, None, None
+
+
 def conv1d_as_gemm(x, conv, channels_last=False):
     """nn.Conv1d (no padding / dilation / groups) as one GEMM over unfolded windows.  x: (B, C, L), or (B, L, C) with
     channels_last; returns (B, Lout, O) (channels last).  The windows x[b, :, s*l : s*l + k] become rows of a
     (B*Lout, C*k) matrix (c-major, then tap: the layout of conv.weight.view(O, C*k)), so the product is one
     hipBLASLt GEMM + bias, and autograd's unfold backward (a strided scatter-add) gives the input gradient."""
     k, st = conv.kernel_size[0], conv.stride[0]
+    if (channels_last and FOLD_ROWS and x.is_cuda and torch.is_grad_enabled() and x.requires_grad
+            and x.dtype in (torch.bfloat16, torch.float32)):
+        rows = _UnfoldRows.apply(x, k, st)               # (B * Lout, C * k), the HIP gather as its backward
+        B, Lout = x.shape[0], (x.shape[1] - k) // st + 1
+        return _LinearSplitK.apply(rows, conv.weight.reshape(conv.out_channels, -1), conv.bias).view(B, Lout, -1)
     if channels_last:
         win = x.unfold(1, k, st)                      # (B, Lout, C, k)
     else:

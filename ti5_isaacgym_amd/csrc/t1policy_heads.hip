@@ -46,6 +46,17 @@ constexpr int PH_M = 32;      // envs per workgroup (one MFMA column tile)
 #define T1_HEADS_WAVES 8
 #endif
 constexpr int PH_WAVES = T1_HEADS_WAVES;
+// 8-wave ring depths (k-steps in flight) for 1, 2 and >= 3 output tiles per wave: act() 0.1419 ms at 4 / 2 / 1 against
+// 0.1428 at 6 / 3 / 2, 0.1443 at 8 / 4 / 2 and 0.1470 at 12 / 6 / 2 (profiles/r05hd_act_ab.txt; A/B)
+#ifndef T1_HEADS_D1
+#define T1_HEADS_D1 4
+#endif
+#ifndef T1_HEADS_D2
+#define T1_HEADS_D2 2
+#endif
+#ifndef T1_HEADS_D3
+#define T1_HEADS_D3 1
+#endif
 constexpr int PH_OBS_SHORT = 235, PH_CRITIC = 219, PH_Y1 = 14 * 32;
 constexpr int PH_NLAYER = 15;
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2 };
@@ -278,8 +289,9 @@ struct PhOut {  // the global outputs (OUT_MEAN / OUT_VALUE layers)
 template <int L> struct PhRing {
   static constexpr int NT = ph_nt(L), KS = PH_L[L].ks, T = (NT + PH_WAVES - 1) / PH_WAVES;
   // two waves per SIMD (PH_WAVES 8): the other wave covers part of the latency, and 256 VGPRs hold the accumulators
-  // and a ring of 2-8 steps without spills (4 waves: 512 registers, 4-16 steps)
-  static constexpr int D0 = PH_WAVES == 8 ? (T >= 3 ? 2 : (T >= 2 ? 4 : 8)) : (T >= 4 ? 4 : (T >= 2 ? 8 : 16));
+  // and a ring of 1-4 steps (4 waves: 512 registers, 4-16 steps)
+  static constexpr int D0 = PH_WAVES == 8 ? (T >= 3 ? T1_HEADS_D3 : (T >= 2 ? T1_HEADS_D2 : T1_HEADS_D1))
+                                          : (T >= 4 ? 4 : (T >= 2 ? 8 : 16));
   static constexpr int D = D0 < KS ? D0 : KS - 1;
   static constexpr int R = D + 1;
   h8 w[R][T][2];

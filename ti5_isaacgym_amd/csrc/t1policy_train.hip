@@ -348,6 +348,32 @@ __global__ __launch_bounds__(256) void k_slice_sum1(const float* __restrict__ pa
   out[i] = s;
 }
 
+// ---- the input gradient of an unfolded channels-last Conv1d (dh_policy._UnfoldRows: the history encoder's second conv
+// as unfold + GEMM in the update): gx[b, l, c] = sum over taps t with l - t = stride p, 0 <= p < lout, of
+// g[b, p, c, t] -- torch's unfold backward (a zero-filled scatter-add, 88 us per minibatch) as a gather, one thread
+// per (b, l, c), the taps in ascending order summed in fp32 and rounded once to the element type (bit-identical to
+// the scatter-add when at most two taps meet, as at kernel 4 / stride 2)
+template <typename E>
+__global__ __launch_bounds__(256) void k_fold_rows(const E* __restrict__ g, E* __restrict__ gx, long long total,
+                                                   int length, int channels, int kernel, int stride, int lout) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c = (int)(e % channels);
+  const long long bl = e / channels;
+  const int l = (int)(bl % length);
+  const long long b = bl / length;
+  float s = 0.0f;
+  for (int t = 0; t < kernel; ++t) {
+    const int d = l - t;
+    if (d < 0 || d % stride != 0 || d / stride >= lout) continue;
+    const long long src = ((b * lout + d / stride) * channels + c) * kernel + t;
+    if constexpr (sizeof(E) == 2) s += bf16_float(g[src]);
+    else s += __uint_as_float(g[src]);
+  }
+  if constexpr (sizeof(E) == 2) gx[e] = bf16_bits(s);
+  else gx[e] = __float_as_uint(s);
+}
+
 bool tc_shape(int channels, int length, int out_channels, int kernel, int stride) {
   return channels == TC_C && length == TC_L && out_channels == TC_O && kernel == TC_K && stride == TC_S;
 }
@@ -422,6 +448,26 @@ int t1policy_colsum(const void* g, int elem_bytes, int rows, int cols, void* wor
     return -1;
   hipLaunchKernelGGL(k_colsum_final, dim3((cols + 255) / 256), dim3(256), 0, (hipStream_t)stream, part, chunks, cols,
                      out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_fold_rows(const void* g, void* gx, int batch, int length, int channels, int kernel, int stride,
+                       int elem_bytes, void* stream) {
+  if (!g || !gx || batch < 0 || length <= 0 || channels <= 0 || kernel <= 0 || stride <= 0 || length < kernel)
+    return -1;
+  if (elem_bytes != 2 && elem_bytes != 4) return -1;
+  if (batch == 0) return 0;
+  const int lout = (length - kernel) / stride + 1;
+  const long long total = (long long)batch * length * channels;
+  const int grid = (int)((total + 255) / 256);
+  if (elem_bytes == 2)
+    hipLaunchKernelGGL(k_fold_rows<uint16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint16_t*>(g), reinterpret_cast<uint16_t*>(gx), total, length, channels,
+                       kernel, stride, lout);
+  else
+    hipLaunchKernelGGL(k_fold_rows<uint32_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint32_t*>(g), reinterpret_cast<uint32_t*>(gx), total, length, channels,
+                       kernel, stride, lout);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
