@@ -10,14 +10,18 @@ DEV = torch.device("cuda:0")
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32], ids=["bf16", "fp32"])
-@pytest.mark.parametrize("batch", [1, 4099])
-def test_fold_rows_is_torchs_unfold_backward(dtype, batch):
+@pytest.mark.parametrize("batch,length,ch,k,st", [(1, 14, 32, 4, 2), (4099, 14, 32, 4, 2), (9000, 14, 32, 4, 2),
+                                                   (37, 15, 24, 4, 2), (37, 14, 5, 2, 2)])
+def test_fold_rows_is_torchs_unfold_backward(dtype, batch, length, ch, k, st):
+    """The compiled kernel-4 / stride-2 instance (channels dividing 256, batch past the 8192-workgroup grid) and the
+    generic one (24 channels; kernel 2)."""
     from ti5_isaacgym_amd.algo.dh_policy import _UnfoldRows
     g = torch.Generator(device=DEV).manual_seed(batch)
-    x = torch.randn(batch, 14, 32, device=DEV, generator=g).to(dtype)
+    x = torch.randn(batch, length, ch, device=DEV, generator=g).to(dtype)
     x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
-    rows = _UnfoldRows.apply(x1, 4, 2)
-    ref = x2.unfold(1, 4, 2).reshape(batch * 6, 32 * 4)
+    rows = _UnfoldRows.apply(x1, k, st)
+    lout = (length - k) // st + 1
+    ref = x2.unfold(1, k, st).reshape(batch * lout, ch * k)
     assert torch.equal(rows, ref)
     gr = torch.randn(rows.shape, device=DEV, generator=g).to(dtype)
     rows.backward(gr)

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void k_conv1_pack_bf16(const float* __restrict
 }
 
 // One wave per SIMD, four waves per workgroup, each wave a contiguous run of samples staged in its own LDS rows
-// (the next sample's loads in flight while the current one multiplies).
+// (the next two samples' loads in flight while the current one multiplies).
 constexpr int TF_WAVES = 4;
 constexpr int TF_PER_LANE = (TC_SAMPLE / 2 + 63) / 64;  // 25 32-bit words per lane (1,551 per sample)
 __global__ __launch_bounds__(64 * TF_WAVES) __attribute__((amdgpu_waves_per_eu(1, 2)))
@@ -79,26 +79,34 @@ void k_conv1_fwd_bf16(const uint16_t* __restrict__ x, const bf8* __restrict__ fr
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) bo[nt] = bf16_float(bf16_bits(bias[16 * nt + (lane & 15)]));
   const uint32_t* xw = reinterpret_cast<const uint32_t*>(x);  // a sample is 6,204 B: 4-byte aligned
-  uint32_t pa[TF_PER_LANE];
-  auto load = [&](int bs) {
+  if (b0 >= b1) return;  // an empty run (batch below the wave count); the kernel has no workgroup barrier
+  // two samples' loads in flight (register slots pa, pb); a slot is refilled with the sample two ahead (past the run:
+  // the run's last sample again, an L2 hit) as soon as it is staged, unconditionally, so each wait counts only that
+  // slot's loads
+  uint32_t pa[TF_PER_LANE], pb[TF_PER_LANE];
+  auto load = [&](uint32_t (&p)[TF_PER_LANE], int bs) {
     const uint32_t* src = xw + (size_t)(bs < b1 ? bs : b1 - 1) * (TC_SAMPLE / 2);
 #pragma unroll
     for (int k = 0; k < TF_PER_LANE; ++k) {
       const int i = lane + 64 * k;
-      pa[k] = src[i < TC_SAMPLE / 2 ? i : TC_SAMPLE / 2 - 1];
+      p[k] = src[i < TC_SAMPLE / 2 ? i : TC_SAMPLE / 2 - 1];
     }
   };
-  if (b0 < b1) load(b0);
+  load(pa, b0);
+  __builtin_amdgcn_sched_barrier(0);
+  load(pb, b0 + 1);
+  __builtin_amdgcn_sched_barrier(0);
   const int r = lane & 15, kg = lane >> 4;
   const int rr = r < TC_LOUT ? r : TC_LOUT - 1;  // rows 14, 15: row 13's inputs, never stored
   const uint16_t* Xh = reinterpret_cast<const uint16_t*>(X);
-  for (int b = b0; b < b1; ++b) {
+  auto process = [&](uint32_t (&p)[TF_PER_LANE], int b) {
 #pragma unroll
     for (int k = 0; k < TF_PER_LANE; ++k) {
       const int i = lane + 64 * k;
-      if (i < TC_SAMPLE / 2) X[i] = pa[k];
+      if (i < TC_SAMPLE / 2) X[i] = p[k];
     }
-    load(b + 1);  // past the run: the run's last sample again (an L2 hit)
+    load(p, b + 2);
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -125,6 +133,11 @@ void k_conv1_fwd_bf16(const uint16_t* __restrict__ x, const bf8* __restrict__ fr
       }
     }
     __builtin_amdgcn_wave_barrier();  // the next staging overwrites X after every lane's reads of it
+  };
+  for (int b = b0; b < b1; b += 2) {
+    process(pa, b);
+    if (b + 1 >= b1) break;
+    process(pb, b + 1);
   }
 }
 
@@ -144,20 +157,25 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf16(const uint16_t* __rest
   const int b0 = (int)((long long)blockIdx.x * batch / gridDim.x), b1 = (int)((long long)(blockIdx.x + 1) * batch / gridDim.x);
   const uint32_t* xw = reinterpret_cast<const uint32_t*>(x);
   const uint32_t* gw = reinterpret_cast<const uint32_t*>(gy);
-  uint32_t px[TW_LX], pg[TW_LG];
-  auto load = [&](int bs) {
+  // three samples' loads in flight: register slots 0, 1, 2 hold samples b, b + 1, b + 2; a slot is refilled with sample
+  // b + 3 (past the run: its last sample again, an L2 hit) as soon as it is staged, unconditionally, so the wait before
+  // each staging counts only that slot's loads (one sample ahead: 2.5 TB/s, latency-bound)
+  struct Slot {
+    uint32_t x[TW_LX], g[TW_LG];
+  };
+  auto load = [&](Slot& sl, int bs) {
     const int bc = bs < b1 ? bs : b1 - 1;
     const uint32_t* sx = xw + (size_t)bc * TW_X;
     const uint32_t* sg = gw + (size_t)bc * TW_G;
 #pragma unroll
     for (int k = 0; k < TW_LX; ++k) {
       const int i = t + 256 * k;
-      px[k] = sx[i < TW_X ? i : TW_X - 1];
+      sl.x[k] = sx[i < TW_X ? i : TW_X - 1];
     }
 #pragma unroll
     for (int k = 0; k < TW_LG; ++k) {
       const int i = t + 256 * k;
-      pg[k] = sg[i < TW_G ? i : TW_G - 1];
+      sl.g[k] = sg[i < TW_G ? i : TW_G - 1];
     }
   };
   // the tiles' (c, t) columns: col = 32 tile + n, c = col / 6, t = col % 6 (0 past the 396)
@@ -177,20 +195,26 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf16(const uint16_t* __rest
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[i][q] = 0.0f;
   float gbs = 0.0f;  // sum of this lane's gy values (o = n, positions 8 h .. 8 h + 7)
-  if (b0 < b1) load(b0);
+  Slot sl[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    load(sl[k], b0 + k);
+    __builtin_amdgcn_sched_barrier(0);  // slot order = issue order
+  }
   int buf = 0;
-  for (int b = b0; b < b1; ++b, buf ^= 1) {
+  auto sample = [&](Slot& cur, int b) {
 #pragma unroll
     for (int k = 0; k < TW_LX; ++k) {
       const int i = t + 256 * k;
-      if (i < TW_X) XS[buf][i] = px[k];
+      if (i < TW_X) XS[buf][i] = cur.x[k];
     }
 #pragma unroll
     for (int k = 0; k < TW_LG; ++k) {
       const int i = t + 256 * k;
-      if (i < TW_G) GS[buf][i] = pg[k];
+      if (i < TW_G) GS[buf][i] = cur.g[k];
     }
-    load(b + 1);
+    load(cur, b + 3);
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();  // staged (double-buffered: the sample before last's readers are done)
     const uint16_t* Xh = reinterpret_cast<const uint16_t*>(XS[buf]);
     const uint16_t* Gh = reinterpret_cast<const uint16_t*>(GS[buf]);
@@ -216,6 +240,14 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf16(const uint16_t* __rest
       }
       acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(bf8, bv), acc[i], 0, 0, 0);
     }
+    buf ^= 1;
+  };
+  for (int b = b0; b < b1; b += 3) {
+    sample(sl[0], b);
+    if (b + 1 >= b1) break;
+    sample(sl[1], b + 1);
+    if (b + 2 >= b1) break;
+    sample(sl[2], b + 2);
   }
   // the partial: [o][tile * 32 + n] (C/D: column n, row o = (q & 3) + 8 (q >> 2) + 4 h), then the 32 bias sums
   float* P = part + (size_t)blockIdx.x * TC_PART;
@@ -350,28 +382,71 @@ __global__ __launch_bounds__(256) void k_slice_sum1(const float* __restrict__ pa
 
 // ---- the input gradient of an unfolded channels-last Conv1d (dh_policy._UnfoldRows: the history encoder's second conv
 // as unfold + GEMM in the update): gx[b, l, c] = sum over taps t with l - t = stride p, 0 <= p < lout, of
-// g[b, p, c, t] -- torch's unfold backward (a zero-filled scatter-add, 88 us per minibatch) as a gather, one thread
-// per (b, l, c), the taps in ascending order summed in fp32 and rounded once to the element type (bit-identical to
-// the scatter-add when at most two taps meet, as at kernel 4 / stride 2)
+// g[b, p, c, t] -- torch's unfold backward (a zero-filled scatter-add, 88 us per minibatch) as a gather, one
+// workgroup per sample and one thread per (l, c), the taps in ascending order summed in fp32 and rounded once to the
+// element type (bit-identical to the scatter-add when at most two taps meet, as at kernel 4 / stride 2)
 template <typename E>
-__global__ __launch_bounds__(256) void k_fold_rows(const E* __restrict__ g, E* __restrict__ gx, long long total,
-                                                   int length, int channels, int kernel, int stride, int lout) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= total) return;
-  const int c = (int)(e % channels);
-  const long long bl = e / channels;
-  const int l = (int)(bl % length);
-  const long long b = bl / length;
-  float s = 0.0f;
-  for (int t = 0; t < kernel; ++t) {
-    const int d = l - t;
-    if (d < 0 || d % stride != 0 || d / stride >= lout) continue;
-    const long long src = ((b * lout + d / stride) * channels + c) * kernel + t;
-    if constexpr (sizeof(E) == 2) s += bf16_float(g[src]);
-    else s += __uint_as_float(g[src]);
+__global__ __launch_bounds__(256) void k_fold_rows(const E* __restrict__ g, E* __restrict__ gx, int batch, int length,
+                                                   int channels, int kernel, int stride, int lout) {
+  // one workgroup per sample (grid-stride), threads over the sample's (l, c) outputs: 32-bit index math inside a sample
+  const int per = length * channels;
+  for (int b = blockIdx.x; b < batch; b += gridDim.x) {
+    const E* gb = g + (size_t)b * lout * channels * kernel;
+    E* xb = gx + (size_t)b * per;
+    for (int e = threadIdx.x; e < per; e += blockDim.x) {
+      const int l = e / channels, c = e - l * channels;
+      float s = 0.0f;
+      for (int t = 0; t < kernel; ++t) {
+        const int d = l - t;
+        if (d < 0 || d % stride != 0 || d / stride >= lout) continue;
+        const E v = gb[((d / stride) * channels + c) * kernel + t];
+        if constexpr (sizeof(E) == 2) s += bf16_float(v);
+        else s += __uint_as_float(v);
+      }
+      if constexpr (sizeof(E) == 2) xb[e] = bf16_bits(s);
+      else xb[e] = __float_as_uint(s);
+    }
   }
-  if constexpr (sizeof(E) == 2) gx[e] = bf16_bits(s);
-  else gx[e] = __float_as_uint(s);
+}
+
+// the same for the update's shape, channels C / kernel K / stride S known at compile time: a thread owns one (l, c) of
+// FR_SB consecutive samples and issues all their tap loads before any sum (the per-sample loop waited a full memory
+// latency per sample: 74-97 us per minibatch)
+constexpr int FR_SB = 8;
+template <typename E, int C, int K, int S>
+__global__ __launch_bounds__(256) void k_fold_rows_ks(const E* __restrict__ g, E* __restrict__ gx, int batch,
+                                                      int length, int lout) {
+  const int tid = blockIdx.x * 256 + threadIdx.x;
+  const int c = tid % C, r = tid / C;
+  const int l = r % length, b0 = (r / length) * FR_SB;
+  if (b0 >= batch) return;
+  E v[K][FR_SB];
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    const int d = l - t;
+    const bool ok = d >= 0 && d % S == 0 && d / S < lout;
+    const int p = ok ? d / S : 0;
+#pragma unroll
+    for (int u = 0; u < FR_SB; ++u) {
+      const int b = b0 + u < batch ? b0 + u : batch - 1;
+      v[t][u] = ok ? g[(((size_t)b * lout + p) * C + c) * K + t] : E(0);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < FR_SB; ++u) {
+    if (b0 + u >= batch) break;
+    float s = 0.0f;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int d = l - t;
+      if (d < 0 || d % S != 0 || d / S >= lout) continue;
+      if constexpr (sizeof(E) == 2) s += bf16_float(v[t][u]);
+      else s += __uint_as_float(v[t][u]);
+    }
+    E* xb = gx + ((size_t)(b0 + u) * length + l) * C + c;
+    if constexpr (sizeof(E) == 2) *xb = bf16_bits(s);
+    else *xb = __float_as_uint(s);
+  }
 }
 
 bool tc_shape(int channels, int length, int out_channels, int kernel, int stride) {
@@ -458,15 +533,24 @@ int t1policy_fold_rows(const void* g, void* gx, int batch, int length, int chann
   if (elem_bytes != 2 && elem_bytes != 4) return -1;
   if (batch == 0) return 0;
   const int lout = (length - kernel) / stride + 1;
-  const long long total = (long long)batch * length * channels;
-  const int grid = (int)((total + 255) / 256);
-  if (elem_bytes == 2)
+  if ((long long)lout * channels * kernel >= (1LL << 31) || (long long)length * channels >= (1LL << 31)) return -1;
+  const int grid = batch < 8192 ? batch : 8192;
+  if (kernel == 4 && stride == 2 && channels == 32) {
+    const long long threads = ((long long)(batch + FR_SB - 1) / FR_SB) * length * 32;
+    const int fgrid = (int)((threads + 255) / 256);
+    if (elem_bytes == 2)
+      hipLaunchKernelGGL((k_fold_rows_ks<uint16_t, 32, 4, 2>), dim3(fgrid), dim3(256), 0, (hipStream_t)stream,
+                         reinterpret_cast<const uint16_t*>(g), reinterpret_cast<uint16_t*>(gx), batch, length, lout);
+    else
+      hipLaunchKernelGGL((k_fold_rows_ks<uint32_t, 32, 4, 2>), dim3(fgrid), dim3(256), 0, (hipStream_t)stream,
+                         reinterpret_cast<const uint32_t*>(g), reinterpret_cast<uint32_t*>(gx), batch, length, lout);
+  } else if (elem_bytes == 2)
     hipLaunchKernelGGL(k_fold_rows<uint16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const uint16_t*>(g), reinterpret_cast<uint16_t*>(gx), total, length, channels,
+                       reinterpret_cast<const uint16_t*>(g), reinterpret_cast<uint16_t*>(gx), batch, length, channels,
                        kernel, stride, lout);
   else
     hipLaunchKernelGGL(k_fold_rows<uint32_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const uint32_t*>(g), reinterpret_cast<uint32_t*>(gx), total, length, channels,
+                       reinterpret_cast<const uint32_t*>(g), reinterpret_cast<uint32_t*>(gx), batch, length, channels,
                        kernel, stride, lout);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

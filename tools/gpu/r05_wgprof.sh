@@ -8,7 +8,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_linear_wgrad.py > $out/tests_wgrad.log 2>&1
 tail -1 $out/tests_wgrad.log
-for k in ${WGPC:-2 1}; do
+for k in ${WGPC:-2 1 3}; do
   T1_WGRAD_WG_PER_CU=$k timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof$k -o wg -- python tools/wgrad_bench.py --reps 10 > $out/wgrad_bench$k.json 2> $out/prof$k.err
   echo profiled $k
 done
