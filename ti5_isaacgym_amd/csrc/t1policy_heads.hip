@@ -25,8 +25,8 @@
 // Bounds: per 32-env tile the actor chain is 976 step-tiles and the critic 792 (one step-tile = a
 // 32 x 16 weight fragment pair = 3 MFMAs, 2 KB of fragments): 3.6 MB of fragments streamed from L2 per tile pair and
 // 1.4 M MFMA-cycles per tile pair -- at the XCD L2's ~70 GB/s/CU of shared rows the fragment stream, not the matrix
-// cores, sets the time.  Actor workgroups run on XCDs 0-3 and critic workgroups on XCDs 4-7 (blockIdx mod 8 = XCD),
-// so each XCD's 4 MB L2 holds only its role's fragments (1.9 or 1.6 MB).
+// cores, sets the time.  Every XCD (blockIdx mod 8) runs both roles, alternating in its dispatch order, so the longer
+// actor chain is spread over all CUs; its 4 MB L2 holds both roles' 3.6 MB of fragments.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -432,8 +432,10 @@ void k_heads(PhParams P, const h8* __restrict__ frag, const float* __restrict__ 
   // role and tile: blockIdx mod 8 is the XCD; actor tiles on XCDs 0-3, critic tiles on 4-7 (xcd_split), else
   // alternating
   const int bid = blockIdx.x;
-  const bool critic = xcd_split ? (bid & 4) != 0 : (bid & 1) != 0;
-  const int tile = xcd_split ? (bid >> 3) * 4 + (bid & 3) : bid >> 1;
+  // xcd_split 2: both roles on every XCD, alternating in each XCD's dispatch order (a CU's two workgroups tend to be
+  // one actor chain and one critic; each L2 then holds both roles' 3.6 MB of fragments)
+  const bool critic = xcd_split == 2 ? ((bid >> 3) & 1) != 0 : (xcd_split ? (bid & 4) != 0 : (bid & 1) != 0);
+  const int tile = xcd_split == 2 ? ((bid >> 4) << 3) + (bid & 7) : (xcd_split ? (bid >> 3) * 4 + (bid & 3) : bid >> 1);
   const int env0 = tile * PH_M;
   if (env0 >= batch) return;
   const int env = env0 + (lane & 31);
@@ -550,8 +552,11 @@ int t1policy_heads_forward(const uint64_t* params, const int* dims, const void* 
   PhOut G{eps, P.std, mean, actions, sigma, logp, value, 0, false};
   const int tiles = (batch + PH_M - 1) / PH_M;
   const char* xv = getenv("T1POLICY_HEADS_XCD");
-  const int xcd_split = !(xv && xv[0] == '0');
-  const int grid = xcd_split ? 8 * ((tiles + 3) / 4) : 2 * tiles;
+  // T1POLICY_HEADS_XCD (A/B): 2 (default) both roles alternating on every XCD, act() 0.139-0.140 ms; 1 actor on XCDs
+  // 0-3 / critic on 4-7, 0.142 (the actor chain is 23% longer, so the actor XCDs finish last); 0 alternating
+  // workgroups, 0.140 (profiles/r05hx_act_ab.txt)
+  const int xcd_split = xv && xv[0] == '0' ? 0 : (xv && xv[0] == '1' ? 1 : 2);
+  const int grid = xcd_split == 2 ? 16 * ((tiles + 7) / 8) : (xcd_split ? 8 * ((tiles + 3) / 4) : 2 * tiles);
   hipLaunchKernelGGL(k_heads, dim3(grid), dim3(64 * PH_WAVES), 0, (hipStream_t)stream, P,
                      reinterpret_cast<const h8*>(frag), y1, obs, obs_cols, critic_obs, critic_cols, G, batch,
                      xcd_split);
