@@ -565,11 +565,12 @@ class ActorCriticDH(nn.Module):
     def entropy(self):
         return self.distribution.entropy().sum(dim=-1)
 
-    def actor_input(self, observations):
-        """[short history | estimated base velocity | long-history code] (302 features)."""
+    def actor_input(self, observations, es_vel=None):
+        """[short history | estimated base velocity | long-history code] (302 features); es_vel: the state estimator's
+        output on this short history when the caller already has it."""
         short = observations[..., -self.num_short_obs:]
         code = self.long_history(observations.view(-1, self.in_channels, self.num_proprio_obs))
-        return torch.cat((short, self.state_estimator(short), code), dim=-1)
+        return torch.cat((short, self.state_estimator(short) if es_vel is None else es_vel, code), dim=-1)
 
     def update_distribution(self, actor_obs):
         mean = self.actor(actor_obs).float()   # fp32 distribution under the opt-in bf16 update (no-op in fp32)

@@ -501,10 +501,16 @@ class DHPPO:
         # alone (a sample's std >= 0 check is a host sync, which no graph capture allows; the losses do not use it); on
         # the CPU the sample is drawn and dropped like the reference's, so the global RNG stream -- the next rollout's
         # action samples -- stays the reference's (tests/test_runner_golden.py)
-        ac.update_distribution(ac.actor_input(obs_b))
-        if not obs_b.is_cuda:
+        if obs_b.is_cuda:
+            # one state-estimator pass feeds both the actor input and the estimator loss (the reference evaluates the
+            # same network on the same rows twice, dh_ppo.py:123-126: the same values; the two uses' gradients are
+            # summed at its output instead of in its parameters) -- its forward and backward once per minibatch
+            est_lin_vel = ac.state_estimator(obs_b[:, -self.num_short_obs:])
+            ac.update_distribution(ac.actor_input(obs_b, est_lin_vel))
+        else:
+            ac.update_distribution(ac.actor_input(obs_b))
             ac.distribution.sample()
-        est_lin_vel = ac.state_estimator(obs_b[:, -self.num_short_obs:])
+            est_lin_vel = ac.state_estimator(obs_b[:, -self.num_short_obs:])
         ref_lin_vel = critic_b[:, self.lin_vel_idx:self.lin_vel_idx + 3].clone()
         logp_b = ac.get_actions_log_prob(actions_b)
         value_b = ac.evaluate(critic_b, masks=masks_b, hidden_states=hid_b[1])
