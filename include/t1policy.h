@@ -107,14 +107,17 @@ int t1policy_fold_rows(const void* g, void* gx, int batch, int length, int chann
 /* A Linear layer's weight and bias gradients in the PPO update under the opt-in bf16 update (the gradients
  * loss.backward() forms for every nn.Linear of actor_critic_dh.py:45-111 at dh_ppo.py:180; replaces the split-K
  * batched GEMM + t1policy_slice_sum + torch's dim-0 bias sum of dh_policy._LinearSplitK.backward):
- *   grad_weight[m, n] = sum_r gy[r, m] x[r, n]   (M x N fp32, row-major)
- *   grad_bias[m]      = sum_r gy[r, m]           (fp32; grad_bias NULL: not formed)
+ *   grad_weight[m, n] (+)= sum_r gy[r, m] x[r, n]   (M x N fp32, row-major)
+ *   grad_bias[m]      (+)= sum_r gy[r, m]           (fp32; grad_bias NULL: not formed)
+ * accumulate != 0: added to the gradients already there (autograd's accumulation into an existing .grad), else
+ * stored.
  * gy (rows, M) and x (rows, N) are row-major bf16 with 4-byte-aligned bases; the sums are fp32 over exact bf16
  * products in a fixed order (deterministic).  workspace: workspace_bytes(rows, M, N) device bytes, 16-byte aligned.
  * Returns 0, -1 on bad arguments, -2 on a launch / device error (workspace_bytes: the size, or -1 / -2). */
 long long t1policy_linear_wgrad_workspace_bytes(int rows, int M, int N);
 int t1policy_linear_wgrad_bf16(const void* gy, const void* x, int rows, int M, int N, void* workspace,
-                               long long workspace_bytes, float* grad_weight, float* grad_bias, void* stream);
+                               long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
+                               void* stream);
 
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py

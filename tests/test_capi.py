@@ -91,7 +91,7 @@ def test_policy_header_exports(lib):
     assert lib.t1policy_conv1d_pack_weights(None, None, 66, 32, 6, None) == -1
     assert lib.t1policy_conv1d_frag_bytes() == 17 * 2 * 2 * 64 * 16
     assert lib.t1policy_linear_wgrad_workspace_bytes(0, 4, 4) == -1
-    assert lib.t1policy_linear_wgrad_bf16(None, None, 8, 4, 4, None, 0, None, None, None) == -1
+    assert lib.t1policy_linear_wgrad_bf16(None, None, 8, 4, 4, None, 0, None, None, 0, None) == -1
     # fused heads: 1,768 step-tiles (32 outputs x 16 inputs) of hi + lo fragments, 90 output tiles of bias
     assert lib.t1policy_heads_frag_bytes() == 1768 * 2 * 64 * 16 + 90 * 4 * 64 * 16   # + the bias fragments
     assert lib.t1policy_heads_pack(None, None, None, None) == -1

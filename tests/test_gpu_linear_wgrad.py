@@ -16,7 +16,8 @@ DEV = torch.device("cuda:0")
 # load path: the state estimator's 235 inputs, the critic's 219, the estimator head's 3 outputs, the value head's 1),
 # the second conv as a GEMM (294,912 rows), and ragged / tiny shapes
 SHAPES = [(49152, 768, 219), (49152, 256, 235), (49152, 512, 302), (49152, 3, 64), (49152, 1, 128),
-          (294912, 16, 128), (49152, 256, 768), (1000, 12, 128), (31, 5, 7), (4097, 130, 97), (64, 300, 2)]
+          (294912, 16, 128), (49152, 256, 768), (1000, 12, 128), (31, 5, 7), (4097, 130, 97), (64, 300, 2),
+          (777, 219, 235), (3001, 1, 3)]
 
 
 def _operands(rows, M, N, seed):
@@ -95,4 +96,31 @@ def test_linear_wgrad_rejects_bad_arguments():
     gw = torch.empty(8, 8, device=DEV)
     # a workspace smaller than workspace_bytes is refused, not overrun
     assert lib.t1policy_linear_wgrad_bf16(gy.data_ptr(), x.data_ptr(), 64, 8, 8, ws.data_ptr(), 16, gw.data_ptr(),
-                                          None, torch.cuda.current_stream().cuda_stream) == -1
+                                          None, 0, torch.cuda.current_stream().cuda_stream) == -1
+
+
+def test_linear_wgrad_accumulates_into_existing_grads(monkeypatch):
+    """into=: the sums ADDED to existing fp32 gradients; through autograd (GRAD_DIRECT, the PPO update's bucket views) a
+    preset .grad ends as the same bits as autograd's own accumulation of the returned gradient."""
+    from ti5_isaacgym_amd.algo import dh_policy
+    gy, x = _operands(3000, 96, 130, 11)
+    base_w = torch.randn(96, 130, device=DEV)
+    base_b = torch.randn(96, device=DEV)
+    gw0, gb0 = dh_policy.linear_wgrad_bf16(gy, x)
+    w, b = base_w.clone(), base_b.clone()
+    dh_policy.linear_wgrad_bf16(gy, x, into=(w, b))
+    assert torch.equal(w, base_w + gw0) and torch.equal(b, base_b + gb0)
+    torch.manual_seed(1)
+    lin = dh_policy.Linear(130, 96).to(DEV)
+
+    def grads(flag):
+        monkeypatch.setattr(dh_policy, "GRAD_DIRECT", flag)
+        lin.weight.grad, lin.bias.grad = base_w.clone(), base_b.clone()
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+            y = lin(x)
+        y.backward(gy)
+        return lin.weight.grad.clone(), lin.bias.grad.clone()
+
+    (wd, bd), (wa, ba) = grads(True), grads(False)
+    assert torch.equal(wd, wa) and torch.equal(bd, ba)
+    assert torch.equal(wd, base_w + gw0)

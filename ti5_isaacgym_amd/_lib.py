@@ -152,7 +152,7 @@ def load():
         "t1policy_colsum": ([vp, i32, i32, i32, vp, vp, vp], C.c_int),
         "t1policy_slice_sum": ([vp, i32, i32, vp, vp], C.c_int),
         "t1policy_linear_wgrad_workspace_bytes": ([i32, i32, i32], C.c_longlong),
-        "t1policy_linear_wgrad_bf16": ([vp, vp, i32, i32, i32, vp, C.c_longlong, vp, vp, vp], C.c_int),
+        "t1policy_linear_wgrad_bf16": ([vp, vp, i32, i32, i32, vp, C.c_longlong, vp, vp, i32, vp], C.c_int),
         "t1policy_fold_rows": ([vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():

@@ -116,14 +116,19 @@ def bias_grad(gy):
     return out
 
 
+# ... added by that kernel straight into an existing .grad of the layer's leaf parameters (T1_GRAD_DIRECT=0: returned
+# to autograd, which adds them, A/B)
+GRAD_DIRECT = os.environ.get("T1_GRAD_DIRECT", "1") != "0"
 # the bf16 update's Linear weight + bias gradients as one HIP MFMA kernel (t1policy_linear_wgrad_bf16); T1_LINEAR_WGRAD=0:
 # the split-K batched GEMM + slice sum + torch's bias sum (A/B)
 LINEAR_WGRAD = os.environ.get("T1_LINEAR_WGRAD", "1") != "0"
 
 
-def linear_wgrad_bf16(gy, x, need_bias=True):
+def linear_wgrad_bf16(gy, x, need_bias=True, into=None):
     """(gy^T x, gy.sum(0)) in fp32 for bf16 gy (K, M) and x (K, N) (x in fp32 is rounded to bf16 first, as autocast's
-    GEMM would): the HIP wgrad kernel, fixed-order fp32 sums of the exact bf16 products.  Device tensors only."""
+    GEMM would): the HIP wgrad kernel, fixed-order fp32 sums of the exact bf16 products.  Device tensors only.
+    into = (gw, gb): existing fp32 gradients (gb may be None) the sums are ADDED to (autograd's accumulation into a
+    .grad, done by the kernel's last pass); returns them."""
     from .. import _lib
     lib = _lib.load()
     gy = gy.contiguous()
@@ -136,10 +141,17 @@ def linear_wgrad_bf16(gy, x, need_bias=True):
     if nbytes <= 0:
         raise RuntimeError(f"t1policy_linear_wgrad_workspace_bytes failed ({nbytes})")
     ws = torch.empty(nbytes, device=gy.device, dtype=torch.uint8)
-    gw = torch.empty(M, N, device=gy.device, dtype=torch.float32)
-    gb = torch.empty(M, device=gy.device, dtype=torch.float32) if need_bias else None
+    if into is not None:
+        gw, gb = into
+        ok = lambda t, shape: (t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == shape  # noqa: E731
+                               and t.device == gy.device)
+        if not ok(gw, (M, N)) or (gb is not None and not ok(gb, (M,))):
+            raise ValueError("linear_wgrad_bf16: into= needs contiguous fp32 (M, N) / (M,) device gradients")
+    else:
+        gw = torch.empty(M, N, device=gy.device, dtype=torch.float32)
+        gb = torch.empty(M, device=gy.device, dtype=torch.float32) if need_bias else None
     rc = lib.t1policy_linear_wgrad_bf16(gy.data_ptr(), x.data_ptr(), K, M, N, ws.data_ptr(), nbytes, gw.data_ptr(),
-                                        gb.data_ptr() if gb is not None else None,
+                                        gb.data_ptr() if gb is not None else None, int(into is not None),
                                         torch.cuda.current_stream(gy.device).cuda_stream)
     if rc != 0:
         raise RuntimeError(f"t1policy_linear_wgrad_bf16 failed (rc={rc})")
@@ -152,6 +164,8 @@ class _LinearSplitK(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, x, w, b):
+        # the leaf parameters, for the backward's direct accumulation into their .grad (GRAD_DIRECT)
+        ctx.leaves = (w if w.is_leaf else None, b if b.is_leaf else None)
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             # the operands cast once, here, and saved cast: the backward's input-gradient GEMM and weight gradient use
             # the same bf16 weight / input instead of casting the fp32 ones again (19 weight casts per minibatch; the
@@ -168,7 +182,17 @@ class _LinearSplitK(torch.autograd.Function):
         gy = gy.contiguous()
         gx = gy.mm(w) if ctx.needs_input_grad[0] else None
         if LINEAR_WGRAD and gy.is_cuda and gy.dtype == torch.bfloat16 and ctx.needs_input_grad[1]:
-            gw, gb = linear_wgrad_bf16(gy, x, need_bias=ctx.needs_input_grad[2])
+            wl, bl = ctx.leaves
+            need_b = ctx.needs_input_grad[2]
+            if (GRAD_DIRECT and wl is not None and wl.grad is not None and wl.grad.dtype == torch.float32
+                    and wl.grad.is_contiguous() and (not need_b or (bl is not None and bl.grad is not None
+                                                                    and bl.grad.dtype == torch.float32))):
+                # the weight / bias gradients added straight into the existing .grad (the PPO update's views into
+                # the all-reduce bucket) by the kernel's reduction: autograd's accumulation pass per parameter
+                # (one add_ kernel each, ~38 per minibatch) is not needed, so no gradient is returned for them
+                linear_wgrad_bf16(gy, x, into=(wl.grad, bl.grad if need_b else None))
+                return gx, None, None
+            gw, gb = linear_wgrad_bf16(gy, x, need_bias=need_b)
             return gx, gw, gb
         gw = wgrad_splitk(gy, x) if ctx.needs_input_grad[1] else None
         gb = bias_grad(gy) if ctx.needs_input_grad[2] else None

@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256, 2) void k_linear_wgrad_bf16(const uint16_t* __
 // slice count, so the result is deterministic
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, const float* __restrict__ bpart,
                                                       int slices, int groups, int mn, int m, float* __restrict__ gw,
-                                                      float* __restrict__ gb) {
+                                                      float* __restrict__ gb, int accumulate) {
   __shared__ float red[256];
   const int per = 256 / groups, g = threadIdx.x / per, o = threadIdx.x % per;
   const int e = blockIdx.x * per + o;
@@ -230,8 +230,8 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   if (g == 0 && e < total) {
     float sum = red[o];
     for (int q = 1; q < groups; ++q) sum += red[q * per + o];
-    if (e < mn) gw[e] = sum;
-    else gb[e - mn] = sum;
+    float* dst = e < mn ? gw + e : gb + (e - mn);
+    *dst = accumulate ? *dst + sum : sum;  // accumulate: into an existing gradient, as autograd's += would
   }
 }
 
@@ -287,7 +287,8 @@ long long t1policy_linear_wgrad_workspace_bytes(int rows, int M, int N) {
 }
 
 int t1policy_linear_wgrad_bf16(const void* gy, const void* x, int rows, int M, int N, void* workspace,
-                               long long workspace_bytes, float* grad_weight, float* grad_bias, void* stream) {
+                               long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
+                               void* stream) {
   if (!gy || !x || !workspace || !grad_weight || rows <= 0 || M <= 0 || N <= 0) return -1;
   if ((reinterpret_cast<uintptr_t>(gy) & 3u) != 0 || (reinterpret_cast<uintptr_t>(x) & 3u) != 0 ||
       (reinterpret_cast<uintptr_t>(workspace) & 15u) != 0)
@@ -319,7 +320,7 @@ int t1policy_linear_wgrad_bf16(const void* gy, const void* x, int rows, int M, i
   const int total = M * N + (grad_bias ? M : 0);
   const int groups = p.slices <= 8 ? 1 : (p.slices <= 64 ? 4 : 16), per = 256 / groups;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + per - 1) / per), dim3(256), 0, st, part, bpart, p.slices, groups,
-                     M * N, M, grad_weight, grad_bias);
+                     M * N, M, grad_weight, grad_bias, accumulate);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
