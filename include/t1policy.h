@@ -95,6 +95,13 @@ int t1policy_colsum(const void* g, int elem_bytes, int rows, int cols, void* wor
  * error. */
 int t1policy_slice_sum(const float* part, int slices, int n, float* out, void* stream);
 
+/* The PPO minibatch's per-transition fields in one launch (the reference's generator indexes each buffer,
+ * rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py minibatch_source): for f < nfields (<= 12) and
+ * m < rows, dsts[f][m, :] = srcs[f][idx[m], :], rows of widths[f] 32-bit words, row-major.  Returns 0, -1 on bad
+ * arguments, -2 on a launch error. */
+int t1policy_gather_rows(const void* const* srcs, void* const* dsts, const int* widths, int nfields,
+                         const int64_t* idx, int rows, void* stream);
+
 /* The input gradient of a channels-last Conv1d run as unfold + GEMM (the history encoder's second conv in the PPO
  * update, actor_critic_dh.py:83-96; replaces torch's unfold backward inside dh_ppo.py:180's loss.backward()):
  *   gx[b, l, c] = sum over taps t (ascending) with l - t = stride * p, 0 <= p < lout, of g[b, p, c, t]

@@ -32,3 +32,17 @@ def test_history_rows_kernel_matches_torch(dtype, frames):
     assert got.dtype == ref.dtype == dtype
     assert torch.equal(got, ref)
     assert bool((dones[:-1] > 0).any())   # resets inside the rollout are exercised
+
+
+def test_field_gather_is_torch_indexing():
+    """The minibatch's per-transition fields by one launch (t1policy_gather_rows, rollout._FieldGather) == torch's
+    index of each field, bit for bit; a field it cannot take (fp16) keeps torch's path."""
+    from ti5_isaacgym_amd.algo.rollout import _FieldGather
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    rows = 24 * 333
+    fields = [torch.randn(rows, w, device="cuda:0", generator=g) for w in (219, 12, 1, 1, 1, 1, 12, 12)]
+    idx = torch.randperm(rows, device="cuda:0", generator=g)[:4097]
+    got = _FieldGather(fields)(idx)
+    assert all(torch.equal(a, f[idx]) for a, f in zip(got, fields))
+    half = _FieldGather([fields[0].half(), fields[1]])
+    assert not half.ok and all(torch.equal(a, f[idx]) for a, f in zip(half(idx), [fields[0].half(), fields[1]]))

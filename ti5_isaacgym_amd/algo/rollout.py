@@ -12,9 +12,46 @@ when an env resets (t1_dh_stand_env.py:368-481, 548-558).  Storing all 24 x 8192
 newest frame (137 MB in all), and the minibatch generator rebuilds every sampled history from them and the stored
 dones -- the same bits as the full rows.  Callers whose observations are not such a history keep the full storage.
 """
+import os
+
 import torch
 
 from . import distributed as dist_util
+
+
+# the minibatch's per-transition fields gathered by one HIP launch on the device (t1policy_gather_rows; T1_GATHER_ROWS=0:
+# torch's index per field, A/B)
+GATHER_ROWS = os.environ.get("T1_GATHER_ROWS", "1") != "0"
+
+
+class _FieldGather:
+    """fields[k][idx] for every field by one launch (t1policy_gather_rows): 2-D, contiguous, 32-bit device tensors of
+    the same row count; anything else is indexed by torch.  Output buffers are fresh per call (graph-pool memory
+    inside a captured update)."""
+
+    def __init__(self, fields):
+        self.fields = fields
+        self.ok = (all(f.is_cuda and f.dim() == 2 and f.is_contiguous() and f.element_size() == 4 for f in fields)
+                   and len({f.shape[0] for f in fields}) == 1 and len(fields) <= 12)
+
+    def __call__(self, idx):
+        if not self.ok:
+            return [f[idx] for f in self.fields]
+        import ctypes as C
+        from .. import _lib
+        lib = _lib.load()
+        idx = idx.contiguous()
+        rows = idx.shape[0]
+        outs = [torch.empty(rows, f.shape[1], device=f.device, dtype=f.dtype) for f in self.fields]
+        n = len(self.fields)
+        srcs = (C.c_uint64 * n)(*[f.data_ptr() for f in self.fields])
+        dsts = (C.c_uint64 * n)(*[o.data_ptr() for o in outs])
+        widths = (C.c_int * n)(*[f.shape[1] for f in self.fields])
+        rc = lib.t1policy_gather_rows(srcs, dsts, widths, n, idx.data_ptr(), rows,
+                                      torch.cuda.current_stream(idx.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"t1policy_gather_rows failed (rc={rc})")
+        return outs
 
 
 class RolloutStorage:
@@ -139,7 +176,7 @@ class RolloutStorage:
         idx = torch.cat((flat.new_tensor([-1], dtype=torch.int64), flat.nonzero(as_tuple=False)[:, 0]))
         return (idx[1:] - idx[:-1]).float().mean(), self.rewards.mean()
 
-    def minibatch_source(self, obs_dtype=None):
+    def minibatch_source(self, obs_dtype=None):  # noqa: C901
         """take(idx) -> the reference generator's minibatch tuple (rollout_storage.py:153-173) for the flattened rows
         idx.  Every source is one of this storage's own buffers (the frame-history rows and the obs cast are rebuilt
         in place), so take() reads the same addresses every update and can sit inside a captured HIP graph;
@@ -167,12 +204,18 @@ class RolloutStorage:
         if self.next_proprio_obs is not None:
             extra = (flat(self.next_proprio_obs), flat(self.rewards))
 
+        gather = _FieldGather([critic] + cols) if (GATHER_ROWS and critic is not obs) else None
+
         def take(idx):
-            actions, values, advantages, returns, logp, mu, sigma = (c[idx] for c in cols)
+            if gather is not None and idx.is_cuda:
+                critic_b, actions, values, advantages, returns, logp, mu, sigma = gather(idx)
+            else:
+                critic_b = critic[idx]
+                actions, values, advantages, returns, logp, mu, sigma = (c[idx] for c in cols)
             if extra is not None:
-                return (extra[0][idx], extra[1][idx], obs[idx], critic[idx], actions, values, advantages, returns,
+                return (extra[0][idx], extra[1][idx], obs[idx], critic_b, actions, values, advantages, returns,
                         logp, mu, sigma, (None, None), None)
-            return obs[idx], critic[idx], actions, values, advantages, returns, logp, mu, sigma, (None, None), None
+            return obs[idx], critic_b, actions, values, advantages, returns, logp, mu, sigma, (None, None), None
 
         take.key = (okey, obs_dtype, critic.data_ptr(), *(c.data_ptr() for c in cols))
         return take

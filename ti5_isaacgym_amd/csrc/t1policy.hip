@@ -440,9 +440,54 @@ __global__ __launch_bounds__(256) void k_history_rows_w16(const uint16_t* __rest
   }
 }
 
+// The PPO minibatch's per-transition fields gathered by one launch (rollout.py minibatch_source: critic observations,
+// actions, values, advantages, returns, log-probs, means, sigmas -- eight torch index kernels before): field f's row
+// m = src_f[idx[m]] (width_f 32-bit words).  One thread per (row, word) of the fields' concatenated row, so every field
+// width is copied by whole waves.
+constexpr int GR_MAX = 12;
+struct GrFields {
+  const uint32_t* src[GR_MAX];
+  uint32_t* dst[GR_MAX];
+  int width[GR_MAX];
+  int off[GR_MAX + 1];  // prefix sums of the widths
+  int n;
+};
+__global__ __launch_bounds__(256) void k_gather_rows(GrFields F, const int64_t* __restrict__ idx, int rows) {
+  const int total = F.off[F.n];
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)rows * total) return;
+  const int m = (int)(t / total), k = (int)(t - (long long)m * total);
+  int f = 0;
+#pragma unroll
+  for (int q = 1; q < GR_MAX; ++q) f += (q < F.n && k >= F.off[q]) ? 1 : 0;
+  const int w = F.width[f], c = k - F.off[f];
+  F.dst[f][(size_t)m * w + c] = F.src[f][(size_t)idx[m] * w + c];
+}
+
 }  // namespace
 
 extern "C" {
+
+int t1policy_gather_rows(const void* const* srcs, void* const* dsts, const int* widths, int nfields,
+                         const int64_t* idx, int rows, void* stream) {
+  if (!srcs || !dsts || !widths || !idx || nfields <= 0 || nfields > GR_MAX || rows < 0) return -1;
+  if (rows == 0) return 0;
+  GrFields F{};
+  F.off[0] = 0;
+  for (int f = 0; f < nfields; ++f) {
+    if (!srcs[f] || !dsts[f] || widths[f] <= 0 || widths[f] > (1 << 20)) return -1;
+    F.src[f] = reinterpret_cast<const uint32_t*>(srcs[f]);
+    F.dst[f] = reinterpret_cast<uint32_t*>(dsts[f]);
+    F.width[f] = widths[f];
+    F.off[f + 1] = F.off[f] + widths[f];
+  }
+  F.n = nfields;
+  const long long threads = (long long)rows * F.off[nfields];
+  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, F, idx,
+                     rows);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 
 int t1policy_history_rows(const void* seq, const int64_t* first, const int64_t* idx, void* out, int rows, int num_envs,
                           int steps, int frames, int frame, int elem_bytes, void* stream) {
