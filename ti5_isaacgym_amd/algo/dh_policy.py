@@ -14,6 +14,7 @@ Same architecture, parameter names and initialisation as the reference, so its c
 856,972 parameters with the t1 config.  On MI355X the dense layers run as hipBLASLt GEMMs
 through PyTorch-ROCm; the per-step inference batch is every env on the rank.
 """
+import contextlib
 import os
 
 import torch
@@ -158,6 +159,41 @@ def linear_wgrad_bf16(gy, x, need_bias=True, into=None):
     return gw, gb
 
 
+# the update's bf16 weight copies made by one multi-tensor cast per minibatch (param_shadows) instead of one cast
+# kernel per Linear weight and bias (T1_PARAM_SHADOWS=0: the per-layer casts, A/B)
+PARAM_SHADOWS = os.environ.get("T1_PARAM_SHADOWS", "1") != "0"
+_ACTIVE_SHADOWS = {}
+
+
+@contextlib.contextmanager
+def param_shadows(module, dtype):
+    """Inside the block, the device fp32 parameters of `module` have `dtype` copies made by one torch._foreach_copy_
+    (persistent buffers on the module, rewritten on entry), which _LinearSplitK's forward uses instead of casting each
+    weight and bias itself -- the same values as its per-layer cast.  The copies stay valid until the parameters
+    change (the forward saves them for its backward; the optimizer step comes after the backward)."""
+    params = [p for p in module.parameters() if p.is_cuda and p.dtype == torch.float32]
+    st = getattr(module, "_t1_shadows", None)
+    if (st is None or st[0] != dtype or len(st[1]) != len(params)
+            or any(b.shape != p.shape or b.device != p.device for p, b in zip(params, st[1]))):
+        st = module._t1_shadows = (dtype, [torch.empty_like(p, dtype=dtype) for p in params])
+    if params:
+        torch._foreach_copy_(st[1], [p.detach() for p in params])
+    prev = dict(_ACTIVE_SHADOWS)
+    _ACTIVE_SHADOWS.update({id(p): (p, b) for p, b in zip(params, st[1])})
+    try:
+        yield
+    finally:
+        _ACTIVE_SHADOWS.clear()
+        _ACTIVE_SHADOWS.update(prev)
+
+
+def _cast_param(t, dt):
+    e = _ACTIVE_SHADOWS.get(id(t))
+    if e is not None and e[0] is t and e[1].dtype == dt:
+        return e[1]
+    return t.to(dt)
+
+
 class _LinearSplitK(torch.autograd.Function):
     # custom_fwd / custom_bwd: under torch.autocast (the opt-in bf16 update) the GEMMs run in the autocast dtype in
     # both passes; autograd casts the returned gradients to the fp32 parameters' dtype
@@ -171,7 +207,7 @@ class _LinearSplitK(torch.autograd.Function):
             # the same bf16 weight / input instead of casting the fp32 ones again (19 weight casts per minibatch; the
             # values are the casts autocast's addmm would make, so the results are the same bits)
             dt = torch.get_autocast_dtype("cuda")
-            x, w, b = x.to(dt), w.to(dt), b.to(dt)
+            x, w, b = x.to(dt), _cast_param(w, dt), _cast_param(b, dt)
         ctx.save_for_backward(x, w)
         return torch.addmm(b, x, w.t())
 

@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.optim as optim
 from torch.distributions import Normal
 
+from . import dh_policy
 from . import distributed as dist_util
 from .dh_policy import ActorCriticDH, heads_forward, refresh_packed_weights
 from .rollout import RolloutStorage
@@ -509,9 +510,17 @@ class DHPPO:
                 self.value_loss_coef, self.entropy_coef, self.max_grad_norm, self.use_clipped_value_loss,
                 self.lin_vel_idx, dist_util.active())
 
-    def _losses(self, ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
-                old_sigma_b, hid_b, masks_b, mse):
-        """The reference's minibatch losses (dh_ppo.py:130-178); the distribution terms in fp32 under autocast."""
+    def _losses(self, ac, *args):
+        """The reference's minibatch losses (dh_ppo.py:130-178); the distribution terms in fp32 under autocast.  Under
+        the device autocast the parameters' low-precision copies are made by one multi-tensor cast first
+        (dh_policy.param_shadows: the same values as the per-layer casts)."""
+        if args[0].is_cuda and torch.is_autocast_enabled("cuda") and dh_policy.PARAM_SHADOWS:
+            with dh_policy.param_shadows(ac, torch.get_autocast_dtype("cuda")):
+                return self._losses_body(ac, *args)
+        return self._losses_body(ac, *args)
+
+    def _losses_body(self, ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
+                     old_sigma_b, hid_b, masks_b, mse):
         # the reference calls ac.act() here for its distribution and drops the sample.  On the device the distribution
         # alone (a sample's std >= 0 check is a host sync, which no graph capture allows; the losses do not use it); on
         # the CPU the sample is drawn and dropped like the reference's, so the global RNG stream -- the next rollout's
