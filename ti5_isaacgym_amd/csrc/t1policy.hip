@@ -568,7 +568,9 @@ int t1policy_conv1d_forward_packed(const float* x, const void* frag, const float
     hipLaunchKernelGGL(k_conv1d_regs, dim3(grid), dim3(64 * CR_WAVES), 0, (hipStream_t)stream, x,
                        reinterpret_cast<const h8*>(frag), bias, y, batch);
   } else {
-    const long long slots = (long long)cus * CP_PAIRS_PER_CU;
+    const char* pv = getenv("T1POLICY_CONV_PAIRS");  // pairs per CU (A/B; 1-6 fit the LDS)
+    const int pairs = pv && atoi(pv) >= 1 && atoi(pv) <= 6 ? atoi(pv) : CP_PAIRS_PER_CU;
+    const long long slots = (long long)cus * pairs;
     const int grid = (int)(batch < slots ? batch : slots);
     hipLaunchKernelGGL(k_conv1d_pair, dim3(grid), dim3(128), 0, (hipStream_t)stream, x,
                        reinterpret_cast<const h8*>(frag), bias, y, batch);
