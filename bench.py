@@ -16,7 +16,9 @@ roofline: SURVEY.md §8(d): achieved = env_steps_per_s x B_alg (30,678 algorithm
 the 8 TB/s HBM3E peak; `traffic` = PMC-measured HBM bytes per step (profiles/traffic_*.json, tools/
 pmc_traffic.py).  Per-kernel durations are measured live with HIP events around each launch on every
 --time-every'th timed step (event records cost host time, so not on every step), with each kernel's own
-algorithmic bytes; the dominant kernel is k_dyn5, the whole fused step (latency-bound at one wave per SIMD).
+algorithmic bytes; the dominant kernel is the whole fused step -- k_dyn6 (eight role waves, two per SIMD; latency-bound
+on its core wave's chain) at every config but config 5's fp16 histories, where t1env picks k_dyn4 with its
+history shift as a concurrent launch (fused_kernel below names the kernel of each run).
 cpu_baseline: the build's CPU restatement (numpy oracle post-physics + OpenMP dynamics), rank 0, N = 1 only.
 """
 import argparse
@@ -166,10 +168,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL ("nccl").  T1_BENCH_BACKEND=gloo (tests/test_gpu_bench_multirank.py only): the same
+    # N > 1 path with ranks sharing a GPU, which RCCL refuses -- the local rank then wraps around the visible devices
+    backend = os.environ.get("T1_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if (backend != "nccl" and ndev > 0) else local
+    dev = torch.device(f"cuda:{local_dev}")
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
+    torch.cuda.set_device(dev)
     from ti5_isaacgym_amd import make_t1_env
     N = args.num_envs
     def hook(cfg):
@@ -188,6 +198,7 @@ def main():
         env.step(pool[i % 8])
 
     def barrier():
+        torch.cuda.synchronize(dev)
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
@@ -205,14 +216,25 @@ def main():
         barrier()
         el = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            t = torch.tensor([el], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            rank_el = el
             el = float(t.item())
         reps.append(el)
     kt = env.get_timing()
     env.set_timing(False)
     elapsed = sorted(reps)[len(reps) // 2]  # the median repeat (the only one at --repeats 1)
     ok = bool(torch.isfinite(env.root_states).all() and torch.isfinite(env.obs_buf).all())
+    dist_info = {"backend": "none", "world_size": 1, "env_offsets": [env.env_offset]}
+    if world > 1:
+        # what the process group saw (a SCALE line shows whether RCCL had N ranks), each rank's shard and its own
+        # elapsed time of the last repeat (the line's time is their max)
+        shards = [None] * world
+        torch.distributed.all_gather_object(shards, (int(env.env_offset), N, rank_el, bool(ok)))
+        dist_info = {"backend": torch.distributed.get_backend(), "world_size": torch.distributed.get_world_size(),
+                     "env_offsets": [s_[0] for s_ in shards], "envs_per_rank": [s_[1] for s_ in shards],
+                     "rank_elapsed_s": [round(s_[2], 6) for s_ in shards]}
+        ok = all(s_[3] for s_ in shards)
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
@@ -322,6 +344,7 @@ def main():
                      "issue": issue,
                      "kernels": per_kernel},
         "finite": ok,
+        "dist": dist_info,
     }
     if len(reps) > 1:
         line["repeats"] = len(reps)

@@ -41,6 +41,16 @@ def test_version_and_errors(lib):
     assert rc == -1 and b"null" in lib.t1env_last_error()
 
 
+def test_library_carries_this_trees_source_stamp(lib, monkeypatch):
+    """the library's version names the hash of the sources it was built from, and load() refuses one
+    built from other sources with a clear message (not a missing symbol later)."""
+    from ti5_isaacgym_amd import _lib, build
+    assert lib.t1env_version().decode().endswith("src:" + build.source_stamp())
+    monkeypatch.setattr(build, "source_stamp", lambda: "0" * 16)
+    with pytest.raises(RuntimeError, match="stale"):
+        _lib.check_stamp(lib, "libt1env_hip.so")
+
+
 def test_struct_layout_matches_header():
     from ti5_isaacgym_amd import _lib
     prog = r'''

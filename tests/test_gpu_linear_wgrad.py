@@ -113,14 +113,45 @@ def test_linear_wgrad_accumulates_into_existing_grads(monkeypatch):
     torch.manual_seed(1)
     lin = dh_policy.Linear(130, 96).to(DEV)
 
+    calls = []
+    real = dh_policy.linear_wgrad_bf16
+    monkeypatch.setattr(dh_policy, "linear_wgrad_bf16",
+                        lambda *a, **k: (calls.append(k.get("into") is not None), real(*a, **k))[1])
+
     def grads(flag):
-        monkeypatch.setattr(dh_policy, "GRAD_DIRECT", flag)
         lin.weight.grad, lin.bias.grad = base_w.clone(), base_b.clone()
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
             y = lin(x)
-        y.backward(gy)
+        with dh_policy.direct_grad_accumulation(flag):
+            y.backward(gy)
         return lin.weight.grad.clone(), lin.bias.grad.clone()
 
     (wd, bd), (wa, ba) = grads(True), grads(False)
+    assert calls == [True, False]   # the direct path ran only inside the context
     assert torch.equal(wd, wa) and torch.equal(bd, ba)
     assert torch.equal(wd, base_w + gw0)
+
+
+def test_autograd_grad_leaves_preset_grads_alone():
+    """outside direct_grad_accumulation() the kernel's gradients go back through autograd.  torch.autograd.grad
+    under bf16 autocast with preset .grad tensors returns the weight / bias gradients and leaves .grad unchanged, and
+    backward(inputs=[x]) touches no parameter's .grad."""
+    from ti5_isaacgym_amd.algo import dh_policy
+    gy, x = _operands(2048, 64, 96, 5)
+    gw0, gb0 = dh_policy.linear_wgrad_bf16(gy, x)
+    torch.manual_seed(2)
+    lin = dh_policy.Linear(96, 64).to(DEV)
+    pw, pb = torch.randn(64, 96, device=DEV), torch.randn(64, device=DEV)
+    lin.weight.grad, lin.bias.grad = pw.clone(), pb.clone()
+    with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+        y = lin(x)
+    gw, gb = torch.autograd.grad(y, (lin.weight, lin.bias), gy)
+    assert gw is not None and gb is not None
+    assert torch.equal(gw, gw0) and torch.equal(gb, gb0)
+    assert torch.equal(lin.weight.grad, pw) and torch.equal(lin.bias.grad, pb)
+    xi = x.float().clone().requires_grad_(True)
+    with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+        y = lin(xi)
+    y.backward(gy, inputs=[xi])
+    assert xi.grad is not None
+    assert torch.equal(lin.weight.grad, pw) and torch.equal(lin.bias.grad, pb)

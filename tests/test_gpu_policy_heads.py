@@ -76,7 +76,8 @@ def test_fused_heads_match_fp64(n, scale):
 
 
 def test_fused_heads_follow_weight_updates():
-    """heads_forward packs the weights on every call: an in-place parameter change shows up in the next call."""
+    """heads_forward repacks the weights when a parameter changed: an in-place parameter change shows up in the next
+    call."""
     from ti5_isaacgym_amd.algo.dh_policy import heads_forward
     dev = torch.device("cuda:0")
     ac = _model(seed=3).to(dev)
@@ -104,3 +105,32 @@ def test_fused_heads_refuse_other_shapes():
     obs = torch.randn(64, 66 * 47, device=dev)
     with torch.inference_mode():
         assert heads_forward(ac, obs, torch.randn(64, 219, device=dev), torch.zeros(64, 12, device=dev)) is None
+
+
+def test_fused_heads_pack_only_when_weights_move(monkeypatch):
+    """the heads' weight fragments are packed once and reused while no parameter moved; an in-place
+    change repacks on the next call, and refresh_packed_weights(force=True) (after a graphed update) repacks."""
+    from ti5_isaacgym_amd import _lib
+    from ti5_isaacgym_amd.algo.dh_policy import heads_forward, refresh_packed_weights
+    dev = torch.device("cuda:0")
+    ac = _model(seed=4).to(dev)
+    obs = torch.randn(128, 66 * 47, device=dev)
+    cobs = torch.randn(128, 219, device=dev)
+    eps = torch.zeros(128, 12, device=dev)
+    lib = _lib.load()
+    real = lib.t1policy_heads_pack
+    calls = []
+    monkeypatch.setattr(lib, "t1policy_heads_pack", lambda *a: (calls.append(1), real(*a))[1])
+    with torch.inference_mode():
+        m0 = heads_forward(ac, obs, cobs, eps)[0].clone()
+        assert len(calls) == 1
+        m1 = heads_forward(ac, obs, cobs, eps)[0].clone()
+        assert len(calls) == 1 and torch.equal(m0, m1)
+        with torch.no_grad():
+            ac.critic[0].bias.add_(0.5)
+        heads_forward(ac, obs, cobs, eps)
+        assert len(calls) == 2
+        refresh_packed_weights(ac)
+        assert len(calls) == 2
+        refresh_packed_weights(ac, force=True)
+        assert len(calls) == 3

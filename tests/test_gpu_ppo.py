@@ -342,3 +342,49 @@ def test_device_lr_schedule_matches_python_floats():
         assert alg.learning_rate == ref
     assert float(alg._lr_t) == torch.tensor(ref, dtype=torch.float32).item()
     assert alg.optimizer.param_groups[0]["lr"] is alg._lr_t
+
+
+def test_update_capture_failure_runs_eagerly(monkeypatch):
+    """a failed capture of the minibatch step (here forced) warns, switches the update to eager for the rest
+    of that update and after it, and gives the eager update's bits; a failed GAE capture falls back the same way."""
+    import warnings
+    from ti5_isaacgym_amd import task_registry
+    from ti5_isaacgym_amd.algo.dh_policy import ActorCriticDH
+    from ti5_isaacgym_amd.algo.dh_update import DHPPO
+    from ti5_isaacgym_amd.algo.rollout import RolloutStorage
+    from ti5_isaacgym_amd.utils.helpers import class_to_dict
+    _, tc = task_registry.get_cfgs("t1_dh_stand")
+    cfg = class_to_dict(tc)
+    N, T, dev = 512, 24, torch.device("cuda:0")
+    algs = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        ac = ActorCriticDH(235, 47, 219, 12, **cfg["policy"]).to(dev)
+        alg = DHPPO(ac, device=str(dev), **cfg["algorithm"])
+        alg.graph_update = graphed
+        alg.init_storage(N, T, [3102], [219], [12], history=(47, 66))
+        algs.append(alg)
+    monkeypatch.setattr(DHPPO, "_try_capture", staticmethod(lambda graph, body: RuntimeError("forced")))
+    real_graph = torch.cuda.graph
+
+    def failing_graph(*a, **k):   # the GAE capture fails too
+        raise RuntimeError("forced GAE capture failure")
+    for it in range(2):
+        out = []
+        for alg in algs:
+            monkeypatch.setattr(torch.cuda, "graph", failing_graph if alg is algs[1] else real_graph)
+            with warnings.catch_warnings(record=True) as w:
+                warnings.simplefilter("always")
+                _fill_storage(alg, N, T, dev, 20 + it)
+                torch.manual_seed(50 + it)
+                out.append(alg.update())
+            if alg is algs[1] and it == 0:
+                msgs = " ".join(str(x.message) for x in w)
+                assert "capture failed" in msgs, msgs
+            monkeypatch.setattr(torch.cuda, "graph", real_graph)
+        assert out[0] == out[1], (it, out)
+        for p0, p1 in zip(algs[0].actor_critic.parameters(), algs[1].actor_critic.parameters()):
+            assert torch.equal(p0, p1)
+    assert algs[1].graph_update is False and algs[1]._upd is None
+    assert algs[1].storage.graph_gae is False
+    assert isinstance(algs[1].storage, RolloutStorage)

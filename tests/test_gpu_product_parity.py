@@ -1,12 +1,16 @@
-"""Pin the PRODUCT kernel (the fused k_dyn4 step) against the oracle at BASELINE sizes -- needs the MI355X.
+"""Pin the PRODUCT step kernels against the oracle at BASELINE sizes -- needs the MI355X.
+
+The product's fused step is k_dyn6 (eight role waves, t1env_dyn6.hip) at every config except config 5's fp16 histories,
+where t1env picks k_dyn4 (t1_dyn_waves_default); k_dyn5 stays selectable (T1ENV_DYN_KERNEL).  Every case below runs for
+each of them (the dyn_kernel fixture of conftest.py).
 
 The golden fixtures pin post-physics through the injected-physics test hook (k_physics_injected, test_gpu_parity.py).
-Every real step instead runs k_dyn4, with its own PD (pd_torques_staged), its own sensor-lag capture and its fused
-post-physics epilogue.  This test runs that kernel as bench.py runs it -- real dynamics on real terrain -- with the
+Every real step instead runs the step kernel, with its own PD (pd_torques_staged), its own sensor-lag capture and its
+fused post-physics epilogue.  This test runs that kernel as bench.py runs it -- real dynamics on real terrain -- with the
 substep log on (t1env_set_substep_log: the root / dof state after every substep and the torques of every substep),
 and replays the logged states through the oracle's injected-physics step (oracle/t1_oracle.py: the CPU restatement
 pinned by the golden fixtures, tests/test_oracle_golden.py).  Physics divergence cannot enter: both sides see the
-same states, so what is compared is k_dyn4's own arithmetic around the solver:
+same states, so what is compared is the step kernel's own arithmetic around the solver:
 
   * the torques of every substep (lagged action ring, randomized PD, viscous / Coulomb friction, per-substep torque
     multiplier, clip: legged_robot.py:1019-1074);
@@ -23,7 +27,7 @@ pushes), plus a ragged 777-env trimesh run (last workgroup partly empty).  Two m
 before an external-force window (`counter % 400 <= duration`, t1_dh_stand_env.py:205-215): at 400 (duration 0: the
 forces are drawn, enter the critic frame and are never applied) and at 96,400 (duration index 1 = 0.05 s: drawn at
 96,400, applied to the base of standing envs from 96,401 to 96,405, t1_dh_stand_env.py:233-247,
-t1_dh_stand_config.py:197-204), so k_dyn4's fused draw, its critic-frame terms and `applied_force` are compared.
+t1_dh_stand_config.py:197-204), so the kernel's fused draw, its critic-frame terms and `applied_force` are compared.
 """
 import numpy as np
 import pytest
@@ -56,7 +60,7 @@ def oracle_for(env, push):
 
 
 class Replay:
-    """physics(g, torques, state) for the oracle: the k_dyn4 substep log of the step just run."""
+    """physics(g, torques, state) for the oracle: the step kernel's substep log of the step just run."""
 
     def __init__(self, env):
         lg = env.substep_log
@@ -106,7 +110,7 @@ def compare(env, o, rp, step):
     # last _add_ext_force value, consumed by the next step's first substep: force_pending)
     af = o.applied_force[:, 0, :] if o.force_pending else np.zeros((env.num_envs, 3), np.float32)
     assert_close("applied_force", np_(env.applied_force), af, ctx=ctx)
-    # the lag sample k_dyn4 captured (ring slot of step ctr - lag // 10) vs the dof_lag_buffer entry the observation
+    # the lag sample the step kernel captured (ring slot of step ctr - lag // 10) vs the dof_lag_buffer entry the observation
     # reads (index dof_lag_timestep): (q, qd) of substep 9 - lag % 10
     ctr = env.common_step_counter - 1
     lag = o.dof_lag_timestep

@@ -121,18 +121,27 @@ def test_sharded_mixed_kernels_agree(tmp_path, monkeypatch):
     shards = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     n = n_per_rank * world
     rows = np.zeros(n, bool)   # envs that took a different discrete branch at this or an earlier step
-    report = []
+    report, stated = [], []
     for t in range(STEPS):
         got = {k: np.concatenate([s[f"{k}_{t}"] for s in shards], 0) for k in KEYS}
-        rows |= got["reset_buf"] != full[t]["reset_buf"]
+        new_reset = (got["reset_buf"] != full[t]["reset_buf"]) & ~rows
+        rows |= new_reset
         rel = np.zeros(n)
         for k in FLOAT_KEYS:
             a, b = got[k].astype(np.float64).reshape(n, -1), full[t][k].astype(np.float64).reshape(n, -1)
             rel = np.maximum(rel, (np.abs(a - b) / (1.0 + np.abs(b))).max(axis=1))
-        rows |= rel > FLOAT_TOL
+        new_gap = (rel > FLOAT_TOL) & ~rows
+        rows |= new_gap
         q = np.quantile(rel[~rows], [0.5, 0.99, 0.999, 1.0]) if (~rows).any() else [0.0] * 4
-        report.append(f"step {t}: branched rows {int(rows.sum())}, gap quantiles 50/99/99.9/100% "
-                      + " ".join(f"{v:.1e}" for v in q))
+        # the exempted rows as a stated result: how many, and why (a differing reset decision, or a float gap past the
+        # bound: a contact / threshold event taken on one side only), per step and in total
+        stated.append({"step": t, "exempt_total": int(rows.sum()), "new_by_reset": int(new_reset.sum()),
+                       "new_by_float_gap": int(new_gap.sum()), "exempt_frac": float(rows.mean()),
+                       "gap_quantiles_50_99_999_100": [float(v) for v in q]})
+        report.append(f"step {t}: exempted rows {int(rows.sum())} of {n} (new: {int(new_reset.sum())} by a differing "
+                      f"reset, {int(new_gap.sum())} by a float gap > {FLOAT_TOL:g}), gap quantiles of the rest "
+                      "50/99/99.9/100% " + " ".join(f"{v:.1e}" for v in q))
+        print(report[-1])
         assert rows.mean() <= MAX_ROW_FRAC, f"step {t}: {int(rows.sum())} rows branched\n" + "\n".join(report)
         for k in KEYS:
             if k not in FLOAT_KEYS:
@@ -141,3 +150,9 @@ def test_sharded_mixed_kernels_agree(tmp_path, monkeypatch):
         for s in shards:
             np.testing.assert_array_equal(s[f"cmd_range_{t}"], full[t]["cmd_range"], err_msg=f"command range step {t}")
     print("k_dyn6 shards vs k_dyn4 whole:\n" + "\n".join(report))
+    out = os.environ.get("T1_TEST_REPORT_DIR")
+    if out:   # the GPU runs keep it (profiles/*_sharding_exempt_rows.json)
+        import json
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "sharding_mixed_kernels_exempt_rows.json"), "w") as f:
+            json.dump({"envs": n, "float_tol": FLOAT_TOL, "max_row_frac": MAX_ROW_FRAC, "steps": stated}, f, indent=1)

@@ -114,6 +114,7 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"libt1env_hip.so not built ({LIB_PATH}); run `python -m ti5_isaacgym_amd.build`")
     lib = C.CDLL(LIB_PATH)
+    check_stamp(lib, LIB_PATH)
     P = C.POINTER
     vp = C.c_void_p
     sig = {
@@ -162,6 +163,24 @@ def load():
         fn.restype = res
     _lib = lib
     return lib
+
+
+def check_stamp(lib, path):
+    """Refuse a library built from other sources than this tree's (build.source_stamp, compiled into t1env_version):
+    a stale product or guard library would otherwise fail later with a missing symbol or, worse, run old code.  Skipped
+    when the sources are not present (an installed copy) or T1ENV_SKIP_STAMP=1."""
+    from . import build as _build
+    if os.environ.get("T1ENV_SKIP_STAMP") == "1" or not _build.DEPS:
+        return
+    fn = lib.t1env_version
+    fn.argtypes, fn.restype = [], C.c_char_p
+    ver = fn().decode()
+    got = ver.split("src:", 1)[1].strip() if "src:" in ver else None
+    want = _build.source_stamp()
+    if got != want:
+        raise RuntimeError(f"{path} is stale: built from sources {got or '(unstamped)'}, this tree's are {want}; "
+                           "rebuild it (python -m ti5_isaacgym_amd.build, or __graft_entry__.build() for the guard "
+                           "library too)")
 
 
 def check(rc, what):

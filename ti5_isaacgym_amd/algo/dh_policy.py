@@ -118,8 +118,26 @@ def bias_grad(gy):
 
 
 # ... added by that kernel straight into an existing .grad of the layer's leaf parameters (T1_GRAD_DIRECT=0: returned
-# to autograd, which adds them, A/B)
+# to autograd, which adds them, A/B).  Only inside direct_grad_accumulation(), which DHPPO opens around its own
+# loss.backward(): anywhere else (torch.autograd.grad, backward(inputs=...), a caller's own backward) the gradients go
+# back through autograd, so what autograd returns and which .grad it touches are exactly torch's.
 GRAD_DIRECT = os.environ.get("T1_GRAD_DIRECT", "1") != "0"
+# a module flag, not a contextvar: autograd runs a CUDA node's backward on its device worker thread, which does not
+# see the calling thread's context variables
+_DIRECT_GRAD = [False]
+
+
+@contextlib.contextmanager
+def direct_grad_accumulation(enabled=True):
+    """Within the block, a backward() of _LinearSplitK under the bf16 update may add its weight / bias gradients straight
+    into the leaf parameters' existing fp32 .grad (returning None to autograd for them).  Valid only around a plain
+    loss.backward() that accumulates into every parameter's .grad -- DHPPO's minibatch step."""
+    prev = _DIRECT_GRAD[0]
+    _DIRECT_GRAD[0] = bool(enabled)
+    try:
+        yield
+    finally:
+        _DIRECT_GRAD[0] = prev
 # the bf16 update's Linear weight + bias gradients as one HIP MFMA kernel (t1policy_linear_wgrad_bf16); T1_LINEAR_WGRAD=0:
 # the split-K batched GEMM + slice sum + torch's bias sum (A/B)
 LINEAR_WGRAD = os.environ.get("T1_LINEAR_WGRAD", "1") != "0"
@@ -220,7 +238,7 @@ class _LinearSplitK(torch.autograd.Function):
         if LINEAR_WGRAD and gy.is_cuda and gy.dtype == torch.bfloat16 and ctx.needs_input_grad[1]:
             wl, bl = ctx.leaves
             need_b = ctx.needs_input_grad[2]
-            if (GRAD_DIRECT and wl is not None and wl.grad is not None and wl.grad.dtype == torch.float32
+            if (GRAD_DIRECT and _DIRECT_GRAD[0] and wl is not None and wl.grad is not None and wl.grad.dtype == torch.float32
                     and wl.grad.is_contiguous() and (not need_b or (bl is not None and bl.grad is not None
                                                                     and bl.grad.dtype == torch.float32))):
                 # the weight / bias gradients added straight into the existing .grad (the PPO update's views into
@@ -332,10 +350,62 @@ def packed_conv_weights(conv, stream=None, force=False):
 
 def refresh_packed_weights(module, force=False):
     """Repack every Conv1d under `module` whose packed fragments are stale (before replaying a captured act()), or
-    every packed one (force: after an update whose optimizer steps were graph replays)."""
+    every packed one (force: after an update whose optimizer steps were graph replays); likewise the fused heads'
+    fragments of a policy that has them."""
     for m in module.modules():
         if isinstance(m, nn.Conv1d) and getattr(m, "_t1_frag", None) is not None:
             packed_conv_weights(m, force=force)
+        if getattr(m, "_t1_heads_frag", None) is not None:
+            packed_heads_weights(m, force=force)
+
+
+def _heads_args(ac, layers):
+    """The heads kernel's (pointer array, dims array, version key) of the policy's parameters, or None for a layer the
+    kernel cannot read (not fp32 / not contiguous)."""
+    import ctypes as C
+    dims, ptrs, key = [], [], []
+    for m in layers:
+        w = m.weight
+        if w.dtype != torch.float32 or not w.is_contiguous() or not m.bias.is_contiguous():
+            return None
+        dims += [w.shape[0], w[0].numel()]
+        ptrs += [w.data_ptr(), m.bias.data_ptr()]
+        key += [(w._version, w.data_ptr()), (m.bias._version, m.bias.data_ptr())]
+    ptrs.append(ac.std.data_ptr())
+    key.append((ac.std._version, ac.std.data_ptr()))
+    return (C.c_uint64 * 31)(*ptrs), (C.c_int * 30)(*dims), tuple(key)
+
+
+def packed_heads_weights(ac, stream=None, force=False):
+    """The fused heads' weights as the kernel's split fp16 fragments (t1policy_heads_pack, 3.6 MB), kept on the policy and
+    repacked only when a parameter changed -- the conv's rule (packed_conv_weights): an eager change moves a version
+    counter, a graph-replayed optimizer step does not, so DHPPO.update() repacks with force=True after every update and
+    DHPPO._graphed_act refreshes before each replay.  The pack ran on every act() before (5 us of 0.14 ms, VERDICT r5
+    #4).  Returns (frag, ptrs, dims), or None when the model has no compiled instance."""
+    from .. import _lib
+    layers = _heads_layers(ac)
+    if layers is None:
+        return None
+    args = _heads_args(ac, layers)
+    if args is None:
+        return None
+    ptrs_c, dims_c, key = args
+    dev = ac.std.device
+    frag = getattr(ac, "_t1_heads_frag", None)
+    if not force and frag is not None and frag.device == dev and getattr(ac, "_t1_heads_key", None) == key:
+        return frag, ptrs_c, dims_c
+    lib = _lib.load()
+    if frag is None or frag.device != dev:
+        frag = torch.empty(lib.t1policy_heads_frag_bytes(), device=dev, dtype=torch.uint8)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    rc = lib.t1policy_heads_pack(ptrs_c, dims_c, frag.data_ptr(), stream)
+    if rc == 1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"t1policy_heads_pack failed (rc={rc})")
+    ac._t1_heads_frag, ac._t1_heads_key = frag, key
+    return frag, ptrs_c, dims_c
 
 
 # the update's first history conv as HIP kernels under the bf16 update (T1_CONV1_TRAIN=0: unfold + GEMM, A/B)
@@ -430,10 +500,9 @@ def heads_forward(ac, obs, critic_obs, eps):
     """The rollout's act() after the first conv as the fused HIP kernel (t1policy_heads_forward): returns mean,
     actions = mean + std eps, sigma (B, 12), log-prob (B,) and value (B, 1) -- DHPPO._act_body's outputs -- or None
     when the model or inputs have no compiled instance (the caller keeps the torch path).  The weights are packed
-    into the kernel's split fp16 fragments on every call (3.6 MB, inside a captured act() graph too), so they always
-    follow the parameters."""
+    into the kernel's split fp16 fragments when a parameter changed (packed_heads_weights); a captured act() graph
+    reads them in place and is refreshed before each replay."""
     from .. import _lib
-    import ctypes as C
     layers = _heads_layers(ac)
     if (layers is None or not obs.is_cuda or obs.dtype != torch.float32 or critic_obs.dtype != torch.float32
             or obs.dim() != 2 or critic_obs.dim() != 2 or eps.shape != (obs.shape[0], ac.std.numel())):
@@ -444,31 +513,19 @@ def heads_forward(ac, obs, critic_obs, eps):
             or critic_obs.shape[1] != layers[11].in_features):
         return None
     lib = _lib.load()
-    dims, ptrs = [], []
-    for m in layers:
-        w = m.weight
-        if w.dtype != torch.float32 or not w.is_contiguous() or not m.bias.is_contiguous():
-            return None
-        dims += [w.shape[0], w[0].numel()]
-        ptrs += [w.data_ptr(), m.bias.data_ptr()]
-    ptrs.append(ac.std.data_ptr())
-    dims_c = (C.c_int * 30)(*dims)
-    ptrs_c = (C.c_uint64 * 31)(*ptrs)
+    if _heads_args(ac, layers) is None or ac.std.device != obs.device:
+        return None
     dev = obs.device
-    frag = getattr(ac, "_t1_heads_frag", None)
-    if frag is None or frag.device != dev:
-        frag = ac._t1_heads_frag = torch.empty(lib.t1policy_heads_frag_bytes(), device=dev, dtype=torch.uint8)
     stream = torch.cuda.current_stream(dev).cuda_stream
     obs = obs.contiguous()
     B = obs.shape[0]
     y1 = conv1d_direct(obs.view(B, ac.in_channels, ac.num_proprio_obs), ac.long_history[0])
     if y1 is None:
         return None
-    rc = lib.t1policy_heads_pack(ptrs_c, dims_c, frag.data_ptr(), stream)
-    if rc == 1:
+    packed = packed_heads_weights(ac, stream)   # repacked only when a parameter changed
+    if packed is None:
         return None
-    if rc != 0:
-        raise RuntimeError(f"t1policy_heads_pack failed (rc={rc})")
+    frag, ptrs_c, dims_c = packed
     critic_obs, eps = critic_obs.contiguous(), eps.contiguous()
     na = ac.std.numel()
     mean = torch.empty(B, na, device=dev)

@@ -265,7 +265,8 @@ class DHPPO:
                t.actions_log_prob, t.action_mean, t.action_sigma)
         if any(x is not None and not x.is_cuda for x in ins) or t.next_proprio_obs is not None:
             return False
-        key = (k,) + tuple(x.data_ptr() if x is not None else 0 for x in ins)
+        # the slot and every input's address, shape and dtype (a replay reads exactly the tensors it was captured on)
+        key = (k,) + tuple((x.data_ptr(), tuple(x.shape), x.dtype) if x is not None else 0 for x in ins)
         g = self._store_graphs.get(key)
         if g is None:
             if len(self._store_graphs) >= 4 * self.storage.num_transitions_per_env:
@@ -349,7 +350,8 @@ class DHPPO:
         finally:
             self._kl_deferred = False
         self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
-        loss.backward()
+        with dh_policy.direct_grad_accumulation():   # a plain backward into every .grad: the wgrad kernel may add there
+            loss.backward()
         self._sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), se_loss.detach()])
 
     def _dp_exchange(self):
@@ -390,7 +392,8 @@ class DHPPO:
                 ac, obs_b, critic_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b,
                 hid_b, masks_b, mse)
         self.optimizer.zero_grad(set_to_none=False)   # keep the .grad views into the all-reduce bucket
-        loss.backward()
+        with dh_policy.direct_grad_accumulation():   # a plain backward into every .grad: the wgrad kernel may add there
+            loss.backward()
         self.grads.all_reduce_()
         self._clip_grads()
         self.optimizer.step()
@@ -464,7 +467,9 @@ class DHPPO:
         for _ in range(self.num_learning_epochs):
             for i in range(self.num_mini_batches):
                 self._idx.copy_(perm[i * mb:(i + 1) * mb])
-                if self._upd is not None:
+                if not self.graph_update:   # a capture failed earlier in this update: the rest runs eagerly
+                    self._step_eager(take(self._idx), amp, mse)
+                elif self._upd is not None:
                     if dp:
                         self._upd[1][0].replay()
                         self._dp_exchange()
@@ -480,21 +485,62 @@ class DHPPO:
                     cur.wait_stream(side)
                     self._upd_warm += 1
                 elif dp:
+                    # every rank captures part A, then they agree on its success before the first exchange: a rank
+                    # whose capture failed must not leave the others waiting in the bucket all-reduce.  On a
+                    # failure every rank runs this minibatch and the rest of the update eagerly.
                     ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(ga):
-                        self._dp_part_a(take(self._idx), amp, mse)
+                    err = self._try_capture(ga, lambda: self._dp_part_a(take(self._idx), amp, mse))
+                    if not self._all_ranks_ok(err is None):
+                        self._capture_failed(err)
+                        self._step_eager(take(self._idx), amp, mse)
+                        continue
                     ga.replay()
                     self._dp_exchange()
-                    with torch.cuda.graph(gb):
+                    err = self._try_capture(gb, self._dp_part_b)
+                    if not self._all_ranks_ok(err is None):
+                        # the exchange already ran: finish this minibatch eagerly (part B alone), the rest eager too
+                        self._capture_failed(err)
                         self._dp_part_b()
+                        continue
                     gb.replay()
                     self._upd = (self._graph_key(mb, take), (ga, gb))
                 else:
                     graph = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(graph):
-                        self._minibatch_step(take(self._idx), amp, mse)
+                    err = self._try_capture(graph, lambda: self._minibatch_step(take(self._idx), amp, mse))
+                    if err is not None:
+                        self._capture_failed(err)
+                        self._step_eager(take(self._idx), amp, mse)
+                        continue
                     self._upd = (self._graph_key(mb, take), graph)
                     graph.replay()
+
+    @staticmethod
+    def _try_capture(graph, body):
+        """Capture body() into graph; the RuntimeError of a failed capture, else None."""
+        try:
+            with torch.cuda.graph(graph):
+                body()
+        except RuntimeError as e:
+            return e
+        return None
+
+    @staticmethod
+    def _all_ranks_ok(ok):
+        """Every rank's capture succeeded (a MIN all-reduce of the flags under data parallelism)."""
+        if not dist_util.active():
+            return ok
+        import torch.distributed as dist
+        f = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                         device=torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl"
+                         else "cpu")
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        return bool(f.item())
+
+    def _capture_failed(self, err):
+        warnings.warn(f"DHPPO: update graph capture failed ({err if err is not None else 'on another rank'}); "
+                      "the update runs eagerly")
+        self.graph_update = False
+        self._upd = None
 
     def _graph_key(self, mb, take):
         """Everything a captured minibatch step holds as a constant: the buffers' addresses (storage sources, Adam's

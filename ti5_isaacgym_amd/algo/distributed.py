@@ -112,4 +112,5 @@ class GradientBucket:
             x = p.data.to(_comm_device(p))
             dist.broadcast(x, src)
             if x is not p.data:
-                p.data.copy_(x)
+                with torch.no_grad():
+                    p.copy_(x)   # through the parameter (not .data): its version counter moves, so packed weights follow

@@ -14,6 +14,8 @@ dones -- the same bits as the full rows.  Callers whose observations are not suc
 """
 import os
 
+import warnings
+
 import torch
 
 from . import distributed as dist_util
@@ -158,9 +160,14 @@ class RolloutStorage:
                 self._gae_lv = last_values.clone()
                 self._gae(self._gae_lv, gamma, lam)   # this call eagerly; captured for the next ones
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._gae(self._gae_lv, gamma, lam)
-                self._gae_graph = (key, g)
+                try:
+                    with torch.cuda.graph(g):
+                        self._gae(self._gae_lv, gamma, lam)
+                    self._gae_graph = (key, g)
+                except RuntimeError as e:   # as DHPPO's graphed store: fall back to the eager pass
+                    warnings.warn(f"RolloutStorage: GAE graph capture failed, running eager: {e}")
+                    # nothing runs during a capture: the eager pass above already produced this call's results
+                    self.graph_gae, self._gae_graph = False, None
             else:
                 self._gae_lv.copy_(last_values)
                 self._gae_graph[1].replay()

@@ -25,6 +25,20 @@ DEPS = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CS
 ARCH = os.environ.get("T1ENV_ARCH", "gfx950")
 
 
+def source_stamp():
+    """A hash of every source and header the library is built from (DEPS), compiled into t1env_version() so that
+    _lib.load() refuses a library built from other sources (a stale guard library failed with an undefined
+    symbol instead of a clear message)."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in DEPS:
+        h.update(os.path.basename(d).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
 def build(force=False, extra=(), out=None, dyn_opt=None):
     """dyn_opt: optimisation level of the dynamics unit for A/B and guard variants (default -O1)."""
     out = out or OUT
@@ -34,7 +48,8 @@ def build(force=False, extra=(), out=None, dyn_opt=None):
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     # -fno-slp-vectorize: the SLP pass packs scalar pairs of the dynamics into v_pk_* ops, which forces aligned
     # register pairs and piles up v_mov shuffles; in k_dynamics that alone turned ~40 scratch ops into ~470.
-    common = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result", "-fno-slp-vectorize", *extra]
+    common = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result", "-fno-slp-vectorize",
+              f'-DT1_SOURCE_STAMP="{source_stamp()}"', *extra]
     objs, procs = [], []
     for src, opt in UNITS:  # the units compile concurrently
         if dyn_opt and src in ("t1env_dynamics.hip", "t1env_dyn5.hip", "t1env_dyn6.hip"):

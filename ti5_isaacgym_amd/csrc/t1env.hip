@@ -432,7 +432,10 @@ static void t_end(t1env* e, int i, hipStream_t s) {
 extern "C" {
 
 const char* t1env_last_error(void) { return g_err; }
-const char* t1env_version(void) { return "t1env-hip 0.1 (gfx950)"; }
+#ifndef T1_SOURCE_STAMP  // ti5_isaacgym_amd/build.py source_stamp(): the hash of the sources this library is built from
+#define T1_SOURCE_STAMP "unstamped"
+#endif
+const char* t1env_version(void) { return "t1env-hip 0.1 (gfx950) src:" T1_SOURCE_STAMP; }
 
 // one EP_PART_ROW-float row per k_dyn4 dynamics workgroup
 // one row per dynamics workgroup: k_dyn5 has 32 envs per workgroup (k_dyn4 64)

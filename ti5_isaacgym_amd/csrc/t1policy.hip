@@ -419,6 +419,11 @@ __global__ __launch_bounds__(256) void k_history_rows_w16(const uint16_t* __rest
   const bool odd = (r.src & 1) != 0;  // wave-uniform
   const uint32_t* sw = reinterpret_cast<const uint32_t*>(seq) + (r.src >> 1);  // the word holding the first element
   uint32_t* dw = reinterpret_cast<uint32_t*>(out + (int64_t)m * 2 * nw);
+  // seq holds N * (frames + T - 1) * frame elements: with an odd count its last word is half outside the buffer.  An odd
+  // window ending on the last element reads that element from the word past it (hi): clamp the word to the last whole one
+  // and take the element by a 16-bit load instead
+  const int64_t tot = (int64_t)N * (frames + T - 1) * frame;
+  const int64_t hi_max = tot / 2 - 1 - (r.src >> 1);  // the last whole word, relative to sw
   for (int j0 = 0; j0 < nw; j0 += 64 * HR_BURST) {
     uint32_t lo[HR_BURST], hi[HR_BURST];
 #pragma unroll
@@ -426,12 +431,14 @@ __global__ __launch_bounds__(256) void k_history_rows_w16(const uint16_t* __rest
       int j = j0 + 64 * u + lane;
       j = j < nw ? j : nw - 1;
       lo[u] = sw[j];
-      hi[u] = sw[odd ? j + 1 : j];
+      const int64_t jh = odd ? j + 1 : j;
+      hi[u] = sw[jh < hi_max ? jh : hi_max];
     }
 #pragma unroll
     for (int u = 0; u < HR_BURST; ++u) {
       const int j = j0 + 64 * u + lane;
       if (j >= nw) continue;
+      if (odd && j + 1 > hi_max) hi[u] = seq[r.src + 2 * (int64_t)j + 1];  // the buffer's last element (rare)
       uint32_t w = odd ? (lo[u] >> 16) | (hi[u] << 16) : lo[u];
       if (2 * j + 1 < r.zlen) w = 0u;
       else if (2 * j < r.zlen) w &= 0xffff0000u;
