@@ -259,8 +259,18 @@ def main():
         name = FUSED_KERNEL if (fused and k == "k_dynamics") else k
         per_kernel[name] = {"avg_ms": round(ms, 5), "timed_launches": kt[k]["launches"], "alg_bytes_per_launch": alg,
                             "alg_GBs": round(alg / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
-    dom = max(per_kernel, key=lambda k: per_kernel[k]["avg_ms"] * per_kernel[k]["timed_launches"])
     step_span_ms = kt["step"]["ms"] / kt["step"]["launches"] if kt["step"]["launches"] else None
+    # config 5 (k_dyn4, fp16 histories): the history shift runs as a concurrent launch (k_shift4c) on a second stream
+    # beside the dynamics (T1ENV_D4_SHIFT, default on), so neither launch's own span is the step's: the pair is timed
+    # as the step's fork-to-join span with the whole B_alg
+    conc = pre_shift and FUSED_KERNEL == "k_dyn4" and os.environ.get("T1ENV_D4_SHIFT", "1") != "0"
+    if conc and step_span_ms:
+        per_kernel["k_dyn4 || k_shift4c"] = {
+            "avg_ms": round(step_span_ms, 5), "timed_launches": kt["step"]["launches"], "alg_bytes_per_launch": b_alg * N,
+            "alg_GBs": round(b_alg * N / (step_span_ms * 1e-3) / 1e9, 1), "note": "concurrent pair, fork-to-join span"}
+        dom = "k_dyn4 || k_shift4c"
+    else:
+        dom = max(per_kernel, key=lambda k: per_kernel[k]["avg_ms"] * per_kernel[k]["timed_launches"])
     # roofline of the dominant kernel: its algorithmic bytes per launch (SURVEY.md §8(d) B_alg x envs when the launch
     # is the whole fused step) / its live HIP-event launch duration.  Without sampled events (--time-every 0) fall
     # back to the wall clock of the timed steps (env_steps_per_s x B_alg).
@@ -345,6 +355,10 @@ def main():
                      "kernels": per_kernel},
         "finite": ok,
         "dist": dist_info,
+        # the history buffers' device addresses (A/B records: step-time modes across processes vs buffer placement)
+        "buffers": {k: hex(t.data_ptr()) for k, t in (("obs0", env._obs[0]), ("obs1", env._obs[1]),
+                                                      ("priv0", env._priv[0]), ("priv1", env._priv[1]))}
+                   if hasattr(env, "_priv") else None,
     }
     if len(reps) > 1:
         line["repeats"] = len(reps)

@@ -195,9 +195,8 @@ __global__ __launch_bounds__(256) void k_shift(ShiftArgs S) {
 // k_dyn4 protocol, t1env_fused.h) -- whichever of the shift and k_dyn5's epilogue finishes a unit last zeroes its
 // reset rows.  Not FUSED (the split step): k_post_b zeroes them after the caller's join.
 // ---------------------------------------------------------------------------------------------------
-template <bool FUSED>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8)))
-void k_shift5(ShiftArgs S, FusedArgs FA, int N) {
+template <bool FUSED, int U>
+__device__ __forceinline__ void shift_conc_body(ShiftArgs S, FusedArgs FA, int N) {
   __shared__ uint32_t words[256];
   const int units = (N + SHIFT_UNIT - 1) / SHIFT_UNIT;
   const int nsw = gridDim.x, j = blockIdx.x;
@@ -206,7 +205,7 @@ void k_shift5(ShiftArgs S, FusedArgs FA, int N) {
   const int mine = u1 - u0;
   if (mine > 0) {
     const int64_t r0 = (int64_t)u0 * SHIFT_UNIT, r1 = (int64_t)u1 * SHIFT_UNIT < N ? (int64_t)u1 * SHIFT_UNIT : N;
-    shift_rows_range_sc1<T1_D5_SHIFT_UNROLL>(S, r0, r1, threadIdx.x, 256);
+    shift_rows_range_sc1<U>(S, r0, r1, threadIdx.x, 256);
   }
   if constexpr (FUSED) {
     // every lane's sc1 stores complete (visible at agent scope) before any handoff
@@ -224,11 +223,34 @@ void k_shift5(ShiftArgs S, FusedArgs FA, int N) {
   }
 }
 
-int t1_launch_shift5(const ShiftArgs& S, const FusedArgs* fused, int num_envs, int cus, hipStream_t s) {
+template <bool FUSED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8)))
+void k_shift5(ShiftArgs S, FusedArgs FA, int N) {
+  shift_conc_body<FUSED, T1_D5_SHIFT_UNROLL>(S, FA, N);
+}
+
+// k_shift4c: the same concurrent shift beside k_dyn4 (config 5: 32768 envs, fp16 histories).  A k_dyn4
+// wave holds 433 of a SIMD's 512 registers per lane, so a shift wave must stay within 72 (amdgpu_waves_per_eu(7, 8)) to
+// share the SIMD; its 148 KB of LDS leaves room for the shift's 1 KB of handoff words.
+#ifndef T1_D4_SHIFT_UNROLL
+#define T1_D4_SHIFT_UNROLL 3
+#endif
+template <bool FUSED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8)))
+void k_shift4c(ShiftArgs S, FusedArgs FA, int N) {
+  shift_conc_body<FUSED, T1_D4_SHIFT_UNROLL>(S, FA, N);
+}
+
+int t1_launch_shift5(const ShiftArgs& S, const FusedArgs* fused, int num_envs, int cus, hipStream_t s, bool beside4) {
   const int units = (num_envs + SHIFT_UNIT - 1) / SHIFT_UNIT;
   const int grid = units < cus ? units : cus;
-  if (fused) hipLaunchKernelGGL(k_shift5<true>, dim3(grid), dim3(256), 0, s, S, *fused, num_envs);
-  else hipLaunchKernelGGL(k_shift5<false>, dim3(grid), dim3(256), 0, s, S, FusedArgs{}, num_envs);
+  if (beside4) {
+    if (fused) hipLaunchKernelGGL(k_shift4c<true>, dim3(grid), dim3(256), 0, s, S, *fused, num_envs);
+    else hipLaunchKernelGGL(k_shift4c<false>, dim3(grid), dim3(256), 0, s, S, FusedArgs{}, num_envs);
+  } else {
+    if (fused) hipLaunchKernelGGL(k_shift5<true>, dim3(grid), dim3(256), 0, s, S, *fused, num_envs);
+    else hipLaunchKernelGGL(k_shift5<false>, dim3(grid), dim3(256), 0, s, S, FusedArgs{}, num_envs);
+  }
   return (int)hipGetLastError();
 }
 
@@ -494,6 +516,9 @@ int t1env_create(const t1env_model* model, const t1env_config* cfg, const t1env_
     e->dyn.d5_shift = 0;
     if (const char* ds = getenv("T1ENV_D5_SHIFT"))  // A/B: 1 = the shift as a concurrent launch (k_shift5)
       if (atoi(ds) == 0 || atoi(ds) == 1) e->dyn.d5_shift = atoi(ds);
+    e->dyn.d4_shift = 1;
+    if (const char* ds = getenv("T1ENV_D4_SHIFT"))  // A/B: 0 = k_dyn4's stand-alone shift ahead of it, in stream order
+      if (atoi(ds) == 0 || atoi(ds) == 1) e->dyn.d4_shift = atoi(ds);
     if (const char* sd = getenv("T1ENV_SHIFT_DELAY"))  // tuning: delayed start of the in-launch shift (100 MHz ticks)
       if (atoi(sd) >= 0) e->dyn.shift_delay = atoi(sd);
   }
@@ -573,16 +598,26 @@ static int launch_shift(t1env* e, const t1env_step_args* a, hipStream_t s) {
   return 0;
 }
 
-// k_dyn5 with the concurrent shift (DynLaunch::d5_shift): the side stream starts after everything enqueued on s so far
-// (fork), runs k_shift5 beside the dynamics launch, and s waits for it before anything after the step (join)
-static bool concurrent_shift(const t1env* e) { return e->dyn.waves == 5 && e->dyn.d5_shift == 1; }
+// The concurrent shift: k_dyn5 with DynLaunch::d5_shift, or k_dyn4 where its shift would otherwise run as its own
+// launch ahead of it (t1_shift_prelaunch: config 5) with DynLaunch::d4_shift.  The side stream starts after everything
+// enqueued on s so far (fork), runs the shift beside the dynamics launch, and s waits for it before anything after the
+// step (join).  The fused epilogue and the shift hand each 8-row unit off (the k_dyn4 protocol, t1env_fused.h).
+static bool concurrent_shift4(const t1env* e) {
+  return e->dyn.waves == 4 && e->dyn.d4_shift == 1 && t1_shift_prelaunch(e->cfg.num_envs, e->dyn);
+}
+static bool concurrent_shift(const t1env* e) {
+  return (e->dyn.waves == 5 && e->dyn.d5_shift == 1) || concurrent_shift4(e);
+}
 static int shift_fork(t1env* e, hipStream_t s) {
   HIP_TRY(hipEventRecord(e->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fork, 0));
   return 0;
 }
 static int shift_join(t1env* e, const t1env_step_args* a, const FusedArgs* fa, hipStream_t s) {
-  HIP_TRY((hipError_t)t1_launch_shift5(shift_args(e, a), fa, e->cfg.num_envs, e->dyn.cus, e->side));
+  const int t = t_begin(e, 3, e->side);  // the shift's own span, on its stream (bench.py: k_shift)
+  HIP_TRY((hipError_t)t1_launch_shift5(shift_args(e, a), fa, e->cfg.num_envs, e->dyn.cus, e->side,
+                                       e->dyn.waves == 4));
+  t_end(e, t, e->side);
   HIP_TRY(hipEventRecord(e->ev_join, e->side));
   HIP_TRY(hipStreamWaitEvent(s, e->ev_join, 0));
   return 0;
@@ -594,11 +629,12 @@ static int launch_physics(t1env* e, const float* actions, const t1env_step_args*
   if (e->log_on && !inj) return fail(T1ENV_E_STATE, "substep log set: only the fused step logs (t1env_set_substep_log)");
   const int N = e->cfg.num_envs;
   e->step_timer = t_begin(e, 5, s);
-  // large N: the shift as its own launch ahead of the dynamics (k_post_b zeroes the reset rows)
-  const bool pre = !inj && t1_shift_prelaunch(N, e->dyn);
-  if (pre)
-    if (int rc = launch_shift(e, a, s)) return rc;
+  // large N: the shift as its own launch, ahead of the dynamics or beside them (k_post_b zeroes the reset rows after
+  // the join)
   const bool conc = !inj && concurrent_shift(e);
+  const bool pre = !inj && t1_shift_prelaunch(N, e->dyn);
+  if (pre && !conc)
+    if (int rc = launch_shift(e, a, s)) return rc;
   if (conc)
     if (int rc = shift_fork(e, s)) return rc;
   int t = t_begin(e, 0, s);
@@ -659,16 +695,16 @@ int t1env_step_reset_and_observe(t1env* e, const t1env_step_args* a, void* strea
 static int launch_fused(t1env* e, const float* actions, const t1env_step_args* a, hipStream_t s) {
   if (a->obs_slot != 0 && a->obs_slot != 1) return fail(T1ENV_E_ARG, "obs_slot must be 0 or 1");
   e->step_timer = t_begin(e, 5, s);
-  // large N: no idle CUs for shift workgroups -- the shift runs as its own launch first, the epilogue then
-  // zeroes the reset rows without the handoff
-  const bool pre = t1_shift_prelaunch(e->cfg.num_envs, e->dyn);
-  if (pre)
-    if (int rc = launch_shift(e, a, s)) return rc;
+  // large N: no idle CUs for shift workgroups -- the shift runs as its own launch, beside the dynamics (concurrent:
+  // the epilogue hands its reset rows off) or first (the epilogue then zeroes them without the handoff)
   const bool conc = concurrent_shift(e);
+  const bool pre = t1_shift_prelaunch(e->cfg.num_envs, e->dyn);
+  if (pre && !conc)
+    if (int rc = launch_shift(e, a, s)) return rc;
   if (conc)
     if (int rc = shift_fork(e, s)) return rc;
   const int t = t_begin(e, 0, s);
-  const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch, pre ? 1 : 0, e->d_ep_part};
+  const FusedArgs FA{e->d_done, e->d_unit_state, ++e->epoch, (pre && !conc) ? 1 : 0, e->d_ep_part};
   HIP_TRY((hipError_t)t1_launch_dynamics(e->d_model, e->d_cfg, e->buf, e->terrain, actions, *a, e->cfg.num_envs,
                                          shift_args(e, a), e->dyn, &FA, s, pre, e->log_on ? &e->log : nullptr));
   t_end(e, t, s);

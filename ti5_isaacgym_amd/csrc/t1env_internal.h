@@ -43,6 +43,9 @@ struct DynLaunch {
   int shift_delay;   // in-launch shift workgroups start this many 100 MHz ticks late (T1ENV_SHIFT_DELAY; 0 = at once)
   int d5_shift;      // k_dyn5's history shift: 0 = in the workgroup through LDS-DMA (default), 1 = a concurrent launch
                      // on a second stream (k_shift5; T1ENV_D5_SHIFT=1, A/B: the same step time, r04e)
+  int d4_shift;      // k_dyn4's history shift where the dynamics fill the CUs (t1_shift_prelaunch, config 5): 1 = a
+                     // concurrent launch on a second stream beside the dynamics (k_shift4c, the default), 0 = its own
+                     // launch ahead of them in stream order (T1ENV_D4_SHIFT=0, A/B)
 };
 int t1_dyn_waves_default(int num_envs, int cus, bool obs_half);
 
@@ -68,4 +71,6 @@ int t1_launch_dyn6(const t1::DynModel* d_model, const t1env_config* d_cfg, const
                    const FusedArgs* fused, hipStream_t s, const SubLog* log);
 // k_dyn5's history shift as its own launch (k_shift5), for a second stream beside k_dyn5 (d5_shift = 1); fused: the
 // unit handoff with the fused epilogue, else plain (k_post_b zeroes the reset rows)
-int t1_launch_shift5(const t1::ShiftArgs& S, const FusedArgs* fused, int num_envs, int cus, hipStream_t s);
+// beside4: the k_dyn4 form (k_shift4c, <= 72 registers per lane so a wave fits beside a k_dyn4 wave on its SIMD)
+int t1_launch_shift5(const t1::ShiftArgs& S, const FusedArgs* fused, int num_envs, int cus, hipStream_t s,
+                     bool beside4 = false);
