@@ -82,6 +82,15 @@ int t1policy_conv1_forward_bf16(const void* x, const void* frag, const float* bi
 int t1policy_conv1_wgrad_bf16(const void* x, const void* gy, void* workspace, float* grad_weight, float* grad_bias,
                               int batch, int channels, int length, int out_channels, int kernel, int stride,
                               void* stream);
+/* The same weight gradient on fp32 x (batch, channels, length) and gy (batch, Lout, out_channels) -- the fp32 update,
+ * the reference's precision (dh_ppo.py:155-182) -- on the matrix cores: each fp32 operand split into three bf16 parts,
+ * the six part products down to 2^-16 of each product formed by v_mfma_f32_32x32x16_bf16 and summed in fp32
+ * (fp32-class: within 2e-6 of |gy|^T |x| of the fp64 sum in tests/test_gpu_conv1_train.py); grad_bias the fp32 sum of
+ * gy.  workspace: t1policy_conv1_bf16_workspace_bytes() device bytes; the same fixed-order partial sums
+ * (deterministic).  The forward of the fp32 update is t1policy_conv1d_forward_packed (fp32-accurate, above). */
+int t1policy_conv1_wgrad_f32(const float* x, const float* gy, void* workspace, float* grad_weight, float* grad_bias,
+                             int batch, int channels, int length, int out_channels, int kernel, int stride,
+                             void* stream);
 
 /* Column sums of a (rows, cols) row-major gradient, bf16 (elem_bytes 2) or fp32 (4): out[c] = sum_r g[r, c] in fp32,
  * in a fixed order (workspace of colsum_workspace_bytes(rows, cols) device bytes): the PPO update's Linear bias
@@ -125,6 +134,14 @@ long long t1policy_linear_wgrad_workspace_bytes(int rows, int M, int N);
 int t1policy_linear_wgrad_bf16(const void* gy, const void* x, int rows, int M, int N, void* workspace,
                                long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
                                void* stream);
+/* The same on fp32 gy (rows, M) and x (rows, N) -- the fp32 update, the reference's precision (dh_ppo.py:155-182) --
+ * on the matrix cores: each fp32 value split into three bf16 parts, the six part products down to 2^-16 of each
+ * product formed by v_mfma_f32_32x32x16_bf16 and summed in fp32 (fp32-class: within 2e-6 of |gy|^T |x| of the fp64 sum
+ * in tests/test_gpu_linear_wgrad.py), grad_bias the fp32 sum of gy; the same workspace, accumulate and fixed-order
+ * sums (deterministic).  Replaces the fp32 update's split-K batched GEMM + slice sum + bias sum. */
+int t1policy_linear_wgrad_f32(const float* gy, const float* x, int rows, int M, int N, void* workspace,
+                              long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
+                              void* stream);
 
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py

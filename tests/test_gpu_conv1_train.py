@@ -112,3 +112,70 @@ def test_wgrad_splitk_uses_slice_sum_and_matches_fp64():
     ref = gy.double().t() @ x.double()
     assert gw.dtype == torch.float32
     torch.testing.assert_close(gw.double(), ref, rtol=1e-4, atol=1e-2)
+
+
+# ---- the fp32 update (the reference's precision): the fp32-accurate packed forward and the three-part-split weight
+# gradient (t1policy_conv1_wgrad_f32), both against fp64 on the fp32 operands at fp32-class bounds
+@pytest.mark.parametrize("n", [1, 777, 8192])
+def test_conv1_f32_forward_matches_fp64(n):
+    from ti5_isaacgym_amd.algo.dh_policy import conv1d_train_f32
+    conv = _conv()
+    g = torch.Generator(device=DEV).manual_seed(n + 7)
+    x = torch.randn(n, 66, 47, device=DEV, generator=g) * 2.0
+    y = conv1d_train_f32(x, conv)
+    assert y is not None and y.dtype == torch.float32 and y.shape == (n, 14, 32)
+    ref = torch.nn.functional.conv1d(x.double(), conv.weight.detach().double(), conv.bias.detach().double(),
+                                     stride=3).transpose(1, 2)
+    mag = torch.nn.functional.conv1d(x.double().abs(), conv.weight.detach().double().abs(),
+                                     conv.bias.detach().double().abs(), stride=3).transpose(1, 2)
+    err = (y.double() - ref).abs()
+    assert (err <= 2e-6 * mag + 1e-30).all(), float((err / mag).max())
+
+
+@pytest.mark.parametrize("n", [777, 49152])
+def test_conv1_f32_weight_gradient_matches_fp64(n):
+    """fp32-class: every gW / gb element within 2e-6 of sum |gy| |x| of the fp64 sum (fp32's unit roundoff is 6e-8;
+    a few dozen roundings along the fixed-order sum), the same bits on a second backward."""
+    from ti5_isaacgym_amd.algo.dh_policy import conv1d_train_f32
+    conv = _conv()
+    g = torch.Generator(device=DEV).manual_seed(n + 3)
+    x = torch.randn(n, 66, 47, device=DEV, generator=g) * 2.0
+    gy = torch.randn(n, 14, 32, device=DEV, generator=g) * 1e-3
+    y = conv1d_train_f32(x, conv)
+    y.backward(gy)
+    gw, gb = conv.weight.grad.clone(), conv.bias.grad.clone()
+    win = x.double().unfold(2, 6, 3)                       # (B, 66, 14, 6)
+    ref_w = torch.einsum("blo,bclt->oct", gy.double(), win)
+    mag_w = torch.einsum("blo,bclt->oct", gy.double().abs(), win.abs())
+    ref_b, mag_b = gy.double().sum((0, 1)), gy.double().abs().sum((0, 1))
+    ew = (gw.double() - ref_w).abs()
+    eb = (gb.double() - ref_b).abs()
+    print(f"n={n}: max |gW err| / (|gy|^T|x|) = {float((ew / mag_w).max()):.2e}, bias {float((eb / mag_b).max()):.2e}")
+    assert (ew <= 2e-6 * mag_w).all() and (eb <= 2e-6 * mag_b).all()
+    conv.weight.grad = None
+    conv.bias.grad = None
+    conv1d_train_f32(x, conv).backward(gy)
+    assert torch.equal(conv.weight.grad, gw) and torch.equal(conv.bias.grad, gb)
+
+
+def test_history_encoder_fp32_update_uses_the_hip_conv(monkeypatch):
+    """Under autograd in fp32 the history encoder's first conv takes conv1d_train_f32 (no unfold), and the encoder's
+    output and weight gradients match the unfold + GEMM path (T1_CONV1_TRAIN off) within fp32 summation order."""
+    from ti5_isaacgym_amd.algo import dh_policy
+    torch.manual_seed(1)
+    enc = dh_policy._history_encoder(66, 47, [32, 16], [6, 4], [3, 2], 16).to(DEV)
+    x = torch.randn(512, 66, 47, device=DEV)
+    calls = []
+    real = dh_policy.conv1d_train_f32
+    monkeypatch.setattr(dh_policy, "conv1d_train_f32", lambda *a: (calls.append(1), real(*a))[1])
+    out = enc(x)
+    out.square().sum().backward()
+    g1 = [p.grad.clone() for p in enc.parameters()]
+    assert calls, "the fp32 HIP conv was not used"
+    enc.zero_grad()
+    monkeypatch.setattr(dh_policy, "CONV1_TRAIN", False)
+    out2 = enc(x)
+    out2.square().sum().backward()
+    torch.testing.assert_close(out, out2, rtol=1e-5, atol=1e-6)
+    for a, b in zip(g1, [p.grad for p in enc.parameters()]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6 * b.abs().max().item())

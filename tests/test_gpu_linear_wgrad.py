@@ -155,3 +155,50 @@ def test_autograd_grad_leaves_preset_grads_alone():
     y.backward(gy, inputs=[xi])
     assert xi.grad is not None
     assert torch.equal(lin.weight.grad, pw) and torch.equal(lin.bias.grad, pb)
+
+
+# ---- the fp32 update's kernel (t1policy_linear_wgrad_f32): fp32 operands, three-part bf16 split, fp32-class sums
+def _operands_f32(rows, M, N, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.randn(rows, M, device=DEV, generator=g) * 1e-2, torch.randn(rows, N, device=DEV, generator=g)
+
+
+@pytest.mark.parametrize("rows,M,N", SHAPES)
+def test_linear_wgrad_f32_matches_fp64(rows, M, N):
+    """Every gW / gb element within 2e-6 of |gy|^T |x| of the fp64 sum (fp32-class: the bf16 kernel's bound is 1e-5 on
+    already-rounded operands; here the operands are the fp32 values themselves), the same bits on a second call."""
+    from ti5_isaacgym_amd.algo.dh_policy import linear_wgrad_f32
+    gy, x = _operands_f32(rows, M, N, rows + M + N)
+    gw, gb = linear_wgrad_f32(gy, x)
+    gyd, xd = gy.double(), x.double()
+    ew = (gw.double() - gyd.t() @ xd).abs()
+    mw = gyd.abs().t() @ xd.abs()
+    eb = (gb.double() - gyd.sum(0)).abs()
+    mb = gyd.abs().sum(0)
+    assert (ew <= 2e-6 * mw + 1e-30).all(), float((ew / (mw + 1e-30)).max())
+    assert (eb <= 2e-6 * mb + 1e-30).all(), float((eb / (mb + 1e-30)).max())
+    gw2, gb2 = linear_wgrad_f32(gy, x)
+    assert torch.equal(gw, gw2) and torch.equal(gb, gb2)
+
+
+def test_linear_backward_uses_the_f32_kernel(monkeypatch):
+    """In fp32 (no autocast) the Linear's weight / bias gradients come from t1policy_linear_wgrad_f32, within fp32
+    summation order of torch's, and inside direct_grad_accumulation() they are added into the existing .grad."""
+    from ti5_isaacgym_amd.algo import dh_policy
+    calls = []
+    real = dh_policy.linear_wgrad_f32
+    monkeypatch.setattr(dh_policy, "linear_wgrad_f32", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
+    torch.manual_seed(3)
+    lin = dh_policy.Linear(219, 768).to(DEV)
+    x = torch.randn(4096, 219, device=DEV)
+    gy = torch.randn(4096, 768, device=DEV) * 1e-2
+    lin(x).backward(gy)
+    assert calls
+    ref_w = (gy.double().t() @ x.double()).float()
+    torch.testing.assert_close(lin.weight.grad, ref_w, rtol=1e-5, atol=1e-5 * ref_w.abs().max().item())
+    torch.testing.assert_close(lin.bias.grad, gy.sum(0), rtol=1e-5, atol=1e-6)
+    pw, pb = lin.weight.grad.clone(), lin.bias.grad.clone()
+    with dh_policy.direct_grad_accumulation():
+        lin(x).backward(gy)
+    torch.testing.assert_close(lin.weight.grad, 2 * pw, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(lin.bias.grad, 2 * pb, rtol=1e-6, atol=1e-7)

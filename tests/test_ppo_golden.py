@@ -90,19 +90,24 @@ def replay(device, monkeypatch):
 def check_update(fx, ac, before, lrs, losses, loss_rtol, lr_rtol=0.0):
     # the host keeps the reference's float64 learning rate; the device an fp32 tensor (DHPPO._lr_t)
     np.testing.assert_allclose(np.array(lrs), fx["lrs"], rtol=lr_rtol, atol=0)
+    rel = np.abs(np.asarray(losses, np.float64) - fx["losses"]) / np.abs(fx["losses"])
+    print("losses relative error vs the reference:", rel)
     close("losses", losses, fx["losses"], loss_rtol)
     names = [str(n) for n in fx["names"]]
     sd = ac.state_dict()
+    worst = 0.0
     assert names == list(sd.keys())
     for i, k in enumerate(names):
         d = (sd[k].detach().double().cpu() - before[k]).reshape(-1)
         s, a, _ = fx["delta_stats"][i]
         assert a > 0 or k == "std", k
+        worst = max(worst, abs(d.abs().sum().item() - a) / a if a > 0 else 0.0)
         assert abs(d.abs().sum().item() - a) <= 0.01 * a + 1e-12, (k, d.abs().sum().item(), a)
         assert abs(d.sum().item() - s) <= 0.01 * a + 1e-12, (k, d.sum().item(), s, a)
         p = d[torch.from_numpy(probe_index(d.numel()))].numpy()
         ref = fx["delta_probes"][i]
         assert np.abs(p - ref).max() <= 0.02 * np.abs(ref).max() + 1e-12, (k, p, ref)
+    print(f"weight deltas: worst abs-sum relative gap {worst:.2e}")
 
 
 def test_update_matches_reference_cpu(monkeypatch):

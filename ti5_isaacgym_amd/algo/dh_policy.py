@@ -143,19 +143,36 @@ def direct_grad_accumulation(enabled=True):
 LINEAR_WGRAD = os.environ.get("T1_LINEAR_WGRAD", "1") != "0"
 
 
+# the fp32 update's Linear weight + bias gradients as the HIP three-part-split kernel (t1policy_linear_wgrad_f32);
+# T1_LINEAR_WGRAD_F32=0: the split-K batched GEMM + slice sum + bias sum (A/B)
+LINEAR_WGRAD_F32 = os.environ.get("T1_LINEAR_WGRAD_F32", "1") != "0"
+
+
 def linear_wgrad_bf16(gy, x, need_bias=True, into=None):
     """(gy^T x, gy.sum(0)) in fp32 for bf16 gy (K, M) and x (K, N) (x in fp32 is rounded to bf16 first, as autocast's
     GEMM would): the HIP wgrad kernel, fixed-order fp32 sums of the exact bf16 products.  Device tensors only.
     into = (gw, gb): existing fp32 gradients (gb may be None) the sums are ADDED to (autograd's accumulation into a
     .grad, done by the kernel's last pass); returns them."""
-    from .. import _lib
-    lib = _lib.load()
     gy = gy.contiguous()
     x = (x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)).contiguous()
+    return _linear_wgrad("t1policy_linear_wgrad_bf16", gy, x, need_bias, into)
+
+
+def linear_wgrad_f32(gy, x, need_bias=True, into=None):
+    """linear_wgrad_bf16 for the fp32 update: fp32 gy and x, each value split into three bf16 parts on the matrix cores
+    (six part products per product, fp32-class fixed-order sums; t1policy_linear_wgrad_f32)."""
+    gy = gy.float().contiguous()
+    x = x.float().contiguous()
+    return _linear_wgrad("t1policy_linear_wgrad_f32", gy, x, need_bias, into)
+
+
+def _linear_wgrad(fn, gy, x, need_bias, into):
+    from .. import _lib
+    lib = _lib.load()
     K, M = gy.shape
     N = x.shape[1]
     if x.shape[0] != K:
-        raise ValueError(f"linear_wgrad_bf16: {K} gradient rows against {x.shape[0]} input rows")
+        raise ValueError(f"{fn}: {K} gradient rows against {x.shape[0]} input rows")
     nbytes = lib.t1policy_linear_wgrad_workspace_bytes(K, M, N)
     if nbytes <= 0:
         raise RuntimeError(f"t1policy_linear_wgrad_workspace_bytes failed ({nbytes})")
@@ -165,15 +182,15 @@ def linear_wgrad_bf16(gy, x, need_bias=True, into=None):
         ok = lambda t, shape: (t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == shape  # noqa: E731
                                and t.device == gy.device)
         if not ok(gw, (M, N)) or (gb is not None and not ok(gb, (M,))):
-            raise ValueError("linear_wgrad_bf16: into= needs contiguous fp32 (M, N) / (M,) device gradients")
+            raise ValueError(f"{fn}: into= needs contiguous fp32 (M, N) / (M,) device gradients")
     else:
         gw = torch.empty(M, N, device=gy.device, dtype=torch.float32)
         gb = torch.empty(M, device=gy.device, dtype=torch.float32) if need_bias else None
-    rc = lib.t1policy_linear_wgrad_bf16(gy.data_ptr(), x.data_ptr(), K, M, N, ws.data_ptr(), nbytes, gw.data_ptr(),
-                                        gb.data_ptr() if gb is not None else None, int(into is not None),
-                                        torch.cuda.current_stream(gy.device).cuda_stream)
+    rc = getattr(lib, fn)(gy.data_ptr(), x.data_ptr(), K, M, N, ws.data_ptr(), nbytes, gw.data_ptr(),
+                          gb.data_ptr() if gb is not None else None, int(into is not None),
+                          torch.cuda.current_stream(gy.device).cuda_stream)
     if rc != 0:
-        raise RuntimeError(f"t1policy_linear_wgrad_bf16 failed (rc={rc})")
+        raise RuntimeError(f"{fn} failed (rc={rc})")
     return gw, gb
 
 
@@ -235,7 +252,13 @@ class _LinearSplitK(torch.autograd.Function):
         x, w = ctx.saved_tensors
         gy = gy.contiguous()
         gx = gy.mm(w) if ctx.needs_input_grad[0] else None
-        if LINEAR_WGRAD and gy.is_cuda and gy.dtype == torch.bfloat16 and ctx.needs_input_grad[1]:
+        kern = None
+        if gy.is_cuda and ctx.needs_input_grad[1]:
+            if LINEAR_WGRAD and gy.dtype == torch.bfloat16:
+                kern = linear_wgrad_bf16
+            elif LINEAR_WGRAD_F32 and gy.dtype == torch.float32 and x.dtype == torch.float32:
+                kern = linear_wgrad_f32   # the fp32 update (the reference's precision)
+        if kern is not None:
             wl, bl = ctx.leaves
             need_b = ctx.needs_input_grad[2]
             if (GRAD_DIRECT and _DIRECT_GRAD[0] and wl is not None and wl.grad is not None and wl.grad.dtype == torch.float32
@@ -244,9 +267,9 @@ class _LinearSplitK(torch.autograd.Function):
                 # the weight / bias gradients added straight into the existing .grad (the PPO update's views into
                 # the all-reduce bucket) by the kernel's reduction: autograd's accumulation pass per parameter
                 # (one add_ kernel each, ~38 per minibatch) is not needed, so no gradient is returned for them
-                linear_wgrad_bf16(gy, x, into=(wl.grad, bl.grad if need_b else None))
+                kern(gy, x, into=(wl.grad, bl.grad if need_b else None))
                 return gx, None, None
-            gw, gb = linear_wgrad_bf16(gy, x, need_bias=need_b)
+            gw, gb = kern(gy, x, need_bias=need_b)
             return gx, gw, gb
         gw = wgrad_splitk(gy, x) if ctx.needs_input_grad[1] else None
         gb = bias_grad(gy) if ctx.needs_input_grad[2] else None
@@ -459,6 +482,64 @@ class _HistoryConvBf16(torch.autograd.Function):
         return None, gw, gb
 
 
+class _HistoryConvF32(torch.autograd.Function):
+    """The history encoder's first Conv1d in the fp32 PPO update (the reference's precision, dh_ppo.py:155-182): the
+    forward as the fp32-accurate packed direct conv (t1policy_conv1d_forward_packed: split fp16 operands, the rollout's
+    inference kernel), the weights packed on every call (inside a captured update graph the optimizer's replayed steps
+    move no version counter), and the weight gradient as t1policy_conv1_wgrad_f32 (three-part bf16 split, six MFMAs:
+    fp32-class, fixed-order sums) -- no unfolded (B x 14, 396) copy (667 us per minibatch) and no split-K GEMM on it.
+    Channels-last (B, 14, 32) fp32 out, as conv1d_as_gemm.  The input is the observation history (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from .. import _lib
+        lib = _lib.load()
+        B, C, L = x.shape
+        O, _, K = weight.shape
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        frag = torch.empty(lib.t1policy_conv1d_frag_bytes(), device=x.device, dtype=torch.uint8)
+        _conv1_train_call(lib.t1policy_conv1d_pack_weights(weight.detach().contiguous().data_ptr(), frag.data_ptr(), C,
+                                                           O, K, stream), "t1policy_conv1d_pack_weights")
+        lout = (L - K) // 3 + 1
+        y = torch.empty(B, lout, O, device=x.device, dtype=torch.float32)
+        _conv1_train_call(lib.t1policy_conv1d_forward_packed(x.data_ptr(), frag.data_ptr(),
+                                                             bias.detach().contiguous().data_ptr(), y.data_ptr(), B, C,
+                                                             L, O, K, 3, stream), "t1policy_conv1d_forward_packed")
+        ctx.save_for_backward(x)
+        ctx.shape = (C, L, O, K)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _lib
+        lib = _lib.load()
+        x, = ctx.saved_tensors
+        C, L, O, K = ctx.shape
+        gy = gy.float().contiguous()
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        ws = torch.empty(lib.t1policy_conv1_bf16_workspace_bytes(), device=x.device, dtype=torch.uint8)
+        gw = torch.empty(O, C, K, device=x.device, dtype=torch.float32)
+        gb = torch.empty(O, device=x.device, dtype=torch.float32)
+        _conv1_train_call(lib.t1policy_conv1_wgrad_f32(x.data_ptr(), gy.data_ptr(), ws.data_ptr(), gw.data_ptr(),
+                                                       gb.data_ptr(), x.shape[0], C, L, O, K, 3, stream),
+                          "t1policy_conv1_wgrad_f32")
+        return None, gw, gb
+
+
+def conv1d_train_f32(x, conv):
+    """The first history conv of the fp32 update on an fp32 (B, 66, 47) input as the HIP kernels (channels-last (B, 14,
+    32) fp32 out), or None when the conv or the input is not that shape (the caller keeps unfold + GEMM)."""
+    if (conv.in_channels, conv.out_channels, conv.kernel_size[0], conv.stride[0]) != (66, 32, 6, 3) or \
+            x.dim() != 3 or x.shape[1:] != (66, 47) or x.dtype != torch.float32 or conv.padding != (0,) or \
+            conv.dilation != (1,) or conv.groups != 1 or conv.bias is None or conv.weight.dtype != torch.float32 or \
+            torch.is_autocast_enabled("cuda"):
+        return None
+    x = x.contiguous()
+    if x.data_ptr() % 16 != 0 or x.numel() * 4 >= 2 ** 31:
+        return None
+    return _HistoryConvF32.apply(x, conv.weight, conv.bias)
+
+
 def _bf16_operands(x):
     """x reaches the conv's GEMM as bf16: already bf16 (the cast-once observations), or fp32 under a bf16 autocast."""
     if x.dtype == torch.bfloat16:
@@ -618,6 +699,9 @@ class HistoryEncoder(nn.Sequential):
                 elif not last and torch.is_grad_enabled() and CONV1_TRAIN and _bf16_operands(x):
                     # the bf16 update: the HIP forward + weight gradient on the bf16 operands autocast would make
                     y = conv1d_train_bf16(x.to(torch.bfloat16), m)
+                elif not last and torch.is_grad_enabled() and CONV1_TRAIN and x.dtype == torch.float32:
+                    # the fp32 update: the fp32-accurate HIP forward + three-part-split weight gradient
+                    y = conv1d_train_f32(x, m)
                 x = y if y is not None else conv1d_as_gemm(x, m, channels_last=last)
                 last = True
             elif isinstance(m, nn.Flatten) and last:

@@ -46,6 +46,36 @@
 // probe build only: the hardware placement of every wave of the last launch (HW_ID: SIMD, CU, SE), [block][wave]
 __device__ unsigned g_t1_simd6[4096][8];
 #endif
+#ifdef T1_PROBE_CLOCK
+// probe build only (tools/clock_probe.py): per workgroup, W0's shader cycles (s_memtime) and 100 MHz constant-clock
+// ticks (s_memrealtime) from its start to the end of its epilogue, summed over workgroups and launches, and the count
+__device__ unsigned long long g_t1_clock6[4];
+// and the timeline of the last launch, per workgroup: {start, W0 end, last wave's end} in 100 MHz ticks
+__device__ unsigned long long g_t1_wgtime6[4096][3];
+#define T1_CLOCK_BEGIN()                                                           \
+  unsigned long long t1c_cyc0 = 0, t1c_rt0 = 0;                                    \
+  if (threadIdx.x == 0) {                                                          \
+    t1c_cyc0 = __builtin_amdgcn_s_memtime();                                       \
+    t1c_rt0 = __builtin_amdgcn_s_memrealtime();                                    \
+    if (blockIdx.x < 4096) { g_t1_wgtime6[blockIdx.x][0] = t1c_rt0; g_t1_wgtime6[blockIdx.x][2] = 0; } \
+  }
+#define T1_CLOCK_END()                                                             \
+  if (threadIdx.x == 0) {                                                          \
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime(); \
+    atomicAdd(&g_t1_clock6[0], c1 - t1c_cyc0);                                     \
+    atomicAdd(&g_t1_clock6[1], r1 - t1c_rt0);                                      \
+    atomicAdd(&g_t1_clock6[2], 1ull);                                              \
+    if (blockIdx.x < 4096) g_t1_wgtime6[blockIdx.x][1] = r1;                      \
+  }                                                                                \
+  T1_CLOCK_WAVE_END();
+#define T1_CLOCK_WAVE_END()                                                        \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                \
+    atomicMax(&g_t1_wgtime6[blockIdx.x][2], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#else
+#define T1_CLOCK_BEGIN() ((void)0)
+#define T1_CLOCK_END() ((void)0)
+#define T1_CLOCK_WAVE_END() ((void)0)
+#endif
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py --kernel 6): lane 0 of every wave accumulates shader-clock deltas
 // between T1_PROF_MARK points into per-phase buckets; never part of the product build.
 #ifdef T1_PHASE_PROF
@@ -490,6 +520,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
                                                    t1env_step_args A, ShiftArgs S, int dyn_blocks, FusedArgs FA,
                                                    SubLog LG) {
   __shared__ Dyn6Lds lds;
+  T1_CLOCK_BEGIN();
   {  // the model to LDS
     constexpr int NW = (int)(sizeof(DynModel) / 4);
     static_assert(sizeof(DynModel) % 4 == 0, "the model copies as words");
@@ -677,6 +708,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     }
     T1_PROF_MARK(10);
     if constexpr (FUSED) __syncthreads();  // the epilogue barrier
+    T1_CLOCK_WAVE_END();
     T1_PROF_END();
     return;
   }
@@ -913,6 +945,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         fused_epilogue_obs<POST_OBS_ACTOR, NE6>(M, C, B, A, lane, lds.epi, lds.fr, lds.act, lds.act + NLEG);
       T1_PROF_MARK(15);
     }
+    T1_CLOCK_WAVE_END();
     T1_PROF_END();
     return;
   }
@@ -1077,12 +1110,29 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     fused_epilogue_staged<POST_A_REWARDS, NE6, true>(M, C, B, A, S, FA, dyn_blocks, lane, lds.epi, lds.fr, lds.act,
                                                      lds.act + NLEG);
   }
+  T1_CLOCK_END();
   T1_PROF_END();
 }
 
 #ifdef T1_PROBE_SIMD
 extern "C" int t1env_debug_simd6(unsigned* out, int blocks) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_simd6), sizeof(unsigned) * 8 * (size_t)blocks);
+}
+#endif
+
+#ifdef T1_PROBE_CLOCK
+// probe build only: {cycles, constant-clock ticks, workgroup count} summed since the last reset (reset != 0: zeroed after
+// the read)
+extern "C" int t1env_debug_wgtime6(unsigned long long* out, int blocks) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_wgtime6), sizeof(unsigned long long) * 3 * (size_t)blocks);
+}
+extern "C" int t1env_debug_clock6(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_clock6), sizeof(g_t1_clock6));
+  if (e == hipSuccess && reset) {
+    static const unsigned long long zero[4] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_t1_clock6), zero, sizeof(zero));
+  }
+  return (int)e;
 }
 #endif
 

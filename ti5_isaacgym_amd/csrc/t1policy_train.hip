@@ -266,6 +266,151 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf16(const uint16_t* __rest
   }
 }
 
+// ---- the same weight gradient on fp32 operands (the fp32 update, the reference's precision: dh_ppo.py:155-182).  Each
+// fp32 operand is split into three bf16 parts, v = v1 + v2 + v3 (v1 = bf16(v), v2 = bf16(v - v1), v3 = bf16(v - v1 - v2):
+// 24+ significant bits, exact for normal fp32 values), and a product is formed from the six part products of order up
+// to 2^-16 (a1 b1, a1 b2, a2 b1, a1 b3, a2 b2, a3 b1; the three dropped ones are below 2^-24 of |a b|), each exact in
+// fp32 and accumulated by the MFMA in fp32: fp32-class sums (the tests hold them to 2e-6 of |gy|^T |x| against fp64).
+// The staging, fragments and partials are k_conv1_wgrad_bf16's with fp32 rows in LDS (the parts are formed from them
+// at fragment time); the bias sums the fp32 gy values.
+struct Bf3 {
+  bf8 p[3];
+};
+__device__ __forceinline__ void split_bf3(const float (&v)[8], Bf3& out) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h1 = (__bf16)v[j];
+    const float r1 = v[j] - (float)h1;
+    const __bf16 h2 = (__bf16)r1;
+    const float r2 = r1 - (float)h2;
+    out.p[0][j] = h1;
+    out.p[1][j] = h2;
+    out.p[2][j] = (__bf16)r2;
+  }
+}
+// acc += a b from the split operands: the smallest part products first
+__device__ __forceinline__ f16v mfma_bf3(const Bf3& a, const Bf3& b, f16v acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
+}
+constexpr int TW32_X = TC_SAMPLE;          // 3,102 words
+constexpr int TW32_G = TC_LOUT * TC_O;     // 448 words
+constexpr int TW32_LX = (TW32_X + 255) / 256, TW32_LG = (TW32_G + 255) / 256;  // words per thread: 13, 2
+__global__ __launch_bounds__(256) void k_conv1_wgrad_f32(const float* __restrict__ x, const float* __restrict__ gy,
+                                                         float* __restrict__ part, int batch) {
+  __shared__ float XS[2][TW32_X + 1];
+  __shared__ float GS[2][TW32_G];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, h = lane >> 5, n = lane & 31;
+  const int b0 = (int)((long long)blockIdx.x * batch / gridDim.x), b1 = (int)((long long)(blockIdx.x + 1) * batch / gridDim.x);
+  // three samples' loads in flight, as k_conv1_wgrad_bf16
+  struct Slot {
+    float x[TW32_LX], g[TW32_LG];
+  };
+  auto load = [&](Slot& sl, int bs) {
+    const int bc = bs < b1 ? bs : b1 - 1;
+    const float* sx = x + (size_t)bc * TW32_X;
+    const float* sg = gy + (size_t)bc * TW32_G;
+#pragma unroll
+    for (int k = 0; k < TW32_LX; ++k) {
+      const int i = t + 256 * k;
+      sl.x[k] = sx[i < TW32_X ? i : TW32_X - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < TW32_LG; ++k) {
+      const int i = t + 256 * k;
+      sl.g[k] = sg[i < TW32_G ? i : TW32_G - 1];
+    }
+  };
+  constexpr int TPW = (TC_CT + 3) / 4;
+  int xoff[TPW];
+  bool xcol[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int col = 32 * (wave + 4 * i) + n;
+    xcol[i] = (wave + 4 * i) < TC_CT && col < TC_COLS;
+    const int cc = xcol[i] ? col / TC_K : 0, tt = xcol[i] ? col % TC_K : 0;
+    xoff[i] = cc * TC_L + tt;
+  }
+  f16v acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[i][q] = 0.0f;
+  float gbs = 0.0f;
+  Slot sl[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    load(sl[k], b0 + k);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int buf = 0;
+  auto sample = [&](Slot& cur, int b) {
+#pragma unroll
+    for (int k = 0; k < TW32_LX; ++k) {
+      const int i = t + 256 * k;
+      if (i < TW32_X) XS[buf][i] = cur.x[k];
+    }
+#pragma unroll
+    for (int k = 0; k < TW32_LG; ++k) {
+      const int i = t + 256 * k;
+      if (i < TW32_G) GS[buf][i] = cur.g[k];
+    }
+    load(cur, b + 3);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    const float* X = XS[buf];
+    const float* G = GS[buf];
+    float av[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int l = 8 * h + j;
+      av[j] = l < TC_LOUT ? G[l * TC_O + n] : 0.0f;
+      gbs += av[j];
+    }
+    Bf3 a;
+    split_bf3(av, a);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      if (wave + 4 * i >= TC_CT) break;  // wave-uniform
+      float bv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int l = 8 * h + j;
+        bv[j] = (l < TC_LOUT && xcol[i]) ? X[xoff[i] + TC_S * l] : 0.0f;
+      }
+      Bf3 bb;
+      split_bf3(bv, bb);
+      acc[i] = mfma_bf3(a, bb, acc[i]);
+    }
+    buf ^= 1;
+  };
+  for (int b = b0; b < b1; b += 3) {
+    sample(sl[0], b);
+    if (b + 1 >= b1) break;
+    sample(sl[1], b + 1);
+    if (b + 2 >= b1) break;
+    sample(sl[2], b + 2);
+  }
+  float* P = part + (size_t)blockIdx.x * TC_PART;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    if (wave + 4 * i >= TC_CT) break;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int o = (q & 3) + 8 * (q >> 2) + 4 * h;
+      P[(size_t)o * (TC_CT * 32) + 32 * (wave + 4 * i) + n] = acc[i][q];
+    }
+  }
+  if (wave == 0) {
+    gbs += __shfl_xor(gbs, 32);
+    if (h == 0) P[TC_O * TC_CT * 32 + n] = gbs;
+  }
+}
+
 // gW[o, c, t] (the (32, 66, 6) fp32 weight layout) and gb[o]: the partials summed in a fixed tree -- 16 groups per
 // output (thread (g, o) sums partials g, g + 16, ... in order, eight loads in flight), then the 16 group sums in order
 // (the one-thread-per-output chain of 512 dependent loads took 120 us, profiles/r05upd_*)
@@ -485,6 +630,19 @@ int t1policy_conv1_forward_bf16(const void* x, const void* frag, const float* bi
   hipLaunchKernelGGL(k_conv1_fwd_bf16, dim3(grid), dim3(64 * TF_WAVES), 0, (hipStream_t)stream,
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const bf8*>(frag), bias,
                      reinterpret_cast<uint16_t*>(y), batch);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_conv1_wgrad_f32(const float* x, const float* gy, void* workspace, float* grad_weight, float* grad_bias,
+                             int batch, int channels, int length, int out_channels, int kernel, int stride,
+                             void* stream) {
+  if (!x || !gy || !workspace || !grad_weight || !grad_bias || batch <= 0) return -1;
+  if (!tc_shape(channels, length, out_channels, kernel, stride)) return 1;
+  const int parts = batch < TC_WG_BLOCKS ? batch : TC_WG_BLOCKS;
+  float* part = reinterpret_cast<float*>(workspace);
+  hipLaunchKernelGGL(k_conv1_wgrad_f32, dim3(parts), dim3(256), 0, (hipStream_t)stream, x, gy, part, batch);
+  hipLaunchKernelGGL(k_conv1_wgrad_reduce, dim3((TC_O * TC_COLS + TC_O + TR_PER - 1) / TR_PER), dim3(256), 0,
+                     (hipStream_t)stream, part, parts, grad_weight, grad_bias);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -200,6 +200,159 @@ __global__ __launch_bounds__(256, 2) void k_linear_wgrad_bf16(const uint16_t* __
   }
 }
 
+// ---- the fp32 update (the reference's precision, dh_ppo.py:155-182): the same tiles, slices, partials and reduction on
+// fp32 gy and x.  A chunk of 32 rows is staged as fp32 rows (pitch 132 words: a fragment read's two 32-lane halves,
+// 8 rows apart, cover the 64 banks once); a wave reads each 8-element fragment column with eight ds_read_b32 and splits
+// every value into three bf16 parts (v1 = bf16(v), v2 = bf16(v - v1), v3 = bf16(v - v1 - v2): 24+ bits, exact for
+// normal fp32), and each 32 x 32 tile takes the six part products down to 2^-16 of |a b| (the three dropped ones are
+// below 2^-24): fp32-class sums of exact bf16 products, deterministic as the bf16 kernel's.  The bias sums the fp32 gy.
+constexpr int WG32_PITCH = WG_T + 4;  // fp32 words per staged row
+constexpr int WG32_RPT = WG_ROWS / 2;  // rows per thread per chunk (two rows per 256 threads' pass of 128 columns)
+struct Wg32Stage {
+  float v[WG32_RPT];
+};
+// thread t loads column c0 + (t & 127) of rows r0 + (t >> 7) + 2 i (coalesced 256-B wave rows), clamped in-matrix and
+// issued unconditionally (the store below zeroes what lies outside the slice or the width)
+__device__ __forceinline__ void wg32_load(const float* __restrict__ z, int W, int c0, int r0, int r1, int t,
+                                          Wg32Stage& v) {
+  const int col = c0 + (t & 127);
+  const int colc = col < W ? col : W - 1;
+#pragma unroll
+  for (int i = 0; i < WG32_RPT; ++i) {
+    const int r = r0 + (t >> 7) + 2 * i;
+    v.v[i] = z[(size_t)(r < r1 ? r : r1 - 1) * W + colc];
+  }
+}
+__device__ __forceinline__ void wg32_store(float* img, int W, int c0, int r0, int r1, int t, const Wg32Stage& v) {
+  const bool c_ok = c0 + (t & 127) < W;
+#pragma unroll
+  for (int i = 0; i < WG32_RPT; ++i) {
+    const int rr = (t >> 7) + 2 * i;
+    img[rr * WG32_PITCH + (t & 127)] = (c_ok && r0 + rr < r1) ? v.v[i] : 0.0f;
+  }
+}
+struct Bf3f {
+  bf8 p[3];
+};
+// the fragment of k-step ks for column col0 + (lane & 31): rows 16 ks + 8 (lane >> 5) + j, j = 0 .. 7, split in three
+__device__ __forceinline__ void wg32_frag(const float* img, int ks, int col0, int lane, Bf3f& f, float* sum) {
+  const int row = 16 * ks + 8 * (lane >> 5), col = col0 + (lane & 31);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = img[(row + j) * WG32_PITCH + col];
+  if (sum) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *sum += v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h1 = (__bf16)v[j];
+    const float r1 = v[j] - (float)h1;
+    const __bf16 h2 = (__bf16)r1;
+    f.p[0][j] = h1;
+    f.p[1][j] = h2;
+    f.p[2][j] = (__bf16)(r1 - (float)h2);
+  }
+}
+__device__ __forceinline__ f16v mfma_bf3f(const Bf3f& a, const Bf3f& b, f16v acc) {  // the smallest products first
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
+}
+__global__ __launch_bounds__(256, 2) void k_linear_wgrad_f32(const float* __restrict__ gy, const float* __restrict__ x,
+                                                             int rows, int M, int N, int tiles_m, int rows_per_slice,
+                                                             float* __restrict__ part, float* __restrict__ bpart) {
+  __shared__ __attribute__((aligned(16))) float IMG[2][2][WG_ROWS * WG32_PITCH];  // [buffer][gy, x]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, h = lane >> 5;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int tm = blockIdx.x % tiles_m, tn = blockIdx.x / tiles_m, s = blockIdx.y;
+  const int m0 = WG_T * tm, n0 = WG_T * tn;
+  const int r0 = s * rows_per_slice;
+  const int r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
+  const int m_rem = M - (m0 + 64 * wm), n_rem = N - (n0 + 64 * wn);
+  const int mb_n = m_rem <= 0 ? 0 : (m_rem > 32 ? 2 : 1), nb_n = n_rem <= 0 ? 0 : (n_rem > 32 ? 2 : 1);
+  const bool bias = bpart != nullptr && tn == 0 && wn == 0;
+  f16v acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+  float bsum[2] = {0.0f, 0.0f};
+  // two chunks of loads in flight (register slots 0, 1), refilled as soon as staged (two LDS buffers, one barrier per
+  // chunk)
+  Wg32Stage vg[2], vx[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    wg32_load(gy, M, m0, r0 + k * WG_ROWS, r1, t, vg[k]);
+    wg32_load(x, N, n0, r0 + k * WG_ROWS, r1, t, vx[k]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int buf = 0;
+  auto chunk = [&](Wg32Stage& rg, Wg32Stage& rx, int c) {
+    wg32_store(IMG[buf][0], M, m0, c, r1, t, rg);
+    wg32_store(IMG[buf][1], N, n0, c, r1, t, rx);
+    wg32_load(gy, M, m0, c + 2 * WG_ROWS, r1, t, rg);
+    wg32_load(x, N, n0, c + 2 * WG_ROWS, r1, t, rx);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if (mb_n > 0 && nb_n > 0) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        Bf3f fa[2], fb[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+          wg32_frag(IMG[buf][0], ks, 64 * wm + 32 * a, lane, fa[a], bias && a < mb_n ? &bsum[a] : nullptr);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) wg32_frag(IMG[buf][1], ks, 64 * wn + 32 * b, lane, fb[b], nullptr);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          if (a >= mb_n) break;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if (b >= nb_n) break;
+            acc[a][b] = mfma_bf3f(fa[a], fb[b], acc[a][b]);
+          }
+        }
+      }
+    }
+    buf ^= 1;
+  };
+  for (int c = r0; c < r1; c += 2 * WG_ROWS) {
+    chunk(vg[0], vx[0], c);
+    if (c + WG_ROWS >= r1) break;
+    chunk(vg[1], vx[1], c + WG_ROWS);
+  }
+  float* P = part + (size_t)s * M * N;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    if (a >= mb_n) break;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if (b >= nb_n) break;
+      const int n = n0 + 64 * wn + 32 * b + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 64 * wm + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M && n < N) P[(size_t)m * N + n] = acc[a][b][r];
+      }
+    }
+  }
+  if (bias) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      if (a >= mb_n) break;
+      const float v = bsum[a] + __shfl_xor(bsum[a], 32);
+      const int m = m0 + 64 * wm + 32 * a + (lane & 31);
+      if (h == 0 && m < M) bpart[(size_t)s * M + m] = v;
+    }
+  }
+}
+
 // gW[i] = sum_s part[s][i] (i < M N) and gb[m] = sum_s bpart[s][m]: G slice groups per output (thread (g, o) sums
 // slices g, g + G, ... in order, eight loads in flight), then the G group sums in order -- a fixed tree for a given
 // slice count, so the result is deterministic
@@ -317,6 +470,28 @@ int t1policy_linear_wgrad_bf16(const void* gy, const void* x, int rows, int M, i
   else
     hipLaunchKernelGGL((k_linear_wgrad_bf16<false, false>), grid, dim3(256), 0, st, g16, x16, rows, M, N, p.tiles_m,
                        p.rows_per_slice, part, bpart);
+  const int total = M * N + (grad_bias ? M : 0);
+  const int groups = p.slices <= 8 ? 1 : (p.slices <= 64 ? 4 : 16), per = 256 / groups;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + per - 1) / per), dim3(256), 0, st, part, bpart, p.slices, groups,
+                     M * N, M, grad_weight, grad_bias, accumulate);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_linear_wgrad_f32(const float* gy, const float* x, int rows, int M, int N, void* workspace,
+                              long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
+                              void* stream) {
+  if (!gy || !x || !workspace || !grad_weight || rows <= 0 || M <= 0 || N <= 0) return -1;
+  if ((reinterpret_cast<uintptr_t>(workspace) & 15u) != 0) return -1;
+  if ((long long)M * N >= (1LL << 31) - M || (long long)rows * (M > N ? M : N) >= (1LL << 31)) return -1;
+  const int cus = wg_cus();
+  if (cus <= 0) return -2;
+  const WgPlan p = wg_plan(rows, M, N, cus);
+  if (workspace_bytes < (long long)p.slices * ((long long)M * N + M) * 4) return -1;
+  float* part = reinterpret_cast<float*>(workspace);
+  float* bpart = grad_bias ? part + (size_t)p.slices * M * N : nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_linear_wgrad_f32, dim3(p.tiles, p.slices), dim3(256), 0, st, gy, x, rows, M, N, p.tiles_m,
+                     p.rows_per_slice, part, bpart);
   const int total = M * N + (grad_bias ? M : 0);
   const int groups = p.slices <= 8 ? 1 : (p.slices <= 64 ? 4 : 16), per = 256 / groups;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + per - 1) / per), dim3(256), 0, st, part, bpart, p.slices, groups,

@@ -1,0 +1,61 @@
+"""Dev probe: the shader clock k_dyn6 runs at (a -DT1_PROBE_CLOCK build: lane 0 of every workgroup's wave 0 reads the
+shader-cycle counter (s_memtime) and the 100 MHz constant counter (s_memrealtime) at the start and end of the launch and
+adds the deltas to two device counters), against the step time -- to tell a clock (power-management) mode from a code
+mode when a build's step time differs across processes (VERDICT r5 #1b, the -O2 slow mode).
+
+    T1ENV_LIB=ti5_isaacgym_amd/_lib/var/<probe build>.so python tools/clock_probe.py [--steps 300]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ti5_isaacgym_amd import make_t1_env  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--steps", type=int, default=300)
+    p.add_argument("--num-envs", type=int, default=8192)
+    a = p.parse_args()
+    N = a.num_envs
+    env = make_t1_env(num_envs=N, mesh_type="trimesh", seed=5, device="cuda:0")
+    env.reset()
+    acts = torch.randn(8, N, 12, device="cuda:0")
+    for i in range(50):
+        env.step(acts[i % 8])
+    torch.cuda.synchronize()
+    lib = ctypes.CDLL(os.environ["T1ENV_LIB"])
+    out = np.zeros(4, np.uint64)
+    lib.t1env_debug_clock6(out.ctypes.data_as(ctypes.c_void_p), 1)   # read and reset
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        env.step(acts[i % 8])
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / a.steps * 1e3
+    lib.t1env_debug_clock6(out.ctypes.data_as(ctypes.c_void_p), 0)
+    cycles, ticks, launches = int(out[0]), int(out[1]), int(out[2])
+    mhz = cycles / (ticks / 100.0) if ticks else None   # s_memrealtime: 100 MHz
+    # the last launch's timeline (us from its first workgroup's start): start spread, W0 lifetimes, last-wave ends
+    wg = (N + 31) // 32
+    tl = np.zeros((wg, 3), np.uint64)
+    lib.t1env_debug_wgtime6(tl.ctypes.data_as(ctypes.c_void_p), wg)
+    t0 = int(tl[:, 0].min())
+    st, w0e, end = ((tl[:, k].astype(np.int64) - t0) / 100.0 for k in range(3))
+    q = lambda v: [round(float(x), 2) for x in np.quantile(v, [0, 0.5, 0.9, 1.0])]  # noqa: E731
+    print(json.dumps({"ms_per_step": round(ms, 4), "launches_x_workgroups": launches,
+                      "shader_mhz": round(mhz, 1) if mhz else None,
+                      "w0_lifetime_us_mean": round(ticks / max(1, launches) / 100.0, 2),
+                      "last_launch_us": {"start_q0_50_90_100": q(st), "w0_life_q": q(w0e - st),
+                                         "wg_end_q": q(end), "after_w0_q": q(end - w0e)},
+                      "lib": os.path.basename(os.environ["T1ENV_LIB"])}))
+
+
+if __name__ == "__main__":
+    main()

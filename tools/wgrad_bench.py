@@ -2,7 +2,9 @@
 against the split-K batched GEMM + slice sum + torch's bias sum it replaces, on the update's layer shapes at the
 49,152-row minibatch.  Prints one JSON line.
 
-    python tools/wgrad_bench.py [--reps 20]
+    python tools/wgrad_bench.py [--reps 20] [--f32]
+
+--f32: the fp32 update's kernel (t1policy_linear_wgrad_f32, three-part bf16 split) against the fp32 split-K path.
 """
 import argparse
 import json
@@ -38,21 +40,25 @@ def timed(fn, reps):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--f32", action="store_true")
     a = p.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     rows_out, tot_new, tot_old = [], 0.0, 0.0
     for rows, M, N in LAYERS:
-        gy = (torch.randn(rows, M, device=dev, generator=g) * 0.1).to(torch.bfloat16)
-        x = torch.randn(rows, N, device=dev, generator=g).to(torch.bfloat16)
-        t_new = timed(lambda: dh_policy.linear_wgrad_bf16(gy, x), a.reps)
+        dt = torch.float32 if a.f32 else torch.bfloat16
+        gy = (torch.randn(rows, M, device=dev, generator=g) * 0.1).to(dt)
+        x = torch.randn(rows, N, device=dev, generator=g).to(dt)
+        kern = dh_policy.linear_wgrad_f32 if a.f32 else dh_policy.linear_wgrad_bf16
+        t_new = timed(lambda: kern(gy, x), a.reps)
         t_old = timed(lambda: (dh_policy.wgrad_splitk(gy, x), dh_policy.bias_grad(gy)), a.reps)
         flops = 2.0 * rows * M * N
         rows_out.append({"rows": rows, "M": M, "N": N, "us_kernel": round(t_new, 2), "us_splitk": round(t_old, 2),
                          "tflops_kernel": round(flops / t_new * 1e-6, 1)})
         tot_new += t_new
         tot_old += t_old
-    print(json.dumps({"bench": "linear_wgrad_bf16", "layers": rows_out, "us_per_minibatch_kernel": round(tot_new, 1),
+    print(json.dumps({"bench": "linear_wgrad_f32" if a.f32 else "linear_wgrad_bf16",
+                      "wg_per_cu": os.environ.get("T1_WGRAD_WG_PER_CU", "2"), "layers": rows_out, "us_per_minibatch_kernel": round(tot_new, 1),
                       "us_per_minibatch_splitk": round(tot_old, 1)}))
 
 
