@@ -202,3 +202,46 @@ def test_linear_backward_uses_the_f32_kernel(monkeypatch):
         lin(x).backward(gy)
     torch.testing.assert_close(lin.weight.grad, 2 * pw, rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(lin.bias.grad, 2 * pb, rtol=1e-6, atol=1e-7)
+
+
+# ---- the fp32 update's forward / input-gradient GEMM (t1policy_gemm_nt_f32)
+GEMM_SHAPES = [(49152, 768, 219), (49152, 256, 768), (49152, 512, 302), (49152, 3, 64), (49152, 1, 128),
+               (294912, 16, 128), (49152, 219, 768), (777, 130, 97), (31, 5, 7), (64, 300, 2)]
+
+
+@pytest.mark.parametrize("R,N,K", GEMM_SHAPES)
+def test_gemm_nt_f32_matches_fp64(R, N, K):
+    """a b^T + bias within 2e-6 of |a| |b|^T + |bias| of the fp64 value (fp32-class), ELU applied after the same sum
+    (act=1), and the same bits on a second call."""
+    from ti5_isaacgym_amd.algo.dh_policy import gemm_nt_f32
+    g = torch.Generator(device=DEV).manual_seed(R + N + K)
+    a = torch.randn(R, K, device=DEV, generator=g)
+    b = torch.randn(N, K, device=DEV, generator=g) * 0.1
+    bias = torch.randn(N, device=DEV, generator=g)
+    y = gemm_nt_f32(a, b, bias)
+    ref = a.double() @ b.double().t() + bias.double()
+    mag = a.double().abs() @ b.double().abs().t() + bias.double().abs()
+    err = (y.double() - ref).abs()
+    assert (err <= 2e-6 * mag).all(), float((err / mag).max())
+    assert torch.equal(y, gemm_nt_f32(a, b, bias))
+    ye = gemm_nt_f32(a, b, bias, act=1)
+    torch.testing.assert_close(ye, torch.nn.functional.elu(y), rtol=1e-6, atol=1e-7)
+
+
+def test_linear_fp32_forward_and_input_gradient_use_the_gemm(monkeypatch):
+    """In fp32 under autograd the Linear's forward and input gradient come from t1policy_gemm_nt_f32, within fp32
+    summation order of torch's; T1 GEMM_F32 off gives torch's."""
+    from ti5_isaacgym_amd.algo import dh_policy
+    calls = []
+    real = dh_policy.gemm_nt_f32
+    monkeypatch.setattr(dh_policy, "gemm_nt_f32", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
+    torch.manual_seed(5)
+    lin = dh_policy.Linear(302, 512).to(DEV)
+    x = torch.randn(8192, 302, device=DEV, requires_grad=True)
+    gy = torch.randn(8192, 512, device=DEV) * 1e-2
+    y = lin(x)
+    y.backward(gy)
+    assert len(calls) == 2   # forward and input gradient
+    ref_y = torch.addmm(lin.bias, x, lin.weight.t())
+    torch.testing.assert_close(y, ref_y, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad, gy @ lin.weight, rtol=1e-5, atol=1e-6)

@@ -166,6 +166,33 @@ def linear_wgrad_f32(gy, x, need_bias=True, into=None):
     return _linear_wgrad("t1policy_linear_wgrad_f32", gy, x, need_bias, into)
 
 
+# the fp32 update's Linear forward / input-gradient GEMMs as the HIP three-part-split GEMM (t1policy_gemm_nt_f32);
+# T1_GEMM_F32=0: hipBLASLt's fp32 addmm / mm (A/B)
+GEMM_F32 = os.environ.get("T1_GEMM_F32", "1") != "0"
+
+
+def gemm_nt_f32(a, b, bias=None, act=0):
+    """a (R, K) @ b (N, K)^T (+ bias) (ELU with act=1) in fp32 on the matrix cores (t1policy_gemm_nt_f32: each value in
+    three bf16 parts, fp32-class sums in k order).  Device fp32 tensors."""
+    from .. import _lib
+    lib = _lib.load()
+    a, b = a.contiguous(), b.contiguous()
+    R, K = a.shape
+    N = b.shape[0]
+    if b.shape[1] != K or a.dtype != torch.float32 or b.dtype != torch.float32:
+        raise ValueError(f"gemm_nt_f32: {tuple(a.shape)} x {tuple(b.shape)}^T ({a.dtype}, {b.dtype})")
+    out = torch.empty(R, N, device=a.device, dtype=torch.float32)
+    bp = None
+    if bias is not None:
+        bias = bias.contiguous()
+        bp = bias.data_ptr()
+    rc = lib.t1policy_gemm_nt_f32(a.data_ptr(), b.data_ptr(), bp, out.data_ptr(), R, N, K, act,
+                                  torch.cuda.current_stream(a.device).cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"t1policy_gemm_nt_f32 failed (rc={rc})")
+    return out
+
+
 def _linear_wgrad(fn, gy, x, need_bias, into):
     from .. import _lib
     lib = _lib.load()
@@ -244,6 +271,9 @@ class _LinearSplitK(torch.autograd.Function):
             dt = torch.get_autocast_dtype("cuda")
             x, w, b = x.to(dt), _cast_param(w, dt), _cast_param(b, dt)
         ctx.save_for_backward(x, w)
+        if (GEMM_F32 and x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 2
+                and not torch.is_autocast_enabled("cuda")):
+            return gemm_nt_f32(x, w, b)   # the fp32 update: the three-part-split HIP GEMM
         return torch.addmm(b, x, w.t())
 
     @staticmethod
@@ -251,7 +281,12 @@ class _LinearSplitK(torch.autograd.Function):
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gy = gy.contiguous()
-        gx = gy.mm(w) if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            if GEMM_F32 and gy.is_cuda and gy.dtype == torch.float32 and w.dtype == torch.float32:
+                gx = gemm_nt_f32(gy, w.t())   # gy W as gy (W^T)^T: the reduction index contiguous in both operands
+            else:
+                gx = gy.mm(w)
         kern = None
         if gy.is_cuda and ctx.needs_input_grad[1]:
             if LINEAR_WGRAD and gy.dtype == torch.bfloat16:

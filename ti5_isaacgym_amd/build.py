@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, "csrc")
 UNITS = [("t1env.hip", "-O3"), ("t1env_dynamics.hip", "-O1"), ("t1env_dyn5.hip", "-O1"), ("t1env_dyn6.hip", "-O1"),
          ("t1policy.hip", "-O3"),
          ("t1policy_heads.hip", "-O3"), ("t1policy_train.hip", "-O3"),
-         ("t1policy_wgrad.hip", "-O3")]
+         ("t1policy_wgrad.hip", "-O3"), ("t1policy_gemm.hip", "-O3")]
 OUT = os.path.join(HERE, "_lib", "libt1env_hip.so")
 # guard build: the dynamics unit at -O3 (tests/test_gpu_opt_levels.py keeps it under the fp64 dynamics check)
 OUT_O3 = os.path.join(HERE, "_lib", "var", "libt1env_hip_dyn_o3.so")

@@ -50,8 +50,14 @@ __device__ unsigned g_t1_simd6[4096][8];
 // probe build only (tools/clock_probe.py): per workgroup, W0's shader cycles (s_memtime) and 100 MHz constant-clock
 // ticks (s_memrealtime) from its start to the end of its epilogue, summed over workgroups and launches, and the count
 __device__ unsigned long long g_t1_clock6[4];
-// and the timeline of the last launch, per workgroup: {start, W0 end, last wave's end} in 100 MHz ticks
+// and the timeline of the last launch, per workgroup: {start, W0 end, last wave's end} in 100 MHz ticks; per workgroup
+// summed over launches: {W0 lifetime, W0's S1 waits, W0's S2 waits} in shader cycles
 __device__ unsigned long long g_t1_wgtime6[4096][3];
+__device__ unsigned long long g_t1_wgsum6[4096][3];
+#define T1_CLOCK_WAIT_BEGIN() const unsigned long long t1c_w0 = __builtin_amdgcn_s_memtime();
+#define T1_CLOCK_WAIT_END(k)                                                       \
+  if (threadIdx.x == 0 && blockIdx.x < 4096)                                       \
+    atomicAdd(&g_t1_wgsum6[blockIdx.x][k], __builtin_amdgcn_s_memtime() - t1c_w0);
 #define T1_CLOCK_BEGIN()                                                           \
   unsigned long long t1c_cyc0 = 0, t1c_rt0 = 0;                                    \
   if (threadIdx.x == 0) {                                                          \
@@ -65,7 +71,10 @@ __device__ unsigned long long g_t1_wgtime6[4096][3];
     atomicAdd(&g_t1_clock6[0], c1 - t1c_cyc0);                                     \
     atomicAdd(&g_t1_clock6[1], r1 - t1c_rt0);                                      \
     atomicAdd(&g_t1_clock6[2], 1ull);                                              \
-    if (blockIdx.x < 4096) g_t1_wgtime6[blockIdx.x][1] = r1;                      \
+    if (blockIdx.x < 4096) {                                                       \
+      g_t1_wgtime6[blockIdx.x][1] = r1;                                            \
+      atomicAdd(&g_t1_wgsum6[blockIdx.x][0], c1 - t1c_cyc0);                       \
+    }                                                                              \
   }                                                                                \
   T1_CLOCK_WAVE_END();
 #define T1_CLOCK_WAVE_END()                                                        \
@@ -75,6 +84,8 @@ __device__ unsigned long long g_t1_wgtime6[4096][3];
 #define T1_CLOCK_BEGIN() ((void)0)
 #define T1_CLOCK_END() ((void)0)
 #define T1_CLOCK_WAVE_END() ((void)0)
+#define T1_CLOCK_WAIT_BEGIN() ((void)0)
+#define T1_CLOCK_WAIT_END(k) ((void)0)
 #endif
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py --kernel 6): lane 0 of every wave accumulates shader-clock deltas
 // between T1_PROF_MARK points into per-phase buckets; never part of the product build.
@@ -979,7 +990,11 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   lds.vish[lane] = vi_sh;
   T1_PROF_MARK(0);
   for (int sub = 0; sub < nsub; ++sub) {
-    __syncthreads();  // S1: the substep state published
+    {
+      T1_CLOCK_WAIT_BEGIN();
+      __syncthreads();  // S1: the substep state published
+      T1_CLOCK_WAIT_END(1);
+    }
     T1_PROF_MARK(1);
     // -DT1_D6_LAUNDER (A/B): the lane and leg through an empty asm each substep, so the lane- and leg-indexed LDS
     // addresses are formed in the loop instead of hoisted and spilled: no scratch reloads in the loop, yet measured
@@ -1008,7 +1023,11 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       }
     }
     T1_PROF_MARK(2);
-    __syncthreads();  // S2: the terms published
+    {
+      T1_CLOCK_WAIT_BEGIN();
+      __syncthreads();  // S2: the terms published
+      T1_CLOCK_WAIT_END(2);
+    }
     T1_PROF_MARK(3);
     {  // the episodes of the shank and foot from the two halves of their points
       vi_sh = restitution_episode(vi_sh, fmaxf(lds.amx[WC_SHA][lane_s], lds.amx[WC_SHB][lane_s]));
@@ -1125,6 +1144,14 @@ extern "C" int t1env_debug_simd6(unsigned* out, int blocks) {
 // the read)
 extern "C" int t1env_debug_wgtime6(unsigned long long* out, int blocks) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_wgtime6), sizeof(unsigned long long) * 3 * (size_t)blocks);
+}
+extern "C" int t1env_debug_wgsum6(unsigned long long* out, int blocks, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_wgsum6), sizeof(unsigned long long) * 3 * (size_t)blocks);
+  if (e == hipSuccess && reset) {
+    static unsigned long long zero[4096][3] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_t1_wgsum6), zero, sizeof(zero));
+  }
+  return (int)e;
 }
 extern "C" int t1env_debug_clock6(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_clock6), sizeof(g_t1_clock6));

@@ -23,6 +23,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--steps", type=int, default=300)
     p.add_argument("--num-envs", type=int, default=8192)
+    p.add_argument("--dump", default=None, help="save the per-workgroup (life, S1 wait, S2 wait) us array (.npy)")
     a = p.parse_args()
     N = a.num_envs
     env = make_t1_env(num_envs=N, mesh_type="trimesh", seed=5, device="cuda:0")
@@ -34,6 +35,9 @@ def main():
     lib = ctypes.CDLL(os.environ["T1ENV_LIB"])
     out = np.zeros(4, np.uint64)
     lib.t1env_debug_clock6(out.ctypes.data_as(ctypes.c_void_p), 1)   # read and reset
+    wg = (N + 31) // 32
+    sums = np.zeros((wg, 3), np.uint64)
+    lib.t1env_debug_wgsum6(sums.ctypes.data_as(ctypes.c_void_p), wg, 1)
     t0 = time.perf_counter()
     for i in range(a.steps):
         env.step(acts[i % 8])
@@ -42,8 +46,16 @@ def main():
     lib.t1env_debug_clock6(out.ctypes.data_as(ctypes.c_void_p), 0)
     cycles, ticks, launches = int(out[0]), int(out[1]), int(out[2])
     mhz = cycles / (ticks / 100.0) if ticks else None   # s_memrealtime: 100 MHz
+    # per workgroup over the timed steps: W0's lifetime and its S1 / S2 waits (us per launch at the measured clock),
+    # and by terrain type (the reference's floor(i / (N / 20)), legged_robot.py:1490) of the workgroup's first env
+    lib.t1env_debug_wgsum6(sums.ctypes.data_as(ctypes.c_void_p), wg, 0)
+    per = sums.astype(np.float64) / a.steps / (mhz if mhz else 2400.0)   # us per launch
+    ttype = (np.arange(wg) * 32) // max(1, N // 20)
+    by_type = {int(k): [round(float(per[ttype == k, j].mean()), 2) for j in range(3)] for k in np.unique(ttype)}
+    slow = np.argsort(-per[:, 0])[:8]
+    if a.dump:
+        np.save(a.dump, per)
     # the last launch's timeline (us from its first workgroup's start): start spread, W0 lifetimes, last-wave ends
-    wg = (N + 31) // 32
     tl = np.zeros((wg, 3), np.uint64)
     lib.t1env_debug_wgtime6(tl.ctypes.data_as(ctypes.c_void_p), wg)
     t0 = int(tl[:, 0].min())
@@ -54,6 +66,9 @@ def main():
                       "w0_lifetime_us_mean": round(ticks / max(1, launches) / 100.0, 2),
                       "last_launch_us": {"start_q0_50_90_100": q(st), "w0_life_q": q(w0e - st),
                                          "wg_end_q": q(end), "after_w0_q": q(end - w0e)},
+                      "per_wg_us_life_s1wait_s2wait_q": [q(per[:, j]) for j in range(3)],
+                      "by_terrain_type_life_s1_s2": by_type,
+                      "slowest_wgs": [[int(b), [round(float(x), 2) for x in per[b]]] for b in slow],
                       "lib": os.path.basename(os.environ["T1ENV_LIB"])}))
 
 

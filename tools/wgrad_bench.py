@@ -53,8 +53,16 @@ def main():
         t_new = timed(lambda: kern(gy, x), a.reps)
         t_old = timed(lambda: (dh_policy.wgrad_splitk(gy, x), dh_policy.bias_grad(gy)), a.reps)
         flops = 2.0 * rows * M * N
-        rows_out.append({"rows": rows, "M": M, "N": N, "us_kernel": round(t_new, 2), "us_splitk": round(t_old, 2),
-                         "tflops_kernel": round(flops / t_new * 1e-6, 1)})
+        row = {"rows": rows, "M": M, "N": N, "us_kernel": round(t_new, 2), "us_splitk": round(t_old, 2),
+               "tflops_kernel": round(flops / t_new * 1e-6, 1)}
+        if a.f32:   # the same layer's forward (x W^T + b) and input gradient (gy W): the HIP GEMM against torch's
+            w = torch.randn(M, N, device=dev, generator=g) * 0.05
+            b = torch.randn(M, device=dev, generator=g)
+            row["us_fwd_gemm"] = round(timed(lambda: dh_policy.gemm_nt_f32(x, w, b), a.reps), 2)
+            row["us_fwd_addmm"] = round(timed(lambda: torch.addmm(b, x, w.t()), a.reps), 2)
+            row["us_dgrad_gemm"] = round(timed(lambda: dh_policy.gemm_nt_f32(gy, w.t()), a.reps), 2)
+            row["us_dgrad_mm"] = round(timed(lambda: gy.mm(w), a.reps), 2)
+        rows_out.append(row)
         tot_new += t_new
         tot_old += t_old
     print(json.dumps({"bench": "linear_wgrad_f32" if a.f32 else "linear_wgrad_bf16",
