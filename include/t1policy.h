@@ -144,13 +144,14 @@ int t1policy_linear_wgrad_f32(const float* gy, const float* x, int rows, int M, 
                               void* stream);
 
 /* The fp32 update's Linear forward and input-gradient GEMMs (t1policy_gemm.hip): C (R, N) = A (R, K) B (N, K)^T
- * (+ bias (N), NULL: none), act 1 then applies ELU (alpha 1), for row-major fp32 A, B, C -- nn.Linear's forward
+ * (+ bias (N), NULL: none); act 1 then applies ELU (alpha 1), act 2 multiplies by ELU's derivative at the ELU outputs
+ * aux (R, N) (1 where aux > 0, else aux + 1; aux NULL otherwise), for row-major fp32 A, B, C -- nn.Linear's forward
  * y = x W^T + b (B = W) and its input gradient gx = gy W (B = W^T) of every layer of actor_critic_dh.py:45-111 in the
  * update (dh_ppo.py:155-182; torch's addmm / mm before).  Each fp32 value split into three bf16 parts, the six part
  * products down to 2^-16 of each product on v_mfma_f32_32x32x16_bf16, fp32 sums in k order (fp32-class; deterministic).
  * Returns 0, -1 on bad arguments, -2 on a launch error. */
-int t1policy_gemm_nt_f32(const float* A, const float* B, const float* bias, float* C, int R, int N, int K, int act,
-                         void* stream);
+int t1policy_gemm_nt_f32(const float* A, const float* B, const float* bias, const float* aux, float* C, int R, int N,
+                         int K, int act, void* stream);
 
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py

@@ -226,6 +226,9 @@ def test_gemm_nt_f32_matches_fp64(R, N, K):
     assert torch.equal(y, gemm_nt_f32(a, b, bias))
     ye = gemm_nt_f32(a, b, bias, act=1)
     torch.testing.assert_close(ye, torch.nn.functional.elu(y), rtol=1e-6, atol=1e-7)
+    aux = torch.randn(R, N, device=DEV, generator=g)
+    yd = gemm_nt_f32(a, b, bias, act=2, aux=aux)
+    assert torch.equal(yd, y * torch.where(aux > 0, torch.ones_like(aux), aux + 1.0))
 
 
 def test_linear_fp32_forward_and_input_gradient_use_the_gemm(monkeypatch):
@@ -245,3 +248,38 @@ def test_linear_fp32_forward_and_input_gradient_use_the_gemm(monkeypatch):
     ref_y = torch.addmm(lin.bias, x, lin.weight.t())
     torch.testing.assert_close(y, ref_y, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(x.grad, gy @ lin.weight, rtol=1e-5, atol=1e-6)
+
+
+def test_mlp_fp32_fused_node_matches_layer_by_layer(monkeypatch):
+    """The fp32 update's MLP as one autograd node (_MlpF32: ELU fused into the forward GEMMs, ELU's derivative into the
+    input-gradient GEMMs) against the layer-by-layer path (T1_MLP_F32 off): outputs and every gradient within fp32
+    summation order, and inside direct_grad_accumulation() the weight gradients added into the existing .grad."""
+    from ti5_isaacgym_amd.algo import dh_policy
+    torch.manual_seed(11)
+    mlp = dh_policy._mlp([302, 512, 256, 128, 12], torch.nn.ELU()).to(DEV)
+    assert isinstance(mlp, dh_policy.MLP) and mlp._fusable()
+    x = torch.randn(6000, 302, device=DEV, requires_grad=True)
+    go = torch.randn(6000, 12, device=DEV)
+
+    def run(flag):
+        monkeypatch.setattr(dh_policy, "MLP_F32", flag)
+        mlp.zero_grad(set_to_none=True)
+        x.grad = None
+        y = mlp(x)
+        y.backward(go)
+        return y.detach().clone(), x.grad.clone(), [p.grad.clone() for p in mlp.parameters()]
+
+    y1, gx1, g1 = run(True)
+    y0, gx0, g0 = run(False)
+    torch.testing.assert_close(y1, y0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gx1, gx0, rtol=1e-4, atol=1e-5 * gx0.abs().max().item())
+    for a, b in zip(g1, g0):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * b.abs().max().item())
+    # direct accumulation: a second backward inside the context doubles every .grad
+    monkeypatch.setattr(dh_policy, "MLP_F32", True)
+    for p, a in zip(mlp.parameters(), g1):
+        p.grad = a.clone()
+    with dh_policy.direct_grad_accumulation():
+        mlp(x).backward(go)
+    for a, p in zip(g1, mlp.parameters()):
+        torch.testing.assert_close(p.grad, 2 * a, rtol=1e-6, atol=1e-7)

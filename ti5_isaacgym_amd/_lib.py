@@ -157,7 +157,7 @@ def load():
         "t1policy_linear_wgrad_workspace_bytes": ([i32, i32, i32], C.c_longlong),
         "t1policy_linear_wgrad_bf16": ([vp, vp, i32, i32, i32, vp, C.c_longlong, vp, vp, i32, vp], C.c_int),
         "t1policy_linear_wgrad_f32": ([vp, vp, i32, i32, i32, vp, C.c_longlong, vp, vp, i32, vp], C.c_int),
-        "t1policy_gemm_nt_f32": ([vp, vp, vp, vp, i32, i32, i32, i32, vp], C.c_int),
+        "t1policy_gemm_nt_f32": ([vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], C.c_int),
         "t1policy_fold_rows": ([vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
         "t1policy_gather_rows": ([vp, vp, vp, i32, vp, i32, vp], C.c_int),
     }

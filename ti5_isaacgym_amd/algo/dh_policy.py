@@ -171,9 +171,10 @@ def linear_wgrad_f32(gy, x, need_bias=True, into=None):
 GEMM_F32 = os.environ.get("T1_GEMM_F32", "1") != "0"
 
 
-def gemm_nt_f32(a, b, bias=None, act=0):
-    """a (R, K) @ b (N, K)^T (+ bias) (ELU with act=1) in fp32 on the matrix cores (t1policy_gemm_nt_f32: each value in
-    three bf16 parts, fp32-class sums in k order).  Device fp32 tensors."""
+def gemm_nt_f32(a, b, bias=None, act=0, aux=None):
+    """a (R, K) @ b (N, K)^T (+ bias) in fp32 on the matrix cores (t1policy_gemm_nt_f32: each value in three bf16 parts,
+    fp32-class sums in k order), then act=1: ELU (alpha 1); act=2: times ELU's derivative at the ELU outputs aux (R, N)
+    (1 where aux > 0, else aux + 1) -- the backward of a Linear whose input came out of an ELU.  Device fp32 tensors."""
     from .. import _lib
     lib = _lib.load()
     a, b = a.contiguous(), b.contiguous()
@@ -182,11 +183,16 @@ def gemm_nt_f32(a, b, bias=None, act=0):
     if b.shape[1] != K or a.dtype != torch.float32 or b.dtype != torch.float32:
         raise ValueError(f"gemm_nt_f32: {tuple(a.shape)} x {tuple(b.shape)}^T ({a.dtype}, {b.dtype})")
     out = torch.empty(R, N, device=a.device, dtype=torch.float32)
-    bp = None
+    bp = xp = None
     if bias is not None:
         bias = bias.contiguous()
         bp = bias.data_ptr()
-    rc = lib.t1policy_gemm_nt_f32(a.data_ptr(), b.data_ptr(), bp, out.data_ptr(), R, N, K, act,
+    if act == 2:
+        if aux is None or tuple(aux.shape) != (R, N) or aux.dtype != torch.float32:
+            raise ValueError("gemm_nt_f32: act=2 needs the (R, N) fp32 ELU outputs")
+        aux = aux.contiguous()
+        xp = aux.data_ptr()
+    rc = lib.t1policy_gemm_nt_f32(a.data_ptr(), b.data_ptr(), bp, xp, out.data_ptr(), R, N, K, act,
                                   torch.cuda.current_stream(a.device).cuda_stream)
     if rc != 0:
         raise RuntimeError(f"t1policy_gemm_nt_f32 failed (rc={rc})")
@@ -339,6 +345,91 @@ def plain_copy(module):
     return copy.deepcopy(module)
 
 
+# the fp32 update's MLPs (actor, critic, state estimator) as one autograd node on the fused HIP GEMMs (_MlpF32);
+# T1_MLP_F32=0: layer by layer (A/B)
+MLP_F32 = os.environ.get("T1_MLP_F32", "1") != "0"
+
+
+class _MlpF32(torch.autograd.Function):
+    """Linear, ELU, Linear, ELU, ..., Linear (actor_critic_dh.py:45-111) in the fp32 update on the matrix cores, with
+    each ELU fused into a GEMM: forward, every hidden layer is gemm_nt_f32(x, W, b, ELU) (no separate ELU pass over
+    the activations); backward, the input gradient of layer i + 1 comes out of its GEMM already multiplied by ELU's
+    derivative at layer i's output (act=2, no separate ELU-backward pass), then layer i's weight gradient is the
+    three-part-split wgrad kernel (added straight into .grad inside direct_grad_accumulation(), as _LinearSplitK).
+    The same sums as the layer-by-layer path in fp32 (up to the ELU being applied to the GEMM's fp32 result in its
+    epilogue instead of by torch's kernel)."""
+
+    @staticmethod
+    def forward(ctx, x, *params):
+        n = len(params) // 2
+        h, outs = x, []
+        for i in range(n):
+            h = gemm_nt_f32(h, params[2 * i], params[2 * i + 1], act=1 if i < n - 1 else 0)
+            if i < n - 1:
+                outs.append(h)
+        ctx.n = n
+        # the leaf parameters (their .grad for the direct accumulation), as _LinearSplitK
+        ctx.leaves = [p if p.is_leaf else None for p in params]
+        ctx.save_for_backward(x, *params, *outs)
+        return h
+
+    @staticmethod
+    def backward(ctx, g):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        x, params, outs = saved[0], saved[1:1 + 2 * n], saved[1 + 2 * n:]
+        grads = [None] * (2 * n)
+        g = g.contiguous()
+        direct = GRAD_DIRECT and _DIRECT_GRAD[0]
+        gx = None
+        for i in range(n - 1, -1, -1):
+            w = params[2 * i]
+            inp = x if i == 0 else outs[i - 1]
+            need_w, need_b = ctx.needs_input_grad[1 + 2 * i], ctx.needs_input_grad[2 + 2 * i]
+            wl, bl = ctx.leaves[2 * i], ctx.leaves[2 * i + 1]
+            if need_w:
+                if (direct and wl is not None and wl.grad is not None and wl.grad.dtype == torch.float32
+                        and wl.grad.is_contiguous() and (not need_b or (bl is not None and bl.grad is not None
+                                                                        and bl.grad.dtype == torch.float32))):
+                    linear_wgrad_f32(g, inp, into=(wl.grad, bl.grad if need_b else None))
+                else:
+                    grads[2 * i], gb = linear_wgrad_f32(g, inp, need_bias=need_b)
+                    grads[2 * i + 1] = gb
+            elif need_b:
+                grads[2 * i + 1] = g.sum(0)
+            if i > 0:
+                g = gemm_nt_f32(g, w.t(), act=2, aux=outs[i - 1])   # (g W) * ELU'(layer i-1's output)
+            elif ctx.needs_input_grad[0]:
+                gx = gemm_nt_f32(g, w.t())
+        return (gx, *grads)
+
+
+class MLP(nn.Sequential):
+    """The reference's MLP (nn.Sequential of Linear and the shared activation, actor_critic_dh.py:45-111; the same
+    parameter names).  On the host, and whenever the layers are not Linear / ELU(alpha 1) alternating, it runs as
+    written; in the fp32 update on the device (autograd on, no autocast) as one _MlpF32 node."""
+
+    def _fusable(self):
+        mods = list(self)
+        if len(mods) % 2 != 1:
+            return False
+        for i, m in enumerate(mods):
+            if i % 2 == 0 and not (isinstance(m, nn.Linear) and m.bias is not None and m.weight.dtype == torch.float32):
+                return False
+            if i % 2 == 1 and not (isinstance(m, nn.ELU) and m.alpha == 1.0):
+                return False
+        return True
+
+    def forward(self, x):
+        if (MLP_F32 and GEMM_F32 and LINEAR_WGRAD_F32 and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+                and torch.is_grad_enabled() and not torch.is_autocast_enabled("cuda") and self._fusable()):
+            params = []
+            for m in list(self)[::2]:
+                params += [m.weight, m.bias]
+            return _MlpF32.apply(x.contiguous(), *params)
+        return super().forward(x)
+
+
 def _mlp(sizes, act):
     """Linear layers between consecutive sizes, `act` after every hidden layer (not after the output)."""
     layers = []
@@ -346,7 +437,7 @@ def _mlp(sizes, act):
         layers.append(Linear(a, b))
         if i < len(sizes) - 2:
             layers.append(act)
-    return nn.Sequential(*layers)
+    return MLP(*layers)
 
 
 def conv1d_direct(x, conv):

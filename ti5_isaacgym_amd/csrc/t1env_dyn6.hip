@@ -159,6 +159,13 @@ enum : int { WC_SHA = 0, WC_SHB = 1, WC_FTA = 2, WC_FTB = 3, WC_SSH = 4, WC_SFT 
 #define T1_D6_SHIFT_MASK ((1 << 1) | (1 << 5) | (1 << 2) | (1 << 6) | (1 << 3) | (1 << 7))
 #endif
 constexpr int SHIFT6_MASK = T1_D6_SHIFT_MASK;  // by role (below)
+// the shift roles that commit their slice (and issue the next one's loads) before S2, in the slack their role work
+// leaves ahead of the core wave's pre-S2 chain, instead of after S2 where the core wave may wait for them at S1
+// (-DT1_D6_SHIFT_PRE_MASK=..., by role; 0: every shift role after S2)
+#ifndef T1_D6_SHIFT_PRE_MASK
+#define T1_D6_SHIFT_PRE_MASK 0
+#endif
+constexpr int SHIFT6_PRE_MASK = T1_D6_SHIFT_PRE_MASK;
 // The role of each wave: role ids are the wave numbers of the table at the top (0 core, 4 base, 1 RNEA, 5 self, 2 / 6
 // shank halves, 3 / 7 foot halves); T1_D6_ROLE_MAP holds the role of wave w in hex digit w, so the SIMD pairs (w, w + 4)
 // can be re-dealt for A/B (the core stays wave 0: its partner is wave 4's role)
@@ -190,6 +197,7 @@ struct Dyn6Lds {
   float vish[64];         // the shank's restitution episode (W0 updates it after S2; W2 / W6 read it)
   float vift[64];         // the foot's (W0; W3 / W7)
   float amx[4][64];       // the fastest approach among the points of the shank halves [0, 1] and foot halves [2, 3]
+  int s1flag;             // T1_D6_S1_FLAG: the number of substep states W0 has published (S1 as a one-way signal)
   LegParams<float> pl[64];   // W0's per-lane leg parameters (CRBA) and base parameters (report, log): LDS, not
   BaseParams<float> pb[64];  // registers held across the substep loop
   float rtf[2][3][64];    // the report: terrain forces on the shank [0] (W2) / foot [1] (W3)
@@ -373,6 +381,28 @@ __device__ __forceinline__ const DynModel& model_in_loop(const DynModel& m) {
   asm volatile("" : "+s"(p));
   return *(const DynModel*)p;
 }
+
+// S1 as a one-way signal (-DT1_D6_S1_FLAG): W0 publishes the substep state and counts it in an LDS word instead of
+// meeting the other seven waves at a workgroup barrier, so it starts its next pre-S2 chain at once; a role wave waits
+// for the count before it reads the state.  What S1 also ordered still holds: W0 finishes its reads of the role rows
+// (wb, w1, wc, amx) before it publishes, and the role waves write them only after the count, and S2 (a full barrier)
+// keeps W0 from publishing over a state a role still reads.  The wait is bounded (it never runs long: W0 signals
+// every substep), so a fault cannot turn into a hang.
+__device__ __forceinline__ void s1_signal(int* flag, int value) {
+  __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void s1_wait(int* flag, int target) {
+  for (int i = 0; i < (1 << 22); ++i) {
+    const int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (v >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+#ifdef T1_D6_S1_FLAG
+#define D6_S1(target) s1_wait(&lds.s1flag, (target))
+#else
+#define D6_S1(target) __syncthreads()
+#endif
 
 // the other leg's capsule ends and velocity (from the other half of the wave) for the self-contact terms / forces
 __device__ __forceinline__ void self_bodies(const DynModel& M, int leg, const BodyKin<float> (&Ko)[2],
@@ -560,6 +590,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   const int nsub = C.decimation;
   const int64_t r0 = (int64_t)blockIdx.x * NE6, r1 = r0 + NE6 < N ? r0 + NE6 : N;
   T1_PROF_BEGIN();
+  if (threadIdx.x == 0) lds.s1flag = 0;
   __syncthreads();  // the model in LDS
   const DynModel& M = lds.model;
 
@@ -628,7 +659,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     base_contact_range(M, leg, cb, ce);
     T1_PROF_MARK(0);
     for (int sub = 0; sub < nsub; ++sub) {
-      __syncthreads();  // S1: the substep state published
+      D6_S1(sub + 1);  // S1: the substep state published
       T1_PROF_MARK(1);
       const DynModel& M = model_in_loop(lds.model);
       BaseState<float> sb;
@@ -743,7 +774,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       if (wi >= 0) shp_issue_slice(S, r0, r1, 0, nsub, wi, lane, hold);
       for (int sub = 0; sub < nsub; ++sub) {
         T1_PROF_MARK(4);
-        __syncthreads();  // S1
+        D6_S1(sub + 1);  // S1
         T1_PROF_MARK(1);
         BaseState<float> sb;
         float q[NLEG], qd[NLEG];
@@ -758,11 +789,15 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 6; ++i) v[R_G + i] = G[i];
         put4(lds.w1, lane, v);
+        if (wi >= 0 && ((SHIFT6_PRE_MASK >> role) & 1)) {  // the slice before S2 (T1_D6_SHIFT_PRE_MASK)
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+          shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
+        }
         T1_PROF_MARK(2);
         __syncthreads();  // S2
         T1_PROF_MARK(3);
-        if (wi >= 0) {  // slice sub (its loads issued a substep ago), then slice sub + 1's loads
-          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+        if (wi >= 0 && !((SHIFT6_PRE_MASK >> role) & 1)) {  // slice sub (its loads issued a substep ago), then
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);  // slice sub + 1's loads
           shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
         }
       }
@@ -772,7 +807,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       if (wi >= 0) shp_issue_slice(S, r0, r1, 0, nsub, wi, lane, hold);
       for (int sub = 0; sub < nsub; ++sub) {
         T1_PROF_MARK(4);
-        __syncthreads();  // S1
+        D6_S1(sub + 1);  // S1
         T1_PROF_MARK(1);
         BaseState<float> sb;
         float q[NLEG], qd[NLEG];
@@ -800,11 +835,15 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
           sym_pack(Cs[i], cs[i], v);
           put4(lds.wc[WC_SSH + i], lane, v);
         }
+        if (wi >= 0 && ((SHIFT6_PRE_MASK >> role) & 1)) {  // the slice before S2 (T1_D6_SHIFT_PRE_MASK)
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+          shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
+        }
         T1_PROF_MARK(2);
         __syncthreads();  // S2
         T1_PROF_MARK(3);
-        if (wi >= 0) {  // slice sub (its loads issued a substep ago), then slice sub + 1's loads
-          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+        if (wi >= 0 && !((SHIFT6_PRE_MASK >> role) & 1)) {  // slice sub (its loads issued a substep ago), then
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);  // slice sub + 1's loads
           shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
         }
       }
@@ -825,7 +864,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
       if (wi >= 0) shp_issue_slice(S, r0, r1, 0, nsub, wi, lane, hold);
       for (int sub = 0; sub < nsub; ++sub) {
         T1_PROF_MARK(4);
-        __syncthreads();  // S1
+        D6_S1(sub + 1);  // S1
         T1_PROF_MARK(1);
         BaseState<float> sb;
         float q[NLEG], qd[NLEG];
@@ -851,11 +890,15 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
         sym_pack(Cc, cc, v);
         put4(lds.wc[slot], lane, v);
         lds.amx[slot][lane] = amax;
+        if (wi >= 0 && ((SHIFT6_PRE_MASK >> role) & 1)) {  // the slice before S2 (T1_D6_SHIFT_PRE_MASK)
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+          shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
+        }
         T1_PROF_MARK(2);
         __syncthreads();  // S2
         T1_PROF_MARK(3);
-        if (wi >= 0) {  // slice sub (its loads issued a substep ago), then slice sub + 1's loads
-          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);
+        if (wi >= 0 && !((SHIFT6_PRE_MASK >> role) & 1)) {  // slice sub (its loads issued a substep ago), then
+          shp_commit_slice(S, r0, r1, sub, nsub, wi, lane, hold);  // slice sub + 1's loads
           shp_issue_slice(S, r0, r1, sub + 1, nsub, wi, lane, hold);
         }
       }
@@ -989,12 +1032,17 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
   lds.vift[lane] = vi_ft;
   lds.vish[lane] = vi_sh;
   T1_PROF_MARK(0);
+#ifdef T1_D6_S1_FLAG
+  s1_signal(&lds.s1flag, 1);  // the first substep's state (and the episodes) published
+#endif
   for (int sub = 0; sub < nsub; ++sub) {
+#ifndef T1_D6_S1_FLAG
     {
       T1_CLOCK_WAIT_BEGIN();
       __syncthreads();  // S1: the substep state published
       T1_CLOCK_WAIT_END(1);
     }
+#endif
     T1_PROF_MARK(1);
     // -DT1_D6_LAUNDER (A/B): the lane and leg through an empty asm each substep, so the lane- and leg-indexed LDS
     // addresses are formed in the loop instead of hoisted and spilled: no scratch reloads in the loop, yet measured
@@ -1090,6 +1138,9 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
     float v[Q_N];
     state_pack(sb, q, qd, v);
     put4(lds.st, lane_s, v);  // the roles read the previous state before S2; after the last substep: the report's
+#ifdef T1_D6_S1_FLAG
+    s1_signal(&lds.s1flag, sub + 2);
+#endif
     T1_PROF_MARK(7);
   }
   BaseState<float> sb;

@@ -77,10 +77,11 @@ __device__ __forceinline__ f16v mfma_bf3(const Bf3& a, const Bf3& b, f16v acc) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
 }
 
-// grid.x: row tiles, grid.y: column tiles.  act: 0 none, 1 ELU (alpha 1, the policy's nn.ELU)
+// grid.x: row tiles, grid.y: column tiles.  act: 0 none, 1 ELU (alpha 1, the policy's nn.ELU), 2 times ELU's derivative
+// at the ELU outputs aux (R x N): the input gradient of a Linear whose input is an ELU's output
 __global__ __launch_bounds__(256, 2) void k_gemm_nt_f32x3(const float* __restrict__ A, const float* __restrict__ B,
-                                                          const float* __restrict__ bias, float* __restrict__ C, int R,
-                                                          int N, int K, int act) {
+                                                          const float* __restrict__ bias, const float* __restrict__ aux,
+                                                          float* __restrict__ C, int R, int N, int K, int act) {
   __shared__ __attribute__((aligned(16))) float IMG[2][2][GM_T * GM_PITCH];  // [buffer][A, B]
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, h = lane >> 5;
   const int wm = wave & 1, wn = wave >> 1;
@@ -142,7 +143,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt_f32x3(const float* __restric
         const int m = r0 + 64 * wm + 32 * a + (q & 3) + 8 * (q >> 2) + 4 * h;
         float v = acc[a][b][q] + bv;
         if (act == 1) v = v > 0.0f ? v : expm1f(v);
-        if (m < R && n < N) C[(size_t)m * N + n] = v;
+        if (m < R && n < N) {
+          if (act == 2) {  // times ELU's derivative at the ELU output e (alpha 1: 1 for e > 0, else e + 1)
+            const float e = aux[(size_t)m * N + n];
+            v = v * (e > 0.0f ? 1.0f : e + 1.0f);
+          }
+          C[(size_t)m * N + n] = v;
+        }
       }
     }
   }
@@ -152,12 +159,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt_f32x3(const float* __restric
 
 extern "C" {
 
-int t1policy_gemm_nt_f32(const float* A, const float* B, const float* bias, float* C, int R, int N, int K, int act,
-                         void* stream) {
-  if (!A || !B || !C || R <= 0 || N <= 0 || K <= 0 || act < 0 || act > 1) return -1;
+int t1policy_gemm_nt_f32(const float* A, const float* B, const float* bias, const float* aux, float* C, int R, int N,
+                         int K, int act, void* stream) {
+  if (!A || !B || !C || R <= 0 || N <= 0 || K <= 0 || act < 0 || act > 2 || (act == 2 && !aux)) return -1;
   if ((long long)R * (K > N ? K : N) >= (1LL << 31)) return -1;
   const dim3 grid((R + GM_T - 1) / GM_T, (N + GM_T - 1) / GM_T);
-  hipLaunchKernelGGL(k_gemm_nt_f32x3, grid, dim3(256), 0, (hipStream_t)stream, A, B, bias, C, R, N, K, act);
+  hipLaunchKernelGGL(k_gemm_nt_f32x3, grid, dim3(256), 0, (hipStream_t)stream, A, B, bias, aux, C, R, N, K, act);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -15,7 +15,7 @@ import json
 import sqlite3
 import statistics
 
-STEP_KERNELS = ["k_dyn6", "k_dyn5", "k_shift5", "k_dyn4", "k_dynamics", "k_post_a", "k_post_b", "k_shift", "k_stack", "k_finalize", "k_terrain_level_sum"]
+STEP_KERNELS = ["k_dyn6", "k_dyn5", "k_shift5", "k_shift4c", "k_dyn4", "k_dynamics", "k_post_a", "k_post_b", "k_shift", "k_stack", "k_finalize", "k_terrain_level_sum"]
 FETCH_CORRECTION = 2.0
 
 
