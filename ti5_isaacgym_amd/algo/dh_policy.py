@@ -345,9 +345,10 @@ def plain_copy(module):
     return copy.deepcopy(module)
 
 
-# the fp32 update's MLPs (actor, critic, state estimator) as one autograd node on the fused HIP GEMMs (_MlpF32);
-# T1_MLP_F32=0: layer by layer (A/B)
-MLP_F32 = os.environ.get("T1_MLP_F32", "1") != "0"
+# the fp32 update's MLPs (actor, critic, state estimator) as one autograd node on the fused HIP GEMMs (_MlpF32), opt-in
+# (T1_MLP_F32=1): it removes the ELU passes (3.3 ms per update) but its fused epilogues cost as much -- the update measured
+# 41.3 ms with it against 40.9 layer by layer (profiles/r06h_*, r06f_*)
+MLP_F32 = os.environ.get("T1_MLP_F32", "0") == "1"
 
 
 class _MlpF32(torch.autograd.Function):

@@ -251,6 +251,16 @@ __device__ __forceinline__ void shp_range(int64_t total, int64_t r0, int64_t r1,
   lo = n * (uint32_t)sl / (uint32_t)nsl;
   hi = n * (uint32_t)(sl + 1) / (uint32_t)nsl;
 }
+// One 16-B load from the exact source of a chunk (4-byte aligned for fp32 histories, 2-byte for fp16) -- the hardware
+// serves an unaligned dwordx4 (the unaligned access mode ROCm sets for gfx9; tools/probes/unaligned_x4.hip) -- instead
+// of the two aligned blocks around it and an alignbyte window (-DT1_D6_SHIFT_ALIGNED2, A/B): half the load instructions
+// of a slice and half the registers held across the substep (ShiftHold::b unused)
+#ifndef T1_D6_SHIFT_ALIGNED2
+constexpr bool SHIFT_EXACT32 = true;
+#else
+constexpr bool SHIFT_EXACT32 = false;
+#endif
+typedef float shift_f4 __attribute__((ext_vector_type(4)));
 // the source loads of U chunks (lane t0's, `stride` apart from chunk lo)
 template <int F, bool HALF, int U>
 __device__ __forceinline__ void shift_loads(const uint8_t* in0, uint32_t lo, uint32_t lim, int t0, int stride,
@@ -259,10 +269,17 @@ __device__ __forceinline__ void shift_loads(const uint8_t* in0, uint32_t lo, uin
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t c = lo + (uint32_t)(t0 + u * stride);
-    const uint32_t sa = (c * PER + F) & ~(PER - 1);
-    const uint32_t sc = sa + 2 * PER <= lim ? sa : (lim - 2 * PER) & ~(PER - 1);  // tail: an aligned in-bounds dummy
-    a[u] = *reinterpret_cast<const float4*>(in0 + (size_t)sc * ES);
-    b[u] = *reinterpret_cast<const float4*>(in0 + (size_t)(sc + PER) * ES);
+    if constexpr (SHIFT_EXACT32) {
+      const uint32_t src = c * PER + F;
+      const uint32_t sc = src + PER <= lim ? src : lim - PER;  // tail: an in-bounds dummy
+      const shift_f4 v = *reinterpret_cast<const shift_f4*>(in0 + (size_t)sc * ES);
+      a[u] = make_float4(v.x, v.y, v.z, v.w);
+    } else {
+      const uint32_t sa = (c * PER + F) & ~(PER - 1);
+      const uint32_t sc = sa + 2 * PER <= lim ? sa : (lim - 2 * PER) & ~(PER - 1);  // tail: an aligned in-bounds dummy
+      a[u] = *reinterpret_cast<const float4*>(in0 + (size_t)sc * ES);
+      b[u] = *reinterpret_cast<const float4*>(in0 + (size_t)(sc + PER) * ES);
+    }
   }
 }
 // the stores of U chunks from their loaded source blocks (whole chunks; the rest by the element path)
@@ -275,12 +292,21 @@ __device__ __forceinline__ void shift_stores(const uint8_t* in0, uint8_t* out0, 
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t c = lo + (uint32_t)(t0 + u * stride), i = c * PER;
-    const uint32_t sa = (i + F) & ~(PER - 1);
-    if (c < hi) {
-      if (i + PER <= nel && sa + 2 * PER <= lim)
-        __builtin_nontemporal_store(shift_window<OFF>(a[u], b[u]), reinterpret_cast<u32x4*>(out0 + (size_t)i * ES));
-      else
-        slow |= 1u << u;
+    if constexpr (SHIFT_EXACT32) {
+      if (c < hi) {
+        if (i + PER <= nel && i + F + PER <= lim)
+          __builtin_nontemporal_store(__builtin_bit_cast(u32x4, a[u]), reinterpret_cast<u32x4*>(out0 + (size_t)i * ES));
+        else
+          slow |= 1u << u;
+      }
+    } else {
+      const uint32_t sa = (i + F) & ~(PER - 1);
+      if (c < hi) {
+        if (i + PER <= nel && sa + 2 * PER <= lim)
+          __builtin_nontemporal_store(shift_window<OFF>(a[u], b[u]), reinterpret_cast<u32x4*>(out0 + (size_t)i * ES));
+        else
+          slow |= 1u << u;
+      }
     }
   }
   if (slow) {
