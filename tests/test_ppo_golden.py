@@ -15,8 +15,9 @@ through the build with the reference's recorded actions and minibatch permutatio
     hence the abs-sum-relative bounds rather than elementwise equality.
 
 CPU here (the reference's device): measured, the updated weights come out bit-identical to the reference's and the
-losses within 2e-7 (the build sums them on the device).  The same replay runs on the MI355X (hipBLASLt / MIOpen
-kernels) in the gpu test, with the bounds above.
+losses within 2e-7 (the build sums them on the device).  The same replay runs on the MI355X (the HIP fp32 update
+kernels: three-part bf16 split weight gradients, the packed conv, hipBLASLt or the HIP GEMM) in the gpu test, with the
+same bounds (measured: losses within 2.5e-5, weight-delta abs-sums within 1.1e-6).
 """
 import numpy as np
 import pytest
@@ -116,4 +117,6 @@ def test_update_matches_reference_cpu(monkeypatch):
 
 @pytest.mark.gpu
 def test_update_matches_reference_gpu(monkeypatch):
-    check_update(*replay("cuda:0", monkeypatch), loss_rtol=1e-3, lr_rtol=1e-6)
+    # the CPU's loss bound: the fp32 update's weight gradients are fp32-class on the device too (three-part bf16 split
+    # on the matrix cores; measured within 2.5e-5 relative of the reference's losses, profiles/r06e_update_tests.txt)
+    check_update(*replay("cuda:0", monkeypatch), loss_rtol=1e-4, lr_rtol=1e-6)
