@@ -52,9 +52,11 @@ __device__ unsigned g_t1_simd6[4096][8];
 __device__ unsigned long long g_t1_clock6[4];
 // and the timeline of the last launch, per workgroup: {start, W0 end, last wave's end} in 100 MHz ticks; per workgroup
 // summed over launches: {W0 lifetime, W0's S1 waits, W0's S2 waits} in shader cycles
-__device__ unsigned long long g_t1_wgtime6[4096][3];
+__device__ unsigned long long g_t1_wgtime6[4096][4];  // + [3]: W0's substep loop end
 __device__ unsigned long long g_t1_wgsum6[4096][3];
 #define T1_CLOCK_WAIT_BEGIN() const unsigned long long t1c_w0 = __builtin_amdgcn_s_memtime();
+#define T1_CLOCK_LOOP_END()                                                        \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) g_t1_wgtime6[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
 #define T1_CLOCK_WAIT_END(k)                                                       \
   if (threadIdx.x == 0 && blockIdx.x < 4096)                                       \
     atomicAdd(&g_t1_wgsum6[blockIdx.x][k], __builtin_amdgcn_s_memtime() - t1c_w0);
@@ -86,6 +88,7 @@ __device__ unsigned long long g_t1_wgsum6[4096][3];
 #define T1_CLOCK_WAVE_END() ((void)0)
 #define T1_CLOCK_WAIT_BEGIN() ((void)0)
 #define T1_CLOCK_WAIT_END(k) ((void)0)
+#define T1_CLOCK_LOOP_END() ((void)0)
 #endif
 // -DT1_PHASE_PROF (tools/prof_dynamics_phases.py --kernel 6): lane 0 of every wave accumulates shader-clock deltas
 // between T1_PROF_MARK points into per-phase buckets; never part of the product build.
@@ -1169,6 +1172,7 @@ __global__ __launch_bounds__(D6_BLOCK) void k_dyn6(const DynModel* __restrict__ 
 #endif
     T1_PROF_MARK(7);
   }
+  T1_CLOCK_LOOP_END();
   BaseState<float> sb;
   float q[NLEG], qd[NLEG];
   read_state_rows(lds.st, lane, sb, q, qd);
@@ -1220,7 +1224,7 @@ extern "C" int t1env_debug_simd6(unsigned* out, int blocks) {
 // probe build only: {cycles, constant-clock ticks, workgroup count} summed since the last reset (reset != 0: zeroed after
 // the read)
 extern "C" int t1env_debug_wgtime6(unsigned long long* out, int blocks) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_wgtime6), sizeof(unsigned long long) * 3 * (size_t)blocks);
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_wgtime6), sizeof(unsigned long long) * 4 * (size_t)blocks);
 }
 extern "C" int t1env_debug_wgsum6(unsigned long long* out, int blocks, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_wgsum6), sizeof(unsigned long long) * 3 * (size_t)blocks);

@@ -56,16 +56,26 @@ def main():
     if a.dump:
         np.save(a.dump, per)
     # the last launch's timeline (us from its first workgroup's start): start spread, W0 lifetimes, last-wave ends
-    tl = np.zeros((wg, 3), np.uint64)
+    tl = np.zeros((wg, 4), np.uint64)
     lib.t1env_debug_wgtime6(tl.ctypes.data_as(ctypes.c_void_p), wg)
     t0 = int(tl[:, 0].min())
-    st, w0e, end = ((tl[:, k].astype(np.int64) - t0) / 100.0 for k in range(3))
+    st, w0e, end, lend = ((tl[:, k].astype(np.int64) - t0) / 100.0 for k in range(4))
+    # the last launch's resets per workgroup (the reset buffer after the step) against its loop / epilogue times
+    rs = env.reset_buf.detach().to(torch.int32).cpu().numpy()[: wg * 32].reshape(wg, 32).sum(1)
+    loop_t, epi_t = lend - st, w0e - lend
+    epi_by_resets = {"0": round(float(epi_t[rs == 0].mean()), 2) if (rs == 0).any() else None,
+                     ">=1": round(float(epi_t[rs > 0].mean()), 2) if (rs > 0).any() else None,
+                     "wgs_with_resets": int((rs > 0).sum())}
     q = lambda v: [round(float(x), 2) for x in np.quantile(v, [0, 0.5, 0.9, 1.0])]  # noqa: E731
     print(json.dumps({"ms_per_step": round(ms, 4), "launches_x_workgroups": launches,
                       "shader_mhz": round(mhz, 1) if mhz else None,
                       "w0_lifetime_us_mean": round(ticks / max(1, launches) / 100.0, 2),
                       "last_launch_us": {"start_q0_50_90_100": q(st), "w0_life_q": q(w0e - st),
-                                         "wg_end_q": q(end), "after_w0_q": q(end - w0e)},
+                                         "wg_end_q": q(end), "after_w0_q": q(end - w0e),
+                                         "loop_q": q(loop_t), "epilogue_q": q(epi_t),
+                                         "epilogue_by_resets": epi_by_resets,
+                                         "slowest_end_wgs": [[int(b), round(float(loop_t[b]), 2), round(float(epi_t[b]), 2),
+                                                              int(rs[b])] for b in np.argsort(-end)[:6]]},
                       "per_wg_us_life_s1wait_s2wait_q": [q(per[:, j]) for j in range(3)],
                       "by_terrain_type_life_s1_s2": by_type,
                       "slowest_wgs": [[int(b), [round(float(x), 2) for x in per[b]]] for b in slow],
