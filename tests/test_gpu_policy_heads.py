@@ -45,7 +45,9 @@ def _copy(ac):
     return m
 
 
-@pytest.mark.parametrize("n,scale", [(1000, 1.0), (4096, 1.5), (33, 1.0)])
+# 3000: the batch of round 5's reverted side-stream split, whose first test faulted -- the shipped
+# one-launch kernel at that ragged batch (93 full 32-env workgroups and a 24-env tail)
+@pytest.mark.parametrize("n,scale", [(1000, 1.0), (4096, 1.5), (33, 1.0), (3000, 1.0)])
 def test_fused_heads_match_fp64(n, scale):
     from ti5_isaacgym_amd.algo.dh_policy import heads_forward
     ac = _model(scale=scale)

@@ -5,6 +5,8 @@ set -e
 tag=${1:-final}
 out=$GRAFT_REPO_ROOT/gpurun_out/$tag
 mkdir -p $out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_policy_heads.py -m gpu -x -q --timeout 120 --timeout-method thread > $out/heads_tests.log 2>&1
+tail -1 $out/heads_tests.log
 cd /tmp && export TMPDIR=/tmp
 B="$GRAFT_REPO_ROOT/bench.py --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out -o run -- python3 $B --steps 100 --warmup 20 > $out/bench_prof.json 2> $out/prof.log
