@@ -36,6 +36,9 @@ sys.path.insert(0, REPO)
 B_ALG = 30678          # algorithmic bytes per env-step (fp32, default t1 config)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SHADER_GHZ = 2.4       # MI355X peak engine clock
+# the committed PMC traffic profiles (tools/pmc_traffic.py over rocprofv3 FETCH_SIZE / WRITE_SIZE passes): config 3
+# (the metric) and config 5; the roofline's "traffic" is the one whose workload matches the run's, else null
+TRAFFIC_PROFILES = [os.path.join(REPO, "profiles", f) for f in ("traffic_r06fb.json", "traffic_r06fb_cfg5.json")]
 LONE_WAVE_VALU_PER_CYCLE = 0.25  # one VALU instruction per 4 cycles for a wave alone on its SIMD (MI355X_MICROARCH.md,
                                  # 'vector-instruction ISSUE cost'); k_dyn5 runs one wave per SIMD (405 registers)
 SIMD_VALU_PER_CYCLE = 0.5        # a SIMD with two or more waves: one wave64 VALU instruction per 2 cycles (k_dyn6)
@@ -92,9 +95,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--cpu-shards", type=int, default=32,
                    help="CPU baseline: env shards stepped on Python threads (at most the affinity's core count)")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r05fa.json"),
-                   help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); included when present")
-    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r05fa_sq_counters.json"),
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC-measured HBM bytes per kernel (from tools/pmc_traffic.py); default: the committed profile "
+                        "of this workload (TRAFFIC_PROFILES), included when one matches")
+    p.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "r06fb_sq_counters.json"),
                    help="SQ instruction counters of the fused kernel (tools/pmc_sq_summary.py): the VALU-issue roofline")
     return p.parse_args()
 
@@ -280,12 +284,15 @@ def main():
     else:
         achieved, basis = value / world * b_alg / 1e9, "wall clock: env-steps/s x B_alg"
     traffic = None
-    if os.path.exists(args.traffic_json):
+    for path in ([args.traffic_json] if args.traffic_json else TRAFFIC_PROFILES):
+        if not os.path.exists(path):
+            continue
         try:
-            tj = json.load(open(args.traffic_json))
+            tj = json.load(open(path))
             if tj.get("num_envs") == N and tj.get("mesh") == args.mesh and \
-                    tj.get("state_dtype", "fp32") == args.state_dtype:
+                    tj.get("state_dtype", "fp32") == args.state_dtype and bool(tj.get("push", False)) == bool(args.push):
                 traffic = tj.get("hbm_bytes_per_step")
+                break
         except Exception:
             traffic = None
     # the bound that binds: the fused kernel's dynamics waves are latency / VALU-issue bound.  VALU-issue
