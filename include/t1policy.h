@@ -143,6 +143,12 @@ int t1policy_linear_wgrad_f32(const float* gy, const float* x, int rows, int M, 
                               long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
                               void* stream);
 
+/* t1policy_linear_wgrad_f32 with x's rows ldx >= N elements apart (a column slice read in place: the state estimator's
+ * short history).  Returns 0, -1 on bad arguments (a strided x needs T1_WGRAD_STAGED on), -2 on a launch error. */
+int t1policy_linear_wgrad_f32x(const float* gy, const float* x, int ldx, int rows, int M, int N, void* workspace,
+                               long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
+                               void* stream);
+
 /* The fp32 update's Linear forward and input-gradient GEMMs (t1policy_gemm.hip): C (R, N) = A (R, K) B (N, K)^T
  * (+ bias (N), NULL: none); act 1 then applies ELU (alpha 1), act 2 multiplies by ELU's derivative at the ELU outputs
  * aux (R, N) (1 where aux > 0, else aux + 1; aux NULL otherwise), for row-major fp32 A, B, C -- nn.Linear's forward
@@ -152,6 +158,15 @@ int t1policy_linear_wgrad_f32(const float* gy, const float* x, int rows, int M, 
  * Returns 0, -1 on bad arguments, -2 on a launch error. */
 int t1policy_gemm_nt_f32(const float* A, const float* B, const float* bias, const float* aux, float* C, int R, int N,
                          int K, int act, void* stream);
+
+/* t1policy_gemm_nt_f32 on strided operands, with no copies for the update's two non-contiguous cases: A rows lda >= K
+ * elements apart (a column slice of a wider matrix: the state estimator's short history, obs[:, -235:]), and B either
+ * (N, K) rows ldb >= K apart (b_kn = 0) or given as its transpose, (K, N) rows ldb >= N apart (b_kn = 1: the input
+ * gradient gx = g W of a Linear reads its weight W (out, in) in place as B = W^T).  The same parts, products and k-order
+ * sums as t1policy_gemm_nt_f32.  Each operand's extent below 1 GiB.  Returns 0, -1 on bad arguments, -2 on a launch
+ * error. */
+int t1policy_gemm_f32(const float* A, int lda, const float* B, int ldb, int b_kn, const float* bias, const float* aux,
+                      float* C, int R, int N, int K, int act, void* stream);
 
 /* The PPO minibatch's actor-observation rows from the frame-history rollout storage (not in the reference, whose
  * RolloutStorage keeps every step's whole history: rollout_storage.py:153-173; ti5_isaacgym_amd/algo/rollout.py

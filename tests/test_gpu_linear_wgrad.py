@@ -231,6 +231,43 @@ def test_gemm_nt_f32_matches_fp64(R, N, K):
     assert torch.equal(yd, y * torch.where(aux > 0, torch.ones_like(aux), aux + 1.0))
 
 
+@pytest.mark.parametrize("R,N,K,wide", [(49152, 256, 235, 3102), (777, 130, 97, 131), (4096, 302, 512, 600),
+                                         (31, 5, 7, 9), (8192, 16, 128, 128)])
+def test_gemm_f32_strided_operands_read_in_place(R, N, K, wide):
+    """t1policy_gemm_f32: A a column slice of a wider matrix (lda > K), B the transpose of a contiguous weight (b_kn: the
+    input gradient's W read in place) or a row-strided slice -- the same bits as the contiguous copies (the same parts,
+    products and k order), and no copy made."""
+    from ti5_isaacgym_amd.algo.dh_policy import gemm_nt_f32
+    g = torch.Generator(device=DEV).manual_seed(R + N + K + wide)
+    big = torch.randn(R, wide, device=DEV, generator=g)
+    a = big[:, wide - K:]                      # (R, K), row stride `wide`
+    w = torch.randn(K, N, device=DEV, generator=g) * 0.1
+    bt = w.t()                                 # (N, K), strides (1, N): b_kn
+    bwide = torch.randn(N, K + 3, device=DEV, generator=g)[:, :K]  # row stride K + 3
+    bias = torch.randn(N, device=DEV, generator=g)
+    aux = torch.randn(R, N, device=DEV, generator=g)
+    for b in (bt, bwide):
+        for act in (0, 1, 2):
+            y = gemm_nt_f32(a, b, bias, act=act, aux=aux if act == 2 else None)
+            y0 = gemm_nt_f32(a.contiguous(), b.contiguous(), bias, act=act, aux=aux if act == 2 else None)
+            assert torch.equal(y, y0), (act, float((y - y0).abs().max()))
+    ref = a.double() @ bt.double().t() + bias.double()
+    mag = a.double().abs() @ bt.double().abs().t() + bias.double().abs()
+    assert ((gemm_nt_f32(a, bt, bias).double() - ref).abs() <= 2e-6 * mag).all()
+
+
+@pytest.mark.parametrize("rows,M,N,wide", [(49152, 256, 235, 3102), (777, 219, 235, 240), (3001, 1, 3, 8)])
+def test_linear_wgrad_f32_strided_x_read_in_place(rows, M, N, wide):
+    """t1policy_linear_wgrad_f32x: x a column slice (row stride > N) -- the same bits as on the contiguous copy."""
+    from ti5_isaacgym_amd.algo.dh_policy import linear_wgrad_f32
+    g = torch.Generator(device=DEV).manual_seed(rows + M + N)
+    gy = torch.randn(rows, M, device=DEV, generator=g) * 0.1
+    x = torch.randn(rows, wide, device=DEV, generator=g)[:, wide - N:]
+    gw, gb = linear_wgrad_f32(gy, x)
+    gw0, gb0 = linear_wgrad_f32(gy, x.contiguous())
+    assert torch.equal(gw, gw0) and torch.equal(gb, gb0)
+
+
 def test_linear_fp32_forward_and_input_gradient_use_the_gemm(monkeypatch):
     """In fp32 under autograd the Linear's forward and input gradient come from t1policy_gemm_nt_f32, within fp32
     summation order of torch's; T1 GEMM_F32 off gives torch's."""

@@ -102,7 +102,8 @@ POLICY_EXPORTS = ["t1policy_conv1d_forward", "t1policy_history_rows", "t1policy_
                   "t1policy_conv1_wgrad_bf16", "t1policy_colsum_workspace_bytes", "t1policy_colsum",
                   "t1policy_slice_sum", "t1policy_linear_wgrad_workspace_bytes", "t1policy_linear_wgrad_bf16",
                   "t1policy_fold_rows", "t1policy_gather_rows", "t1policy_conv1_wgrad_f32",
-                  "t1policy_linear_wgrad_f32", "t1policy_gemm_nt_f32"]
+                  "t1policy_linear_wgrad_f32", "t1policy_gemm_nt_f32", "t1policy_gemm_f32",
+                  "t1policy_linear_wgrad_f32x"]
 
 _lib = None
 
@@ -157,7 +158,9 @@ def load():
         "t1policy_linear_wgrad_workspace_bytes": ([i32, i32, i32], C.c_longlong),
         "t1policy_linear_wgrad_bf16": ([vp, vp, i32, i32, i32, vp, C.c_longlong, vp, vp, i32, vp], C.c_int),
         "t1policy_linear_wgrad_f32": ([vp, vp, i32, i32, i32, vp, C.c_longlong, vp, vp, i32, vp], C.c_int),
+        "t1policy_linear_wgrad_f32x": ([vp, vp, i32, i32, i32, i32, vp, C.c_longlong, vp, vp, i32, vp], C.c_int),
         "t1policy_gemm_nt_f32": ([vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], C.c_int),
+        "t1policy_gemm_f32": ([vp, i32, vp, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp], C.c_int),
         "t1policy_fold_rows": ([vp, vp, i32, i32, i32, i32, i32, i32, vp], C.c_int),
         "t1policy_gather_rows": ([vp, vp, vp, i32, vp, i32, vp], C.c_int),
     }

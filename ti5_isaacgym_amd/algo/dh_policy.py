@@ -162,8 +162,10 @@ def linear_wgrad_f32(gy, x, need_bias=True, into=None):
     """linear_wgrad_bf16 for the fp32 update: fp32 gy and x, each value split into three bf16 parts on the matrix cores
     (six part products per product, fp32-class fixed-order sums; t1policy_linear_wgrad_f32)."""
     gy = gy.float().contiguous()
-    x = x.float().contiguous()
-    return _linear_wgrad("t1policy_linear_wgrad_f32", gy, x, need_bias, into)
+    x = x.float()
+    if x.dim() == 2 and x.stride(1) == 1 and x.stride(0) > x.shape[1] and x.shape[0] > 1:  # a column slice, in place
+        return _linear_wgrad("t1policy_linear_wgrad_f32x", gy, x, need_bias, into, ldx=x.stride(0))
+    return _linear_wgrad("t1policy_linear_wgrad_f32", gy, x.contiguous(), need_bias, into)
 
 
 # the fp32 update's Linear forward / input-gradient GEMMs as the HIP three-part-split GEMM (t1policy_gemm_nt_f32);
@@ -177,11 +179,21 @@ def gemm_nt_f32(a, b, bias=None, act=0, aux=None):
     (1 where aux > 0, else aux + 1) -- the backward of a Linear whose input came out of an ELU.  Device fp32 tensors."""
     from .. import _lib
     lib = _lib.load()
-    a, b = a.contiguous(), b.contiguous()
     R, K = a.shape
     N = b.shape[0]
     if b.shape[1] != K or a.dtype != torch.float32 or b.dtype != torch.float32:
         raise ValueError(f"gemm_nt_f32: {tuple(a.shape)} x {tuple(b.shape)}^T ({a.dtype}, {b.dtype})")
+    # strided operands read in place (t1policy_gemm_f32): A a row-strided view (a column slice), B row-strided or the
+    # transpose of a contiguous matrix (a Linear weight's .t() in the input gradient); anything else is copied
+    if a.stride(1) != 1 or a.stride(0) < K or R == 1:
+        a = a.contiguous()
+    if b.stride(1) == 1 and b.stride(0) >= K and N > 1:
+        b_kn, ldb = 0, b.stride(0)
+    elif b.stride(0) == 1 and b.stride(1) >= N and K > 1:
+        b_kn, ldb = 1, b.stride(1)
+    else:
+        b = b.contiguous()
+        b_kn, ldb = 0, K
     out = torch.empty(R, N, device=a.device, dtype=torch.float32)
     bp = xp = None
     if bias is not None:
@@ -192,14 +204,18 @@ def gemm_nt_f32(a, b, bias=None, act=0, aux=None):
             raise ValueError("gemm_nt_f32: act=2 needs the (R, N) fp32 ELU outputs")
         aux = aux.contiguous()
         xp = aux.data_ptr()
-    rc = lib.t1policy_gemm_nt_f32(a.data_ptr(), b.data_ptr(), bp, xp, out.data_ptr(), R, N, K, act,
-                                  torch.cuda.current_stream(a.device).cuda_stream)
+    st = torch.cuda.current_stream(a.device).cuda_stream
+    lda = a.stride(0)
+    if lda == K and ldb == K and not b_kn:
+        rc = lib.t1policy_gemm_nt_f32(a.data_ptr(), b.data_ptr(), bp, xp, out.data_ptr(), R, N, K, act, st)
+    else:
+        rc = lib.t1policy_gemm_f32(a.data_ptr(), lda, b.data_ptr(), ldb, b_kn, bp, xp, out.data_ptr(), R, N, K, act, st)
     if rc != 0:
-        raise RuntimeError(f"t1policy_gemm_nt_f32 failed (rc={rc})")
+        raise RuntimeError(f"t1policy_gemm_f32 failed (rc={rc}; R {R}, N {N}, K {K}, lda {lda}, ldb {ldb}, b_kn {b_kn})")
     return out
 
 
-def _linear_wgrad(fn, gy, x, need_bias, into):
+def _linear_wgrad(fn, gy, x, need_bias, into, ldx=None):
     from .. import _lib
     lib = _lib.load()
     K, M = gy.shape
@@ -219,7 +235,8 @@ def _linear_wgrad(fn, gy, x, need_bias, into):
     else:
         gw = torch.empty(M, N, device=gy.device, dtype=torch.float32)
         gb = torch.empty(M, device=gy.device, dtype=torch.float32) if need_bias else None
-    rc = getattr(lib, fn)(gy.data_ptr(), x.data_ptr(), K, M, N, ws.data_ptr(), nbytes, gw.data_ptr(),
+    rows_args = (K, M, N) if ldx is None else (ldx, K, M, N)
+    rc = getattr(lib, fn)(gy.data_ptr(), x.data_ptr(), *rows_args, ws.data_ptr(), nbytes, gw.data_ptr(),
                           gb.data_ptr() if gb is not None else None, int(into is not None),
                           torch.cuda.current_stream(gy.device).cuda_stream)
     if rc != 0:
@@ -345,10 +362,11 @@ def plain_copy(module):
     return copy.deepcopy(module)
 
 
-# the fp32 update's MLPs (actor, critic, state estimator) as one autograd node on the fused HIP GEMMs (_MlpF32), opt-in
-# (T1_MLP_F32=1): it removes the ELU passes (3.3 ms per update) but its fused epilogues cost as much -- the update measured
-# 41.3 ms with it against 40.9 layer by layer (profiles/r06h_*, r06f_*)
-MLP_F32 = os.environ.get("T1_MLP_F32", "0") == "1"
+# the fp32 update's MLPs (actor, critic, state estimator) as one autograd node on the fused HIP GEMMs (_MlpF32; default,
+# T1_MLP_F32=0 runs them layer by layer): the ELU and ELU-backward passes (3.3 ms per update) go into the GEMM epilogues
+# -- update 38.1-38.2 -> 34.5-35.6 ms (profiles/r06t_*), once the epilogue loads its ELU outputs together (its first
+# form loaded them one by one behind the bounds checks and cost as much as it saved)
+MLP_F32 = os.environ.get("T1_MLP_F32", "1") == "1"
 
 
 class _MlpF32(torch.autograd.Function):

@@ -92,6 +92,26 @@ __device__ __forceinline__ f16v mfma_bf3(const Bf3& a, const Bf3& b, f16v acc) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
 }
 
+// ELU (alpha 1) without the libm expm1f call in the epilogue: expm1(v) for v <= 0 as a degree-10 Taylor polynomial on
+// [-1, 0] (truncation below 2.5e-8 of 1 / 11!, relative to |expm1| >= 0.63 |v| there) and exp(v) - 1 below -1 (no
+// cancellation: |result| > 0.63); max error a few ulp of the result, against torch's expm1 ELU (tests: 2e-6)
+__device__ __forceinline__ float elu1(float v) {
+  if (v > 0.0f) return v;
+  float p = 1.0f / 39916800.0f;  // 1 / 11!
+  p = fmaf(p, v, 1.0f / 3628800.0f);
+  p = fmaf(p, v, 1.0f / 362880.0f);
+  p = fmaf(p, v, 1.0f / 40320.0f);
+  p = fmaf(p, v, 1.0f / 5040.0f);
+  p = fmaf(p, v, 1.0f / 720.0f);
+  p = fmaf(p, v, 1.0f / 120.0f);
+  p = fmaf(p, v, 1.0f / 24.0f);
+  p = fmaf(p, v, 1.0f / 6.0f);
+  p = fmaf(p, v, 0.5f);
+  p = fmaf(p, v, 1.0f);
+  const float poly = p * v;
+  return v >= -1.0f ? poly : __expf(v) - 1.0f;
+}
+
 // C/D of a 32 x 32 tile: column n = lane & 31, row m = (q & 3) + 8 (q >> 2) + 4 h
 __device__ __forceinline__ void gm_epilogue(const f16v (&acc)[2][2], const float* __restrict__ bias,
                                             const float* __restrict__ aux, float* __restrict__ C, int R, int N, int r0,
@@ -105,18 +125,24 @@ __device__ __forceinline__ void gm_epilogue(const f16v (&acc)[2][2], const float
       if (b >= nb_n) break;
       const int n = n0 + 64 * wn + 32 * b + (lane & 31);
       const float bv = (bias != nullptr && n < N) ? bias[n] : 0.0f;
+      // act 2: the tile's 16 ELU outputs loaded together first (clamped in-matrix, unconditional: all in flight)
+      float e[16];
+      if (act == 2) {
+        const int nc = n < N ? n : N - 1;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = r0 + 64 * wm + 32 * a + (q & 3) + 8 * (q >> 2) + 4 * h;
+          e[q] = aux[(size_t)(m < R ? m : R - 1) * N + nc];
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int m = r0 + 64 * wm + 32 * a + (q & 3) + 8 * (q >> 2) + 4 * h;
         float v = acc[a][b][q] + bv;
-        if (act == 1) v = v > 0.0f ? v : expm1f(v);
-        if (m < R && n < N) {
-          if (act == 2) {  // times ELU's derivative at the ELU output e (alpha 1: 1 for e > 0, else e + 1)
-            const float e = aux[(size_t)m * N + n];
-            v = v * (e > 0.0f ? 1.0f : e + 1.0f);
-          }
-          C[(size_t)m * N + n] = v;
-        }
+        if (act == 1) v = elu1(v);
+        // act 2: times ELU's derivative at the ELU output e (alpha 1: 1 for e > 0, else e + 1)
+        if (act == 2) v = v * (e[q] > 0.0f ? 1.0f : e[q] + 1.0f);
+        if (m < R && n < N) C[(size_t)m * N + n] = v;
       }
     }
   }
@@ -241,13 +267,39 @@ struct GsFrags {
 // grid: 8 x per_xcd workgroups (1-D).  Workgroup i runs on XCD i mod 8 and takes output tile q = (i mod 8) per_xcd +
 // i / 8 (column tiles fastest): an XCD works through a contiguous run of tiles, so the column tiles of one row tile run
 // on the same XCD at about the same time and read that row tile of A from HBM once (the other reads hit its L2)
+// B given as [K][N] (BKN, ldb >= N): thread t stages column n0 + (t & 127) of the 8 k-rows k0 + 8 (t >> 7) .. + 7 (each
+// wave load is 64 consecutive columns of one k-row), so it holds 8 consecutive k of one column and stores each part
+// with one ds_write_b128 -- the transposed weight of an input gradient (gx = g W: B = W^T) read in place
+__device__ __forceinline__ void gs_load_kn(__amdgpu_buffer_rsrc_t rs, int base, int rowb, int k0, f4 (&v)[2]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    v[i >> 2][i & 3] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base + (k0 + i) * rowb, 0, 0));
+}
+__device__ __forceinline__ void gs_split_store8(__bf16* img, int col, int g, const f4 (&v)[2]) {
+  bf8 p1, p2, p3;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = v[j >> 2][j & 3];
+    const __bf16 h1 = (__bf16)x;
+    const float r1 = x - (float)h1;
+    const __bf16 h2 = (__bf16)r1;
+    p1[j] = h1;
+    p2[j] = h2;
+    p3[j] = (__bf16)(r1 - (float)h2);
+  }
+  const int o = col * GS_PITCH + 8 * g;
+  *reinterpret_cast<bf8*>(img + o) = p1;
+  *reinterpret_cast<bf8*>(img + GS_IMG + o) = p2;
+  *reinterpret_cast<bf8*>(img + 2 * GS_IMG + o) = p3;
+}
 // NARROW (N <= 64, e.g. the 16-channel history layer over 294,912 rows): the MFMAs of 32 x 32 tiles past N are skipped
-// (wave-uniform branches; at N <= 64 the waves of the second column half have no tile at all)
-template <bool NARROW>
-__global__ __launch_bounds__(256, 2) void k_gemm_nt_f32x3s(const float* __restrict__ A, const float* __restrict__ B,
-                                                           const float* __restrict__ bias, const float* __restrict__ aux,
-                                                           float* __restrict__ C, int R, int N, int K, int act,
-                                                           int col_tiles, int per_xcd) {
+// (wave-uniform branches; at N <= 64 the waves of the second column half have no tile at all).  lda / ldb: the row
+// strides of A ([R][lda]) and B ([N][ldb], or [K][ldb] under BKN), in elements
+template <bool NARROW, bool BKN>
+__global__ __launch_bounds__(256, 2) void k_gemm_nt_f32x3s(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                           int ldb, const float* __restrict__ bias,
+                                                           const float* __restrict__ aux, float* __restrict__ C, int R,
+                                                           int N, int K, int act, int col_tiles, int per_xcd) {
   __shared__ __attribute__((aligned(16))) __bf16 IMG[2][2][3 * GS_IMG];  // [buffer][A, B][part][row][k]
   const int q = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (q >= col_tiles * ((R + GM_T - 1) / GM_T)) return;  // the last XCD's spare workgroups (uniform)
@@ -256,10 +308,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt_f32x3s(const float* __restri
   const int r0 = GM_T * (q / col_tiles), n0 = GM_T * (q % col_tiles);
   const int m_rem = R - (r0 + 64 * wm), n_rem = N - (n0 + 64 * wn);
   const int mb_n = m_rem <= 0 ? 0 : (m_rem > 32 ? 2 : 1), nb_n = n_rem <= 0 ? 0 : (n_rem > 32 ? 2 : 1);
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, R * K * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B), 0, N * K * 4, 0x00020000);
-  const int kq = 4 * (t & 3), srow = t >> 2, row64 = 64 * K * 4;
-  const int ba = ((r0 + srow) * K + kq) * 4, bb = ((n0 + srow) * K + kq) * 4;
+  // num_records: through the last element (rows past the matrix, and under BKN k-rows past K, read 0)
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, ((R - 1) * lda + K) * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(B), 0, (BKN ? (K - 1) * ldb + N : (N - 1) * ldb + K) * 4, 0x00020000);
+  const int kq = 4 * (t & 3), srow = t >> 2, arow64 = 64 * lda * 4, brow64 = 64 * ldb * 4;
+  const int ba = ((r0 + srow) * lda + kq) * 4;
+  const int bcol = t & 127, bg = t >> 7;  // BKN staging
+  const int bb = BKN ? (n0 + bcol < N ? (8 * bg * ldb + n0 + bcol) * 4 : GP_OOB) : ((n0 + srow) * ldb + kq) * 4;
   f16v acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -271,16 +328,23 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt_f32x3s(const float* __restri
   // loads two chunks ahead: register slot j & 1 holds chunk j from its load (two iterations before it is staged)
   f4 va[2][2], vb[2][2];
   auto load = [&](int slot, int k0, auto full) {
-    gs_load<decltype(full)::value>(ra, ba, row64, K, k0, kq, va[slot]);
-    gs_load<decltype(full)::value>(rb, bb, row64, K, k0, kq, vb[slot]);
+    gs_load<decltype(full)::value>(ra, ba, arow64, K, k0, kq, va[slot]);
+    if constexpr (BKN)
+      gs_load_kn(rb, bb, ldb * 4, k0, vb[slot]);
+    else
+      gs_load<decltype(full)::value>(rb, bb, brow64, K, k0, kq, vb[slot]);
   };
   using Full = std::integral_constant<bool, true>;
   using Edge = std::integral_constant<bool, false>;
   auto stage = [&](int buf, int slot) {
     gs_split_store(IMG[buf][0], srow, kq, va[slot][0]);
     gs_split_store(IMG[buf][0], srow + 64, kq, va[slot][1]);
-    gs_split_store(IMG[buf][1], srow, kq, vb[slot][0]);
-    gs_split_store(IMG[buf][1], srow + 64, kq, vb[slot][1]);
+    if constexpr (BKN) {
+      gs_split_store8(IMG[buf][1], bcol, bg, vb[slot]);
+    } else {
+      gs_split_store(IMG[buf][1], srow, kq, vb[slot][0]);
+      gs_split_store(IMG[buf][1], srow + 64, kq, vb[slot][1]);
+    }
   };
   auto frags = [&](int buf, GsFrags& f) {
 #pragma unroll
@@ -364,22 +428,41 @@ bool gemm_staged() {
 
 extern "C" {
 
+int t1policy_gemm_f32(const float* A, int lda, const float* B, int ldb, int b_kn, const float* bias, const float* aux,
+                      float* C, int R, int N, int K, int act, void* stream) {
+  if (!A || !B || !C || R <= 0 || N <= 0 || K <= 0 || act < 0 || act > 2 || (act == 2 && !aux)) return -1;
+  if (lda < K || ldb < (b_kn ? N : K)) return -1;
+  // every byte offset below GP_OOB (the descriptors' 32-bit offsets; 1 GiB per operand)
+  if ((long long)R * lda * 4 >= GP_OOB || (long long)(b_kn ? K : N) * ldb * 4 >= GP_OOB ||
+      (long long)R * N >= (1LL << 31))
+    return -1;
+  const int row_tiles = (R + GM_T - 1) / GM_T, col_tiles = (N + GM_T - 1) / GM_T;
+  const int tiles = row_tiles * col_tiles, per_xcd = (tiles + 7) / 8;
+  const dim3 grid(8 * per_xcd), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (N <= 64 && b_kn)
+    hipLaunchKernelGGL((k_gemm_nt_f32x3s<true, true>), grid, blk, 0, st, A, lda, B, ldb, bias, aux, C, R, N, K, act,
+                       col_tiles, per_xcd);
+  else if (N <= 64)
+    hipLaunchKernelGGL((k_gemm_nt_f32x3s<true, false>), grid, blk, 0, st, A, lda, B, ldb, bias, aux, C, R, N, K, act,
+                       col_tiles, per_xcd);
+  else if (b_kn)
+    hipLaunchKernelGGL((k_gemm_nt_f32x3s<false, true>), grid, blk, 0, st, A, lda, B, ldb, bias, aux, C, R, N, K, act,
+                       col_tiles, per_xcd);
+  else
+    hipLaunchKernelGGL((k_gemm_nt_f32x3s<false, false>), grid, blk, 0, st, A, lda, B, ldb, bias, aux, C, R, N, K, act,
+                       col_tiles, per_xcd);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int t1policy_gemm_nt_f32(const float* A, const float* B, const float* bias, const float* aux, float* C, int R, int N,
                          int K, int act, void* stream) {
   if (!A || !B || !C || R <= 0 || N <= 0 || K <= 0 || act < 0 || act > 2 || (act == 2 && !aux)) return -1;
   if ((long long)R * (K > N ? K : N) >= (1LL << 31)) return -1;
-  const dim3 grid((R + GM_T - 1) / GM_T, (N + GM_T - 1) / GM_T);
   const bool fits = (long long)R * K * 4 < GP_OOB && (long long)N * K * 4 < GP_OOB;
-  if (gemm_staged() && fits) {
-    const int tiles = (int)(grid.x * grid.y), per_xcd = (tiles + 7) / 8;
-    if (N <= 64)
-      hipLaunchKernelGGL(k_gemm_nt_f32x3s<true>, dim3(8 * per_xcd), dim3(256), 0, (hipStream_t)stream, A, B, bias, aux, C,
-                         R, N, K, act, (int)grid.y, per_xcd);
-    else
-      hipLaunchKernelGGL(k_gemm_nt_f32x3s<false>, dim3(8 * per_xcd), dim3(256), 0, (hipStream_t)stream, A, B, bias, aux,
-                         C, R, N, K, act, (int)grid.y, per_xcd);
-  } else
-    hipLaunchKernelGGL(k_gemm_nt_f32x3, grid, dim3(256), 0, (hipStream_t)stream, A, B, bias, aux, C, R, N, K, act);
+  if (gemm_staged() && fits) return t1policy_gemm_f32(A, K, B, K, 0, bias, aux, C, R, N, K, act, stream);
+  const dim3 grid((R + GM_T - 1) / GM_T, (N + GM_T - 1) / GM_T);
+  hipLaunchKernelGGL(k_gemm_nt_f32x3, grid, dim3(256), 0, (hipStream_t)stream, A, B, bias, aux, C, R, N, K, act);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -356,6 +356,167 @@ __global__ __launch_bounds__(256, 2) void k_linear_wgrad_f32(const float* __rest
   }
 }
 
+// ---- the staged-split form of the fp32 kernel (the default; T1_WGRAD_STAGED=0 selects k_linear_wgrad_f32 above): the
+// transpose happens in the registers -- thread t loads column (t & 127) of 8 consecutive rows of a 16-row chunk (each
+// wave load is 64 consecutive columns of one row: 256 coalesced bytes), so it holds 8 consecutive k of one output row
+// / column, splits them into their three bf16 parts ONCE and stores each part as one ds_write_b128 into [part][col][k]
+// images (16 k + 8 pad: 48-B rows, conflict-free b128 stores and reads); the fragments are then one ds_read_b128 per
+// part, no VALU between the LDS and the MFMAs.  A chunk's 24 MFMAs run in two halves, the first beside staging the
+// next chunk and loading the one after next (a two-slot register ring), the second beside reading the next chunk's
+// fragments; one barrier per chunk.  Loads go through buffer descriptors: columns past the width and rows past the
+// matrix read 0.  Workgroups of one row slice run on one XCD (their gy and x rows are shared through its L2).  The bias
+// sums the staged gy values in a fixed order (8 rows per thread per chunk, then the two row halves).
+constexpr int WS_KC = 16, WS_PITCH = 24, WS_IMG = WG_T * WS_PITCH;  // bf16
+constexpr int WS_OOB = 0x40000000;
+typedef float f8v __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void ws_load(__amdgpu_buffer_rsrc_t rs, int base, int rowb, int k0, f8v& v) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base + (k0 + i) * rowb, 0, 0));
+}
+__device__ __forceinline__ void ws_split_store(__bf16* img, int col, int g, const f8v& v) {
+  bf8 p1, p2, p3;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h1 = (__bf16)v[j];
+    const float r1 = v[j] - (float)h1;
+    const __bf16 h2 = (__bf16)r1;
+    p1[j] = h1;
+    p2[j] = h2;
+    p3[j] = (__bf16)(r1 - (float)h2);
+  }
+  const int o = col * WS_PITCH + 8 * g;
+  *reinterpret_cast<bf8*>(img + o) = p1;
+  *reinterpret_cast<bf8*>(img + WS_IMG + o) = p2;
+  *reinterpret_cast<bf8*>(img + 2 * WS_IMG + o) = p3;
+}
+__device__ __forceinline__ void ws_frag(const __bf16* img, int col0, int lane, Bf3f& f) {
+  const int o = (col0 + (lane & 31)) * WS_PITCH + 8 * (lane >> 5);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) f.p[p] = *reinterpret_cast<const bf8*>(img + p * WS_IMG + o);
+}
+struct WsFrags {
+  Bf3f a[2], b[2];
+};
+// grid: 8 x per_xcd workgroups; workgroup i takes unit q = (i mod 8) per_xcd + i / 8 = (slice, tile) with the tile
+// fastest
+__global__ __launch_bounds__(256, 2) void k_linear_wgrad_f32s(const float* __restrict__ gy, const float* __restrict__ x,
+                                                              int ldx, int rows, int M, int N, int tiles_m, int tiles,
+                                                              int rows_per_slice, int units, int per_xcd,
+                                                              float* __restrict__ part, float* __restrict__ bpart) {
+  __shared__ __attribute__((aligned(16))) __bf16 IMG[2][2][3 * WS_IMG];  // [buffer][gy, x][part][col][k]
+  const int q = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (q >= units) return;  // uniform
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, h = lane >> 5;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int tile = q % tiles, s = q / tiles;
+  const int tm = tile % tiles_m, tn = tile / tiles_m;
+  const int m0 = WG_T * tm, n0 = WG_T * tn;
+  const int r0 = s * rows_per_slice;
+  const int r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
+  const int m_rem = M - (m0 + 64 * wm), n_rem = N - (n0 + 64 * wn);
+  const int mb_n = m_rem <= 0 ? 0 : (m_rem > 32 ? 2 : 1), nb_n = n_rem <= 0 ? 0 : (n_rem > 32 ? 2 : 1);
+  const bool bias = bpart != nullptr && tn == 0;
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gy), 0, rows * M * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, ((rows - 1) * ldx + N) * 4, 0x00020000);
+  const int col = t & 127, g = t >> 7;
+  const int bg = m0 + col < M ? ((r0 + 8 * g) * M + m0 + col) * 4 : WS_OOB;
+  const int bx = n0 + col < N ? ((r0 + 8 * g) * ldx + n0 + col) * 4 : WS_OOB;
+  const int rgb = M * 4, rxb = ldx * 4;
+  f16v acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+  float bsum = 0.0f;
+  const int nch = (r1 - r0 + WS_KC - 1) / WS_KC;
+  f8v vg[2], vx[2];  // register slot j & 1 holds chunk j from its load (two iterations before it is staged)
+  auto load = [&](int slot, int c) {
+    ws_load(rg, bg, rgb, c * WS_KC, vg[slot]);
+    ws_load(rx, bx, rxb, c * WS_KC, vx[slot]);
+  };
+  auto stage = [&](int buf, int slot) {
+    ws_split_store(IMG[buf][0], col, g, vg[slot]);
+    ws_split_store(IMG[buf][1], col, g, vx[slot]);
+  };
+  auto frags = [&](int buf, WsFrags& f) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) ws_frag(IMG[buf][1], 64 * wn + 32 * b, lane, f.b[b]);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) ws_frag(IMG[buf][0], 64 * wm + 32 * a, lane, f.a[a]);
+  };
+  // the bias: this thread's 8 gy rows of the chunk in order (rows past the slice or the matrix are 0 or not staged)
+  auto bias_add = [&](int slot, int c) {
+    if (c < nch) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bsum += vg[slot][i];
+    }
+  };
+  load(0, 0);
+  load(1, 1);
+  bias_add(0, 0);
+  stage(0, 0);
+  load(0, 2);
+  __syncthreads();
+  WsFrags f0, f1;
+  frags(0, f0);
+  auto iter = [&](int c, int slot, WsFrags& fc, WsFrags& fn) {
+    const int nxt = (c + 1) & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    bias_add(slot, c + 1);
+    stage(nxt, slot);
+    load(slot, c + 3);
+    acc[0][0] = mfma_bf3f(fc.a[0], fc.b[0], acc[0][0]);
+    acc[0][1] = mfma_bf3f(fc.a[0], fc.b[1], acc[0][1]);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x002, 8, 1);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    frags(nxt, fn);
+    acc[1][0] = mfma_bf3f(fc.a[1], fc.b[0], acc[1][0]);
+    acc[1][1] = mfma_bf3f(fc.a[1], fc.b[1], acc[1][1]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 2);
+    __builtin_amdgcn_sched_group_barrier(0x008, 12, 2);
+  };
+  int c = 0;
+  for (; c + 1 < nch; c += 2) {
+    iter(c, 1, f0, f1);
+    iter(c + 1, 0, f1, f0);
+  }
+  if (c < nch) iter(c, 1, f0, f1);
+  __builtin_amdgcn_sched_barrier(0);
+  float* P = part + (size_t)s * M * N;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    if (a >= mb_n) break;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if (b >= nb_n) break;
+      const int n = n0 + 64 * wn + 32 * b + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 64 * wm + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M && n < N) P[(size_t)m * N + n] = acc[a][b][r];
+      }
+    }
+  }
+  if (bias) {  // the two row halves of column m, in a fixed order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(&IMG[0][0][0]);
+    if (g == 1) red[col] = bsum;
+    __syncthreads();
+    if (g == 0 && m0 + col < M) bpart[(size_t)s * M + m0 + col] = bsum + red[col];
+  }
+}
+
 // gW[i] = sum_s part[s][i] (i < M N) and gb[m] = sum_s bpart[s][m]: G slice groups per output (thread (g, o) sums
 // slices g, g + G, ... in order, eight loads in flight), then the G group sums in order -- a fixed tree for a given
 // slice count, so the result is deterministic
@@ -398,6 +559,15 @@ int wg_per_cu() {
     const char* e = getenv("T1_WGRAD_WG_PER_CU");
     const int k = e ? atoi(e) : 2;
     return k >= 1 && k <= 4 ? k : 2;
+  }();
+  return v;
+}
+
+// T1_WGRAD_STAGED (A/B): 1 (default) k_linear_wgrad_f32s, 0 the first fp32 form k_linear_wgrad_f32
+bool wgrad_staged() {
+  static const bool v = [] {
+    const char* e = getenv("T1_WGRAD_STAGED");
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -480,12 +650,12 @@ int t1policy_linear_wgrad_bf16(const void* gy, const void* x, int rows, int M, i
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int t1policy_linear_wgrad_f32(const float* gy, const float* x, int rows, int M, int N, void* workspace,
-                              long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
-                              void* stream) {
-  if (!gy || !x || !workspace || !grad_weight || rows <= 0 || M <= 0 || N <= 0) return -1;
+int t1policy_linear_wgrad_f32x(const float* gy, const float* x, int ldx, int rows, int M, int N, void* workspace,
+                               long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
+                               void* stream) {
+  if (!gy || !x || !workspace || !grad_weight || rows <= 0 || M <= 0 || N <= 0 || ldx < N) return -1;
   if ((reinterpret_cast<uintptr_t>(workspace) & 15u) != 0) return -1;
-  if ((long long)M * N >= (1LL << 31) - M || (long long)rows * (M > N ? M : N) >= (1LL << 31)) return -1;
+  if ((long long)M * N >= (1LL << 31) - M || (long long)rows * (M > ldx ? M : ldx) >= (1LL << 31)) return -1;
   const int cus = wg_cus();
   if (cus <= 0) return -2;
   const WgPlan p = wg_plan(rows, M, N, cus);
@@ -493,13 +663,28 @@ int t1policy_linear_wgrad_f32(const float* gy, const float* x, int rows, int M, 
   float* part = reinterpret_cast<float*>(workspace);
   float* bpart = grad_bias ? part + (size_t)p.slices * M * N : nullptr;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_linear_wgrad_f32, dim3(p.tiles, p.slices), dim3(256), 0, st, gy, x, rows, M, N, p.tiles_m,
-                     p.rows_per_slice, part, bpart);
+  if (wgrad_staged() && (long long)rows * M * 4 < WS_OOB && (long long)rows * ldx * 4 < WS_OOB) {
+    const int units = p.tiles * p.slices, per_xcd = (units + 7) / 8;
+    hipLaunchKernelGGL(k_linear_wgrad_f32s, dim3(8 * per_xcd), dim3(256), 0, st, gy, x, ldx, rows, M, N, p.tiles_m,
+                       p.tiles, p.rows_per_slice, units, per_xcd, part, bpart);
+  } else if (ldx == N) {
+    hipLaunchKernelGGL(k_linear_wgrad_f32, dim3(p.tiles, p.slices), dim3(256), 0, st, gy, x, rows, M, N, p.tiles_m,
+                       p.rows_per_slice, part, bpart);
+  } else {
+    return -1;  // a strided x needs the staged kernel
+  }
   const int total = M * N + (grad_bias ? M : 0);
   const int groups = p.slices <= 8 ? 1 : (p.slices <= 64 ? 4 : 16), per = 256 / groups;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + per - 1) / per), dim3(256), 0, st, part, bpart, p.slices, groups,
                      M * N, M, grad_weight, grad_bias, accumulate);
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int t1policy_linear_wgrad_f32(const float* gy, const float* x, int rows, int M, int N, void* workspace,
+                              long long workspace_bytes, float* grad_weight, float* grad_bias, int accumulate,
+                              void* stream) {
+  return t1policy_linear_wgrad_f32x(gy, x, N, rows, M, N, workspace, workspace_bytes, grad_weight, grad_bias,
+                                    accumulate, stream);
 }
 
 }  // extern "C"
