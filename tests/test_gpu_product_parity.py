@@ -23,7 +23,8 @@ same states, so what is compared is the step kernel's own arithmetic around the 
 Tolerance: 1e-4 relative with a 1e-6 absolute floor (golden_util.RTOL / ATOL), exact for bool / integer buffers.
 Every 7th env starts near its time-out so the reset path runs inside the fused epilogue.  Cases: BASELINE configs[1]
 (4096 envs, plane), configs[2] (8192 envs, trimesh curriculum + full DR) and configs[4] (32768 envs, height field,
-pushes), plus a ragged 777-env trimesh run (last workgroup partly empty).  Two more cases start the step counter just
+pushes), plus a ragged 777-env trimesh run (last workgroup partly empty), also replayed over 60 steps (the kernel's
+state carried through many resets, pushes and lag-ring wraps, each step compared).  Two more cases start the step counter just
 before an external-force window (`counter % 400 <= duration`, t1_dh_stand_env.py:205-215): at 400 (duration 0: the
 forces are drawn, enter the critic frame and are never applied) and at 96,400 (duration index 1 = 0.05 s: drawn at
 96,400, applied to the base of standing envs from 96,401 to 96,405, t1_dh_stand_env.py:233-247,
@@ -122,9 +123,10 @@ def compare(env, o, rp, step):
 
 @pytest.mark.parametrize("n,mesh,push,steps,counter0", [
     (4096, "plane", False, 6, None), (8192, "trimesh", False, 6, None), (32768, "heightfield", True, 4, None),
-    (777, "trimesh", True, 5, None), (4096, "trimesh", False, 5, 397), (8192, "trimesh", False, 10, 96397)],
+    (777, "trimesh", True, 5, None), (4096, "trimesh", False, 5, 397), (8192, "trimesh", False, 10, 96397),
+    (777, "trimesh", True, 60, None)],
     ids=["config2_4096_plane", "config3_8192_trimesh", "config5_32768_hf_push", "ragged777_trimesh_push",
-         "extforce_window_400", "extforce_window_96400_applied"])
+         "extforce_window_400", "extforce_window_96400_applied", "ragged777_trimesh_push_long60"])
 def test_product_kernel_matches_oracle(n, mesh, push, steps, counter0, dyn_solver):
     from ti5_isaacgym_amd import make_t1_env
     env = make_t1_env(num_envs=n, mesh_type=mesh, seed=3, device="cuda:0", cfg_hook=_push_hook if push else None)
