@@ -228,17 +228,72 @@ struct CriticLds {
   Frag p[48];  // 768-wide activations
   Frag q[16];  // the staged privileged observations (14 steps), then 256-wide activations
 };
-union PhLds {
-  ActorLds a;
-  CriticLds c;
+// split-K on the narrow layers (8 waves): a layer of NT < 8 output tiles deals each tile's k-steps over SK waves
+// (NT SK <= 8, at least two k-steps each, SK a power of two); waves kh = 1 .. SK-1 leave their partial 32 x 32 sums
+// (hi.hi + 2^-11 (hi.lo + lo.hi), one fp32 per element) in LDS and wave kh = 0 adds them in kh order before the bias
+// and the activation.  Measured +-0 (act() 0.1276-0.1292 ms off, 0.1282-0.1298 on, profiles/r07c_act_ab.txt): the
+// waves' k chains are not what bounds the kernel, its fragment stream from L2 is, so it stays off (A/B).
+#ifndef T1_HEADS_SPLITK
+#define T1_HEADS_SPLITK 0
+#endif
+constexpr int PH_RED_TILES = 4;  // partial tiles in LDS at once: (SK - 1) NT <= 4
+constexpr int ph_sk(int l) {
+  if (!T1_HEADS_SPLITK || PH_WAVES != 8) return 1;
+  const int nt = ph_nt(l), ks = PH_L[l].ks;
+  int sk = 1;
+  while (nt * sk * 2 <= PH_WAVES && ks % (sk * 2) == 0 && ks / (sk * 2) >= 2 && (sk * 2 - 1) * nt <= PH_RED_TILES)
+    sk *= 2;
+  return sk;
+}
+struct PhLds {
+  union {
+    ActorLds a;
+    CriticLds c;
+  };
+#if T1_HEADS_SPLITK
+  float4 red[PH_RED_TILES][4][64];  // split-K partial sums: [(kh - 1) NT + tile][register quad][lane]
+#endif
 };
+
+#ifndef T1_HEADS_FAST_ELU
+#define T1_HEADS_FAST_ELU 1  // act() 0.1336 -> 0.1279 ms at 8192 envs (profiles/r07b_act_ab.txt)
+#endif
+// expm1(v) for ELU's negative branch, branch-free.  1: the device library's expm1f algorithm (range reduction by
+// n = rint(v log2 e) with ln 2 in two parts, the same degree-7 polynomial, 2^n expm1(r) + (2^n - 1)) without its
+// overflow and v < -17 fix-ups, which v <= 0 never needs once v is clamped at -88: bit-identical to expm1f there.
+// 2: 2^(v log2 e) - 1 on the hardware exponential below -1/4, a degree-6 Taylor polynomial above (not bit-identical).
+__device__ __forceinline__ float ph_expm1_neg(float v) {
+#if T1_HEADS_FAST_ELU == 2
+  const float e = __builtin_amdgcn_exp2f(v * 1.44269504088896341f) - 1.0f;
+  float p = fmaf(v, 1.0f / 720.0f, 1.0f / 120.0f);
+  p = fmaf(v, p, 1.0f / 24.0f);
+  p = fmaf(v, p, 1.0f / 6.0f);
+  p = fmaf(v, p, 0.5f);
+  p = fmaf(v * v, p, v);
+  return v < -0.25f ? e : p;
+#else
+  v = fmaxf(v, -88.0f);
+  const float n = __builtin_rintf(v * __builtin_bit_cast(float, 0x3fb8aa3bu));
+  float r = fmaf(n, __builtin_bit_cast(float, 0xbf317218u), v);
+  r = fmaf(n, __builtin_bit_cast(float, 0x3102e308u), r);
+  float p = fmaf(r, __builtin_bit_cast(float, 0x395133b1u), __builtin_bit_cast(float, 0x3ab69700u));
+  p = fmaf(r, p, __builtin_bit_cast(float, 0x3c0887f9u));
+  p = fmaf(r, p, __builtin_bit_cast(float, 0x3d2aaa81u));
+  p = fmaf(r, p, __builtin_bit_cast(float, 0x3e2aaaabu));
+  p = fmaf(r, p, 0.5f);
+  p = r * p;
+  const float m = fmaf(r, p, r);  // expm1(r)
+  const float t = __builtin_ldexpf(1.0f, (int)n);
+  return fmaf(t, m, t - 1.0f);
+#endif
+}
 
 __device__ __forceinline__ float ph_act(float v, int act) {
   if (act == ACT_RELU) return v > 0.0f ? v : 0.0f;
 #ifdef T1_HEADS_WHATIF_NOELU  // timing-only what-if build: ELU as ReLU
   if (act == ACT_ELU) return v > 0.0f ? v : 0.0f;
 #else
-  if (act == ACT_ELU) return v > 0.0f ? v : expm1f(v);
+  if (act == ACT_ELU) return v > 0.0f ? v : (T1_HEADS_FAST_ELU ? ph_expm1_neg(v) : expm1f(v));
 #endif
   return v;
 }
@@ -256,6 +311,7 @@ __device__ __forceinline__ void ph_stage(Frag* dst, int steps, const float* __re
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = 16 * s + 8 * h + j;
+      // (non-temporal loads here, so the once-read inputs would not evict fragments: act() 0.129 -> 0.153 ms, r07c)
       float x = (live && c < len) ? row[c] : 0.0f;
       v[j] = RELU ? (x > 0.0f ? x : 0.0f) : x;
     }
@@ -287,12 +343,20 @@ struct PhOut {  // the global outputs (OUT_MEAN / OUT_VALUE layers)
 // (about 16 x 96 MFMA cycles of cover over an L2 hit under load); its first D steps are issued during the previous
 // layer (ph_prologue), so no layer starts on an empty pipeline
 template <int L> struct PhRing {
-  static constexpr int NT = ph_nt(L), KS = PH_L[L].ks, T = (NT + PH_WAVES - 1) / PH_WAVES;
+  static constexpr int NT = ph_nt(L), KS = PH_L[L].ks, SK = ph_sk(L), KL = KS / SK;
+  static constexpr int T = SK > 1 ? 1 : (NT + PH_WAVES - 1) / PH_WAVES;
+  // the wave's output tile i and the first of its KL k-steps (idle waves: a valid tile, loaded and never used)
+  static __device__ __forceinline__ int tile(int wave, int i) {
+    if constexpr (SK > 1) return wave % NT;
+    return (wave + PH_WAVES * i) < NT ? wave + PH_WAVES * i : NT - 1;
+  }
+  static __device__ __forceinline__ int kpart(int wave) { return SK > 1 && wave < NT * SK ? wave / NT : 0; }
+  static __device__ __forceinline__ bool busy(int wave) { return PH_WAVES == 4 || wave < NT * SK; }
   // two waves per SIMD (PH_WAVES 8): the other wave covers part of the latency, and 256 VGPRs hold the accumulators
   // and a ring of 1-4 steps (4 waves: 512 registers, 4-16 steps)
   static constexpr int D0 = PH_WAVES == 8 ? (T >= 3 ? T1_HEADS_D3 : (T >= 2 ? T1_HEADS_D2 : T1_HEADS_D1))
                                           : (T >= 4 ? 4 : (T >= 2 ? 8 : 16));
-  static constexpr int D = D0 < KS ? D0 : KS - 1;
+  static constexpr int D = D0 < KL ? D0 : KL - 1;
   static constexpr int R = D + 1;
   h8 w[R][T][2];
 };
@@ -301,13 +365,14 @@ __device__ __forceinline__ void ph_load(const h8* __restrict__ frag, PhRing<L>& 
                                         int lane) {
   typedef PhRing<L> G;
   constexpr int OFF = ph_off(L);
+  const int ks = G::kpart(wave) * G::KL + s;  // s counts the wave's own k-steps
 #pragma unroll
   for (int i = 0; i < G::T; ++i) {
-    const int nt = (wave + PH_WAVES * i) < G::NT ? wave + PH_WAVES * i : G::NT - 1;
+    const int nt = G::tile(wave, i);
 #ifdef T1_HEADS_WHATIF_NOLOAD  // timing-only what-if build: every fragment load hits the same 2 KB (L1)
-    const h8* w = frag + lane + (size_t)(((OFF + nt * G::KS + s) & 0) * 2) * 64;
+    const h8* w = frag + lane + (size_t)(((OFF + nt * G::KS + ks) & 0) * 2) * 64;
 #else
-    const h8* w = frag + lane + (size_t)((OFF + nt * G::KS + s) * 2) * 64;
+    const h8* w = frag + lane + (size_t)((OFF + nt * G::KS + ks) * 2) * 64;
 #endif
     rg.w[slot][i][0] = w[0];
     rg.w[slot][i][1] = w[64];
@@ -327,11 +392,12 @@ __device__ __forceinline__ void ph_prologue(const h8* __restrict__ frag, PhRing<
 template <int L, int OUT, int LN>
 __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhParams& P, const Frag* in, Frag* out,
                                          int out0, const PhOut& G, int wave, int lane, PhRing<L>& rg,
-                                         PhRing<(LN < 0 ? L : LN)>* nx) {
+                                         PhRing<(LN < 0 ? L : LN)>* nx, float4 (*red)[4][64]) {
   constexpr Layer Y = PH_L[L];
   typedef PhRing<L> RG;
-  constexpr int NT = RG::NT, KS = RG::KS, T = RG::T, D = RG::D, R = RG::R;
+  constexpr int NT = RG::NT, KL = RG::KL, SK = RG::SK, T = RG::T, D = RG::D, R = RG::R;
   const int h = lane >> 5;
+  const int k0 = RG::kpart(wave) * KL;  // the wave's first k-step (split-K), wave-uniform
   f16v acc0[T], acc1[T];
 #pragma unroll
   for (int i = 0; i < T; ++i)
@@ -339,25 +405,25 @@ __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhPa
     for (int r = 0; r < 16; ++r) acc0[i][r] = acc1[i][r] = 0.0f;
   float4 bias[T][4];
   h8 bq[2][2];
-  bq[0][0] = in[0][0][lane];
-  bq[0][1] = in[0][1][lane];
-  // a wave past the layer's tile count (PH_WAVES 8 on the narrow layers) skips the K loop (it stores nothing)
-  if (PH_WAVES == 4 || wave < NT)
+  bq[0][0] = in[k0][0][lane];
+  bq[0][1] = in[k0][1][lane];
+  // a wave past the layer's tiles x k parts (PH_WAVES 8 on the narrow layers) skips the K loop (it stores nothing)
+  if (RG::busy(wave))
 #pragma clang loop unroll(full)
-  for (int s = 0; s < KS; ++s) {
-    if (s + D < KS) ph_load<L>(frag, rg, (s + D) % R, s + D, wave, lane);
-    if (s == KS - 1 - D) {  // the bias fragments behind the layer's last weight loads (no drain at the epilogue)
+  for (int s = 0; s < KL; ++s) {
+    if (s + D < KL) ph_load<L>(frag, rg, (s + D) % R, s + D, wave, lane);
+    if (s == KL - 1 - D) {  // the bias fragments behind the layer's last weight loads (no drain at the epilogue)
       const float4* bf = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(frag) + PH_WFRAG_BYTES);
 #pragma unroll
       for (int i = 0; i < T; ++i) {
-        const int nt = (wave + PH_WAVES * i) < NT ? wave + PH_WAVES * i : NT - 1;
+        const int nt = RG::tile(wave, i);
 #pragma unroll
         for (int q = 0; q < 4; ++q) bias[i][q] = bf[((ph_toff(L) + nt) * 4 + q) * 64 + lane];
       }
     }
-    if (s + 1 < KS) {
-      bq[(s + 1) & 1][0] = in[s + 1][0][lane];
-      bq[(s + 1) & 1][1] = in[s + 1][1][lane];
+    if (s + 1 < KL) {
+      bq[(s + 1) & 1][0] = in[k0 + s + 1][0][lane];
+      bq[(s + 1) & 1][1] = in[k0 + s + 1][1][lane];
     }
     __builtin_amdgcn_sched_barrier(0);
     const h8 bh = bq[s & 1][0], bl = bq[s & 1][1];
@@ -375,16 +441,41 @@ __device__ __forceinline__ void ph_layer(const h8* __restrict__ frag, const PhPa
     __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (LN >= 0) ph_prologue<LN>(frag, *nx, wave, lane);  // the next layer's first fragments in flight
+  float y[T][16];  // hi.hi + 2^-11 (hi.lo + lo.hi) per element, then the split-K partials in k order
+#pragma unroll
+  for (int i = 0; i < T; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) y[i][r] = acc0[i][r] + acc1[i][r] * (1.0f / PH_SPLIT);
+  if constexpr (SK > 1) {
+    const int kh = RG::kpart(wave);
+    if (RG::busy(wave) && kh > 0) {
+      float4(*dst)[64] = red[(kh - 1) * NT + wave % NT];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[q][lane] = make_float4(y[0][4 * q], y[0][4 * q + 1], y[0][4 * q + 2], y[0][4 * q + 3]);
+    }
+    __syncthreads();  // every wave: the partials in LDS
+    if (wave < NT) {
+#pragma unroll
+      for (int p = 1; p < SK; ++p) {
+        const float4(*src)[64] = red[(p - 1) * NT + wave];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 u = src[q][lane];
+          y[0][4 * q] += u.x; y[0][4 * q + 1] += u.y; y[0][4 * q + 2] += u.z; y[0][4 * q + 3] += u.w;
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < T; ++i) {
     const int nt = wave + PH_WAVES * i;
-    if (nt >= NT) break;  // wave-uniform
+    if (nt >= NT) break;  // wave-uniform (split-K: the kh = 0 waves, 0 .. NT - 1)
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float4 b4 = bias[i][r >> 2];
       const float b = (r & 3) == 0 ? b4.x : (r & 3) == 1 ? b4.y : (r & 3) == 2 ? b4.z : b4.w;
-      v[r] = ph_act(acc0[i][r] + acc1[i][r] * (1.0f / PH_SPLIT) + b, Y.act);
+      v[r] = ph_act(y[i][r] + b, Y.act);
     }
     if constexpr (OUT == OUT_LDS || OUT == OUT_LDS_HALF) {
 #pragma unroll
@@ -427,6 +518,11 @@ __global__ __launch_bounds__(64 * PH_WAVES) __attribute__((amdgpu_waves_per_eu(P
 void k_heads(PhParams P, const h8* __restrict__ frag, const float* __restrict__ y1, const float* __restrict__ obs,
              int obs_cols, const float* __restrict__ cobs, int cobs_cols, PhOut G, int batch, int xcd_split) {
   __shared__ PhLds S;
+#if T1_HEADS_SPLITK
+  float4(*red)[4][64] = S.red;
+#else
+  float4(*red)[4][64] = nullptr;
+#endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   // role and tile: blockIdx mod 8 is the XCD; actor tiles on XCDs 0-3, critic tiles on 4-7 (xcd_split), else
@@ -451,35 +547,35 @@ void k_heads(PhParams P, const h8* __restrict__ frag, const float* __restrict__ 
     ph_prologue<0>(frag, g0, wave, lane);  // the first layer's fragments load across the barrier
     __syncthreads();
     PhRing<1> g1;
-    ph_layer<0, OUT_LDS, 1>(frag, P, A.p, A.q, 0, G, wave, lane, g0, &g1);
+    ph_layer<0, OUT_LDS, 1>(frag, P, A.p, A.q, 0, G, wave, lane, g0, &g1, red);
     __syncthreads();
     PhRing<2> g2;
-    ph_layer<1, OUT_LDS, 2>(frag, P, A.q, A.p, 0, G, wave, lane, g1, &g2);
+    ph_layer<1, OUT_LDS, 2>(frag, P, A.q, A.p, 0, G, wave, lane, g1, &g2, red);
     __syncthreads();
     PhRing<3> g3;
-    ph_layer<2, OUT_LDS, 3>(frag, P, A.p, A.x, 16, G, wave, lane, g2, &g3);  // history code -> actor input 16..19
+    ph_layer<2, OUT_LDS, 3>(frag, P, A.p, A.x, 16, G, wave, lane, g2, &g3, red);  // history code -> actor input 16..19
     PhRing<4> g4;
-    ph_layer<3, OUT_LDS, 4>(frag, P, A.x, A.q, 0, G, wave, lane, g3, &g4);  // reads steps 0..14 only: no barrier
+    ph_layer<3, OUT_LDS, 4>(frag, P, A.x, A.q, 0, G, wave, lane, g3, &g4, red);  // reads steps 0..14 only: no barrier
     __syncthreads();
     PhRing<5> g5;
-    ph_layer<4, OUT_LDS, 5>(frag, P, A.q, A.p, 0, G, wave, lane, g4, &g5);
+    ph_layer<4, OUT_LDS, 5>(frag, P, A.q, A.p, 0, G, wave, lane, g4, &g5, red);
     __syncthreads();
     PhRing<6> g6;
-    ph_layer<5, OUT_LDS, 6>(frag, P, A.p, A.q, 0, G, wave, lane, g5, &g6);
+    ph_layer<5, OUT_LDS, 6>(frag, P, A.p, A.q, 0, G, wave, lane, g5, &g6, red);
     __syncthreads();
     PhRing<7> g7;
-    ph_layer<6, OUT_LDS_HALF, 7>(frag, P, A.q, A.x, 15, G, wave, lane, g6, &g7);  // estimate -> actor input 15
+    ph_layer<6, OUT_LDS_HALF, 7>(frag, P, A.q, A.x, 15, G, wave, lane, g6, &g7, red);  // estimate -> actor input 15
     __syncthreads();
     PhRing<8> g8;
-    ph_layer<7, OUT_LDS, 8>(frag, P, A.x, A.p, 0, G, wave, lane, g7, &g8);
+    ph_layer<7, OUT_LDS, 8>(frag, P, A.x, A.p, 0, G, wave, lane, g7, &g8, red);
     __syncthreads();
     PhRing<9> g9;
-    ph_layer<8, OUT_LDS, 9>(frag, P, A.p, A.q, 0, G, wave, lane, g8, &g9);
+    ph_layer<8, OUT_LDS, 9>(frag, P, A.p, A.q, 0, G, wave, lane, g8, &g9, red);
     __syncthreads();
     PhRing<10> g10;
-    ph_layer<9, OUT_LDS, 10>(frag, P, A.q, A.p, 0, G, wave, lane, g9, &g10);
+    ph_layer<9, OUT_LDS, 10>(frag, P, A.q, A.p, 0, G, wave, lane, g9, &g10, red);
     __syncthreads();
-    ph_layer<10, OUT_MEAN, -1>(frag, P, A.p, nullptr, 0, G, wave, lane, g10, nullptr);
+    ph_layer<10, OUT_MEAN, -1>(frag, P, A.p, nullptr, 0, G, wave, lane, g10, nullptr, red);
   } else {
     CriticLds& C = S.c;
     ph_stage<false>(C.q, 14, cobs, cobs_cols, 0, PH_CRITIC, envc, live, wave, lane);
@@ -487,15 +583,15 @@ void k_heads(PhParams P, const h8* __restrict__ frag, const float* __restrict__ 
     ph_prologue<11>(frag, g11, wave, lane);
     __syncthreads();
     PhRing<12> g12;
-    ph_layer<11, OUT_LDS, 12>(frag, P, C.q, C.p, 0, G, wave, lane, g11, &g12);
+    ph_layer<11, OUT_LDS, 12>(frag, P, C.q, C.p, 0, G, wave, lane, g11, &g12, red);
     __syncthreads();
     PhRing<13> g13;
-    ph_layer<12, OUT_LDS, 13>(frag, P, C.p, C.q, 0, G, wave, lane, g12, &g13);
+    ph_layer<12, OUT_LDS, 13>(frag, P, C.p, C.q, 0, G, wave, lane, g12, &g13, red);
     __syncthreads();
     PhRing<14> g14;
-    ph_layer<13, OUT_LDS, 14>(frag, P, C.q, C.p, 0, G, wave, lane, g13, &g14);
+    ph_layer<13, OUT_LDS, 14>(frag, P, C.q, C.p, 0, G, wave, lane, g13, &g14, red);
     __syncthreads();
-    ph_layer<14, OUT_VALUE, -1>(frag, P, C.p, nullptr, 0, G, wave, lane, g14, nullptr);
+    ph_layer<14, OUT_VALUE, -1>(frag, P, C.p, nullptr, 0, G, wave, lane, g14, nullptr, red);
   }
 }
 
