@@ -77,6 +77,35 @@ def test_fused_heads_match_fp64(n, scale):
     assert (value - rv).abs().max() <= 4 * (v32 - rv).abs().max() + 1e-6
 
 
+def test_fused_heads_propagate_nan_like_torch():
+    """A NaN in one env's inputs reaches that env's outputs as NaN (torch's ELU keeps NaN; the kernel's expm1 for ELU's
+    negative branch must not clamp it to -1), and no other env is touched."""
+    from ti5_isaacgym_amd.algo.dh_policy import heads_forward
+    ac = _model()
+    dev = torch.device("cuda:0")
+    acd = _copy(ac).to(dev)
+    n = 96
+    g = torch.Generator().manual_seed(7)
+    obs = (torch.randn(n, 66 * 47, generator=g) * 2.0).clamp(-18, 18)
+    cobs = torch.randn(n, 219, generator=g) * 2.0
+    eps = torch.randn(n, 12, generator=g)
+    obs[5, -3] = float("nan")     # the short history: the estimator and the actor
+    cobs[40, 7] = float("nan")    # the critic
+    with torch.inference_mode():
+        mean, act, sigma, logp, value = [t.cpu() for t in heads_forward(acd, obs.to(dev), cobs.to(dev), eps.to(dev))]
+        m32 = acd.actor(acd.actor_input(obs.to(dev))).cpu()
+        v32 = acd.critic(cobs.to(dev)).cpu()
+    assert torch.isnan(m32[5]).all() and torch.isnan(v32[40]).all()   # torch's own layers
+    assert torch.isnan(mean[5]).all() and torch.isnan(logp[5])
+    assert torch.isnan(value[40]).all()
+    keep = torch.ones(n, dtype=torch.bool)
+    keep[5] = False
+    assert torch.isfinite(mean[keep]).all() and torch.isfinite(logp[keep]).all()
+    keep = torch.ones(n, dtype=torch.bool)
+    keep[40] = False
+    assert torch.isfinite(value[keep]).all()
+
+
 def test_fused_heads_follow_weight_updates():
     """heads_forward repacks the weights when a parameter changed: an in-place parameter change shows up in the next
     call."""

@@ -260,7 +260,8 @@ struct PhLds {
 #endif
 // expm1(v) for ELU's negative branch, branch-free.  1: the device library's expm1f algorithm (range reduction by
 // n = rint(v log2 e) with ln 2 in two parts, the same degree-7 polynomial, 2^n expm1(r) + (2^n - 1)) without its
-// overflow and v < -17 fix-ups, which v <= 0 never needs once v is clamped at -88: bit-identical to expm1f there.
+// overflow and v < -17 fix-ups, which v <= 0 never needs once v is clamped at -88: bit-identical to expm1f there (NaN
+// included).
 // 2: 2^(v log2 e) - 1 on the hardware exponential below -1/4, a degree-6 Taylor polynomial above (not bit-identical).
 __device__ __forceinline__ float ph_expm1_neg(float v) {
 #if T1_HEADS_FAST_ELU == 2
@@ -272,7 +273,7 @@ __device__ __forceinline__ float ph_expm1_neg(float v) {
   p = fmaf(v * v, p, v);
   return v < -0.25f ? e : p;
 #else
-  v = fmaxf(v, -88.0f);
+  v = v < -88.0f ? -88.0f : v;  // (not fmaxf: a NaN stays a NaN, as in expm1f and torch's ELU)
   const float n = __builtin_rintf(v * __builtin_bit_cast(float, 0x3fb8aa3bu));
   float r = fmaf(n, __builtin_bit_cast(float, 0xbf317218u), v);
   r = fmaf(n, __builtin_bit_cast(float, 0x3102e308u), r);
@@ -293,7 +294,16 @@ __device__ __forceinline__ float ph_act(float v, int act) {
 #ifdef T1_HEADS_WHATIF_NOELU  // timing-only what-if build: ELU as ReLU
   if (act == ACT_ELU) return v > 0.0f ? v : 0.0f;
 #else
-  if (act == ACT_ELU) return v > 0.0f ? v : (T1_HEADS_FAST_ELU ? ph_expm1_neg(v) : expm1f(v));
+#if T1_HEADS_FAST_ELU && defined(T1_HEADS_ELU_BRANCH)  // A/B: the expm1 under a branch per value (hipcc's choice)
+  if (act == ACT_ELU) return v > 0.0f ? v : ph_expm1_neg(v);
+#elif T1_HEADS_FAST_ELU
+  if (act == ACT_ELU) {  // branch-free: expm1 of min(v, 0) (a NaN passes through), then the select
+    const float e = ph_expm1_neg(v > 0.0f ? 0.0f : v);
+    return v > 0.0f ? v : e;
+  }
+#else
+  if (act == ACT_ELU) return v > 0.0f ? v : expm1f(v);
+#endif
 #endif
   return v;
 }
