@@ -77,6 +77,28 @@ def test_fused_heads_match_fp64(n, scale):
     assert (value - rv).abs().max() <= 4 * (v32 - rv).abs().max() + 1e-6
 
 
+@pytest.mark.parametrize("n", [3000, 8192, 33])
+def test_heads64_equals_heads32(n, monkeypatch):
+    """k_heads64 (64 envs per workgroup, the 512- / 768-wide layers in halves / thirds feeding the next layer's
+    accumulators) against the 32-env k_heads (T1POLICY_HEADS64=0): the same fragments, the same k order into the same
+    fp32 accumulators per env column, so every output is bit-identical."""
+    from ti5_isaacgym_amd.algo.dh_policy import heads_forward
+    ac = _model(scale=1.5)
+    dev = torch.device("cuda:0")
+    acd = _copy(ac).to(dev)
+    g = torch.Generator().manual_seed(n + 1)
+    obs = ((torch.randn(n, 66 * 47, generator=g) * 2.0).clamp(-18, 18)).to(dev)
+    cobs = (torch.randn(n, 219, generator=g) * 2.0).to(dev)
+    eps = torch.randn(n, 12, generator=g).to(dev)
+    with torch.inference_mode():
+        monkeypatch.setenv("T1POLICY_HEADS64", "1")
+        o64 = [t.clone() for t in heads_forward(acd, obs, cobs, eps)]
+        monkeypatch.setenv("T1POLICY_HEADS64", "0")
+        o32 = [t.clone() for t in heads_forward(acd, obs, cobs, eps)]
+    for name, a, b in zip(("mean", "actions", "sigma", "logp", "value"), o64, o32):
+        assert torch.equal(a, b), (name, (a - b).abs().max().item())
+
+
 def test_fused_heads_propagate_nan_like_torch():
     """A NaN in one env's inputs reaches that env's outputs as NaN (torch's ELU keeps NaN; the kernel's expm1 for ELU's
     negative branch must not clamp it to -1), and no other env is touched."""

@@ -9,7 +9,8 @@
 // plus the Normal sample, its log-prob and the broadcast sigma (DHPPO._act_body), from the first conv's output
 // (t1policy_conv1d_forward_packed), the actor and critic observations and a standard-normal draw.
 //
-// A workgroup owns 32 envs and one role (actor chain or critic), eight waves (two per SIMD) splitting each layer's
+// A workgroup owns 64 envs (k_heads64, the default: two 32-env column tiles sharing every weight fragment, below) or
+// 32 (k_heads, A/B) and one role (actor chain or critic), eight waves (two per SIMD) splitting each layer's
 // 32-output tiles; every layer is a chain of
 // v_mfma_f32_32x32x16_f16 with the WEIGHTS as the A operand (32 output features x 16 inputs) and the ACTIVATIONS as
 // the B operand (16 inputs x 32 envs), so a layer's 32 x 32 result has the env on the lane and the features in the
@@ -605,6 +606,285 @@ void k_heads(PhParams P, const h8* __restrict__ frag, const float* __restrict__ 
   }
 }
 
+// ---- 64 envs per workgroup (k_heads64, the default; T1POLICY_HEADS64=0: the 32-env k_heads above, A/B).  At 32 envs
+// a workgroup takes ~42 us whether 256 or 512 of them run (4096 / 8192 envs, profiles/r07e), and its 139 KB of LDS
+// leaves one per CU, so 8192 envs take two rounds.  Here each weight fragment feeds BOTH 32-env column tiles (six
+// MFMAs per step-tile instead of three, the same fragment stream per workgroup), so 8192 envs take one round.  The LDS
+// holds 64 envs' activations in 144 KB because no layer output wider than 256 is ever resident: the actor's 512-wide
+// layer runs in two halves of 8 output tiles and the critic's 768-wide one in three, each half / third feeding the
+// next layer's accumulators (held in registers across the calls) before the next one overwrites it; the short
+// history is staged twice (the estimator's first layer, then the actor's).  Every layer call has one output tile per
+// wave (8 waves, T = 1).
+typedef h8 Frag2[2][2][64];  // one k-step of B fragments of both 32-env tiles: [env tile][hi, lo][lane]
+struct Heads64Lds {
+  Frag2 px[36];  // actor: PX[0..35]; critic: PX[0..31] (layout per phase in k_heads64)
+};
+
+// one layer call: layer L's output tiles [TB, TB + 8) (or to the layer's last tile) over its k-steps [KB, KE)
+template <int L_, int KB_, int KE_, int TB_> struct P6Ring {
+  static constexpr int L = L_, KB = KB_, KE = KE_, TB = TB_;
+  static constexpr int NTL = ph_nt(L), TE = TB + PH_WAVES < NTL ? TB + PH_WAVES : NTL, NW = TE - TB;
+  static constexpr int KL = KE - KB, D = T1_HEADS_D1 < KL ? T1_HEADS_D1 : KL - 1, R = D + 1;
+  static_assert(PH_WAVES == 8 && KL >= 1 && NW >= 1 && KE <= PH_L[L].ks, "one output tile per wave");
+  static __device__ __forceinline__ int tile(int wave) { return wave < NW ? TB + wave : TE - 1; }
+  h8 w[R][2];
+};
+struct P6None {
+  static constexpr int L = -1;
+};
+template <class RG>
+__device__ __forceinline__ void ph6_load(const h8* __restrict__ frag, RG& rg, int slot, int s, int wave, int lane) {
+  const h8* w = frag + lane + (size_t)((ph_off(RG::L) + RG::tile(wave) * PH_L[RG::L].ks + RG::KB + s) * 2) * 64;
+  rg.w[slot][0] = w[0];
+  rg.w[slot][1] = w[64];
+}
+template <class RG>
+__device__ __forceinline__ void ph6_prologue(const h8* __restrict__ frag, RG& rg, int wave, int lane) {
+#pragma clang loop unroll(full)
+  for (int s = 0; s < RG::D; ++s) ph6_load(frag, rg, s, s, wave, lane);
+}
+
+struct PhOut64 {  // the global outputs and the workgroup's envs
+  const float* eps;
+  const float* std;
+  float* mean;
+  float* actions;
+  float* sigma;
+  float* logp;
+  float* value;
+  int env0;
+  int batch;
+};
+
+// staging as ph_stage, for both env tiles: element j of lane (r, h) of step s, tile et = src[env0 + 32 et + r][col0 +
+// 16 s + 8 h + j]
+template <bool RELU>
+__device__ __forceinline__ void ph6_stage(Frag2* dst, int steps, const float* __restrict__ src, long long stride,
+                                          int col0, int len, int env0, int batch, int wave, int lane) {
+  const int h = lane >> 5;
+  for (int s = wave; s < steps; s += PH_WAVES) {
+#pragma unroll
+    for (int et = 0; et < 2; ++et) {
+      const int env = env0 + 32 * et + (lane & 31);
+      const bool live = env < batch;
+      const float* row = src + (long long)(live ? env : batch - 1) * stride + col0;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 16 * s + 8 * h + j;
+        const float x = (live && c < len) ? row[c] : 0.0f;
+        v[j] = RELU ? (x > 0.0f ? x : 0.0f) : x;
+      }
+      h8 hi, lo;
+      split8(v, hi, lo);
+      dst[s][et][0][lane] = hi;
+      dst[s][et][1][lane] = lo;
+    }
+  }
+}
+
+// one layer call (see P6Ring): B fragments in[0 .. KL) from LDS, A fragments through the ring rg (prologue issued by the
+// previous call), six MFMAs per k-step into acc (ZERO: start from 0; the caller owns acc, so a layer split over calls
+// keeps its sums); EPI: result + bias through the activation into out (k-steps out0 + 2 (tile - TB) + {0, 1}) or the
+// global outputs.  NX: the next call's ring, whose first fragments are issued before this call's epilogue.
+template <class RG, int OUT, bool ZERO, bool EPI, class NX>
+__device__ __forceinline__ void ph6_call(const h8* __restrict__ frag, const Frag2* in, Frag2* out, int out0,
+                                         const PhOut64& G, int wave, int lane, RG& rg, NX* nx, f16v (&acc0)[2],
+                                         f16v (&acc1)[2]) {
+  constexpr Layer Y = PH_L[RG::L];
+  constexpr int KL = RG::KL, D = RG::D, R = RG::R;
+  const int h = lane >> 5;
+  const bool busy = wave < RG::NW;  // wave-uniform
+  if constexpr (ZERO) {
+#pragma unroll
+    for (int et = 0; et < 2; ++et)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc0[et][r] = acc1[et][r] = 0.0f;
+  }
+  float4 bias[4];
+  h8 bq[2][2][2];  // [buffer][env tile][hi, lo]
+#pragma unroll
+  for (int et = 0; et < 2; ++et) {
+    bq[0][et][0] = in[0][et][0][lane];
+    bq[0][et][1] = in[0][et][1][lane];
+  }
+  if (busy)
+#pragma clang loop unroll(full)
+    for (int s = 0; s < KL; ++s) {
+      if (s + D < KL) ph6_load(frag, rg, (s + D) % R, s + D, wave, lane);
+      if (EPI && s == KL - 1 - D) {  // the bias fragments behind the call's last weight loads
+        const float4* bf = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(frag) + PH_WFRAG_BYTES);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bias[q] = bf[((ph_toff(RG::L) + RG::tile(wave)) * 4 + q) * 64 + lane];
+      }
+      if (s + 1 < KL) {
+#pragma unroll
+        for (int et = 0; et < 2; ++et) {
+          bq[(s + 1) & 1][et][0] = in[s + 1][et][0][lane];
+          bq[(s + 1) & 1][et][1] = in[s + 1][et][1][lane];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const h8 ah = rg.w[s % R][0], al = rg.w[s % R][1];
+#pragma unroll
+      for (int et = 0; et < 2; ++et) {
+        const h8 bh = bq[s & 1][et][0], bl = bq[s & 1][et][1];
+        acc0[et] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc0[et], 0, 0, 0);
+        acc1[et] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc1[et], 0, 0, 0);
+        acc1[et] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc1[et], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  if constexpr (NX::L >= 0) ph6_prologue(frag, *nx, wave, lane);  // the next call's first fragments in flight
+  if constexpr (EPI) {
+    if (!busy) return;
+    const int nt = RG::TB + wave;
+#pragma unroll
+    for (int et = 0; et < 2; ++et) {
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float4 b4 = bias[r >> 2];
+        const float b = (r & 3) == 0 ? b4.x : (r & 3) == 1 ? b4.y : (r & 3) == 2 ? b4.z : b4.w;
+        v[r] = ph_act(acc0[et][r] + acc1[et][r] * (1.0f / PH_SPLIT) + b, Y.act);
+      }
+      const int env = G.env0 + 32 * et + (lane & 31);
+      const bool live = env < G.batch;
+      if constexpr (OUT == OUT_LDS || OUT == OUT_LDS_HALF) {
+#pragma unroll
+        for (int s = 0; s < (OUT == OUT_LDS ? 2 : 1); ++s) {
+          float u[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) u[j] = v[8 * s + j];
+          h8 hi, lo;
+          split8(u, hi, lo);
+          out[out0 + 2 * (nt - RG::TB) + s][et][0][lane] = hi;
+          out[out0 + 2 * (nt - RG::TB) + s][et][1][lane] = lo;
+        }
+      } else if constexpr (OUT == OUT_MEAN) {  // as ph_layer's OUT_MEAN
+        float lp = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (row < Y.n && live) {
+            const float sd = G.std[row];
+            const size_t ix = (size_t)env * Y.n + row;
+            const float a = v[r] + sd * G.eps[ix];
+            const float d = a - v[r];
+            lp += -(d * d) / (2.0f * (sd * sd)) - logf(sd) - 0.91893853320467274178f;  // log(sqrt(2 pi))
+            G.mean[ix] = v[r];
+            G.actions[ix] = a;
+            G.sigma[ix] = sd;
+          }
+        }
+        lp += __shfl_xor(lp, 32);
+        if (h == 0 && live) G.logp[env] = lp;
+      } else {
+        if (h == 0 && live) G.value[env] = v[0];
+      }
+    }
+  }
+}
+
+template <int L, int KB, int KE, int TB = 0> using R6 = P6Ring<L, KB, KE, TB>;
+template <int L> using R6F = P6Ring<L, 0, PH_L[L].ks, 0>;  // a whole layer
+
+__global__ __launch_bounds__(64 * PH_WAVES) __attribute__((amdgpu_waves_per_eu(PH_WAVES / 4, PH_WAVES / 4)))
+void k_heads64(const h8* __restrict__ frag, const float* __restrict__ y1, const float* __restrict__ obs, int obs_cols,
+               const float* __restrict__ cobs, int cobs_cols, PhOut64 G, int batch) {
+  __shared__ Heads64Lds S;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // both roles on every XCD (blockIdx mod 8), alternating in each XCD's dispatch order (k_heads' xcd_split 2)
+  const int bid = blockIdx.x;
+  const bool critic = ((bid >> 3) & 1) != 0;
+  const int tile = ((bid >> 4) << 3) + (bid & 7);
+  G.env0 = tile * 64;
+  G.batch = batch;
+  if (G.env0 >= batch) return;
+  Frag2* X = S.px;
+  f16v a0[2], a1[2];  // the current call's accumulators
+  f16v b0[2], b1[2];  // the layer after a split one: its sums across the split layer's calls
+  if (!critic) {
+    // PX[0..27] the relu'd conv1 output; L0 -> PX[28..33]; L1 -> PX[0..7]; short history -> PX[16..30]; L2 (the
+    // history code) -> PX[32..35]; L3 -> PX[0..15]; L4 -> PX[16..23]; L5 -> PX[0..3]; L6 (the estimate) -> PX[31];
+    // short history again -> PX[16..30]; the actor input is PX[16..35]; L7 halves -> PX[0..15], each into L8's sums;
+    // L8 -> PX[16..31]; L9 -> PX[0..7]; L10 -> the outputs
+    ph6_stage<true>(X, 28, y1, PH_Y1, 0, PH_Y1, G.env0, batch, wave, lane);
+    R6F<0> g0;
+    ph6_prologue(frag, g0, wave, lane);
+    __syncthreads();
+    R6F<1> g1;
+    ph6_call<R6F<0>, OUT_LDS, true, true>(frag, X, X, 28, G, wave, lane, g0, &g1, a0, a1);
+    __syncthreads();
+    R6F<2> g2;
+    ph6_call<R6F<1>, OUT_LDS, true, true>(frag, X + 28, X, 0, G, wave, lane, g1, &g2, a0, a1);
+    __syncthreads();
+    ph6_stage<false>(X + 16, 15, obs, obs_cols, obs_cols - PH_OBS_SHORT, PH_OBS_SHORT, G.env0, batch, wave, lane);
+    R6F<3> g3;
+    ph6_call<R6F<2>, OUT_LDS, true, true>(frag, X, X, 32, G, wave, lane, g2, &g3, a0, a1);
+    __syncthreads();
+    R6F<4> g4;
+    ph6_call<R6F<3>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g3, &g4, a0, a1);
+    __syncthreads();
+    R6F<5> g5;
+    ph6_call<R6F<4>, OUT_LDS, true, true>(frag, X, X, 16, G, wave, lane, g4, &g5, a0, a1);
+    __syncthreads();
+    R6F<6> g6;
+    ph6_call<R6F<5>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g5, &g6, a0, a1);
+    __syncthreads();
+    R6<7, 0, 20, 0> g7a;
+    ph6_call<R6F<6>, OUT_LDS_HALF, true, true>(frag, X, X, 31, G, wave, lane, g6, &g7a, a0, a1);
+    ph6_stage<false>(X + 16, 15, obs, obs_cols, obs_cols - PH_OBS_SHORT, PH_OBS_SHORT, G.env0, batch, wave, lane);
+    __syncthreads();
+    R6<8, 0, 16> g8a;
+    ph6_call<R6<7, 0, 20, 0>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g7a, &g8a, a0, a1);
+    __syncthreads();
+    R6<7, 0, 20, 8> g7b;
+    ph6_call<R6<8, 0, 16>, OUT_LDS, true, false>(frag, X, nullptr, 0, G, wave, lane, g8a, &g7b, b0, b1);
+    __syncthreads();
+    R6<8, 16, 32> g8b;
+    ph6_call<R6<7, 0, 20, 8>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g7b, &g8b, a0, a1);
+    __syncthreads();
+    R6F<9> g9;
+    ph6_call<R6<8, 16, 32>, OUT_LDS, false, true>(frag, X, X, 16, G, wave, lane, g8b, &g9, b0, b1);
+    __syncthreads();
+    R6F<10> g10;
+    ph6_call<R6F<9>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g9, &g10, a0, a1);
+    __syncthreads();
+    ph6_call<R6F<10>, OUT_MEAN, true, true, P6None>(frag, X, nullptr, 0, G, wave, lane, g10, nullptr, a0, a1);
+  } else {
+    // PX[16..29] the privileged observations; L11 thirds -> PX[0..15], each into L12's sums; L12 -> PX[16..31];
+    // L13 -> PX[0..7]; L14 -> the value
+    ph6_stage<false>(X + 16, 14, cobs, cobs_cols, 0, PH_CRITIC, G.env0, batch, wave, lane);
+    R6<11, 0, 14, 0> g11a;
+    ph6_prologue(frag, g11a, wave, lane);
+    __syncthreads();
+    R6<12, 0, 16> g12a;
+    ph6_call<R6<11, 0, 14, 0>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g11a, &g12a, a0, a1);
+    __syncthreads();
+    R6<11, 0, 14, 8> g11b;
+    ph6_call<R6<12, 0, 16>, OUT_LDS, true, false>(frag, X, nullptr, 0, G, wave, lane, g12a, &g11b, b0, b1);
+    __syncthreads();
+    R6<12, 16, 32> g12b;
+    ph6_call<R6<11, 0, 14, 8>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g11b, &g12b, a0, a1);
+    __syncthreads();
+    R6<11, 0, 14, 16> g11c;
+    ph6_call<R6<12, 16, 32>, OUT_LDS, false, false>(frag, X, nullptr, 0, G, wave, lane, g12b, &g11c, b0, b1);
+    __syncthreads();
+    R6<12, 32, 48> g12c;
+    ph6_call<R6<11, 0, 14, 16>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g11c, &g12c, a0, a1);
+    __syncthreads();
+    R6F<13> g13;
+    ph6_call<R6<12, 32, 48>, OUT_LDS, false, true>(frag, X, X, 16, G, wave, lane, g12c, &g13, b0, b1);
+    __syncthreads();
+    R6F<14> g14;
+    ph6_call<R6F<13>, OUT_LDS, true, true>(frag, X + 16, X, 0, G, wave, lane, g13, &g14, a0, a1);
+    __syncthreads();
+    ph6_call<R6F<14>, OUT_VALUE, true, true, P6None>(frag, X, nullptr, 0, G, wave, lane, g14, nullptr, a0, a1);
+  }
+}
+
 bool ph_params(const uint64_t* params, PhParams& P) {
   for (int l = 0; l < PH_NLAYER; ++l) {
     P.w[l] = reinterpret_cast<const float*>(params[2 * l]);
@@ -655,6 +935,14 @@ int t1policy_heads_forward(const uint64_t* params, const int* dims, const void* 
   if ((reinterpret_cast<uintptr_t>(frag) & 15u) != 0) return -1;
   PhParams P;
   if (!ph_params(params, P)) return -1;
+  const char* hv = getenv("T1POLICY_HEADS64");  // 0: the 32-env k_heads (A/B)
+  if (!(hv && hv[0] == '0')) {
+    const PhOut64 G{eps, P.std, mean, actions, sigma, logp, value, 0, batch};
+    const int tiles = (batch + 63) / 64;
+    hipLaunchKernelGGL(k_heads64, dim3(16 * ((tiles + 7) / 8)), dim3(64 * PH_WAVES), 0, (hipStream_t)stream,
+                       reinterpret_cast<const h8*>(frag), y1, obs, obs_cols, critic_obs, critic_cols, G, batch);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   PhOut G{eps, P.std, mean, actions, sigma, logp, value, 0, false};
   const int tiles = (batch + PH_M - 1) / PH_M;
   const char* xv = getenv("T1POLICY_HEADS_XCD");
