@@ -182,17 +182,19 @@ class DHPPO:
     def train_mode(self):
         self.actor_critic.train()
 
-    def _act_body(self, obs, critic_obs):
+    def _act_body(self, obs, critic_obs, eps=None):
         """act() as one fixed kernel sequence (ActorCriticDH.act / evaluate / get_actions_log_prob).  Two host
         checks cannot run inside a graph: the distribution's argument validation (built without it) and
-        torch.normal's std >= 0 test (the sample is drawn as mean + std * N(0, 1), the same distribution)."""
+        torch.normal's std >= 0 test (the sample is drawn as mean + std * N(0, 1), the same distribution).
+        eps: the N(0, 1) draw of the mean's shape, made by the caller (the graphed act() draws it before each replay,
+        so its graph holds no RNG kernel); None: drawn here."""
         ac = self.actor_critic
         obs, critic_obs = obs.float(), critic_obs.float()   # fp16 env histories (state_dtype="fp16"): no-op for fp32
-        eps = None
         if obs.is_cuda and FUSED_ACT:
             # the fused HIP heads (t1policy_heads_forward): the same draw (randn of the mean's shape), one kernel for
             # every layer after the first conv plus the sample and its log-prob
-            eps = torch.randn(obs.shape[0], ac.std.numel(), device=obs.device)
+            if eps is None:
+                eps = torch.randn(obs.shape[0], ac.std.numel(), device=obs.device)
             out = heads_forward(ac, obs, critic_obs, eps)
             if out is not None:
                 mean, actions, sigma, logp, value = out
@@ -211,22 +213,27 @@ class DHPPO:
         if entry is None:
             if len(self._act_graphs) >= 4:  # not the env's fixed buffers: stay eager
                 return None
+            # the sample's N(0, 1) draw lives outside the graph (eps.normal_() before each replay, the values
+            # torch.randn would draw): a graph with an RNG kernel makes every replay first refill the generator's seed
+            # and offset tensors (two fill launches, ~9 us per act at 8192 envs, profiles/r07e)
+            eps = torch.empty(obs.shape[0], self.actor_critic.std.numel(), device=obs.device)
             side = torch.cuda.Stream(device=obs.device)
             side.wait_stream(torch.cuda.current_stream(obs.device))
             with torch.cuda.stream(side):  # warm-up outside the capture (allocator, library handles)
                 for _ in range(2):
-                    self._act_body(obs, critic_obs)
+                    self._act_body(obs, critic_obs, eps.normal_())
             torch.cuda.current_stream(obs.device).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             try:
                 with torch.cuda.graph(graph):
-                    outs = self._act_body(obs, critic_obs)
+                    outs = self._act_body(obs, critic_obs, eps)
             except RuntimeError as e:  # a library call that cannot be captured: the eager act() from now on
                 warnings.warn(f"DHPPO: act() graph capture failed, running eager: {e}")
                 self.graph_act = False
                 return None
-            entry = self._act_graphs[key] = (graph, outs)
+            entry = self._act_graphs[key] = (graph, outs, eps)
         refresh_packed_weights(self.actor_critic)  # the conv's packed weights after a PPO update (in place)
+        entry[2].normal_()
         entry[0].replay()
         return entry[1]
 
